@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 / CIFAR-10 bf16 training throughput (images/sec, whole job).
+
+BASELINE.json metric: "images/sec (whole node) ResNet-50/CIFAR-10 bf16 at 1/2/4/8 MI355X".
+One process per GPU (torchrun contract: RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), RCCL
+bucketed all-reduce overlapped with backward, fused momentum-SGD on the flat master
+buffer.  Weak scaling: ``--batch`` images per GPU, global batch = batch * N.
+Synthetic CIFAR-shaped data (uint8 32x32x3 images + int64 labels generated on device,
+normalised per step), random-init weights: there is no dataset or network on the box.
+
+Timing: W untimed warmup steps; barrier + synchronize; K timed steps; barrier +
+synchronize; the MAX elapsed over ranks is reported.  Rank 0 prints ONE JSON line.
+
+``--impl torch`` runs a stock PyTorch-ROCm eager ResNet-50 (torch.nn + MIOpen,
+channels_last, bf16 autocast) for a labelled comparison; the headline is ``--impl native``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
+from tensorflow_examples_amd.optim import MomentumOptimizer  # noqa: E402
+from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed  # noqa: E402
+from tensorflow_examples_amd.train import ClassifierTrainer  # noqa: E402
+
+METRIC = "images/sec (whole node) ResNet-50/CIFAR-10 bf16 at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no number for this metric
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--impl", choices=["native", "torch"], default="native")
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph (N=1 only)")
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
+    return ap.parse_args(argv)
+
+
+def synthetic_batches(n, batch, device, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    out = []
+    for _ in range(n):
+        img = torch.randint(0, 256, (batch, 32, 32, 3), dtype=torch.uint8, generator=g)
+        lab = torch.randint(0, 10, (batch,), dtype=torch.long, generator=g)
+        out.append((img.to(device), lab.to(device)))
+    return out
+
+
+def main(argv=None):
+    a = parse(argv)
+    dev = init_distributed(device="cuda")
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    torch.manual_seed(1234 + rank)
+    data = synthetic_batches(a.nbatches, a.batch, dev, seed=1000 + rank)
+
+    if a.impl == "native":
+        store, model = build_resnet_cifar(device=dev, depth=a.depth, dtype=torch.bfloat16, seed=0)
+        broadcast_variables(store)
+        opt = MomentumOptimizer(store, a.lr, momentum=0.9, weight_decay=5e-4)
+        dp = GradAllReduce(store, bucket_bytes=int(a.bucket_mb * (1 << 20))) if world > 1 else None
+        trainer = ClassifierTrainer(store, model, opt, dp)
+
+        def step(i):
+            img, lab = data[i % len(data)]
+            return trainer.step(to_model_input(img), lab)
+
+        if a.graph and world == 1:
+            img, lab = data[0]
+            trainer.capture(to_model_input(img), lab)
+        nparams = store.num_params()
+    else:
+        from tensorflow_examples_amd.models.torch_baseline import TorchResNet50Cifar
+        net = TorchResNet50Cifar().to(dev).to(memory_format=torch.channels_last)
+        if world > 1:
+            net = torch.nn.parallel.DistributedDataParallel(net, device_ids=[dev.index],
+                                                            bucket_cap_mb=a.bucket_mb)
+        topt = torch.optim.SGD(net.parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-4, foreach=True)
+        mean = torch.tensor([0.4914, 0.4822, 0.4465], device=dev).view(1, 3, 1, 1)
+        std = torch.tensor([0.2470, 0.2435, 0.2616], device=dev).view(1, 3, 1, 1)
+        nparams = sum(p.numel() for p in net.parameters())
+
+        def step(i):
+            img, lab = data[i % len(data)]
+            x = ((img.permute(0, 3, 1, 2).float() / 255.0 - mean) / std).contiguous(memory_format=torch.channels_last)
+            topt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = torch.nn.functional.cross_entropy(net(x), lab)
+            loss.backward()
+            topt.step()
+            return loss.detach()
+
+    for i in range(a.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    final_loss = float(loss.float().item())
+    images = a.batch * world * a.steps
+    value = images / elapsed
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1000 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+            "dtype": "bf16",
+            "data": "synthetic (CIFAR-10-shaped uint8 32x32x3 images, random labels, random-init weights)",
+            "config": {
+                "model": "ResNet-%d (CIFAR-10 adaptation: 3x3 stem, bottleneck [3,4,6,3])" % a.depth,
+                "global_batch": a.batch * world,
+                "per_gpu_batch": a.batch,
+                "seq_len": None,
+                "image_hw": [32, 32],
+                "parallelism": "dp%d" % world,
+                "impl": a.impl,
+                "optimizer": "momentum-SGD 0.9, wd 5e-4 (fused flat-buffer kernel)" if a.impl == "native" else "torch.optim.SGD foreach",
+                "allreduce_bucket_mb": a.bucket_mb,
+                "hip_graph": bool(a.graph and world == 1 and a.impl == "native"),
+                "params": nparams,
+                "final_loss": round(final_loss, 4),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,75 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of tensorflow_examples_amd.
+// Wave = 64 lanes everywhere; bf16 is handled as raw 16-bit payloads and
+// vectorised as 16-byte loads (8 x bf16) per lane (cdna_hip_programming.md G13).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TFX_WAVE 64
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef uint16_t u16x8_t __attribute__((ext_vector_type(8)));
+
+struct alignas(16) U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// Round-to-nearest-even; a plain cast lowers to v_cvt_pk_bf16_f32 on gfx950 and keeps NaNs.
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+__device__ __forceinline__ void unpack8(const U4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ U4 pack8(const float* f) {
+  U4 r;
+  r.x = pack_bf16x2(f[0], f[1]);
+  r.y = pack_bf16x2(f[2], f[3]);
+  r.z = pack_bf16x2(f[4], f[5]);
+  r.w = pack_bf16x2(f[6], f[7]);
+  return r;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5, T1):
+// blocks b and b+8 share an XCD's L2 under round-robin dispatch, so hand each XCD a
+// contiguous run of logical tiles.  Pure speed: correctness never depends on placement.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  if (nwg < nx) return bid;
+  const int q = nwg / nx, r = nwg % nx, xcd = bid % nx, idx = bid / nx;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+#define TFX_HIP_CHECK(expr)                                                        \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) {                                                        \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, \
+              __LINE__);                                                           \
+      abort();                                                                     \
+    }                                                                              \
+  } while (0)

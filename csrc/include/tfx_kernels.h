@@ -1,0 +1,66 @@
+// Host-callable launchers of every HIP kernel in csrc/kernels (torch-free; raw pointers +
+// hipStream_t).  The TORCH_LIBRARY bindings in csrc/torch_ops validate shapes and call these.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+namespace tfx {
+
+// ---------------------------------------------------------------- implicit GEMM
+enum { MODE_GEMM = 0, MODE_FWD = 1, MODE_DGRAD = 2, MODE_WGRAD = 3 };
+enum { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ADD = 2, OUT_F32_ATOMIC = 3 };
+
+struct IgemmArgs {
+  const uint16_t* A = nullptr;
+  const uint16_t* B = nullptr;
+  void* Cp = nullptr;
+  const float* bias = nullptr;
+  int M = 0, N = 0, K = 0;
+  int lda = 0, ldb = 0, ldc = 0;
+  int a_kmajor = 1, b_kmajor = 1;
+  // conv geometry (NHWC input [Nb][H][W][C], weight [Ko][R][S][C], output [Nb][P][Q][Ko])
+  int Nb = 0, H = 0, W = 0, C = 0, Ko = 0, R = 1, S = 1, P = 0, Q = 0;
+  int sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
+  int out_mode = OUT_BF16;
+  int relu = 0;
+  int zero_out = 1;
+  // filled by the launcher
+  int kps = 0, tiles_m = 0, tiles_n = 0;
+};
+void igemm_launch(IgemmArgs a, int mode, hipStream_t s);
+
+// ---------------------------------------------------------------- f32 GEMM (MFMA f32, exact)
+// C[M][N] = act(alpha * op(A) op(B) + bias) (+ C if accumulate); op = transpose flags
+void sgemm_launch(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int lda,
+                  int ldb, int ldc, bool transA, bool transB, int act, bool accumulate, hipStream_t s);
+
+// ---------------------------------------------------------------- batch norm (NHWC)
+void bn_stats(const uint16_t* x, int64_t M, int C, float* sums, hipStream_t s);
+void bn_finalize(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
+                 float momentum, float* run_mean, float* run_var, float* save, hipStream_t s);
+void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
+                  const float* run_var, float* save, hipStream_t s);
+void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
+              uint16_t* y, hipStream_t s);
+void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const float* save, int64_t M,
+                 int C, bool relu, float* red, uint16_t* dx, uint16_t* dres, hipStream_t s);
+
+// ---------------------------------------------------------------- loss / pooling
+void softmax_xent(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,
+                  bool naive, float gscale, float* loss_rows, float* dz, float* probs, hipStream_t s);
+void accuracy_count(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,
+                    float* count, hipStream_t s);
+void gap_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y16, float* y32, hipStream_t s);
+void gap_bwd(const void* dy, bool dy_bf16, int N, int HW, int C, uint16_t* dx, hipStream_t s);
+
+// ---------------------------------------------------------------- optimizers (flat buffers)
+void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, float* v, int64_t n,
+                     const float* lr, float gscale, float wd, float b1, float b2, float eps, const float* step,
+                     const float* sumsq, float max_norm, uint16_t* pbf, hipStream_t s);
+void sumsq_flat(const void* g, bool g_bf16, int64_t n, float* out, hipStream_t s);
+void cast_f32_bf16(const float* x, int64_t n, uint16_t* y, hipStream_t s);
+
+}  // namespace tfx

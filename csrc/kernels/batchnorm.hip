@@ -1,0 +1,403 @@
+// Batch normalisation for NHWC bf16 activations (f32 statistics), with ReLU and the
+// residual add of a ResNet bottleneck fused into the apply pass.
+//
+// Layout: x is [M][C] with M = N*H*W rows (channels-last), C contiguous.
+// Forward  : stats (sum, sumsq per channel, f32 atomics) -> finalize (mean, invstd,
+//            scale = gamma*invstd, shift = beta - mean*scale, running-stat update)
+//            -> apply  y = relu?(x*scale + shift (+ res)).
+// Backward : reduce (sum g', sum g'*xhat with g' = g * [z > 0] recomputed from x/res)
+//            -> apply  dx = scale*(g' - sum_g/M - xhat*sum_gx/M), dres = g'.
+// Memory-bound: every pass moves 16 B per lane (8 channels), grid-stride.
+#include "tfx_common.h"
+#include "tfx_kernels.h"
+
+namespace tfx {
+
+// ------------------------------------------------------------------ stats (vector)
+// TPR threads per row (C/8), RPB = 256/TPR rows per block-iteration.
+__global__ void __launch_bounds__(256) bn_stats_vec_kernel(const uint16_t* __restrict__ x, int64_t M,
+                                                           int C, float* __restrict__ sums) {
+  const int tpr = C >> 3;
+  const int rpb = 256 / tpr;
+  const int t = threadIdx.x;
+  const int cv = t % tpr;       // which 8-channel vector
+  const int r0 = t / tpr;       // row lane
+  float s[8] = {0}, q[8] = {0};
+  const int64_t stride = (int64_t)gridDim.x * rpb;
+  for (int64_t r = (int64_t)blockIdx.x * rpb + r0; r < M; r += stride) {
+    U4 v = *reinterpret_cast<const U4*>(x + r * C + cv * 8);
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s[i] += f[i]; q[i] = fmaf(f[i], f[i], q[i]); }
+  }
+  // reduce across the rpb row lanes sharing a channel vector (LDS tree)
+  __shared__ float red[256 * 8 + 8];
+  for (int pass = 0; pass < 2; ++pass) {
+    float* v = pass ? q : s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[i * 256 + t] = v[i];
+    __syncthreads();
+    for (int h = rpb >> 1; h > 0; h >>= 1) {
+      if (r0 < h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[i * 256 + t] += red[i * 256 + t + h * tpr];
+      }
+      __syncthreads();
+    }
+    if (r0 == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) atomicAdd(&sums[pass * C + cv * 8 + i], red[i * 256 + t]);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ stats (generic C)
+__global__ void __launch_bounds__(256) bn_stats_gen_kernel(const uint16_t* __restrict__ x, int64_t M,
+                                                           int C, float* __restrict__ sums) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    for (int64_t r = (int64_t)blockIdx.y * 4 + ty; r < M; r += (int64_t)gridDim.y * 4) {
+      float f = bf16_to_f32(x[r * C + c]);
+      s += f;
+      q = fmaf(f, f, q);
+    }
+  }
+  __shared__ float rs[256], rq[256];
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    s = rs[tx] + rs[tx + 64] + rs[tx + 128] + rs[tx + 192];
+    q = rq[tx] + rq[tx + 64] + rq[tx + 128] + rq[tx + 192];
+    atomicAdd(&sums[c], s);
+    atomicAdd(&sums[C + c], q);
+  }
+}
+
+// ------------------------------------------------------------------ finalize
+// sums[0:C]=Σx, sums[C:2C]=Σx²  ->  save[0:C]=mean, save[C:2C]=invstd, save[2C:3C]=scale,
+// save[3C:4C]=shift; running stats updated in place (unbiased variance, PyTorch/TF momentum form).
+__global__ void bn_finalize_kernel(const float* __restrict__ sums, int64_t M, int C,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float eps, float momentum, float* __restrict__ run_mean,
+                                   float* __restrict__ run_var, float* __restrict__ save) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv_m = 1.f / (float)M;
+  const float mean = sums[c] * inv_m;
+  const float var = fmaxf(sums[C + c] * inv_m - mean * mean, 0.f);
+  const float invstd = rsqrtf(var + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  const float scale = g * invstd;
+  save[c] = mean;
+  save[C + c] = invstd;
+  save[2 * C + c] = scale;
+  save[3 * C + c] = b - mean * scale;
+  if (run_mean) {
+    const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
+// inference: scale/shift from running statistics
+__global__ void bn_eval_prep_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    float eps, const float* __restrict__ run_mean,
+                                    const float* __restrict__ run_var, float* __restrict__ save) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(run_var[c] + eps);
+  const float scale = (gamma ? gamma[c] : 1.f) * invstd;
+  save[c] = run_mean[c];
+  save[C + c] = invstd;
+  save[2 * C + c] = scale;
+  save[3 * C + c] = (beta ? beta[c] : 0.f) - run_mean[c] * scale;
+}
+
+// ------------------------------------------------------------------ apply
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(256) bn_apply_vec_kernel(const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ res,
+                                                           const float* __restrict__ save, int64_t nvec,
+                                                           int C, uint16_t* __restrict__ y) {
+  const float* scale = save + 2 * C;
+  const float* shift = save + 3 * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)((i * 8) % C);
+    float f[8], r[8];
+    unpack8(reinterpret_cast<const U4*>(x)[i], f);
+    if (RES) unpack8(reinterpret_cast<const U4*>(res)[i], r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float z = fmaf(f[k], scale[c0 + k], shift[c0 + k]);
+      if (RES) z += r[k];
+      f[k] = RELU ? fmaxf(z, 0.f) : z;
+    }
+    reinterpret_cast<U4*>(y)[i] = pack8(f);
+  }
+}
+
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(256) bn_apply_gen_kernel(const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ res,
+                                                           const float* __restrict__ save, int64_t n, int C,
+                                                           uint16_t* __restrict__ y) {
+  const float* scale = save + 2 * C;
+  const float* shift = save + 3 * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    float z = fmaf(bf16_to_f32(x[i]), scale[c], shift[c]);
+    if (RES) z += bf16_to_f32(res[i]);
+    y[i] = f32_to_bf16(RELU ? fmaxf(z, 0.f) : z);
+  }
+}
+
+// ------------------------------------------------------------------ backward reduce
+// red[0:C] = Σ g', red[C:2C] = Σ g'·xhat
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* __restrict__ g,
+                                                                const uint16_t* __restrict__ x,
+                                                                const uint16_t* __restrict__ res,
+                                                                const float* __restrict__ save, int64_t M,
+                                                                int C, float* __restrict__ red) {
+  const int tpr = C >> 3;
+  const int rpb = 256 / tpr;
+  const int t = threadIdx.x;
+  const int cv = t % tpr, r0 = t / tpr;
+  const float* mean = save;
+  const float* invstd = save + C;
+  const float* scale = save + 2 * C;
+  const float* shift = save + 3 * C;
+  float mu[8], is[8], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = mean[cv * 8 + k];
+    is[k] = invstd[cv * 8 + k];
+    sc[k] = scale[cv * 8 + k];
+    sh[k] = shift[cv * 8 + k];
+  }
+  float sg[8] = {0}, sx[8] = {0};
+  const int64_t stride = (int64_t)gridDim.x * rpb;
+  for (int64_t r = (int64_t)blockIdx.x * rpb + r0; r < M; r += stride) {
+    const int64_t off = r * C + cv * 8;
+    float gf[8], xf[8], rf[8];
+    unpack8(*reinterpret_cast<const U4*>(g + off), gf);
+    unpack8(*reinterpret_cast<const U4*>(x + off), xf);
+    if (RES && RELU) unpack8(*reinterpret_cast<const U4*>(res + off), rf);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float gg = gf[k];
+      if (RELU) {
+        float z = fmaf(xf[k], sc[k], sh[k]);
+        if (RES) z += rf[k];
+        gg = z > 0.f ? gg : 0.f;
+      }
+      sg[k] += gg;
+      sx[k] = fmaf(gg, (xf[k] - mu[k]) * is[k], sx[k]);
+    }
+  }
+  __shared__ float lds[256 * 8 + 8];
+  for (int pass = 0; pass < 2; ++pass) {
+    float* v = pass ? sx : sg;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lds[i * 256 + t] = v[i];
+    __syncthreads();
+    for (int h = rpb >> 1; h > 0; h >>= 1) {
+      if (r0 < h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) lds[i * 256 + t] += lds[i * 256 + t + h * tpr];
+      }
+      __syncthreads();
+    }
+    if (r0 == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) atomicAdd(&red[pass * C + cv * 8 + i], lds[i * 256 + t]);
+    }
+    __syncthreads();
+  }
+}
+
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_gen_kernel(const uint16_t* __restrict__ g,
+                                                                const uint16_t* __restrict__ x,
+                                                                const uint16_t* __restrict__ res,
+                                                                const float* __restrict__ save, int64_t M,
+                                                                int C, float* __restrict__ red) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float sg = 0.f, sx = 0.f;
+  if (c < C) {
+    const float mu = save[c], is = save[C + c], sc = save[2 * C + c], sh = save[3 * C + c];
+    for (int64_t r = (int64_t)blockIdx.y * 4 + ty; r < M; r += (int64_t)gridDim.y * 4) {
+      const int64_t off = r * C + c;
+      float gg = bf16_to_f32(g[off]);
+      const float xf = bf16_to_f32(x[off]);
+      if (RELU) {
+        float z = fmaf(xf, sc, sh);
+        if (RES) z += bf16_to_f32(res[off]);
+        gg = z > 0.f ? gg : 0.f;
+      }
+      sg += gg;
+      sx = fmaf(gg, (xf - mu) * is, sx);
+    }
+  }
+  __shared__ float a[256], b[256];
+  a[threadIdx.x] = sg;
+  b[threadIdx.x] = sx;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    atomicAdd(&red[c], a[tx] + a[tx + 64] + a[tx + 128] + a[tx + 192]);
+    atomicAdd(&red[C + c], b[tx] + b[tx + 64] + b[tx + 128] + b[tx + 192]);
+  }
+}
+
+// ------------------------------------------------------------------ backward apply
+// dx = scale * (g' - Σg'/M - xhat * Σg'xhat/M); dres = g' (residual branch gradient)
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* __restrict__ g,
+                                                               const uint16_t* __restrict__ x,
+                                                               const uint16_t* __restrict__ res,
+                                                               const float* __restrict__ save,
+                                                               const float* __restrict__ red, int64_t nvec,
+                                                               int64_t M, int C, uint16_t* __restrict__ dx,
+                                                               uint16_t* __restrict__ dres) {
+  const float inv_m = 1.f / (float)M;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)((i * 8) % C);
+    float gf[8], xf[8], rf[8], o[8];
+    unpack8(reinterpret_cast<const U4*>(g)[i], gf);
+    unpack8(reinterpret_cast<const U4*>(x)[i], xf);
+    if (RES && RELU) unpack8(reinterpret_cast<const U4*>(res)[i], rf);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float mu = save[c], is = save[C + c], sc = save[2 * C + c], sh = save[3 * C + c];
+      float gg = gf[k];
+      if (RELU) {
+        float z = fmaf(xf[k], sc, sh);
+        if (RES) z += rf[k];
+        gg = z > 0.f ? gg : 0.f;
+      }
+      gf[k] = gg;
+      const float xh = (xf[k] - mu) * is;
+      o[k] = sc * (gg - red[c] * inv_m - xh * red[C + c] * inv_m);
+    }
+    reinterpret_cast<U4*>(dx)[i] = pack8(o);
+    if (RES) reinterpret_cast<U4*>(dres)[i] = pack8(gf);
+  }
+}
+
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(256) bn_bwd_apply_gen_kernel(const uint16_t* __restrict__ g,
+                                                               const uint16_t* __restrict__ x,
+                                                               const uint16_t* __restrict__ res,
+                                                               const float* __restrict__ save,
+                                                               const float* __restrict__ red, int64_t n,
+                                                               int64_t M, int C, uint16_t* __restrict__ dx,
+                                                               uint16_t* __restrict__ dres) {
+  const float inv_m = 1.f / (float)M;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const float mu = save[c], is = save[C + c], sc = save[2 * C + c], sh = save[3 * C + c];
+    float gg = bf16_to_f32(g[i]);
+    const float xf = bf16_to_f32(x[i]);
+    if (RELU) {
+      float z = fmaf(xf, sc, sh);
+      if (RES) z += bf16_to_f32(res[i]);
+      gg = z > 0.f ? gg : 0.f;
+    }
+    const float xh = (xf - mu) * is;
+    dx[i] = f32_to_bf16(sc * (gg - red[c] * inv_m - xh * red[C + c] * inv_m));
+    if (RES) dres[i] = f32_to_bf16(gg);
+  }
+}
+
+// ================================================================== launchers
+static inline bool vec_ok(int C) { return (C % 8 == 0) && (C / 8) <= 256 && (256 % (C / 8) == 0); }
+static inline int grid_for(int64_t work, int per_block) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g > 2048) g = 2048;
+  return (int)(g < 1 ? 1 : g);
+}
+
+void bn_stats(const uint16_t* x, int64_t M, int C, float* sums, hipStream_t s) {
+  TFX_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, s));
+  if (vec_ok(C)) {
+    const int rpb = 256 / (C / 8);
+    int g = grid_for(M, rpb * 8);  // >= 8 rows per row-lane
+    bn_stats_vec_kernel<<<g, 256, 0, s>>>(x, M, C, sums);
+  } else {
+    dim3 grid((C + 63) / 64, grid_for(M, 64));
+    bn_stats_gen_kernel<<<grid, 256, 0, s>>>(x, M, C, sums);
+  }
+}
+
+void bn_finalize(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
+                 float momentum, float* run_mean, float* run_var, float* save, hipStream_t s) {
+  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(sums, M, C, gamma, beta, eps, momentum, run_mean,
+                                                     run_var, save);
+}
+
+void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
+                  const float* run_var, float* save, hipStream_t s) {
+  bn_eval_prep_kernel<<<(C + 255) / 256, 256, 0, s>>>(C, gamma, beta, eps, run_mean, run_var, save);
+}
+
+#define TFX_DISPATCH_RR(RES, RELU, ...)            \
+  if (RES) {                                       \
+    if (RELU) { constexpr bool R_ = true, L_ = true; __VA_ARGS__; }   \
+    else { constexpr bool R_ = true, L_ = false; __VA_ARGS__; }       \
+  } else {                                         \
+    if (RELU) { constexpr bool R_ = false, L_ = true; __VA_ARGS__; }  \
+    else { constexpr bool R_ = false, L_ = false; __VA_ARGS__; }      \
+  }
+
+void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
+              uint16_t* y, hipStream_t s) {
+  const int64_t n = M * C;
+  const bool has_res = res != nullptr;
+  if (C % 8 == 0) {
+    const int64_t nvec = n / 8;
+    int g = grid_for(nvec, 256 * 4);
+    TFX_DISPATCH_RR(has_res, relu, (bn_apply_vec_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, nvec, C, y)));
+  } else {
+    int g = grid_for(n, 256 * 4);
+    TFX_DISPATCH_RR(has_res, relu, (bn_apply_gen_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, n, C, y)));
+  }
+}
+
+void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const float* save, int64_t M,
+                 int C, bool relu, float* red, uint16_t* dx, uint16_t* dres, hipStream_t s) {
+  TFX_HIP_CHECK(hipMemsetAsync(red, 0, sizeof(float) * 2 * C, s));
+  const bool has_res = res != nullptr;  // only meaningful for the ReLU mask recompute
+  const int64_t n = M * C;
+  if (vec_ok(C)) {
+    const int rpb = 256 / (C / 8);
+    int gr = grid_for(M, rpb * 8);
+    TFX_DISPATCH_RR(has_res, relu,
+                    (bn_bwd_reduce_vec_kernel<R_, L_><<<gr, 256, 0, s>>>(g, x, res, save, M, C, red)));
+  } else {
+    dim3 grid((C + 63) / 64, grid_for(M, 64));
+    TFX_DISPATCH_RR(has_res, relu,
+                    (bn_bwd_reduce_gen_kernel<R_, L_><<<grid, 256, 0, s>>>(g, x, res, save, M, C, red)));
+  }
+  // With a residual input (bottleneck output BN) dres = g' is always produced: the identity /
+  // projection branch needs it.  The host wrapper guarantees dres != nullptr when res != nullptr.
+  if (C % 8 == 0) {
+    const int64_t nvec = n / 8;
+    int ga = grid_for(nvec, 256 * 4);
+    TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_vec_kernel<R_, L_><<<ga, 256, 0, s>>>(
+                                       g, x, res, save, red, nvec, M, C, dx, dres)));
+  } else {
+    int ga = grid_for(n, 256 * 4);
+    TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_gen_kernel<R_, L_><<<ga, 256, 0, s>>>(
+                                       g, x, res, save, red, n, M, C, dx, dres)));
+  }
+}
+
+}  // namespace tfx

@@ -1,0 +1,173 @@
+// Softmax cross-entropy (fused fwd + bwd), accuracy, and global average pooling.
+//
+// softmax_xent: one wave per row (C <= a few thousand: classes of MNIST/CIFAR/char vocab).
+//   mode 0 (stable): loss_r = logsumexp(z) - z[label]; dz = (p - onehot) * gscale
+//   mode 1 (naive, reference parity R/distributed/distributed.py:99,102):
+//       p = softmax(z), loss_r = -sum y*log(p)  (log of the softmax OUTPUT, may be -inf/NaN like TF1)
+//       dz = (g - sum(g*p)) * p  with g = -y/p * gscale  (TF1's Log-grad -> SoftmaxGrad chain)
+// Targets are either class indices (int64) or dense rows (f32, one-hot or soft).
+#include "tfx_common.h"
+#include "tfx_kernels.h"
+
+namespace tfx {
+
+template <typename TIN>
+__device__ __forceinline__ float ld(const TIN* p, int64_t i);
+template <>
+__device__ __forceinline__ float ld<float>(const float* p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ld<uint16_t>(const uint16_t* p, int64_t i) { return bf16_to_f32(p[i]); }
+
+template <typename TIN>
+__global__ void __launch_bounds__(256) softmax_xent_kernel(const TIN* __restrict__ z, int B, int C,
+                                                           const int64_t* __restrict__ lab_idx,
+                                                           const float* __restrict__ lab_dense, int naive,
+                                                           float gscale, float* __restrict__ loss_rows,
+                                                           float* __restrict__ dz, float* __restrict__ probs) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const TIN* zr = z + (int64_t)row * C;
+  float m = -INFINITY;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, ld(zr, c));
+  m = wave_max(m);
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += __expf(ld(zr, c) - m);
+  s = wave_sum(s);
+  const float inv_s = 1.f / s;
+  const float lse = m + __logf(s);
+  const int64_t lab = lab_idx ? lab_idx[row] : -1;
+  float loss = 0.f, gp = 0.f;
+  // pass 1: loss (+ for naive mode sum(g*p))
+  for (int c = lane; c < C; c += 64) {
+    const float zc = ld(zr, c);
+    const float y = lab_dense ? lab_dense[(int64_t)row * C + c] : (c == lab ? 1.f : 0.f);
+    if (naive) {
+      const float p = __expf(zc - m) * inv_s;
+      if (y != 0.f) loss -= y * logf(p);
+      const float g = -y / p * gscale;  // NaN when y=0,p=0 is avoided below
+      gp += (y != 0.f ? g : 0.f) * p;
+    } else {
+      if (y != 0.f) loss += y * (lse - zc);
+    }
+  }
+  loss = wave_sum(loss);
+  if (naive) gp = wave_sum(gp);
+  if (lane == 0 && loss_rows) loss_rows[row] = loss;
+  if (!dz && !probs) return;
+  for (int c = lane; c < C; c += 64) {
+    const float zc = ld(zr, c);
+    const float p = __expf(zc - m) * inv_s;
+    const float y = lab_dense ? lab_dense[(int64_t)row * C + c] : (c == lab ? 1.f : 0.f);
+    if (probs) probs[(int64_t)row * C + c] = p;
+    if (dz) {
+      float d;
+      if (naive) {
+        const float g = y != 0.f ? -y / p * gscale : 0.f;
+        d = (g - gp) * p;
+      } else {
+        d = (p - y) * gscale;
+      }
+      dz[(int64_t)row * C + c] = d;
+    }
+  }
+}
+
+// correct[row] = argmax(z[row]) == argmax(target[row]) (first max wins, as tf.argmax)
+template <typename TIN>
+__global__ void __launch_bounds__(256) accuracy_kernel(const TIN* __restrict__ z, int B, int C,
+                                                       const int64_t* __restrict__ lab_idx,
+                                                       const float* __restrict__ lab_dense,
+                                                       float* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  float hit = 0.f;
+  if (row < B) {
+    float bv = -INFINITY, tv = -INFINITY;
+    int bi = C, ti = C;
+    for (int c = lane; c < C; c += 64) {
+      const float v = ld(z + (int64_t)row * C, c);
+      if (v > bv) { bv = v; bi = c; }
+      if (lab_dense) {
+        const float t = lab_dense[(int64_t)row * C + c];
+        if (t > tv) { tv = t; ti = c; }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      const float otv = __shfl_xor(tv, o, 64);
+      const int oti = __shfl_xor(ti, o, 64);
+      if (otv > tv || (otv == tv && oti < ti)) { tv = otv; ti = oti; }
+    }
+    const int target = lab_idx ? (int)lab_idx[row] : ti;
+    hit = (lane == 0 && bi == target) ? 1.f : 0.f;
+  }
+  if (lane == 0 && row < B && hit != 0.f) atomicAdd(count, 1.f);
+}
+
+// Global average pool NHWC: x [N][HW][C] bf16 -> y [N][C] (bf16 or f32)
+__global__ void __launch_bounds__(256) gap_fwd_kernel(const uint16_t* __restrict__ x, int N, int HW, int C,
+                                                      uint16_t* __restrict__ y16, float* __restrict__ y32) {
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const uint16_t* xp = x + (int64_t)n * HW * C + c;
+  float s = 0.f;
+  for (int i = 0; i < HW; ++i) s += bf16_to_f32(xp[(int64_t)i * C]);
+  s *= 1.f / (float)HW;
+  if (y16) y16[(int64_t)n * C + c] = f32_to_bf16(s);
+  if (y32) y32[(int64_t)n * C + c] = s;
+}
+
+template <typename TG>
+__global__ void __launch_bounds__(256) gap_bwd_kernel(const TG* __restrict__ dy, int N, int HW, int C,
+                                                      uint16_t* __restrict__ dx) {
+  const int64_t total = (int64_t)N * HW * C;
+  const float inv = 1.f / (float)HW;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const int64_t n = i / ((int64_t)HW * C);
+    dx[i] = f32_to_bf16(ld(dy, n * C + c) * inv);
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+void softmax_xent(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,
+                  bool naive, float gscale, float* loss_rows, float* dz, float* probs, hipStream_t s) {
+  dim3 grid((B + 3) / 4);
+  if (z_bf16)
+    softmax_xent_kernel<uint16_t><<<grid, 256, 0, s>>>((const uint16_t*)z, B, C, lab_idx, lab_dense, naive,
+                                                       gscale, loss_rows, dz, probs);
+  else
+    softmax_xent_kernel<float><<<grid, 256, 0, s>>>((const float*)z, B, C, lab_idx, lab_dense, naive, gscale,
+                                                    loss_rows, dz, probs);
+}
+
+void accuracy_count(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,
+                    float* count, hipStream_t s) {
+  TFX_HIP_CHECK(hipMemsetAsync(count, 0, sizeof(float), s));
+  dim3 grid((B + 3) / 4);
+  if (z_bf16)
+    accuracy_kernel<uint16_t><<<grid, 256, 0, s>>>((const uint16_t*)z, B, C, lab_idx, lab_dense, count);
+  else
+    accuracy_kernel<float><<<grid, 256, 0, s>>>((const float*)z, B, C, lab_idx, lab_dense, count);
+}
+
+void gap_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y16, float* y32, hipStream_t s) {
+  dim3 grid((C + 255) / 256, N);
+  gap_fwd_kernel<<<grid, 256, 0, s>>>(x, N, HW, C, y16, y32);
+}
+
+void gap_bwd(const void* dy, bool dy_bf16, int N, int HW, int C, uint16_t* dx, hipStream_t s) {
+  const int64_t total = (int64_t)N * HW * C;
+  int g = (int)std::min<int64_t>((total + 1023) / 1024, 4096);
+  if (dy_bf16)
+    gap_bwd_kernel<uint16_t><<<g, 256, 0, s>>>((const uint16_t*)dy, N, HW, C, dx);
+  else
+    gap_bwd_kernel<float><<<g, 256, 0, s>>>((const float*)dy, N, HW, C, dx);
+}
+
+}  // namespace tfx

@@ -1,0 +1,336 @@
+// TORCH_LIBRARY(tfx) registrations: shape/dtype validation on the host, then the raw-pointer
+// HIP launchers of csrc/kernels on the current HIP stream (so every op is capturable in a
+// hipGraph and ordered with PyTorch's own work).  The Python autograd layer lives in
+// tensorflow_examples_amd/ops.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <tuple>
+#include <vector>
+
+#include "tfx_kernels.h"
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be f32")
+
+const uint16_t* bf(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bfm(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const float* fp(const optional<Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
+float* fpm(const optional<Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
+
+void check_aligned16(const Tensor& t, const char* name) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+struct ConvGeom {
+  int64_t N, H, W, C, Ko, R, S, P, Q;
+};
+
+ConvGeom geom(const std::vector<int64_t>& xs, const std::vector<int64_t>& ws, int64_t st, int64_t pad, int64_t dil) {
+  TORCH_CHECK(xs.size() == 4 && ws.size() == 4, "conv expects NHWC input and [Ko,R,S,C] weight");
+  ConvGeom g;
+  g.N = xs[0]; g.H = xs[1]; g.W = xs[2]; g.C = xs[3];
+  g.Ko = ws[0]; g.R = ws[1]; g.S = ws[2];
+  TORCH_CHECK(ws[3] == g.C, "weight C mismatch");
+  TORCH_CHECK(g.C % 8 == 0 && g.Ko % 8 == 0, "conv needs C%8==0 and Ko%8==0 (pad channels)");
+  g.P = (g.H + 2 * pad - dil * (g.R - 1) - 1) / st + 1;
+  g.Q = (g.W + 2 * pad - dil * (g.S - 1) - 1) / st + 1;
+  TORCH_CHECK(g.P > 0 && g.Q > 0, "conv output is empty");
+  return g;
+}
+
+tfx::IgemmArgs conv_args(const ConvGeom& g, int64_t st, int64_t pad, int64_t dil) {
+  tfx::IgemmArgs a;
+  a.Nb = g.N; a.H = g.H; a.W = g.W; a.C = g.C; a.Ko = g.Ko; a.R = g.R; a.S = g.S; a.P = g.P; a.Q = g.Q;
+  a.sh = a.sw = st; a.ph = a.pw = pad; a.dh = a.dw = dil;
+  return a;
+}
+
+// ------------------------------------------------------------------ conv
+Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
+  auto g = geom(x.sizes().vec(), w.sizes().vec(), stride, pad, dil);
+  auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
+  auto a = conv_args(g, stride, pad, dil);
+  a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
+  a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
+  a.out_mode = tfx::OUT_BF16;
+  tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
+  return y;
+}
+
+Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
+  auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
+  TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
+  auto dx = at::empty({g.N, g.H, g.W, g.C}, dy.options());
+  auto a = conv_args(g, stride, pad, dil);
+  a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
+  a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+  a.out_mode = tfx::OUT_BF16;
+  tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
+  return dx;
+}
+
+// dW (f32, [Ko][R][S][C]) = or += conv weight gradient
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t dil, bool accumulate) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
+  auto g = geom(x.sizes().vec(), dw.sizes().vec(), stride, pad, dil);
+  TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
+  auto a = conv_args(g, stride, pad, dil);
+  a.A = bf(dy); a.B = bf(x); a.Cp = dw.data_ptr();
+  a.M = g.Ko; a.N = g.R * g.S * g.C; a.K = g.N * g.P * g.Q; a.lda = g.Ko; a.ldc = a.N;
+  a.out_mode = tfx::OUT_F32_ATOMIC;
+  a.zero_out = accumulate ? 0 : 1;
+  tfx::igemm_launch(a, tfx::MODE_WGRAD, cur_stream());
+}
+
+// ------------------------------------------------------------------ dense bf16 GEMM
+// out = op(a) @ op(b) (+bias)(relu); a: [M,K] (or [K,M] if trans_a); b: [K,N] (or [N,K] if trans_b)
+void gemm_setup(tfx::IgemmArgs& g, const Tensor& a, const Tensor& b, bool ta, bool tb) {
+  CHECK_DEV(a); CHECK_BF16(a); CHECK_BF16(b);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm expects 2-D operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm operands need unit inner stride");
+  const int64_t M = ta ? a.size(1) : a.size(0), K = ta ? a.size(0) : a.size(1);
+  const int64_t K2 = tb ? b.size(1) : b.size(0), N = tb ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == K2, "gemm inner dims differ: ", K, " vs ", K2);
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm leading dims must be multiples of 8");
+  TORCH_CHECK((ta ? M : K) % 8 == 0 && (tb ? K : N) % 8 == 0, "gemm contiguous dims must be multiples of 8");
+  check_aligned16(a, "a");
+  check_aligned16(b, "b");
+  g.A = bf(a); g.B = bf(b);
+  g.M = M; g.N = N; g.K = K;
+  g.lda = a.stride(0); g.ldb = b.stride(0);
+  g.a_kmajor = ta ? 0 : 1;
+  g.b_kmajor = tb ? 1 : 0;
+}
+
+Tensor gemm(Tensor a, Tensor b, bool ta, bool tb, optional<Tensor> bias, bool relu, bool out_f32) {
+  tfx::IgemmArgs g;
+  gemm_setup(g, a, b, ta, tb);
+  auto out = at::empty({g.M, g.N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  g.Cp = out.data_ptr(); g.ldc = g.N; g.bias = fp(bias); g.relu = relu;
+  g.out_mode = out_f32 ? tfx::OUT_F32 : tfx::OUT_BF16;
+  if (bias.has_value() && bias->defined()) { CHECK_F32(*bias); TORCH_CHECK(bias->numel() == g.N, "bias size"); }
+  tfx::igemm_launch(g, tfx::MODE_GEMM, cur_stream());
+  return out;
+}
+
+// f32 out (+)= op(a) @ op(b); split-K with atomics when the grid would be small
+void gemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor out, bool accumulate) {
+  tfx::IgemmArgs g;
+  gemm_setup(g, a, b, ta, tb);
+  CHECK_F32(out);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == g.M && out.size(1) == g.N && out.stride(1) == 1, "out shape");
+  g.Cp = out.data_ptr(); g.ldc = out.stride(0);
+  g.out_mode = tfx::OUT_F32_ATOMIC;
+  g.zero_out = accumulate ? 0 : 1;
+  if (!accumulate && out.stride(0) != g.N) {  // zeroing assumes a dense block
+    out.zero_();
+    g.zero_out = 0;
+  }
+  tfx::igemm_launch(g, tfx::MODE_GEMM, cur_stream());
+}
+
+// ------------------------------------------------------------------ f32 GEMM (MFMA f32)
+Tensor sgemm(Tensor a, Tensor b, bool ta, bool tb, optional<Tensor> bias, int64_t act) {
+  CHECK_DEV(a); CHECK_F32(a); CHECK_F32(b);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "sgemm operands");
+  const int64_t M = ta ? a.size(1) : a.size(0), K = ta ? a.size(0) : a.size(1);
+  const int64_t N = tb ? b.size(0) : b.size(1);
+  TORCH_CHECK((tb ? b.size(1) : b.size(0)) == K, "sgemm inner dims");
+  auto out = at::empty({M, N}, a.options());
+  tfx::sgemm_launch(a.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(), fp(bias), M, N, K,
+                    a.stride(0), b.stride(0), N, ta, tb, act, false, cur_stream());
+  return out;
+}
+
+void sgemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor out, bool accumulate) {
+  CHECK_DEV(a); CHECK_F32(a); CHECK_F32(b); CHECK_F32(out);
+  const int64_t M = ta ? a.size(1) : a.size(0), K = ta ? a.size(0) : a.size(1);
+  const int64_t N = tb ? b.size(0) : b.size(1);
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.stride(1) == 1, "sgemm_into out shape");
+  tfx::sgemm_launch(a.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(), nullptr, M, N, K,
+                    a.stride(0), b.stride(0), out.stride(0), ta, tb, 0, accumulate, cur_stream());
+}
+
+// ------------------------------------------------------------------ batch norm
+std::tuple<Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
+                                        optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
+                                        double eps, optional<Tensor> res, bool relu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  auto opts = x.options().dtype(at::kFloat);
+  auto sums = at::empty({2 * C}, opts);
+  auto save = at::empty({4 * C}, opts);
+  auto y = at::empty_like(x);
+  const uint16_t* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    CHECK_BF16(*res); CHECK_CONTIG(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+    r = bf(*res);
+  }
+  auto s = cur_stream();
+  tfx::bn_stats(bf(x), M, C, sums.data_ptr<float>(), s);
+  tfx::bn_finalize(sums.data_ptr<float>(), M, C, fp(gamma), fp(beta), eps, momentum, fpm(run_mean), fpm(run_var),
+                   save.data_ptr<float>(), s);
+  tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y), s);
+  return {y, save};
+}
+
+std::tuple<Tensor, Tensor> bn_fwd_eval(Tensor x, optional<Tensor> gamma, optional<Tensor> beta, Tensor run_mean,
+                                       Tensor run_var, double eps, optional<Tensor> res, bool relu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  auto save = at::empty({4 * C}, x.options().dtype(at::kFloat));
+  auto y = at::empty_like(x);
+  auto s = cur_stream();
+  tfx::bn_eval_prep(C, fp(gamma), fp(beta), eps, run_mean.data_ptr<float>(), run_var.data_ptr<float>(),
+                    save.data_ptr<float>(), s);
+  const uint16_t* r = (res.has_value() && res->defined()) ? bf(*res) : nullptr;
+  tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y), s);
+  return {y, save};
+}
+
+// returns dx, dres (undefined unless res given), red = [dbeta(C) | dgamma(C)]
+std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> res, Tensor save, bool relu) {
+  CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd grad shape");
+  auto red = at::empty({2 * C}, x.options().dtype(at::kFloat));
+  auto dx = at::empty_like(x);
+  Tensor dres;
+  const uint16_t* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    CHECK_CONTIG(*res);
+    r = bf(*res);
+    dres = at::empty_like(x);
+  }
+  tfx::bn_backward(bf(g), bf(x), r, save.data_ptr<float>(), M, C, relu, red.data_ptr<float>(), bfm(dx),
+                   r ? bfm(dres) : nullptr, cur_stream());
+  return {dx, dres, red};
+}
+
+// ------------------------------------------------------------------ loss / metrics / pooling
+std::tuple<Tensor, Tensor> softmax_xent(Tensor z, optional<Tensor> lab_idx, optional<Tensor> lab_dense, bool naive,
+                                        double gscale, bool want_grad) {
+  CHECK_DEV(z); CHECK_CONTIG(z);
+  TORCH_CHECK(z.dim() == 2, "logits must be [B,C]");
+  const bool zb = z.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(zb || z.scalar_type() == at::kFloat, "logits dtype");
+  const int64_t B = z.size(0), C = z.size(1);
+  const int64_t* li = nullptr;
+  const float* ld = nullptr;
+  if (lab_idx.has_value() && lab_idx->defined()) {
+    TORCH_CHECK(lab_idx->scalar_type() == at::kLong && lab_idx->numel() == B, "labels");
+    li = lab_idx->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(lab_dense.has_value() && lab_dense->defined(), "need labels");
+    CHECK_F32(*lab_dense); CHECK_CONTIG(*lab_dense);
+    TORCH_CHECK(lab_dense->size(0) == B && lab_dense->size(1) == C, "dense labels shape");
+    ld = lab_dense->data_ptr<float>();
+  }
+  auto opts = z.options().dtype(at::kFloat);
+  auto loss = at::empty({B}, opts);
+  Tensor dz;
+  if (want_grad) dz = at::empty({B, C}, opts);
+  tfx::softmax_xent(z.data_ptr(), zb, B, C, li, ld, naive, gscale, loss.data_ptr<float>(),
+                    want_grad ? dz.data_ptr<float>() : nullptr, nullptr, cur_stream());
+  return {loss, dz};
+}
+
+Tensor accuracy_count(Tensor z, optional<Tensor> lab_idx, optional<Tensor> lab_dense) {
+  CHECK_DEV(z); CHECK_CONTIG(z);
+  const bool zb = z.scalar_type() == at::kBFloat16;
+  auto out = at::empty({1}, z.options().dtype(at::kFloat));
+  const int64_t* li = (lab_idx.has_value() && lab_idx->defined()) ? lab_idx->data_ptr<int64_t>() : nullptr;
+  const float* ld = (lab_dense.has_value() && lab_dense->defined()) ? lab_dense->data_ptr<float>() : nullptr;
+  TORCH_CHECK(li || ld, "need labels");
+  tfx::accuracy_count(z.data_ptr(), zb, z.size(0), z.size(1), li, ld, out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+Tensor gap_fwd(Tensor x, bool out_f32) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 4, "gap expects NHWC");
+  const int64_t N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto y = at::empty({N, C}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  tfx::gap_fwd(bf(x), N, HW, C, out_f32 ? nullptr : bfm(y), out_f32 ? y.data_ptr<float>() : nullptr, cur_stream());
+  return y;
+}
+
+Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
+  CHECK_DEV(dy); CHECK_CONTIG(dy);
+  const bool b16 = dy.scalar_type() == at::kBFloat16;
+  const int64_t N = dy.size(0), C = dy.size(1);
+  auto dx = at::empty({N, H, W, C}, dy.options().dtype(at::kBFloat16));
+  tfx::gap_bwd(dy.data_ptr(), b16, N, H * W, C, bfm(dx), cur_stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------ optimizers
+void optimizer_apply(int64_t kind, Tensor p, Tensor g, optional<Tensor> m, optional<Tensor> v, Tensor lr,
+                     double gscale, double wd, double b1, double b2, double eps, optional<Tensor> step,
+                     optional<Tensor> sumsq, double max_norm, optional<Tensor> pbf) {
+  CHECK_DEV(p); CHECK_F32(p); CHECK_CONTIG(p); CHECK_CONTIG(g);
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() % 4 == 0, "flat buffers must match and be padded to 4");
+  const bool gb = g.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(gb || g.scalar_type() == at::kFloat, "grad dtype");
+  if (kind >= 1) TORCH_CHECK(m.has_value() && m->numel() == p.numel(), "momentum buffer");
+  if (kind >= 3) TORCH_CHECK(v.has_value() && v->numel() == p.numel() && step.has_value(), "adam buffers");
+  uint16_t* pb = nullptr;
+  if (pbf.has_value() && pbf->defined()) {
+    CHECK_BF16(*pbf);
+    TORCH_CHECK(pbf->numel() == p.numel(), "bf16 shadow size");
+    pb = bfm(*pbf);
+  }
+  tfx::optimizer_apply(kind, p.data_ptr<float>(), g.data_ptr(), gb, fpm(m), fpm(v), p.numel(), lr.data_ptr<float>(),
+                       gscale, wd, b1, b2, eps, fp(step), fp(sumsq), max_norm, pb, cur_stream());
+}
+
+Tensor sumsq(Tensor g) {
+  CHECK_DEV(g); CHECK_CONTIG(g);
+  TORCH_CHECK(g.numel() % 4 == 0, "sumsq needs numel % 4 == 0");
+  auto out = at::empty({1}, g.options().dtype(at::kFloat));
+  tfx::sumsq_flat(g.data_ptr(), g.scalar_type() == at::kBFloat16, g.numel(), out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+void cast_f32_bf16(Tensor x, Tensor y) {
+  CHECK_DEV(x); CHECK_F32(x); CHECK_BF16(y);
+  TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "cast sizes");
+  tfx::cast_f32_bf16(x.data_ptr<float>(), x.numel(), bfm(y), cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(tfx, m) {
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("gemm", &gemm);
+  m.def("gemm_into", &gemm_into);
+  m.def("sgemm", &sgemm);
+  m.def("sgemm_into", &sgemm_into);
+  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_eval", &bn_fwd_eval);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("accuracy_count", &accuracy_count);
+  m.def("gap_fwd", &gap_fwd);
+  m.def("gap_bwd", &gap_bwd);
+  m.def("optimizer_apply", &optimizer_apply);
+  m.def("sumsq", &sumsq);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+}

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One gpurun session: GPU tests, 1-GPU native bench, stock-torch bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a crash/timeout stops the script (no further GPU work).
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+STEPS=${STEPS:-"tests bench torch prof"}
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+      rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+      ok_or_testfail $rc || exit $rc ;;
+    bench)
+      timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_native.log 2>&1
+      rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench_native.log; [ $rc -eq 0 ] || exit $rc ;;
+    graph)
+      timeout -k 10 400 python bench.py --steps 20 --warmup 5 --graph > gpurun_out/bench_graph.log 2>&1
+      rc=$?; echo "graph rc=$rc"; tail -3 gpurun_out/bench_graph.log; [ $rc -eq 0 ] || exit $rc ;;
+    torch)
+      timeout -k 10 400 python bench.py --impl torch --steps 20 --warmup 5 > gpurun_out/bench_torch.log 2>&1
+      rc=$?; echo "torch rc=$rc"; tail -3 gpurun_out/bench_torch.log; [ $rc -eq 0 ] || exit $rc ;;
+    prof)
+      export TMPDIR=/tmp
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 2 > gpurun_out/prof.log 2>&1
+      rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
+  esac
+done
+echo ALL_DONE

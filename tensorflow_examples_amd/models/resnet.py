@@ -1,0 +1,153 @@
+"""ResNet for CIFAR-10 (north-star config 3 of BASELINE.json: ResNet-50/CIFAR-10 bf16 DP).
+
+CIFAR adaptation of ResNet-50 v1.5: 3x3 stride-1 stem (no max-pool), bottleneck stages
+[3, 4, 6, 3] with widths 64/128/256/512 (x4 expansion), stride on the 3x3 conv, 1x1
+projection shortcuts, global average pool, FC 2048 -> 10.  23.5 M parameters.
+
+MI355X layout: activations NHWC bf16 end to end, conv weights [Ko][R][S][C] so every conv
+is an implicit GEMM with the channel axis contiguous (csrc/kernels/igemm.hip); each BN
+pass fuses ReLU and, at a block's tail, the residual add (csrc/kernels/batchnorm.hip).
+The 3-channel RGB input is carried as 8 channels (zeros in 3..7) so the stem conv meets
+the 16-byte vector-load granularity; its weights for channels 3..7 stay exactly zero.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+from .. import ops
+from ..variables import Constant, HeNormal, VariableStore, Zeros
+
+STAGES = {
+    18: ("basic", [2, 2, 2, 2]),
+    34: ("basic", [3, 4, 6, 3]),
+    50: ("bottleneck", [3, 4, 6, 3]),
+    101: ("bottleneck", [3, 4, 23, 3]),
+    152: ("bottleneck", [3, 8, 36, 3]),
+}
+IN_CH_PAD = 8
+
+
+class _BN:
+    def __init__(self, store: VariableStore, c: int, name: str, zero_gamma: bool = False):
+        with store.scope(name):
+            self.gamma = store.variable([c], Constant(0.0 if zero_gamma else 1.0), name="gamma")
+            self.beta = store.variable([c], Zeros(), name="beta")
+            self.mean = store.add_state("moving_mean", torch.zeros(c))
+            self.var = store.add_state("moving_variance", torch.ones(c))
+
+    def __call__(self, x, training, relu=False, residual=None):
+        return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
+                              eps=1e-5, residual=residual, relu=relu)
+
+
+class _Conv:
+    def __init__(self, store: VariableStore, cin: int, cout: int, k: int, stride: int, name: str):
+        self.w = store.variable([cout, k, k, cin], HeNormal(), name=name)
+        self.stride, self.pad = stride, k // 2
+
+    def __call__(self, x):
+        return ops.conv2d(x, self.w, self.stride, self.pad)
+
+
+class Bottleneck:
+    expansion = 4
+
+    def __init__(self, store, cin, width, stride, name):
+        cout = width * 4
+        with store.scope(name):
+            self.c1 = _Conv(store, cin, width, 1, 1, "conv1")
+            self.b1 = _BN(store, width, "bn1")
+            self.c2 = _Conv(store, width, width, 3, stride, "conv2")
+            self.b2 = _BN(store, width, "bn2")
+            self.c3 = _Conv(store, width, cout, 1, 1, "conv3")
+            self.b3 = _BN(store, cout, "bn3", zero_gamma=False)
+            self.proj = None
+            if stride != 1 or cin != cout:
+                self.proj = _Conv(store, cin, cout, 1, stride, "shortcut")
+                self.bp = _BN(store, cout, "shortcut_bn")
+
+    def __call__(self, x, training):
+        o = self.b1(self.c1(x), training, relu=True)
+        o = self.b2(self.c2(o), training, relu=True)
+        sc = x if self.proj is None else self.bp(self.proj(x), training)
+        return self.b3(self.c3(o), training, relu=True, residual=sc)
+
+
+class Basic:
+    expansion = 1
+
+    def __init__(self, store, cin, width, stride, name):
+        with store.scope(name):
+            self.c1 = _Conv(store, cin, width, 3, stride, "conv1")
+            self.b1 = _BN(store, width, "bn1")
+            self.c2 = _Conv(store, width, width, 3, 1, "conv2")
+            self.b2 = _BN(store, width, "bn2")
+            self.proj = None
+            if stride != 1 or cin != width:
+                self.proj = _Conv(store, cin, width, 1, stride, "shortcut")
+                self.bp = _BN(store, width, "shortcut_bn")
+
+    def __call__(self, x, training):
+        o = self.b1(self.c1(x), training, relu=True)
+        sc = x if self.proj is None else self.bp(self.proj(x), training)
+        return self.b2(self.c2(o), training, relu=True, residual=sc)
+
+
+class ResNetCifar:
+    def __init__(self, store: VariableStore, depth: int = 50, num_classes: int = 10, base_width: int = 64):
+        kind, blocks = STAGES[depth]
+        Block = Bottleneck if kind == "bottleneck" else Basic
+        self.store = store
+        with store.scope("resnet%d" % depth):
+            self.stem = _Conv(store, IN_CH_PAD, base_width, 3, 1, "conv0")
+            self.stem_bn = _BN(store, base_width, "bn0")
+            self.blocks: List = []
+            cin = base_width
+            for si, n in enumerate(blocks):
+                width = base_width * (2 ** si)
+                for bi in range(n):
+                    stride = 2 if (bi == 0 and si > 0) else 1
+                    blk = Block(store, cin, width, stride, "stage%d_block%d" % (si + 1, bi + 1))
+                    self.blocks.append(blk)
+                    cin = width * Block.expansion
+            with store.scope("fc"):
+                self.fc_w = store.variable([num_classes, cin], HeNormal(gain=1.0), name="kernel")
+                self.fc_b = store.variable([num_classes], Zeros(), name="bias")
+        self.num_classes = num_classes
+        self.feat = cin
+
+    def post_init(self):
+        """Zero the stem weights of the padded input channels (3..7)."""
+        with torch.no_grad():
+            self.stem.w.master[..., 3:] = 0
+        self.store.refresh_shadow()
+
+    def __call__(self, x: torch.Tensor, training: bool = True) -> torch.Tensor:
+        o = self.stem_bn(self.stem(x), training, relu=True)
+        for blk in self.blocks:
+            o = blk(o, training)
+        f = ops.global_avg_pool(o)
+        return ops.linear(f, self.fc_w, self.fc_b)
+
+
+def build_resnet_cifar(device="cuda", depth=50, num_classes=10, dtype=torch.bfloat16, seed=0) -> Tuple[VariableStore, ResNetCifar]:
+    store = VariableStore(device=device, compute_dtype=dtype, seed=seed)
+    model = ResNetCifar(store, depth=depth, num_classes=num_classes)
+    store.finalize()
+    model.post_init()
+    return store, model
+
+
+def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """[N,32,32,3] images -> [N,32,32,8] normalised NHWC compute tensor (channels 3..7 zero)."""
+    x = images_nhwc_u8_or_f
+    if x.dtype == torch.uint8:
+        x = x.float() / 255.0
+    mean = torch.tensor([0.4914, 0.4822, 0.4465], device=x.device)
+    std = torch.tensor([0.2470, 0.2435, 0.2616], device=x.device)
+    x = (x - mean) / std
+    out = torch.zeros(*x.shape[:-1], IN_CH_PAD, device=x.device, dtype=dtype)
+    out[..., :3] = x.to(dtype)
+    return out

@@ -1,0 +1,340 @@
+"""Differentiable ops of the framework.
+
+Every op has two implementations behind one ``torch.autograd.Function``:
+
+* GPU tensors  -> the hand-written gfx950 HIP kernels (``torch.ops.tfx.*``), bf16
+  activations in NHWC, f32 statistics/accumulation;
+* CPU tensors  -> a PyTorch reference (the numerics oracle of tests/, and the CPU
+  training path used by ``simple/``, the MNIST softmax config and the PS demo).
+
+Trainable parameters are :class:`~tensorflow_examples_amd.variables.Variable` views into a
+flat store; backward passes ACCUMULATE parameter gradients straight into ``var.grad``
+(the flat grad buffer) and fire ``store.grad_ready_hook`` so the data-parallel layer can
+launch a bucket's all-reduce as soon as its last gradient lands.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+from ..variables import Variable
+
+
+def _grad_ready(*vs: Optional[Variable]) -> None:
+    for v in vs:
+        if v is not None and v.store is not None and getattr(v.store, "grad_ready_hook", None) is not None:
+            v.store.grad_ready_hook(v)
+
+
+def _ref_param_grads(fn, x, params, grad_out, x_needs_grad, **kw):
+    """CPU reference backward: re-run the reference forward under autograd."""
+    with torch.enable_grad():
+        xs = x.detach().requires_grad_(x_needs_grad) if x is not None else None
+        ps = [p.master.detach().clone().requires_grad_(True) if p is not None else None for p in params]
+        out = fn(xs, *ps, **kw)
+        if isinstance(out, tuple):
+            out = out[0]
+        leaves = ([xs] if x_needs_grad else []) + [p for p in ps if p is not None]
+        grads = torch.autograd.grad(out, leaves, grad_out, allow_unused=True)
+    gx = grads[0] if x_needs_grad else None
+    gp = list(grads[1:] if x_needs_grad else grads)
+    it = iter(gp)
+    for p in params:
+        if p is not None:
+            g = next(it)
+            if g is not None:
+                p.grad.add_(g.to(p.grad.dtype))
+    _grad_ready(*params)
+    return gx
+
+
+# ====================================================================== conv2d (NHWC, KRSC)
+def _conv_ref(x, w, stride=1, pad=0, dil=1):
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2).to(x.dtype), stride=stride, padding=pad, dilation=dil)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, w: Variable, stride, pad, dil):
+        ctx.w, ctx.cfg = w, (stride, pad, dil)
+        ctx.native = _native.use_native(x)
+        ctx.save_for_backward(x)
+        if ctx.native:
+            return torch.ops.tfx.conv_fwd(x.contiguous(), w.value, stride, pad, dil)
+        return _conv_ref(x, w.value.to(x.dtype), stride, pad, dil)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        w = ctx.w
+        stride, pad, dil = ctx.cfg
+        need_dx = ctx.needs_input_grad[0]
+        if ctx.native:
+            gy = gy.contiguous()
+            dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil) if need_dx else None
+            if w.trainable:
+                torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
+                _grad_ready(w)
+            return dx, None, None, None, None, None
+        dx = _ref_param_grads(lambda xx, ww: _conv_ref(xx, ww, stride, pad, dil), x, [w], gy, need_dx)
+        return dx, None, None, None, None, None
+
+
+def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int = 1) -> torch.Tensor:
+    """NHWC conv, weight stored [Ko, R, S, C]. GPU: implicit-GEMM MFMA kernels (igemm.hip)."""
+    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil)
+
+
+# ====================================================================== batch norm (+res, +relu)
+def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=True):
+    xf = x.float()
+    dims = tuple(range(x.dim() - 1))
+    if training:
+        mean = xf.mean(dims)
+        var = xf.var(dims, unbiased=False)
+        if update and rm is not None:
+            n = xf.numel() // xf.shape[-1]
+            with torch.no_grad():
+                rm.mul_(1 - momentum).add_(mean.detach() * momentum)
+                rv.mul_(1 - momentum).add_(var.detach() * (n / max(n - 1, 1)) * momentum)
+    else:
+        mean, var = rm, rv
+    y = (xf - mean) * torch.rsqrt(var + eps)
+    if gamma is not None:
+        y = y * gamma + beta
+    if res is not None:
+        y = y + res.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+class _BatchNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
+                training):
+        ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
+        ctx.native = _native.use_native(x)
+        ctx.has_res = res is not None
+        g_t = gamma.master if gamma is not None else None
+        b_t = beta.master if beta is not None else None
+        if ctx.native:
+            x = x.contiguous()
+            if training:
+                y, save = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu)
+            else:
+                y, save = torch.ops.tfx.bn_fwd_eval(x, g_t, b_t, rm, rv, eps, res, relu)
+            ctx.save_for_backward(x, res, save)
+            return y
+        ctx.save_for_backward(x, res)
+        with torch.no_grad():
+            return _bn_ref(x, g_t, b_t, rm, rv, momentum, eps, res, relu, training)
+
+    @staticmethod
+    def backward(ctx, gy):
+        rm, rv, momentum, eps, relu, training = ctx.cfg
+        gamma, beta = ctx.gamma, ctx.beta
+        if ctx.native:
+            x, res, save = ctx.saved_tensors
+            if not training:
+                raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
+            dx, dres, red = torch.ops.tfx.bn_bwd(gy.contiguous(), x, res, save, relu)
+            C = x.shape[-1]
+            if gamma is not None and gamma.trainable:
+                gamma.grad.add_(red[C:])
+                beta.grad.add_(red[:C])
+                _grad_ready(gamma, beta)
+            return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None
+        x, res = ctx.saved_tensors
+        with torch.enable_grad():
+            xs = x.detach().requires_grad_(True)
+            rs = res.detach().requires_grad_(True) if res is not None else None
+            ps = [v.master.detach().clone().requires_grad_(True) if v is not None else None for v in (gamma, beta)]
+            y = _bn_ref(xs, ps[0], ps[1], rm, rv, momentum, eps, rs, relu, training, update=False)
+            leaves = [xs] + ([rs] if rs is not None else []) + [p for p in ps if p is not None]
+            grads = list(torch.autograd.grad(y, leaves, gy))
+        dx = grads.pop(0)
+        dres = grads.pop(0) if rs is not None else None
+        if gamma is not None:
+            gamma.grad.add_(grads[0])
+            beta.grad.add_(grads[1])
+            _grad_ready(gamma, beta)
+        return dx, dres, None, None, None, None, None, None, None, None, None
+
+
+def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
+               momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False):
+    """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
+    ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass)."""
+    anchor = gamma.store.anchor if gamma is not None else None
+    return _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training)
+
+
+# ====================================================================== dense
+def _pad_to(t: torch.Tensor, dim: int, mult: int) -> torch.Tensor:
+    n = t.shape[dim]
+    r = (-n) % mult
+    if r == 0:
+        return t
+    pad = [0, 0] * (t.dim() - 1 - dim) + [0, r]
+    return F.pad(t, pad)
+
+
+def _linear_ref(x, w, b=None, relu=False):
+    y = x.float() @ w.float().t()
+    if b is not None:
+        y = y + b
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+class _Linear(torch.autograd.Function):
+    """y = act(x @ W^T + b) with W stored [out, in] (bf16 MFMA GEMM on GPU)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, w: Variable, b: Optional[Variable], relu: bool):
+        ctx.w, ctx.b, ctx.relu = w, b, relu
+        ctx.native = _native.use_native(x) and x.dtype == torch.bfloat16
+        if ctx.native:
+            out_f = w.shape[0]
+            xp = _pad_to(x.contiguous(), 1, 8)
+            wp = _pad_to(_pad_to(w.value, 1, 8), 0, 8)
+            bias = b.master if b is not None else None
+            if bias is not None and wp.shape[0] != out_f:
+                bias = _pad_to(bias, 0, 8)
+            y = torch.ops.tfx.gemm(xp, wp, False, True, bias, relu, False)
+            if y.shape[1] != out_f:
+                y = y[:, :out_f].contiguous()
+            ctx.save_for_backward(x, y if relu else None)
+            return y
+        ctx.save_for_backward(x, None)
+        with torch.no_grad():
+            return _linear_ref(x, w.value.to(x.dtype) if x.dtype != torch.float32 else w.master,
+                               b.master if b is not None else None, relu)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y = ctx.saved_tensors
+        w, b, relu = ctx.w, ctx.b, ctx.relu
+        need_dx = ctx.needs_input_grad[0]
+        if ctx.native:
+            g = gy.to(torch.bfloat16)
+            if relu:
+                g = torch.where(y > 0, g, torch.zeros_like(g))
+            g = g.contiguous()
+            out_f, in_f = w.shape
+            gp = _pad_to(g, 1, 8)
+            dx = None
+            if need_dx:
+                wp = _pad_to(_pad_to(w.value, 1, 8), 0, 8)
+                dx = torch.ops.tfx.gemm(gp, wp, False, False, None, False, False)
+                if dx.shape[1] != in_f:
+                    dx = dx[:, :in_f].contiguous()
+            if w.trainable:
+                xp = _pad_to(x.contiguous(), 1, 8)
+                if gp.shape[1] == out_f and xp.shape[1] == in_f:
+                    torch.ops.tfx.gemm_into(gp, xp, True, False, w.grad, True)
+                else:
+                    tmp = torch.zeros(gp.shape[1], xp.shape[1], device=x.device, dtype=torch.float32)
+                    torch.ops.tfx.gemm_into(gp, xp, True, False, tmp, True)
+                    w.grad.add_(tmp[:out_f, :in_f])
+                if b is not None:
+                    b.grad.add_(g.float().sum(0))
+                _grad_ready(w, b)
+            return dx, None, None, None, None
+        params = [w] + ([b] if b is not None else [])
+        fn = (lambda xx, ww, bb: _linear_ref(xx, ww, bb, relu)) if b is not None else \
+            (lambda xx, ww: _linear_ref(xx, ww, None, relu))
+        dx = _ref_param_grads(fn, x, params, gy, need_dx)
+        return dx, None, None, None, None
+
+
+def linear(x, w: Variable, b: Optional[Variable] = None, relu: bool = False):
+    return _Linear.apply(x, w.store.anchor, w, b, relu)
+
+
+# ====================================================================== pooling
+class _GlobalAvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        ctx.native = _native.use_native(x)
+        if ctx.native:
+            return torch.ops.tfx.gap_fwd(x.contiguous(), False)
+        return x.mean(dim=(1, 2))
+
+    @staticmethod
+    def backward(ctx, gy):
+        N, H, W, C = ctx.shape
+        if ctx.native:
+            return torch.ops.tfx.gap_bwd(gy.contiguous(), H, W)
+        return (gy[:, None, None, :] / (H * W)).expand(N, H, W, C).contiguous()
+
+
+def global_avg_pool(x):
+    """NHWC [N,H,W,C] -> [N,C]."""
+    return _GlobalAvgPool.apply(x)
+
+
+# ====================================================================== losses / metrics
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, naive):
+        ctx.native = _native.use_native(logits)
+        B, C = logits.shape
+        if ctx.native:
+            idx = labels if labels.dtype == torch.long else None
+            dense = labels.float().contiguous() if labels.dtype != torch.long else None
+            loss_rows, dz = torch.ops.tfx.softmax_xent(logits.contiguous(), idx, dense, naive, 1.0 / B,
+                                                       bool(ctx.needs_input_grad[0]))
+            ctx.save_for_backward(dz)
+            ctx.dtype = logits.dtype
+            return loss_rows.mean()
+        ctx.save_for_backward(logits, labels)
+        ctx.naive = naive
+        return _xent_ref(logits, labels, naive)
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.native:
+            (dz,) = ctx.saved_tensors
+            return (dz * g).to(ctx.dtype), None, None
+        logits, labels = ctx.saved_tensors
+        with torch.enable_grad():
+            z = logits.detach().requires_grad_(True)
+            loss = _xent_ref(z, labels, ctx.naive)
+            (dz,) = torch.autograd.grad(loss, [z], g)
+        return dz, None, None
+
+
+def _xent_ref(logits, labels, naive):
+    z = logits.float()
+    if labels.dtype == torch.long:
+        y = F.one_hot(labels, z.shape[1]).float()
+    else:
+        y = labels.float()
+    if naive:  # reference parity: -sum(y * log(softmax(z))) (R/distributed/distributed.py:99,102)
+        p = torch.softmax(z, dim=1)
+        return (-(y * torch.log(p)).sum(1)).mean()
+    return (-(y * torch.log_softmax(z, dim=1)).sum(1)).mean()
+
+
+def softmax_cross_entropy(logits, labels, naive: bool = False):
+    """Mean softmax cross-entropy. ``labels``: int64 class ids or dense [B,C] targets.
+    ``naive=True`` reproduces TF1's ``reduce_mean(-reduce_sum(y_*log(softmax(z))))``."""
+    return _SoftmaxXent.apply(logits, labels, naive)
+
+
+def accuracy(logits, labels) -> torch.Tensor:
+    """Fraction of rows with argmax(logits) == label (tf.equal(argmax, argmax) + mean)."""
+    if _native.use_native(logits):
+        idx = labels if labels.dtype == torch.long else None
+        dense = labels.float().contiguous() if labels.dtype != torch.long else None
+        return torch.ops.tfx.accuracy_count(logits.contiguous(), idx, dense)[0] / logits.shape[0]
+    tgt = labels if labels.dtype == torch.long else labels.argmax(1)
+    return (logits.argmax(1) == tgt).float().mean()

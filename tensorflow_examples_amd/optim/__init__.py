@@ -1,0 +1,108 @@
+"""Fused optimizers over the flat variable store (one launch per step for the whole model).
+
+GPU: ``tfx::optimizer_apply`` (csrc/kernels/optim.hip) updates the f32 master buffer and
+rewrites the bf16 compute shadow in the same pass.  CPU: the same math in PyTorch.
+Reference: ``tf.train.GradientDescentOptimizer(lr).minimize`` (R/simple/simple.py:22-23,
+R/distributed/distributed.py:105-108); Momentum / Adam are the north-star fused optimizers.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..ops import _native
+from ..variables import VariableStore
+
+SGD, MOMENTUM, NESTEROV, ADAM, ADAMW = 0, 1, 2, 3, 4
+
+
+class Optimizer:
+    kind = SGD
+
+    def __init__(self, store: VariableStore, learning_rate: float, weight_decay: float = 0.0,
+                 beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8):
+        self.store = store
+        self.wd, self.b1, self.b2, self.eps = float(weight_decay), float(beta1), float(beta2), float(eps)
+        dev = store.device
+        self.lr_t = torch.tensor([float(learning_rate)], dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.m = torch.zeros_like(store.master) if self.kind >= MOMENTUM else None
+        self.v = torch.zeros_like(store.master) if self.kind >= ADAM else None
+        self.iterations = 0
+
+    @property
+    def learning_rate(self) -> float:
+        return float(self.lr_t.item())
+
+    def set_learning_rate(self, lr: float) -> None:
+        self.lr_t.fill_(float(lr))
+
+    def apply_gradients(self, grad_scale: float = 1.0, sumsq: Optional[torch.Tensor] = None,
+                        max_norm: float = 0.0) -> None:
+        """p <- update(p, grad_scale * g); refreshes the bf16 shadow. ``sumsq`` (device scalar
+        ||g||^2) enables clip-by-global-norm at ``max_norm``."""
+        st = self.store
+        self.iterations += 1
+        self.step_t.add_(1.0)
+        if _native.use_native(st.master):
+            torch.ops.tfx.optimizer_apply(self.kind, st.master, st.grad, self.m, self.v, self.lr_t, grad_scale,
+                                          self.wd, self.b1, self.b2, self.eps, self.step_t, sumsq, max_norm,
+                                          st.shadow)
+            return
+        with torch.no_grad():
+            g = st.grad * grad_scale
+            if sumsq is not None:
+                nrm = float(sumsq.sqrt())
+                if nrm > max_norm:
+                    g = g * (max_norm / nrm)
+            p, lr = st.master, self.lr_t
+            if self.kind == SGD:
+                p.sub_(lr * (g + self.wd * p))
+            elif self.kind in (MOMENTUM, NESTEROV):
+                d = g + self.wd * p
+                self.m.mul_(self.b1).add_(d)
+                p.sub_(lr * ((self.b1 * self.m + d) if self.kind == NESTEROV else self.m))
+            else:
+                d = g + self.wd * p if self.kind == ADAM else g
+                self.m.mul_(self.b1).add_((1 - self.b1) * d)
+                self.v.mul_(self.b2).add_((1 - self.b2) * d * d)
+                t = float(self.step_t)
+                upd = (self.m / (1 - self.b1 ** t)) / ((self.v / (1 - self.b2 ** t)).sqrt() + self.eps)
+                if self.kind == ADAMW:
+                    upd = upd + self.wd * p
+                p.sub_(lr * upd)
+            st.refresh_shadow()
+
+    def global_norm_sq(self) -> torch.Tensor:
+        st = self.store
+        if _native.use_native(st.grad):
+            return torch.ops.tfx.sumsq(st.grad)
+        return (st.grad.double() ** 2).sum().float().reshape(1)
+
+
+class GradientDescentOptimizer(Optimizer):
+    kind = SGD
+
+
+class MomentumOptimizer(Optimizer):
+    kind = MOMENTUM
+
+    def __init__(self, store, learning_rate, momentum=0.9, use_nesterov=False, weight_decay=0.0):
+        if use_nesterov:
+            self.kind = NESTEROV
+        super().__init__(store, learning_rate, weight_decay=weight_decay, beta1=momentum)
+
+
+class AdamOptimizer(Optimizer):
+    kind = ADAM
+
+    def __init__(self, store, learning_rate=1e-3, beta1=0.9, beta2=0.999, epsilon=1e-8, weight_decay=0.0,
+                 decoupled=False):
+        if decoupled:
+            self.kind = ADAMW
+        super().__init__(store, learning_rate, weight_decay, beta1, beta2, epsilon)
+
+
+__all__ = ["Optimizer", "GradientDescentOptimizer", "MomentumOptimizer", "AdamOptimizer",
+           "SGD", "MOMENTUM", "NESTEROV", "ADAM", "ADAMW"]

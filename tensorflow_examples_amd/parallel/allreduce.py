@@ -1,0 +1,129 @@
+"""Synchronous data parallelism: bucketed gradient all-reduce over the flat grad buffer,
+overlapped with backward.
+
+Design for one MI355X node (8 GPUs, 7 point-to-point xGMI links of ~153 GB/s per GPU):
+
+* one process per GPU, ``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm);
+* the gradient of every trainable variable lives in ONE flat f32 buffer laid out in
+  creation (= forward) order, so backward produces gradients from the END of the buffer
+  towards its start.  Buckets are contiguous slices of that buffer, cut in reverse order:
+  a bucket is a single RCCL call on a contiguous view -- no flatten/unflatten copies;
+* a bucket is launched the moment its last gradient has been written (the ops fire
+  ``store.grad_ready_hook``), so RCCL's ring runs on its own stream beside the remaining
+  backward kernels;
+* default bucket size 32 MB: a ring over xGMI is bound by one link per hop
+  (~2(N-1)/N * S / 153 GB/s ~ 0.37 ms for 32 MB at N = 8), large enough to amortise
+  RCCL's launch/latency cost yet small enough that the first bucket starts early in
+  backward (ResNet-50: 94 MB of f32 gradients -> 3 buckets);
+* averaging is folded into the optimizer (``grad_scale = 1/world``), no extra pass;
+* optional bf16 compression halves the bytes on the wire (cast, reduce, cast back).
+
+The reference has no synchronous DP at all -- only a commented-out
+``SyncReplicasOptimizer`` remnant (R/distributed/distributed.py:110-113); this is the
+north-star RCCL path of BASELINE.json (configs 3 and 5).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..variables import Variable, VariableStore
+
+
+class GradAllReduce:
+    def __init__(self, store: VariableStore, bucket_bytes: int = 32 << 20, group=None, overlap: bool = True,
+                 compress_bf16: bool = False):
+        self.store = store
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.overlap = overlap
+        self.compress = compress_bf16
+        elem = store.grad.element_size()
+        cap = max(1, bucket_bytes // elem)
+        self.buckets: List[List[int]] = []  # [lo, hi) element ranges of the flat grad buffer
+        self.members: List[List[Variable]] = []
+        self.var_bucket: Dict[int, int] = {}
+        cur: List[Variable] = []
+        size = 0
+        for v in reversed(store.trainable()):
+            cur.append(v)
+            size += v.numel
+            if size >= cap:
+                self._close(cur)
+                cur, size = [], 0
+        if cur:
+            self._close(cur)
+        self._pending: List[int] = []
+        self._launched: List[bool] = []
+        self._works = []
+        if overlap and self.world > 1:
+            store.grad_ready_hook = self._on_ready
+        self.start_step()
+
+    def _close(self, vs: List[Variable]) -> None:
+        lo = min(v.offset for v in vs)
+        hi = max(v.offset + v.numel for v in vs)
+        b = len(self.buckets)
+        self.buckets.append([lo, hi])
+        self.members.append(list(vs))
+        for v in vs:
+            self.var_bucket[v.index] = b
+
+    @property
+    def bucket_sizes_bytes(self) -> List[int]:
+        e = self.store.grad.element_size()
+        return [(hi - lo) * e for lo, hi in self.buckets]
+
+    def start_step(self) -> None:
+        self._pending = [len(m) for m in self.members]
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+
+    def _on_ready(self, v: Variable) -> None:
+        b = self.var_bucket.get(v.index)
+        if b is None:
+            return
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            self._launch(b)
+
+    def _launch(self, b: int) -> None:
+        if self._launched[b] or self.world == 1:
+            self._launched[b] = True
+            return
+        self._launched[b] = True
+        lo, hi = self.buckets[b]
+        view = self.store.grad[lo:hi]
+        if self.compress:
+            tmp = view.to(torch.bfloat16)
+            work = dist.all_reduce(tmp, group=self.group, async_op=True)
+            self._works.append((work, view, tmp))
+        else:
+            self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+
+    def finish(self) -> None:
+        """Launch buckets not yet started (in order) and make the current stream wait for all."""
+        for b in range(len(self.buckets)):
+            if not self._launched[b]:
+                self._launch(b)
+        for work, view, tmp in self._works:
+            work.wait()
+            if view is not None:
+                view.copy_(tmp)
+        self.start_step()
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0 / self.world
+
+
+def broadcast_variables(store: VariableStore, src: int = 0, group=None) -> None:
+    """Make every rank start from rank ``src``'s weights (one broadcast of the flat buffer)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    dist.broadcast(store.master, src=src, group=group)
+    for t in store.state.values():
+        dist.broadcast(t, src=src, group=group)
+    store.refresh_shadow()

@@ -1,0 +1,255 @@
+"""Flat variable store: every trainable tensor of a model is a view into ONE contiguous
+f32 master buffer, with a matching flat gradient buffer and (for bf16 models) a flat
+bf16 compute shadow.
+
+This replaces TF1's per-variable ``VariableV2`` ops (R/distributed/distributed.py:68-91,
+R/simple/simple.py:11-12) with a layout designed for MI355X:
+
+* one fused optimizer launch updates the whole model and refreshes the bf16 shadow
+  (csrc/kernels/optim.hip);
+* gradient all-reduce works on large contiguous buckets of the flat grad buffer
+  (parallel/allreduce.py) -- few, big RCCL calls over xGMI;
+* the parameter server (cluster/ps.py) ships the flat buffer (or shards of it) in one
+  message instead of one RPC per variable;
+* weight-gradient kernels accumulate straight into their grad view (f32 atomics), so
+  there is no per-parameter ``.grad`` allocation or copy.
+
+Variables keep their TF names (``weights/Variable``, ``biases/Variable_1``, ...) so
+checkpoints and the PS shard map match the reference's naming.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import torch
+
+ALIGN = 64  # elements; keeps every view 128-B aligned in f32 and bf16 buffers
+
+
+def _round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+# ---------------------------------------------------------------- initializers
+class Initializer:
+    def __call__(self, shape: Sequence[int], gen: torch.Generator) -> torch.Tensor:  # pragma: no cover
+        raise NotImplementedError
+
+
+@dataclass
+class Zeros(Initializer):
+    def __call__(self, shape, gen):
+        return torch.zeros(shape, dtype=torch.float32)
+
+
+@dataclass
+class Constant(Initializer):
+    value: float = 0.0
+
+    def __call__(self, shape, gen):
+        return torch.full(shape, float(self.value), dtype=torch.float32)
+
+
+@dataclass
+class RandomNormal(Initializer):
+    """tf.random_normal(shape, mean, stddev) -- R/distributed/distributed.py:85-86 (stddev 1.0)."""
+    mean: float = 0.0
+    stddev: float = 1.0
+
+    def __call__(self, shape, gen):
+        return torch.randn(shape, generator=gen, dtype=torch.float32) * self.stddev + self.mean
+
+
+@dataclass
+class TruncatedNormal(Initializer):
+    mean: float = 0.0
+    stddev: float = 1.0
+
+    def __call__(self, shape, gen):
+        t = torch.randn(shape, generator=gen, dtype=torch.float32)
+        bad = t.abs() > 2
+        while bad.any():
+            t[bad] = torch.randn(int(bad.sum()), generator=gen, dtype=torch.float32)
+            bad = t.abs() > 2
+        return t * self.stddev + self.mean
+
+
+@dataclass
+class Uniform(Initializer):
+    low: float = -1.0
+    high: float = 1.0
+
+    def __call__(self, shape, gen):
+        return torch.rand(shape, generator=gen, dtype=torch.float32) * (self.high - self.low) + self.low
+
+
+@dataclass
+class HeNormal(Initializer):
+    """Kaiming normal with fan_in = prod(shape[1:]) (conv weights stored [Ko,R,S,C])."""
+    gain: float = math.sqrt(2.0)
+
+    def __call__(self, shape, gen):
+        fan_in = int(math.prod(shape[1:])) if len(shape) > 1 else int(shape[0])
+        return torch.randn(shape, generator=gen, dtype=torch.float32) * (self.gain / math.sqrt(fan_in))
+
+
+@dataclass
+class GlorotUniform(Initializer):
+    def __call__(self, shape, gen):
+        if len(shape) == 2:
+            fan_out, fan_in = shape[0], shape[1]
+        else:
+            rf = int(math.prod(shape[1:-1])) if len(shape) > 2 else 1
+            fan_out, fan_in = shape[0] * rf, shape[-1] * rf
+        lim = math.sqrt(6.0 / (fan_in + fan_out))
+        return (torch.rand(shape, generator=gen, dtype=torch.float32) * 2 - 1) * lim
+
+
+# ---------------------------------------------------------------- variables
+@dataclass
+class Variable:
+    name: str
+    shape: tuple
+    initializer: Initializer
+    trainable: bool = True
+    index: int = 0
+    offset: int = 0
+    numel: int = 0
+    store: Optional["VariableStore"] = field(default=None, repr=False)
+
+    @property
+    def master(self) -> torch.Tensor:
+        """f32 master value (view into the flat buffer)."""
+        return self.store.master[self.offset:self.offset + self.numel].view(self.shape)
+
+    @property
+    def value(self) -> torch.Tensor:
+        """Compute copy: bf16 shadow view for bf16 stores, the f32 master otherwise."""
+        buf = self.store.shadow if self.store.shadow is not None else self.store.master
+        return buf[self.offset:self.offset + self.numel].view(self.shape)
+
+    @property
+    def grad(self) -> torch.Tensor:
+        return self.store.grad[self.offset:self.offset + self.numel].view(self.shape)
+
+    def assign(self, t: torch.Tensor) -> None:
+        self.master.copy_(t.to(self.master.dtype).view(self.shape))
+        if self.store.shadow is not None:
+            self.value.copy_(self.master)
+
+
+class VariableStore:
+    """Creates variables (TF naming, creation order preserved) and lays them out flat."""
+
+    def __init__(self, device="cpu", compute_dtype=torch.float32, seed: int = 0):
+        self.device = torch.device(device)
+        self.compute_dtype = compute_dtype
+        self.seed = seed
+        self.vars: List[Variable] = []
+        self.by_name: Dict[str, Variable] = {}
+        self.state: Dict[str, torch.Tensor] = {}  # non-trainable state (BN running stats, global_step)
+        self.master: Optional[torch.Tensor] = None
+        self.grad: Optional[torch.Tensor] = None
+        self.shadow: Optional[torch.Tensor] = None
+        self.total = 0
+        # autograd anchor: a leaf that requires grad, passed to every parameterised op so the
+        # graph is recorded even when no input activation requires grad (params are not
+        # autograd leaves -- their grads are written into the flat buffer by the ops).
+        self.anchor = torch.zeros((), device=self.device, requires_grad=True)
+        self.grad_ready_hook = None
+        self._scopes: List[str] = []
+        self._name_counts: Dict[str, int] = {}
+
+    # -- naming (tf.name_scope + tf.Variable auto-naming "Variable", "Variable_1", ...)
+    def scope(self, name: str):
+        store = self
+
+        class _S:
+            def __enter__(self):
+                store._scopes.append(name)
+
+            def __exit__(self, *a):
+                store._scopes.pop()
+
+        return _S()
+
+    def unique_name(self, base: str) -> str:
+        prefix = "/".join(self._scopes)
+        full = f"{prefix}/{base}" if prefix else base
+        n = self._name_counts.get(full, 0)
+        self._name_counts[full] = n + 1
+        return full if n == 0 else f"{full}_{n}"
+
+    def variable(self, shape, initializer: Initializer, name: str = "Variable", trainable=True) -> Variable:
+        if self.master is not None:
+            raise RuntimeError("VariableStore already finalized")
+        full = self.unique_name(name)
+        v = Variable(full, tuple(int(s) for s in shape), initializer, trainable, index=len(self.vars), store=self)
+        self.vars.append(v)
+        self.by_name[full] = v
+        return v
+
+    def add_state(self, name: str, t: torch.Tensor) -> torch.Tensor:
+        full = self.unique_name(name)
+        t = t.to(self.device)
+        self.state[full] = t
+        return t
+
+    # -- layout
+    def finalize(self, init: bool = True) -> "VariableStore":
+        off = 0
+        for v in self.vars:
+            v.numel = int(math.prod(v.shape)) if v.shape else 1
+            v.offset = off
+            off = _round_up(off + v.numel, ALIGN)
+        self.total = max(off, ALIGN)
+        self.master = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        if self.compute_dtype != torch.float32:
+            self.shadow = torch.zeros(self.total, dtype=self.compute_dtype, device=self.device)
+        if init:
+            self.initialize()
+        return self
+
+    def initialize(self) -> None:
+        """Run every initializer (TF global_variables_initializer). Deterministic per (seed, index)."""
+        host = torch.zeros(self.total, dtype=torch.float32)
+        for v in self.vars:
+            g = torch.Generator().manual_seed(self.seed * 1000003 + v.index)
+            host[v.offset:v.offset + v.numel] = v.initializer(v.shape, g).reshape(-1)
+        self.master.copy_(host)
+        self.refresh_shadow()
+
+    def refresh_shadow(self) -> None:
+        if self.shadow is not None:
+            self.shadow.copy_(self.master)
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def trainable(self) -> List[Variable]:
+        return [v for v in self.vars if v.trainable]
+
+    def num_params(self) -> int:
+        return sum(v.numel for v in self.vars if v.trainable)
+
+    # -- checkpoint helpers (name -> f32 tensor)
+    def named_values(self) -> Dict[str, torch.Tensor]:
+        out = {v.name: v.master.detach() for v in self.vars}
+        out.update({k: t.detach() for k, t in self.state.items()})
+        return out
+
+    def load_named(self, values: Dict[str, torch.Tensor], strict: bool = True) -> None:
+        for v in self.vars:
+            if v.name in values:
+                v.master.copy_(values[v.name].to(self.device, torch.float32).view(v.shape))
+            elif strict:
+                raise KeyError(f"missing variable {v.name}")
+        for k, t in self.state.items():
+            if k in values:
+                t.copy_(values[k].to(t.device, t.dtype).view(t.shape))
+            elif strict:
+                raise KeyError(f"missing state {k}")
+        self.refresh_shadow()

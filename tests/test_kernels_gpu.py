@@ -1,0 +1,201 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+All tests are ``@pytest.mark.gpu`` (run on the MI355X box via gpurun).  Inputs are
+bf16-representable so the only error left is accumulation order / output rounding.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CONV_SHAPES = [
+    # N, H, W, C, Ko, R, stride, pad
+    (4, 8, 8, 64, 64, 1, 1, 0),
+    (2, 8, 8, 64, 128, 3, 1, 1),
+    (3, 9, 7, 32, 64, 3, 2, 1),
+    (2, 8, 8, 64, 256, 1, 2, 0),
+    (2, 32, 32, 8, 64, 3, 1, 1),  # padded-RGB stem
+    (1, 5, 5, 16, 24, 3, 1, 1),   # ragged M / N
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_dgrad_wgrad(gpu, shape):
+    N, H, W, C, Ko, R, st, pad = shape
+    torch.manual_seed(0)
+    x = _bf(torch.randn(N, H, W, C, device=gpu))
+    w = _bf(torch.randn(Ko, R, R, C, device=gpu) * (1.0 / math.sqrt(R * R * C)))
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=st, padding=pad)
+    y = torch.ops.tfx.conv_fwd(x, w, st, pad, 1)
+    assert y.shape == (N, yr.shape[2], yr.shape[3], Ko)
+    assert _rel(y, yr.permute(0, 2, 3, 1)) < 1e-2
+    gy = _bf(torch.randn_like(y.float()))
+    yr.backward(gy.float().permute(0, 3, 1, 2))
+    dx = torch.ops.tfx.conv_dgrad(gy, w, list(x.shape), st, pad, 1)
+    assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    dw = torch.zeros(Ko, R, R, C, device=gpu)
+    torch.ops.tfx.conv_wgrad(gy, x, dw, st, pad, 1, False)
+    assert _rel(dw, wr.grad.permute(0, 2, 3, 1)) < 5e-3
+    # accumulate mode adds on top
+    torch.ops.tfx.conv_wgrad(gy, x, dw, st, pad, 1, True)
+    assert _rel(dw, 2 * wr.grad.permute(0, 2, 3, 1)) < 5e-3
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("mnk", [(256, 128, 64), (200, 136, 328), (64, 16, 1024)])
+def test_gemm_layouts(gpu, ta, tb, mnk):
+    M, N, K = mnk
+    torch.manual_seed(1)
+    A = torch.randn(M, K, device=gpu)
+    B = torch.randn(K, N, device=gpu) + torch.arange(N, device=gpu)[None, :] * 0.01  # asymmetric
+    a = _bf(A.t().contiguous() if ta else A)
+    b = _bf(B.t().contiguous() if tb else B)
+    ref = a.float().t() @ b.float() if ta else a.float() @ (b.float().t() if tb else b.float())
+    ref = (a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float())
+    out = torch.ops.tfx.gemm(a, b, ta, tb, None, False, True)
+    assert _rel(out, ref) < 1e-5 * math.sqrt(K) + 1e-5
+    acc = torch.ones(M, N, device=gpu)
+    torch.ops.tfx.gemm_into(a, b, ta, tb, acc, True)
+    assert _rel(acc, ref + 1) < 1e-4
+
+
+def test_gemm_identity_asymmetric(gpu):
+    # A = I with an asymmetric B catches a transposed C-write (cdna_hip_programming.md §3)
+    I = _bf(torch.eye(128, device=gpu))
+    B = _bf(torch.arange(128 * 128, device=gpu, dtype=torch.float32).view(128, 128) % 97)
+    out = torch.ops.tfx.gemm(I, B, False, False, None, False, True)
+    assert torch.equal(out, B.float())
+
+
+def test_gemm_bias_relu_bf16(gpu):
+    a = _bf(torch.randn(64, 256, device=gpu))
+    w = _bf(torch.randn(96, 256, device=gpu))
+    b = torch.randn(96, device=gpu)
+    out = torch.ops.tfx.gemm(a, w, False, True, b, True, False)
+    ref = torch.relu(a.float() @ w.float().t() + b)
+    assert out.dtype == torch.bfloat16 and _rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True)])
+def test_sgemm_exact_f32(gpu, ta, tb):
+    torch.manual_seed(2)
+    M, N, K = 100, 10, 100
+    A = torch.randn(M, K, device=gpu)
+    B = torch.randn(K, N, device=gpu)
+    a = A.t().contiguous() if ta else A
+    b = B.t().contiguous() if tb else B
+    out = torch.ops.tfx.sgemm(a, b, ta, tb, None, 0)
+    ref = (A.double() @ B.double()).float()
+    assert (out - ref).abs().max().item() < 1e-4
+    bias = torch.randn(N, device=gpu)
+    sig = torch.ops.tfx.sgemm(a, b, ta, tb, bias, 2)
+    assert torch.allclose(sig, torch.sigmoid(ref + bias), atol=1e-5)
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048, 6, 120])
+@pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
+def test_batchnorm_train(gpu, C, res, relu):
+    torch.manual_seed(3)
+    M = 512
+    x = _bf(torch.randn(M, C, device=gpu) * 2 + 0.5)
+    r = _bf(torch.randn(M, C, device=gpu)) if res else None
+    gamma = torch.rand(C, device=gpu) + 0.5
+    beta = torch.randn(C, device=gpu)
+    rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    y, save = torch.ops.tfx.bn_fwd_train(x, gamma, beta, rm, rv, 0.1, 1e-5, r, relu)
+    xr = x.float().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    mean, var = xr.mean(0), xr.var(0, unbiased=False)
+    yr = (xr - mean) / torch.sqrt(var + 1e-5) * gr + br
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    assert _rel(y, yr) < 1e-2
+    assert torch.allclose(rm, 0.1 * mean.detach(), atol=1e-4)
+    assert torch.allclose(rv, 0.9 + 0.1 * var.detach() * M / (M - 1), atol=1e-3)
+    g = _bf(torch.randn(M, C, device=gpu))
+    yr.backward(g.float())
+    dx, dres, red = torch.ops.tfx.bn_bwd(g, x, r, save, relu)
+    assert _rel(dx, xr.grad) < 2e-2
+    assert _rel(red[C:], gr.grad) < 1e-3 and _rel(red[:C], br.grad) < 1e-3
+    if res:
+        assert _rel(dres, rr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("naive", [False, True])
+@pytest.mark.parametrize("dense", [False, True])
+def test_softmax_xent(gpu, naive, dense):
+    torch.manual_seed(4)
+    B, C = 100, 10
+    z = torch.randn(B, C, device=gpu) * 3
+    lab = torch.randint(0, C, (B,), device=gpu)
+    y = F.one_hot(lab, C).float()
+    loss_rows, dz = torch.ops.tfx.softmax_xent(z, None if dense else lab, y if dense else None, naive, 1.0 / B, True)
+    zr = z.clone().requires_grad_(True)
+    if naive:
+        lr = -(y * torch.log(torch.softmax(zr, 1))).sum(1)
+    else:
+        lr = -(y * torch.log_softmax(zr, 1)).sum(1)
+    lr.mean().backward()
+    assert torch.allclose(loss_rows, lr.detach(), atol=1e-4, rtol=1e-4)
+    assert torch.allclose(dz, zr.grad, atol=1e-5, rtol=1e-3)
+    cnt = torch.ops.tfx.accuracy_count(z, lab, None)
+    assert cnt.item() == (z.argmax(1) == lab).sum().item()
+
+
+def test_global_avg_pool(gpu):
+    x = _bf(torch.randn(4, 4, 4, 2048, device=gpu))
+    y = torch.ops.tfx.gap_fwd(x, False)
+    assert _rel(y, x.float().mean((1, 2))) < 1e-2
+    g = _bf(torch.randn(4, 2048, device=gpu))
+    dx = torch.ops.tfx.gap_bwd(g, 4, 4)
+    assert _rel(dx, (g.float() / 16)[:, None, None, :].expand(4, 4, 4, 2048)) < 1e-2
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+def test_optimizer_kernels(gpu, kind):
+    from tensorflow_examples_amd.optim import Optimizer
+    from tensorflow_examples_amd.variables import RandomNormal, VariableStore
+
+    def make(dev):
+        st = VariableStore(dev, torch.bfloat16 if dev.type == "cuda" else torch.float32, seed=7)
+        st.variable([37, 5], RandomNormal())
+        st.variable([11], RandomNormal())
+        st.finalize()
+        st.grad.copy_(torch.linspace(-1, 1, st.total))
+        o = Optimizer.__new__(Optimizer)
+        o.kind = kind
+        Optimizer.__init__(o, st, 0.05, weight_decay=0.01, beta1=0.9, beta2=0.99, eps=1e-6)
+        return st, o
+
+    sg, og = make(gpu)
+    sc, oc = make(torch.device("cpu"))
+    for _ in range(3):
+        og.apply_gradients(grad_scale=0.5)
+        oc.apply_gradients(grad_scale=0.5)
+    assert torch.allclose(sg.master.cpu(), sc.master, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(sg.shadow.float().cpu(), sc.master, atol=1e-2, rtol=1e-2)
+
+
+def test_sumsq_and_clip(gpu):
+    g = torch.randn(4096, device=gpu)
+    s = torch.ops.tfx.sumsq(g)
+    assert abs(s.item() - (g.double() ** 2).sum().item()) / s.item() < 1e-5
