@@ -9,6 +9,30 @@
 
 namespace tfx {
 
+// Cross-block reduction slots for per-channel statistics ([NSLOT][2][C] f32, see batchnorm.hip)
+constexpr int NSLOT = 64;
+
+// Division by a runtime-invariant divisor via multiply-high (valid for n < 2^31).
+struct FastDiv {
+  uint32_t d = 1, m = 0, s = 0;
+  FastDiv() = default;
+  explicit FastDiv(uint32_t dd) : d(dd) {
+    s = 0;
+    while ((1u << s) < d) ++s;
+    m = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+  }
+#ifdef __HIPCC__
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    const uint32_t t = __umulhi(n, m);
+    return (uint32_t)(((uint64_t)t + n) >> s);
+  }
+#endif
+  uint32_t div_host(uint32_t n) const {
+    const uint32_t t = (uint32_t)(((uint64_t)n * m) >> 32);
+    return (uint32_t)(((uint64_t)t + n) >> s);
+  }
+};
+
 // ---------------------------------------------------------------- implicit GEMM
 enum { MODE_GEMM = 0, MODE_FWD = 1, MODE_DGRAD = 2, MODE_WGRAD = 3 };
 enum { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ADD = 2, OUT_F32_ATOMIC = 3 };
@@ -24,8 +48,12 @@ struct IgemmArgs {
   // conv geometry (NHWC input [Nb][H][W][C], weight [Ko][R][S][C], output [Nb][P][Q][Ko])
   int Nb = 0, H = 0, W = 0, C = 0, Ko = 0, R = 1, S = 1, P = 0, Q = 0;
   int sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
+  int sh_log2 = 0, sw_log2 = 0;
   int out_mode = OUT_BF16;
   int relu = 0;
+  // optional per-column BN statistics of the (bf16-rounded) output: [NSLOT][2][N] f32, pre-zeroed
+  float* stats = nullptr;
+  FastDiv fd_C, fd_S, fd_Ko, fd_PQ, fd_Q;
   int zero_out = 1;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;

@@ -2,11 +2,16 @@
 // residual add of a ResNet bottleneck fused into the apply pass.
 //
 // Layout: x is [M][C] with M = N*H*W rows (channels-last), C contiguous.
-// Forward  : stats (sum, sumsq per channel, f32 atomics) -> finalize (mean, invstd,
-//            scale = gamma*invstd, shift = beta - mean*scale, running-stat update)
-//            -> apply  y = relu?(x*scale + shift (+ res)).
+// Forward  : stats -> finalize (mean, invstd, scale = gamma*invstd, shift = beta - mean*scale,
+//            running-stat update) -> apply  y = relu?(x*scale + shift (+ res)).
+//            The stats usually come for free from the producing conv's epilogue
+//            (igemm.hip, MODE_FWD with a stats buffer); bn_stats is the standalone pass.
 // Backward : reduce (sum g', sum g'*xhat with g' = g * [z > 0] recomputed from x/res)
 //            -> apply  dx = scale*(g' - sum_g/M - xhat*sum_gx/M), dres = g'.
+// Cross-block reductions go through NSLOT=64 slot rows [NSLOT][2][C]: block b adds its partial
+// into slot b % NSLOT (<= ~32 adders per address instead of every block on one address, which
+// serialises at the memory side: MI355X_MICROARCH.md "Global float atomics", contention row),
+// and the finalize/reduce kernel sums the 64 slots.
 // Memory-bound: every pass moves 16 B per lane (8 channels), grid-stride.
 #include "tfx_common.h"
 #include "tfx_kernels.h"
@@ -47,7 +52,8 @@ __global__ void __launch_bounds__(256) bn_stats_vec_kernel(const uint16_t* __res
     }
     if (r0 == 0) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) atomicAdd(&sums[pass * C + cv * 8 + i], red[i * 256 + t]);
+      for (int i = 0; i < 8; ++i)
+        atomicAdd(&sums[(blockIdx.x % NSLOT) * 2 * C + pass * C + cv * 8 + i], red[i * 256 + t]);
     }
     __syncthreads();
   }
@@ -73,23 +79,46 @@ __global__ void __launch_bounds__(256) bn_stats_gen_kernel(const uint16_t* __res
   if (ty == 0 && c < C) {
     s = rs[tx] + rs[tx + 64] + rs[tx + 128] + rs[tx + 192];
     q = rq[tx] + rq[tx + 64] + rq[tx + 128] + rq[tx + 192];
-    atomicAdd(&sums[c], s);
-    atomicAdd(&sums[C + c], q);
+    float* slot = sums + (size_t)((blockIdx.y % NSLOT) * 2) * C;
+    atomicAdd(&slot[c], s);
+    atomicAdd(&slot[C + c], q);
   }
 }
 
 // ------------------------------------------------------------------ finalize
 // sums[0:C]=Σx, sums[C:2C]=Σx²  ->  save[0:C]=mean, save[C:2C]=invstd, save[2C:3C]=scale,
 // save[3C:4C]=shift; running stats updated in place (unbiased variance, PyTorch/TF momentum form).
-__global__ void bn_finalize_kernel(const float* __restrict__ sums, int64_t M, int C,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float eps, float momentum, float* __restrict__ run_mean,
-                                   float* __restrict__ run_var, float* __restrict__ save) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Sum the NSLOT slot rows of slots[NSLOT][2][C] into out[2][C] (64 channels x 4 slot-lanes per block)
+__device__ __forceinline__ void slot_sum(const float* __restrict__ slots, int C, int c, int ty, float& s, float& q) {
+  s = 0.f;
+  q = 0.f;
+  if (c < C) {
+    for (int k = ty; k < NSLOT; k += 4) {
+      s += slots[(size_t)k * 2 * C + c];
+      q += slots[(size_t)k * 2 * C + C + c];
+    }
+  }
+  __shared__ float rs[256], rq[256];
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  const int tx = threadIdx.x & 63;
+  s = rs[tx] + rs[tx + 64] + rs[tx + 128] + rs[tx + 192];
+  q = rq[tx] + rq[tx + 64] + rq[tx + 128] + rq[tx + 192];
+}
+
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ slots, int64_t M, int C,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          float eps, float momentum, float* __restrict__ run_mean,
+                                                          float* __restrict__ run_var, float* __restrict__ save) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float sum, sq;
+  slot_sum(slots, C, c, ty, sum, sq);
+  if (ty != 0 || c >= C) return;
   const float inv_m = 1.f / (float)M;
-  const float mean = sums[c] * inv_m;
-  const float var = fmaxf(sums[C + c] * inv_m - mean * mean, 0.f);
+  const float mean = sum * inv_m;
+  const float var = fmaxf(sq * inv_m - mean * mean, 0.f);
   const float invstd = rsqrtf(var + eps);
   const float g = gamma ? gamma[c] : 1.f;
   const float b = beta ? beta[c] : 0.f;
@@ -102,6 +131,19 @@ __global__ void bn_finalize_kernel(const float* __restrict__ sums, int64_t M, in
     const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
     run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
+// backward: slots -> red[2][C]
+__global__ void __launch_bounds__(256) bn_slot_reduce_kernel(const float* __restrict__ slots, int C,
+                                                             float* __restrict__ red) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float s, q;
+  slot_sum(slots, C, c, ty, s, q);
+  if (ty == 0 && c < C) {
+    red[c] = s;
+    red[C + c] = q;
   }
 }
 
@@ -216,7 +258,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* 
     }
     if (r0 == 0) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) atomicAdd(&red[pass * C + cv * 8 + i], lds[i * 256 + t]);
+      for (int i = 0; i < 8; ++i)
+        atomicAdd(&red[(blockIdx.x % NSLOT) * 2 * C + pass * C + cv * 8 + i], lds[i * 256 + t]);
     }
     __syncthreads();
   }
@@ -251,8 +294,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_gen_kernel(const uint16_t* 
   b[threadIdx.x] = sx;
   __syncthreads();
   if (ty == 0 && c < C) {
-    atomicAdd(&red[c], a[tx] + a[tx + 64] + a[tx + 128] + a[tx + 192]);
-    atomicAdd(&red[C + c], b[tx] + b[tx + 64] + b[tx + 128] + b[tx + 192]);
+    float* slot = red + (size_t)((blockIdx.y % NSLOT) * 2) * C;
+    atomicAdd(&slot[c], a[tx] + a[tx + 64] + a[tx + 128] + a[tx + 192]);
+    atomicAdd(&slot[C + c], b[tx] + b[tx + 64] + b[tx + 128] + b[tx + 192]);
   }
 }
 
@@ -326,7 +370,7 @@ static inline int grid_for(int64_t work, int per_block) {
 }
 
 void bn_stats(const uint16_t* x, int64_t M, int C, float* sums, hipStream_t s) {
-  TFX_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, s));
+  TFX_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * NSLOT, s));
   if (vec_ok(C)) {
     const int rpb = 256 / (C / 8);
     int g = grid_for(M, rpb * 8);  // >= 8 rows per row-lane
@@ -339,8 +383,8 @@ void bn_stats(const uint16_t* x, int64_t M, int C, float* sums, hipStream_t s) {
 
 void bn_finalize(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
                  float momentum, float* run_mean, float* run_var, float* save, hipStream_t s) {
-  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(sums, M, C, gamma, beta, eps, momentum, run_mean,
-                                                     run_var, save);
+  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, s>>>(sums, M, C, gamma, beta, eps, momentum, run_mean,
+                                                   run_var, save);
 }
 
 void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
@@ -373,19 +417,22 @@ void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t
 
 void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const float* save, int64_t M,
                  int C, bool relu, float* red, uint16_t* dx, uint16_t* dres, hipStream_t s) {
-  TFX_HIP_CHECK(hipMemsetAsync(red, 0, sizeof(float) * 2 * C, s));
+  // red: [2C] result followed by the [NSLOT][2][C] slot workspace
+  float* slots = red + 2 * C;
+  TFX_HIP_CHECK(hipMemsetAsync(slots, 0, sizeof(float) * 2 * C * NSLOT, s));
   const bool has_res = res != nullptr;  // only meaningful for the ReLU mask recompute
   const int64_t n = M * C;
   if (vec_ok(C)) {
     const int rpb = 256 / (C / 8);
     int gr = grid_for(M, rpb * 8);
     TFX_DISPATCH_RR(has_res, relu,
-                    (bn_bwd_reduce_vec_kernel<R_, L_><<<gr, 256, 0, s>>>(g, x, res, save, M, C, red)));
+                    (bn_bwd_reduce_vec_kernel<R_, L_><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
   } else {
     dim3 grid((C + 63) / 64, grid_for(M, 64));
     TFX_DISPATCH_RR(has_res, relu,
-                    (bn_bwd_reduce_gen_kernel<R_, L_><<<grid, 256, 0, s>>>(g, x, res, save, M, C, red)));
+                    (bn_bwd_reduce_gen_kernel<R_, L_><<<grid, 256, 0, s>>>(g, x, res, save, M, C, slots)));
   }
+  bn_slot_reduce_kernel<<<(C + 63) / 64, 256, 0, s>>>(slots, C, red);
   // With a residual input (bottleneck output BN) dres = g' is always produced: the identity /
   // projection branch needs it.  The host wrapper guarantees dres != nullptr when res != nullptr.
   if (C % 8 == 0) {

@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) ra[i] = ldg16(a.A + a_row[i] + k, kok && a_row[i] >= 0);
       } else if constexpr (MODE == MODE_FWD) {
-        const int rs = k / a.C, cc = k - rs * a.C, r = rs / a.S, s = rs - r * a.S;
+        const int rs = a.fd_C.div(k), cc = k - rs * a.C, r = a.fd_S.div(rs), s = rs - r * a.S;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int iy = a_y[i] + r * a.dh, ix = a_x[i] + s * a.dw;
@@ -159,16 +159,16 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
           ra[i] = ldg16(a.A + off, ok);
         }
       } else {  // DGRAD: A = dY[n][p][q][ko], k = (r,s,ko)
-        const int rs = k / a.Ko, ko = k - rs * a.Ko, r = rs / a.S, s = rs - r * a.S;
+        const int rs = a.fd_Ko.div(k), ko = k - rs * a.Ko, r = a.fd_S.div(rs), s = rs - r * a.S;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int ty = a_y[i] - r * a.dh, tx = a_x[i] - s * a.dw;
           bool ok = kok && a_row[i] >= 0 && ty >= 0 && tx >= 0;
           int p = 0, q = 0;
-          if (ok) {
-            p = ty / a.sh;
-            q = tx / a.sw;
-            ok = (p * a.sh == ty) && (q * a.sw == tx) && p < a.P && q < a.Q;
+          if (ok) {  // strides are powers of two (checked on the host)
+            p = ty >> a.sh_log2;
+            q = tx >> a.sw_log2;
+            ok = ((p << a.sh_log2) == ty) && ((q << a.sw_log2) == tx) && p < a.P && q < a.Q;
           }
           const int64_t off = ok ? (((int64_t)a_row[i] * a.P + p) * a.Q + q) * a.Ko + ko : 0;
           ra[i] = ldg16(a.A + off, ok);
@@ -200,12 +200,12 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
           off = (int64_t)k * a.ldb + b_col;
         } else if constexpr (MODE == MODE_DGRAD) {
           // B(k=(r,s,ko), c) = W[ko][r][s][c]
-          const int rs = k / a.Ko, ko = k - rs * a.Ko, r = rs / a.S, s = rs - r * a.S;
+          const int rs = a.fd_Ko.div(k), ko = k - rs * a.Ko, r = a.fd_S.div(rs), s = rs - r * a.S;
           off = (((int64_t)ko * a.R + r) * a.S + s) * a.C + b_col;
         } else if constexpr (MODE == MODE_WGRAD) {
           // B(k=j=(n,p,q), col=(r,s,c)) = X[n][p*sh-ph+r*dh][q*sw-pw+s*dw][c]
           const int PQ = a.P * a.Q;
-          const int n = k / PQ, pq = k - n * PQ, p = pq / a.Q, q = pq - p * a.Q;
+          const int n = a.fd_PQ.div(k), pq = k - n * PQ, p = a.fd_Q.div(pq), q = pq - p * a.Q;
           const int iy = p * a.sh - a.ph + b_r * a.dh, ix = q * a.sw - a.pw + b_s * a.dw;
           ok = ok && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
           off = (((int64_t)n * a.H + iy) * a.W + ix) * a.C + b_c;
@@ -260,6 +260,53 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
     }
     if (more) store_tile(stage ^ 1);
     __syncthreads();
+  }
+
+  // ---------------- fused BN statistics of the bf16-rounded output (per column, this tile's rows)
+  if (a.stats) {
+    float cs[4], cq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cs[j] = 0.f;
+      cq[j] = 0.f;
+      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+      const float bias = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          float v = acc[i][j][r] + bias;
+          if (a.relu) v = fmaxf(v, 0.f);
+          v = bf16_to_f32(f32_to_bf16(v));
+          if (m < a.M) {
+            cs[j] += v;
+            cq[j] = fmaf(v, v, cq[j]);
+          }
+        }
+      cs[j] += __shfl_xor(cs[j], 16, 64);
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 16, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+    }
+    float* red = reinterpret_cast<float*>(smem);  // [2 wm][128 cols][2]; LDS is free after the loop
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + lane;
+        red[(wm * 128 + col) * 2 + 0] = cs[j];
+        red[(wm * 128 + col) * 2 + 1] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (t < 128) {
+      const int n = n0 + t;
+      if (n < a.N) {
+        float* slot = a.stats + (size_t)(tm % NSLOT) * 2 * a.N;
+        atomicAdd(&slot[n], red[t * 2] + red[(128 + t) * 2]);
+        atomicAdd(&slot[a.N + n], red[t * 2 + 1] + red[(128 + t) * 2 + 1]);
+      }
+    }
   }
 
   // ---------------- epilogue: lane holds rows (lane>>4)*4 + r, column lane&15 of each 16x16 tile

@@ -54,11 +54,15 @@ tfx::IgemmArgs conv_args(const ConvGeom& g, int64_t st, int64_t pad, int64_t dil
   tfx::IgemmArgs a;
   a.Nb = g.N; a.H = g.H; a.W = g.W; a.C = g.C; a.Ko = g.Ko; a.R = g.R; a.S = g.S; a.P = g.P; a.Q = g.Q;
   a.sh = a.sw = st; a.ph = a.pw = pad; a.dh = a.dw = dil;
+  TORCH_CHECK(st > 0 && (st & (st - 1)) == 0, "conv stride must be a power of two");
+  a.sh_log2 = a.sw_log2 = __builtin_ctzll(st);
+  a.fd_C = tfx::FastDiv(g.C); a.fd_S = tfx::FastDiv(g.S); a.fd_Ko = tfx::FastDiv(g.Ko);
+  a.fd_PQ = tfx::FastDiv(g.P * g.Q); a.fd_Q = tfx::FastDiv(g.Q);
   return a;
 }
 
 // ------------------------------------------------------------------ conv
-Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil) {
+Tensor conv_fwd_impl(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, float* stats) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
   auto g = geom(x.sizes().vec(), w.sizes().vec(), stride, pad, dil);
   auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
@@ -66,8 +70,21 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil) {
   a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
   a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
   a.out_mode = tfx::OUT_BF16;
+  a.stats = stats;
   tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
   return y;
+}
+
+Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil) {
+  return conv_fwd_impl(x, w, stride, pad, dil, nullptr);
+}
+
+// conv forward + the per-channel BN statistics of its output, fused into the GEMM epilogue.
+// Returns (y, slots) where slots is the [NSLOT][2][Ko] partial-sum workspace bn_fwd_train consumes.
+std::tuple<Tensor, Tensor> conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil) {
+  auto slots = at::zeros({tfx::NSLOT * 2 * w.size(0)}, x.options().dtype(at::kFloat));
+  auto y = conv_fwd_impl(x, w, stride, pad, dil, slots.data_ptr<float>());
+  return {y, slots};
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil) {
@@ -168,11 +185,13 @@ void sgemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor out, bool accumulat
 // ------------------------------------------------------------------ batch norm
 std::tuple<Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
                                         optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
-                                        double eps, optional<Tensor> res, bool relu) {
+                                        double eps, optional<Tensor> res, bool relu, optional<Tensor> slots) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   auto opts = x.options().dtype(at::kFloat);
-  auto sums = at::empty({2 * C}, opts);
+  const bool have = slots.has_value() && slots->defined();
+  if (have) TORCH_CHECK(slots->numel() == tfx::NSLOT * 2 * C && slots->scalar_type() == at::kFloat, "stat slots");
+  Tensor sums = have ? *slots : at::empty({tfx::NSLOT * 2 * C}, opts);
   auto save = at::empty({4 * C}, opts);
   auto y = at::empty_like(x);
   const uint16_t* r = nullptr;
@@ -182,7 +201,7 @@ std::tuple<Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma, option
     r = bf(*res);
   }
   auto s = cur_stream();
-  tfx::bn_stats(bf(x), M, C, sums.data_ptr<float>(), s);
+  if (!have) tfx::bn_stats(bf(x), M, C, sums.data_ptr<float>(), s);
   tfx::bn_finalize(sums.data_ptr<float>(), M, C, fp(gamma), fp(beta), eps, momentum, fpm(run_mean), fpm(run_var),
                    save.data_ptr<float>(), s);
   tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y), s);
@@ -208,7 +227,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd grad shape");
-  auto red = at::empty({2 * C}, x.options().dtype(at::kFloat));
+  auto red = at::empty({2 * C + tfx::NSLOT * 2 * C}, x.options().dtype(at::kFloat));
   auto dx = at::empty_like(x);
   Tensor dres;
   const uint16_t* r = nullptr;
@@ -219,7 +238,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
   }
   tfx::bn_backward(bf(g), bf(x), r, save.data_ptr<float>(), M, C, relu, red.data_ptr<float>(), bfm(dx),
                    r ? bfm(dres) : nullptr, cur_stream());
-  return {dx, dres, red};
+  return {dx, dres, red.narrow(0, 0, 2 * C)};
 }
 
 // ------------------------------------------------------------------ loss / metrics / pooling
@@ -317,6 +336,7 @@ void cast_f32_bf16(Tensor x, Tensor y) {
 
 TORCH_LIBRARY(tfx, m) {
   m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("gemm", &gemm);

@@ -38,8 +38,11 @@ class _BN:
             self.var = store.add_state("moving_variance", torch.ones(c))
 
     def __call__(self, x, training, relu=False, residual=None):
+        slots = None
+        if isinstance(x, tuple):  # (conv output, fused BN statistics)
+            x, slots = x
         return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
-                              eps=1e-5, residual=residual, relu=relu)
+                              eps=1e-5, residual=residual, relu=relu, slots=slots)
 
 
 class _Conv:
@@ -47,8 +50,9 @@ class _Conv:
         self.w = store.variable([cout, k, k, cin], HeNormal(), name=name)
         self.stride, self.pad = stride, k // 2
 
-    def __call__(self, x):
-        return ops.conv2d(x, self.w, self.stride, self.pad)
+    def __call__(self, x, training=True):
+        # every conv of the network feeds a BN: let its epilogue produce the BN statistics
+        return ops.conv2d(x, self.w, self.stride, self.pad, stats=training)
 
 
 class Bottleneck:
@@ -69,10 +73,10 @@ class Bottleneck:
                 self.bp = _BN(store, cout, "shortcut_bn")
 
     def __call__(self, x, training):
-        o = self.b1(self.c1(x), training, relu=True)
-        o = self.b2(self.c2(o), training, relu=True)
-        sc = x if self.proj is None else self.bp(self.proj(x), training)
-        return self.b3(self.c3(o), training, relu=True, residual=sc)
+        o = self.b1(self.c1(x, training), training, relu=True)
+        o = self.b2(self.c2(o, training), training, relu=True)
+        sc = x if self.proj is None else self.bp(self.proj(x, training), training)
+        return self.b3(self.c3(o, training), training, relu=True, residual=sc)
 
 
 class Basic:
@@ -90,9 +94,9 @@ class Basic:
                 self.bp = _BN(store, width, "shortcut_bn")
 
     def __call__(self, x, training):
-        o = self.b1(self.c1(x), training, relu=True)
-        sc = x if self.proj is None else self.bp(self.proj(x), training)
-        return self.b2(self.c2(o), training, relu=True, residual=sc)
+        o = self.b1(self.c1(x, training), training, relu=True)
+        sc = x if self.proj is None else self.bp(self.proj(x, training), training)
+        return self.b2(self.c2(o, training), training, relu=True, residual=sc)
 
 
 class ResNetCifar:
@@ -125,7 +129,7 @@ class ResNetCifar:
         self.store.refresh_shadow()
 
     def __call__(self, x: torch.Tensor, training: bool = True) -> torch.Tensor:
-        o = self.stem_bn(self.stem(x), training, relu=True)
+        o = self.stem_bn(self.stem(x, training), training, relu=True)
         for blk in self.blocks:
             o = blk(o, training)
         f = ops.global_avg_pool(o)

@@ -59,16 +59,25 @@ def _conv_ref(x, w, stride=1, pad=0, dil=1):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, w: Variable, stride, pad, dil):
+    def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats):
         ctx.w, ctx.cfg = w, (stride, pad, dil)
         ctx.native = _native.use_native(x)
         ctx.save_for_backward(x)
         if ctx.native:
+            if stats:
+                y, slots = torch.ops.tfx.conv_fwd_stats(x.contiguous(), w.value, stride, pad, dil)
+                ctx.mark_non_differentiable(slots)
+                return y, slots
             return torch.ops.tfx.conv_fwd(x.contiguous(), w.value, stride, pad, dil)
-        return _conv_ref(x, w.value.to(x.dtype), stride, pad, dil)
+        y = _conv_ref(x, w.value.to(x.dtype), stride, pad, dil)
+        if stats:
+            empty = torch.empty(0)
+            ctx.mark_non_differentiable(empty)
+            return y, empty
+        return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, *unused):
         (x,) = ctx.saved_tensors
         w = ctx.w
         stride, pad, dil = ctx.cfg
@@ -79,14 +88,18 @@ class _Conv2d(torch.autograd.Function):
             if w.trainable:
                 torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
                 _grad_ready(w)
-            return dx, None, None, None, None, None
+            return dx, None, None, None, None, None, None
         dx = _ref_param_grads(lambda xx, ww: _conv_ref(xx, ww, stride, pad, dil), x, [w], gy, need_dx)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
-def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int = 1) -> torch.Tensor:
-    """NHWC conv, weight stored [Ko, R, S, C]. GPU: implicit-GEMM MFMA kernels (igemm.hip)."""
-    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil)
+def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int = 1, stats: bool = False):
+    """NHWC conv, weight stored [Ko, R, S, C]. GPU: implicit-GEMM MFMA kernels (igemm.hip).
+
+    ``stats=True`` returns ``(y, bn_slots)``: the per-channel sum / sum-of-squares of ``y`` are
+    produced by the conv's GEMM epilogue, so a following :func:`batch_norm` (``slots=``) skips
+    its own statistics pass over ``y`` (on CPU the slots are empty and BN computes them)."""
+    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, stats)
 
 
 # ====================================================================== batch norm (+res, +relu)
@@ -116,7 +129,7 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
-                training):
+                training, slots):
         ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
         ctx.native = _native.use_native(x)
         ctx.has_res = res is not None
@@ -125,7 +138,8 @@ class _BatchNorm(torch.autograd.Function):
         if ctx.native:
             x = x.contiguous()
             if training:
-                y, save = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu)
+                sl = slots if (slots is not None and slots.numel() > 0) else None
+                y, save = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu, sl)
             else:
                 y, save = torch.ops.tfx.bn_fwd_eval(x, g_t, b_t, rm, rv, eps, res, relu)
             ctx.save_for_backward(x, res, save)
@@ -148,7 +162,7 @@ class _BatchNorm(torch.autograd.Function):
                 gamma.grad.add_(red[C:])
                 beta.grad.add_(red[:C])
                 _grad_ready(gamma, beta)
-            return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None
+            return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None
         x, res = ctx.saved_tensors
         with torch.enable_grad():
             xs = x.detach().requires_grad_(True)
@@ -163,15 +177,19 @@ class _BatchNorm(torch.autograd.Function):
             gamma.grad.add_(grads[0])
             beta.grad.add_(grads[1])
             _grad_ready(gamma, beta)
-        return dx, dres, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
-               momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False):
+               momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False,
+               slots: Optional[torch.Tensor] = None):
     """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
     ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass)."""
     anchor = gamma.store.anchor if gamma is not None else None
-    return _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training)
+    if not training:
+        slots = None
+    return _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
+                            slots)
 
 
 # ====================================================================== dense

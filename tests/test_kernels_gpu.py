@@ -116,7 +116,7 @@ def test_batchnorm_train(gpu, C, res, relu):
     gamma = torch.rand(C, device=gpu) + 0.5
     beta = torch.randn(C, device=gpu)
     rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
-    y, save = torch.ops.tfx.bn_fwd_train(x, gamma, beta, rm, rv, 0.1, 1e-5, r, relu)
+    y, save = torch.ops.tfx.bn_fwd_train(x, gamma, beta, rm, rv, 0.1, 1e-5, r, relu, None)
     xr = x.float().requires_grad_(True)
     gr = gamma.clone().requires_grad_(True)
     br = beta.clone().requires_grad_(True)
@@ -198,3 +198,20 @@ def test_sumsq_and_clip(gpu):
     g = torch.randn(4096, device=gpu)
     s = torch.ops.tfx.sumsq(g)
     assert abs(s.item() - (g.double() ** 2).sum().item()) / s.item() < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(4, 8, 8, 64, 64, 1, 1, 0), (3, 9, 7, 32, 136, 3, 2, 1)])
+def test_conv_fwd_fused_bn_stats(gpu, shape):
+    """BN statistics produced by the conv epilogue == statistics of the conv output."""
+    N, H, W, C, Ko, R, st, pad = shape
+    x = _bf(torch.randn(N, H, W, C, device=gpu))
+    w = _bf(torch.randn(Ko, R, R, C, device=gpu) * 0.1)
+    y, slots = torch.ops.tfx.conv_fwd_stats(x, w, st, pad, 1)
+    s = slots.view(64, 2, Ko).sum(0)
+    yf = y.float().reshape(-1, Ko)
+    assert torch.allclose(s[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+    gamma, beta = torch.ones(Ko, device=gpu), torch.zeros(Ko, device=gpu)
+    y1, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots)
+    y2, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, None)
+    assert _rel(y1, y2) < 1e-3
