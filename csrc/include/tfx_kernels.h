@@ -34,12 +34,14 @@ struct FastDiv {
 };
 
 // ---------------------------------------------------------------- implicit GEMM
-enum { MODE_GEMM = 0, MODE_FWD = 1, MODE_DGRAD = 2, MODE_WGRAD = 3 };
+enum { MODE_GEMM = 0, MODE_FWD = 1, MODE_DGRAD = 2, MODE_WGRAD = 3, MODE_WGRAD_T = 4 };
 enum { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ADD = 2, OUT_F32_ATOMIC = 3 };
 
 struct IgemmArgs {
   const uint16_t* A = nullptr;
   const uint16_t* B = nullptr;
+  int64_t a_bytes = 0, b_bytes = 0;  // extents of A/B (buffer-resource bounds; must be < 2 GiB)
+  int trans_out = 0;                 // store C[m][n] at Cp[n*ldc + m]
   void* Cp = nullptr;
   const float* bias = nullptr;
   int M = 0, N = 0, K = 0;

@@ -1,22 +1,27 @@
 // Implicit-GEMM on bf16 MFMA (v_mfma_f32_16x16x32_bf16) for gfx950.
 //
-// One template covers every matmul-shaped op of the framework:
-//   MODE_GEMM : C[M][N] = sum_k A(m,k) B(k,n), A/B each K-major or MN-major (dense, any ld)
-//   MODE_FWD  : NHWC conv forward     A = im2col(X) gathered on the fly, B = W [Ko][R*S*C]
-//   MODE_DGRAD: NHWC conv data-grad   A = gather(dY) (stride handled by parity test),
-//                                     B = W read MN-major (no weight transpose pass)
-//   MODE_WGRAD: NHWC conv weight-grad A = dY^T (MN-major), B = im2col(X) MN-major, split-K
-//                                     over N*P*Q with f32 atomic accumulation into dW
+// One template covers every matmul-shaped op of the framework.  An operand is described by its
+// KIND (how its tile is gathered from global memory) and is staged either K-major or MN-major:
+//   K-major kinds  (LDS image [rows][64 k], fragments by ds_read_b128):
+//     KM_DENSE     A[m*ld + k]
+//     KM_FWD_X     im2col(X) of an NHWC conv forward, gathered on the fly
+//     KM_DGRAD_DY  gather of dY for the conv data-gradient (stride via parity test)
+//   MN-major kinds (LDS image [64 k][cols], fragments by ds_read_b64_tr_b16, no transpose pass):
+//     MN_DENSE     A[k*ld + m]                (also dY^T for the weight gradient)
+//     MN_DGRAD_W   W[ko][r][s][c] read as B(k=(r,s,ko), n=c)
+//     MN_WGRAD_X   im2col(X) rows j=(n,p,q), columns (r,s,c)
+// Ops: conv FWD = <KM_FWD_X, KM_DENSE>, DGRAD = <KM_DGRAD_DY, MN_DGRAD_W>,
+//      WGRAD = <MN_DENSE(dY), MN_WGRAD_X> or transposed <MN_WGRAD_X, MN_DENSE(dY)> (+trans_out),
+//      GEMM = any K/MN-major dense pair.
 //
-// Block tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 MFMA tiles.
-// LDS images (two stages, 64 KiB):
-//   K-major operand  [128 rows][64 k]  128-B rows, 16-B chunk c of row r at c ^ (r&7)
-//                    -> fragment reads are ds_read_b128, conflict-free (T2 swizzle)
-//   MN-major operand [64 k][128 cols] 256-B rows, chunk c of row r at c ^ f(r),
-//                    f(r) = ((r&3)<<2)|((r>>2)&3) -> fragments via ds_read_b64_tr_b16 (T10),
-//                    conflict-free per 32-lane half.
-// Register-staged double buffer: the next tile's global loads are issued before the MFMAs of
-// the current tile and written to the other LDS stage after them (T14), one barrier per tile.
+// Block = 256 threads = 4 waves (2x2), tile BM x BN x 64 with (BM,BN) in {128x128, 256x64, 128x64}.
+// Loads are UNCONDITIONAL buffer_load_dwordx4 through a buffer resource: padding / out-of-range
+// elements get an offset past num_records and the hardware returns zeros, so hipcc never branches
+// around a load and can count vmcnt statically (cdna_hip_programming.md §5 item 4(c)).
+// Pipeline: two register stage sets (tiles t+1, t+2 in flight) feeding two LDS stages, one
+// barrier per k-tile; each load has ~2 tiles of MFMA work to land.
+// LDS swizzles: K-major 128-B rows chunk c ^ (r&7) (conflict-free ds_read_b128, T2); MN-major rows
+// XOR-swizzled so the transposed reads of a 32-lane half hit 8 distinct 32-B slots (T10).
 // blockIdx is remapped XCD-aware (T1).  Reference: the matmuls of R/distributed/distributed.py:96-98
 // and their TF1 gradients; conv/FC layers of the north-star models (BASELINE.json configs 2-5).
 #include "tfx_common.h"
@@ -26,47 +31,191 @@ namespace tfx {
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;
-constexpr int STAGE_BYTES = 2 * 16384;  // A + B image per stage
+enum { KM_DENSE = 0, KM_FWD_X = 1, KM_DGRAD_DY = 2, MN_DENSE = 10, MN_DGRAD_W = 11, MN_WGRAD_X = 12 };
+constexpr uint32_t BAD = 0x80000000u;  // byte offset beyond any num_records -> loads return 0
+constexpr int NT = 256, BKT = 64;
 
 typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef short s8_t __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s4_t lds_s4;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr bool is_kmaj(int kind) { return kind < 10; }
 
 __device__ __forceinline__ int kmaj_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
-__device__ __forceinline__ int mnmaj_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
-__device__ __forceinline__ int mnmaj_off(int r, int c) { return r * 256 + ((c ^ mnmaj_swz(r)) << 4); }
+// MN-major image, rows of `COLS` bf16; swizzle chosen per row length (see header)
+template <int COLS>
+__device__ __forceinline__ int mn_swz(int r) {
+  if constexpr (COLS >= 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1;
+}
+template <int COLS>
+__device__ __forceinline__ int mn_off(int r, int c) {
+  return r * (COLS * 2) + ((c ^ mn_swz<COLS>(r)) << 4);
+}
 
 __device__ __forceinline__ bf16x8_t lds_read_kmaj(const char* img, int row, int chunk) {
   return *reinterpret_cast<const bf16x8_t*>(img + kmaj_off(row, chunk));
 }
 
-// fragment of the MN-major image: lane needs X[col = cb + (l&15)][k = 32kk + 8(l>>4) + j], j=0..7
-__device__ __forceinline__ bf16x8_t lds_read_mnmaj(const char* img, int cb, int kk, int lane) {
+// fragment of an MN-major image: lane needs X[col = cb + (l&15)][k = 32kk + 8(l>>4) + j], j = 0..7
+template <int COLS>
+__device__ __forceinline__ bf16x8_t lds_read_mn(const char* img, int cb, int kk, int lane) {
   const int g = lane >> 4, ii = lane & 15, q = ii >> 2, p = ii & 3;
   const int chunk = (cb >> 3) + (p >> 1);
   s4_t v[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int kr = 32 * kk + 8 * g + 4 * h + q;
-    const int off = kr * 256 + ((chunk ^ mnmaj_swz(kr)) << 4) + (p & 1) * 8;
+    const int off = mn_off<COLS>(kr, chunk) + (p & 1) * 8;
     v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)((__attribute__((address_space(3))) char*)img + off));
   }
-  typedef short s8_t __attribute__((ext_vector_type(8)));
   s8_t r = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
-__device__ __forceinline__ U4 ldg16(const uint16_t* p, bool ok) {
-  if (ok) return *reinterpret_cast<const U4*>(p);
-  U4 z = {0u, 0u, 0u, 0u};
-  return z;
+// ------------------------------------------------------------------ operand loaders
+// ROWS = tile extent of this operand (BM for A, BN for B).  K-major: thread covers chunk t&7 of rows
+// (t>>3) + 32*i.  MN-major: chunk t % (ROWS/8) of k-rows t / (ROWS/8) + (2048/ROWS)*i.
+template <int KIND, int ROWS>
+struct Loader {
+  static constexpr bool KM = is_kmaj(KIND);
+  static constexpr int NP = ROWS / 32;          // 16-B loads per thread per tile
+  static constexpr int CH = ROWS / 8;           // MN-major chunks per k-row
+  static constexpr int RSTEP = NT / CH;         // MN-major k-row step between passes
+  int c0;        // K-major: element offset of chunk in k (8*kc); MN-major: column of the chunk
+  int r0;        // K-major: first row; MN-major: first k-row
+  bool col_ok;   // MN-major column validity
+  int ctx0[NP], ctx1[NP], ctx2[NP];
+  int cr, cs, cc;  // MN_WGRAD_X column decode
+
+  __device__ __forceinline__ void init(const IgemmArgs& a, int base, int lim, int t) {
+    if constexpr (KM) {
+      c0 = 8 * (t & 7);
+      r0 = t >> 3;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int row = base + r0 + 32 * i;
+        const bool ok = row < lim;
+        if constexpr (KIND == KM_DENSE) {
+          ctx0[i] = ok ? row : -1;
+        } else {
+          const int GY = KIND == KM_FWD_X ? a.P : a.H, GX = KIND == KM_FWD_X ? a.Q : a.W;
+          int n = row / (GY * GX), yx = row - n * GY * GX, y = yx / GX, x = yx - y * GX;
+          ctx0[i] = ok ? n : -1;
+          if constexpr (KIND == KM_FWD_X) {
+            ctx1[i] = y * a.sh - a.ph;
+            ctx2[i] = x * a.sw - a.pw;
+          } else {
+            ctx1[i] = y + a.ph;
+            ctx2[i] = x + a.pw;
+          }
+        }
+      }
+    } else {
+      c0 = base + 8 * (t % CH);
+      r0 = t / CH;
+      col_ok = c0 < lim;
+      if constexpr (KIND == MN_WGRAD_X) {
+        const int rs = col_ok ? c0 / a.C : 0;
+        cc = c0 - rs * a.C;
+        cr = rs / a.S;
+        cs = rs - cr * a.S;
+      }
+    }
+  }
+
+  // byte offsets of this thread's NP 16-B pieces of k-tile k0 (BAD = zero fill)
+  // All predicates are combined with bitwise & and resolved by a select: no branches in the
+  // load path, so hipcc can count vmcnt statically.  kend = end of this block's K range.
+  __device__ __forceinline__ void offsets(const IgemmArgs& a, int ld, int k0, int kend, uint32_t* off) const {
+    if constexpr (KM) {
+      const int k = k0 + c0;
+      const bool kok = k < kend;
+      if constexpr (KIND == KM_DENSE) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const uint32_t o = (uint32_t)(ctx0[i] * ld + k) * 2u;
+          off[i] = (kok & (ctx0[i] >= 0)) ? o : BAD;
+        }
+      } else if constexpr (KIND == KM_FWD_X) {
+        const int rs = a.fd_C.div(k), c = k - rs * a.C, r = a.fd_S.div(rs), s = rs - r * a.S;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const int iy = ctx1[i] + r * a.dh, ix = ctx2[i] + s * a.dw;
+          const bool ok = kok & (ctx0[i] >= 0) & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
+          const uint32_t o = (uint32_t)(((ctx0[i] * a.H + iy) * a.W + ix) * a.C + c) * 2u;
+          off[i] = ok ? o : BAD;
+        }
+      } else {  // KM_DGRAD_DY: k = (r, s, ko)
+        const int rs = a.fd_Ko.div(k), ko = k - rs * a.Ko, r = a.fd_S.div(rs), s = rs - r * a.S;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const int ty = ctx1[i] - r * a.dh, tx = ctx2[i] - s * a.dw;
+          const int p = ty >> a.sh_log2, q = tx >> a.sw_log2;
+          const bool ok = kok & (ctx0[i] >= 0) & (ty >= 0) & (tx >= 0) & ((p << a.sh_log2) == ty) &
+                          ((q << a.sw_log2) == tx) & (p < a.P) & (q < a.Q);
+          const uint32_t o = (uint32_t)(((ctx0[i] * a.P + p) * a.Q + q) * a.Ko + ko) * 2u;
+          off[i] = ok ? o : BAD;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int k = k0 + r0 + RSTEP * i;
+        bool ok = col_ok & (k < kend);
+        int e = 0;
+        if constexpr (KIND == MN_DENSE) {
+          e = k * ld + c0;
+        } else if constexpr (KIND == MN_DGRAD_W) {
+          const int rs = a.fd_Ko.div(k), ko = k - rs * a.Ko, r = a.fd_S.div(rs), s = rs - r * a.S;
+          e = ((ko * a.R + r) * a.S + s) * a.C + c0;
+        } else {  // MN_WGRAD_X
+          const int PQ = a.P * a.Q;
+          const int n = a.fd_PQ.div(k), pq = k - n * PQ, p = a.fd_Q.div(pq), q = pq - p * a.Q;
+          const int iy = p * a.sh - a.ph + cr * a.dh, ix = q * a.sw - a.pw + cs * a.dw;
+          ok = ok & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
+          e = ((n * a.H + iy) * a.W + ix) * a.C + cc;
+        }
+        off[i] = ok ? (uint32_t)e * 2u : BAD;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rsrc, const uint32_t* off, u32x4_t* r) const {
+#pragma unroll
+    for (int i = 0; i < NP; ++i) r[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off[i], 0, 0);
+  }
+
+  __device__ __forceinline__ void store(char* img, const u32x4_t* r) const {
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      int o;
+      if constexpr (KM) o = kmaj_off(r0 + 32 * i, c0 >> 3);
+      else o = mn_off<ROWS>(r0 + RSTEP * i, (c0 & (ROWS - 1)) >> 3);
+      *reinterpret_cast<u32x4_t*>(img + o) = r[i];
+    }
+  }
+};
+
+template <int KIND, int ROWS>
+__device__ __forceinline__ bf16x8_t frag(const char* img, int rowbase, int kk, int lane) {
+  if constexpr (is_kmaj(KIND)) return lds_read_kmaj(img, rowbase + (lane & 15), 4 * kk + (lane >> 4));
+  else return lds_read_mn<ROWS>(img, rowbase, kk, lane);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
+  const int n = bytes > 0x7fffffff ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, n, 0x00020000);
 }
 
 }  // namespace
 
-template <int MODE, bool AK, bool BK>
+template <int AKIND, int BKIND, int BM, int BN>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int A_BYTES = BM * BKT * 2, STAGE = (BM + BN) * BKT * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -80,202 +229,97 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
   const int kt1 = min(nkt, kt0 + a.kps);
   if (kt0 >= kt1) return;
 
-  // ---------------- per-thread loader context (fixed for the whole block)
-  // K-major tiles: chunk c = t&7, rows (t>>3) + 32*i ; MN-major tiles: chunk c = t&15, rows (t>>4) + 16*i
-  const int kc = t & 7, kr = t >> 3;
-  const int mc = t & 15, mr = t >> 4;
-  // A context
-  int64_t a_row[4];  // GEMM K-major: element offset of row; FWD/DGRAD: packed n (or -1)
-  int a_y[4], a_x[4];
-  if constexpr (AK) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + kr + 32 * i;
-      if constexpr (MODE == MODE_GEMM) {
-        a_row[i] = m < a.M ? (int64_t)m * a.lda : -1;
-      } else {
-        // m -> (n, oy, ox) over the GEMM-M spatial grid: FWD uses (P,Q), DGRAD uses (H,W)
-        const int GY = MODE == MODE_FWD ? a.P : a.H, GX = MODE == MODE_FWD ? a.Q : a.W;
-        if (m < a.M) {
-          const int n = m / (GY * GX), yx = m - n * GY * GX, y = yx / GX, x = yx - y * GX;
-          a_row[i] = n;
-          if constexpr (MODE == MODE_FWD) {
-            a_y[i] = y * a.sh - a.ph;
-            a_x[i] = x * a.sw - a.pw;
-          } else {
-            a_y[i] = y + a.ph;
-            a_x[i] = x + a.pw;
-          }
-        } else {
-          a_row[i] = -1;
-          a_y[i] = a_x[i] = 0;
-        }
-      }
-    }
-  }
-  // A MN-major: column chunk fixed
-  const int a_col = m0 + 8 * mc;
-  const bool a_col_ok = a_col < a.M;
-  // B K-major: rows n
-  int64_t b_row[4];
-  if constexpr (BK) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = n0 + kr + 32 * i;
-      b_row[i] = n < a.N ? (int64_t)n * a.ldb : -1;
-    }
-  }
-  // B MN-major: column chunk fixed
-  const int b_col = n0 + 8 * mc;
-  const bool b_col_ok = b_col < a.N;
-  int b_r = 0, b_s = 0, b_c = 0;
-  if constexpr (MODE == MODE_WGRAD) {
-    if (b_col_ok) {
-      const int rs = b_col / a.C;
-      b_c = b_col - rs * a.C;
-      b_r = rs / a.S;
-      b_s = rs - b_r * a.S;
-    }
-  }
+  Loader<AKIND, BM> la;
+  Loader<BKIND, BN> lb;
+  la.init(a, m0, a.M, t);
+  lb.init(a, n0, a.N, t);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a.a_bytes), rb = make_rsrc(a.B, a.b_bytes);
 
-  U4 ra[4], rb[4];
+  u32x4_t sa0[Loader<AKIND, BM>::NP], sb0[Loader<BKIND, BN>::NP];
+  u32x4_t sa1[Loader<AKIND, BM>::NP], sb1[Loader<BKIND, BN>::NP];
+  uint32_t oa[Loader<AKIND, BM>::NP], ob[Loader<BKIND, BN>::NP];
 
-  auto load_tile = [&](int kt) {
+  // tiles at or past kt1 are zero-filled (every offset BAD), so an odd tile count can run the
+  // even/odd loop to completion: the extra step multiplies zeros.
+  const int kend = min(a.K, kt1 * BKT);
+  auto issue = [&](int kt, u32x4_t* sa, u32x4_t* sb) {
     const int k0 = kt * BKT;
-    // ---------------- A
-    if constexpr (AK) {
-      const int k = k0 + 8 * kc;
-      const bool kok = k < a.K;
-      if constexpr (MODE == MODE_GEMM) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ra[i] = ldg16(a.A + a_row[i] + k, kok && a_row[i] >= 0);
-      } else if constexpr (MODE == MODE_FWD) {
-        const int rs = a.fd_C.div(k), cc = k - rs * a.C, r = a.fd_S.div(rs), s = rs - r * a.S;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int iy = a_y[i] + r * a.dh, ix = a_x[i] + s * a.dw;
-          const bool ok = kok && a_row[i] >= 0 && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-          const int64_t off = ok ? (((int64_t)a_row[i] * a.H + iy) * a.W + ix) * a.C + cc : 0;
-          ra[i] = ldg16(a.A + off, ok);
-        }
-      } else {  // DGRAD: A = dY[n][p][q][ko], k = (r,s,ko)
-        const int rs = a.fd_Ko.div(k), ko = k - rs * a.Ko, r = a.fd_S.div(rs), s = rs - r * a.S;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ty = a_y[i] - r * a.dh, tx = a_x[i] - s * a.dw;
-          bool ok = kok && a_row[i] >= 0 && ty >= 0 && tx >= 0;
-          int p = 0, q = 0;
-          if (ok) {  // strides are powers of two (checked on the host)
-            p = ty >> a.sh_log2;
-            q = tx >> a.sw_log2;
-            ok = ((p << a.sh_log2) == ty) && ((q << a.sw_log2) == tx) && p < a.P && q < a.Q;
-          }
-          const int64_t off = ok ? (((int64_t)a_row[i] * a.P + p) * a.Q + q) * a.Ko + ko : 0;
-          ra[i] = ldg16(a.A + off, ok);
-        }
-      }
-    } else {
-      // MN-major A: rows are k
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = k0 + mr + 16 * i;
-        const bool ok = a_col_ok && k < a.K;
-        // GEMM: A[k*lda + m]; WGRAD: dY[j*Ko + ko] (lda = Ko)
-        ra[i] = ldg16(a.A + (ok ? (int64_t)k * a.lda + a_col : 0), ok);
-      }
-    }
-    // ---------------- B
-    if constexpr (BK) {
-      const int k = k0 + 8 * kc;
-      const bool kok = k < a.K;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) rb[i] = ldg16(a.B + b_row[i] + k, kok && b_row[i] >= 0);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = k0 + mr + 16 * i;
-        bool ok = b_col_ok && k < a.K;
-        int64_t off = 0;
-        if constexpr (MODE == MODE_GEMM) {
-          off = (int64_t)k * a.ldb + b_col;
-        } else if constexpr (MODE == MODE_DGRAD) {
-          // B(k=(r,s,ko), c) = W[ko][r][s][c]
-          const int rs = a.fd_Ko.div(k), ko = k - rs * a.Ko, r = a.fd_S.div(rs), s = rs - r * a.S;
-          off = (((int64_t)ko * a.R + r) * a.S + s) * a.C + b_col;
-        } else if constexpr (MODE == MODE_WGRAD) {
-          // B(k=j=(n,p,q), col=(r,s,c)) = X[n][p*sh-ph+r*dh][q*sw-pw+s*dw][c]
-          const int PQ = a.P * a.Q;
-          const int n = a.fd_PQ.div(k), pq = k - n * PQ, p = a.fd_Q.div(pq), q = pq - p * a.Q;
-          const int iy = p * a.sh - a.ph + b_r * a.dh, ix = q * a.sw - a.pw + b_s * a.dw;
-          ok = ok && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-          off = (((int64_t)n * a.H + iy) * a.W + ix) * a.C + b_c;
-        }
-        rb[i] = ldg16(a.B + (ok ? off : 0), ok);
-      }
-    }
+    la.offsets(a, a.lda, k0, kend, oa);
+    lb.offsets(a, a.ldb, k0, kend, ob);
+    la.load(ra, oa, sa);
+    lb.load(rb, ob, sb);
+  };
+  auto stage_store = [&](int st, const u32x4_t* sa, const u32x4_t* sb) {
+    char* img = smem + st * STAGE;
+    la.store(img, sa);
+    lb.store(img + A_BYTES, sb);
   };
 
-  auto store_tile = [&](int stage) {
-    char* ia = smem + stage * STAGE_BYTES;
-    char* ib = ia + 16384;
+  f32x4_t acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if constexpr (AK) *reinterpret_cast<U4*>(ia + kmaj_off(kr + 32 * i, kc)) = ra[i];
-      else *reinterpret_cast<U4*>(ia + mnmaj_off(mr + 16 * i, mc)) = ra[i];
-      if constexpr (BK) *reinterpret_cast<U4*>(ib + kmaj_off(kr + 32 * i, kc)) = rb[i];
-      else *reinterpret_cast<U4*>(ib + mnmaj_off(mr + 16 * i, mc)) = rb[i];
-    }
-  };
-
-  f32x4_t acc[4][4];
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  load_tile(kt0);
-  store_tile(0);
-  __syncthreads();
-
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int stage = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) load_tile(kt + 1);
-    const char* ia = smem + stage * STAGE_BYTES;
-    const char* ib = ia + 16384;
+  auto compute = [&](int st) {
+    const char* ia = smem + st * STAGE;
+    const char* ib = ia + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8_t fa[4], fb[4];
+      bf16x8_t fa[TM], fb[TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (AK) fa[i] = lds_read_kmaj(ia, wm * 64 + i * 16 + (lane & 15), 4 * kk + (lane >> 4));
-        else fa[i] = lds_read_mnmaj(ia, wm * 64 + i * 16, kk, lane);
-        if constexpr (BK) fb[i] = lds_read_kmaj(ib, wn * 64 + i * 16 + (lane & 15), 4 * kk + (lane >> 4));
-        else fb[i] = lds_read_mnmaj(ib, wn * 64 + i * 16, kk, lane);
-      }
+      for (int i = 0; i < TM; ++i) fa[i] = frag<AKIND, BM>(ia, wm * WM + i * 16, kk, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < TN; ++j) fb[j] = frag<BKIND, BN>(ib, wn * WN + j * 16, kk, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store_tile(stage ^ 1);
-    __syncthreads();
+  };
+
+  // prologue: tile kt0 -> stage 0, tile kt0+1 in flight in set 1
+  issue(kt0, sa0, sb0);
+  issue(kt0 + 1, sa1, sb1);
+  stage_store(0, sa0, sb0);
+  __syncthreads();
+  if (kt1 - kt0 == 1) {
+    compute(0);
+  } else {
+    // single exit at the bottom: every path into the loop header has set 1 in flight and set 0
+    // free, so the vmcnt bookkeeping is identical on both edges (no conservative vmcnt(0)).
+    // sched_barrier(0) pins the order issue -> MFMAs -> LDS write: without it hipcc hoists the
+    // stage write (and its vmcnt wait on the previous tile's loads) above the MFMAs.
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      issue(kt + 2, sa0, sb0);  // even: stage 0 holds kt, set 1 holds kt+1
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0);
+      __builtin_amdgcn_sched_barrier(0);
+      stage_store(1, sa1, sb1);
+      __syncthreads();
+      issue(kt + 3, sa1, sb1);  // odd: stage 1 holds kt+1, set 0 holds kt+2
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1);
+      __builtin_amdgcn_sched_barrier(0);
+      stage_store(0, sa0, sb0);
+      __syncthreads();
+    }
   }
 
   // ---------------- fused BN statistics of the bf16-rounded output (per column, this tile's rows)
   if (a.stats) {
-    float cs[4], cq[4];
+    float cs[TN], cq[TN];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TN; ++j) {
       cs[j] = 0.f;
       cq[j] = 0.f;
-      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+      const int n = n0 + wn * WN + j * 16 + (lane & 15);
       const float bias = (a.bias && n < a.N) ? a.bias[n] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
           float v = acc[i][j][r] + bias;
           if (a.relu) v = fmaxf(v, 0.f);
           v = bf16_to_f32(f32_to_bf16(v));
@@ -289,22 +333,22 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
       cq[j] += __shfl_xor(cq[j], 16, 64);
       cq[j] += __shfl_xor(cq[j], 32, 64);
     }
-    float* red = reinterpret_cast<float*>(smem);  // [2 wm][128 cols][2]; LDS is free after the loop
+    float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN cols][2]; LDS is free after the loop
     if (lane < 16) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wn * 64 + j * 16 + lane;
-        red[(wm * 128 + col) * 2 + 0] = cs[j];
-        red[(wm * 128 + col) * 2 + 1] = cq[j];
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + lane;
+        red[(wm * BN + col) * 2 + 0] = cs[j];
+        red[(wm * BN + col) * 2 + 1] = cq[j];
       }
     }
     __syncthreads();
-    if (t < 128) {
+    if (t < BN) {
       const int n = n0 + t;
       if (n < a.N) {
         float* slot = a.stats + (size_t)(tm % NSLOT) * 2 * a.N;
-        atomicAdd(&slot[n], red[t * 2] + red[(128 + t) * 2]);
-        atomicAdd(&slot[a.N + n], red[t * 2 + 1] + red[(128 + t) * 2 + 1]);
+        atomicAdd(&slot[n], red[t * 2] + red[(BN + t) * 2]);
+        atomicAdd(&slot[a.N + n], red[t * 2 + 1] + red[(BN + t) * 2 + 1]);
       }
     }
   }
@@ -312,19 +356,19 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
   // ---------------- epilogue: lane holds rows (lane>>4)*4 + r, column lane&15 of each 16x16 tile
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + col_l;
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + col_l;
     if (n >= a.N) continue;
     const float bias = a.bias ? a.bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + row_l + r;
+        const int m = m0 + wm * WM + i * 16 + row_l + r;
         if (m >= a.M) continue;
         float v = acc[i][j][r] + bias;
         if (a.relu) v = fmaxf(v, 0.f);
-        const int64_t o = (int64_t)m * a.ldc + n;
+        const int64_t o = a.trans_out ? (int64_t)n * a.ldc + m : (int64_t)m * a.ldc + n;
         if (a.out_mode == OUT_BF16) reinterpret_cast<uint16_t*>(a.Cp)[o] = f32_to_bf16(v);
         else if (a.out_mode == OUT_F32) reinterpret_cast<float*>(a.Cp)[o] = v;
         else if (a.out_mode == OUT_F32_ADD) reinterpret_cast<float*>(a.Cp)[o] += v;
@@ -335,35 +379,61 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
 }
 
 // ============================================================ host launcher
-static int pick_splits(int tiles, int nkt, int want_blocks) {
+namespace {
+
+int pick_splits(int tiles, int nkt, int want_blocks) {
   if (tiles >= want_blocks) return 1;
   int s = (want_blocks + tiles - 1) / tiles;
   const int max_s = std::max(1, nkt / 4);  // keep >= 4 k-tiles per split
   return std::max(1, std::min(s, max_s));
 }
 
-void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
+template <int AK, int BK, int BM, int BN>
+void launch_t(IgemmArgs& a, hipStream_t s) {
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + BN - 1) / BN;
   const int nkt = (a.K + BKT - 1) / BKT;
   const int tiles = a.tiles_m * a.tiles_n;
   int splits = 1;
-  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, 1024);
+  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, 512);
   a.kps = (nkt + splits - 1) / splits;
+  if (splits > 1) a.kps += a.kps & 1;  // even k-tiles per split: no zero step in the loop
   splits = (nkt + a.kps - 1) / a.kps;
-  if (a.out_mode == OUT_F32_ATOMIC && a.zero_out)
-    TFX_HIP_CHECK(hipMemsetAsync(a.Cp, 0, sizeof(float) * (size_t)a.M * a.ldc, s));
   const int grid = tiles * splits;
   if (grid == 0) return;
+  igemm_kernel<AK, BK, BM, BN><<<grid, NT, 0, s>>>(a);
+}
+
+// tile choice: narrow N -> 256x64 (if M is large) or 128x64; otherwise 128x128
+template <int AK, int BK, bool ALLOW256 = true>
+void launch_shape(IgemmArgs& a, hipStream_t s) {
+  if (a.N <= 64) {
+    if constexpr (ALLOW256) {
+      if (a.M >= 256 * 256) return launch_t<AK, BK, 256, 64>(a, s);
+    }
+    launch_t<AK, BK, 128, 64>(a, s);
+  } else {
+    launch_t<AK, BK, 128, 128>(a, s);
+  }
+}
+
+}  // namespace
+
+void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
+  if (a.out_mode == OUT_F32_ATOMIC && a.zero_out) {
+    const size_t rows = a.trans_out ? a.N : a.M;
+    TFX_HIP_CHECK(hipMemsetAsync(a.Cp, 0, sizeof(float) * rows * a.ldc, s));
+  }
   switch (mode) {
-    case MODE_FWD: igemm_kernel<MODE_FWD, true, true><<<grid, NT, 0, s>>>(a); break;
-    case MODE_DGRAD: igemm_kernel<MODE_DGRAD, true, false><<<grid, NT, 0, s>>>(a); break;
-    case MODE_WGRAD: igemm_kernel<MODE_WGRAD, false, false><<<grid, NT, 0, s>>>(a); break;
+    case MODE_FWD: launch_shape<KM_FWD_X, KM_DENSE>(a, s); break;
+    case MODE_DGRAD: launch_shape<KM_DGRAD_DY, MN_DGRAD_W>(a, s); break;
+    case MODE_WGRAD: launch_shape<MN_DENSE, MN_WGRAD_X, false>(a, s); break;
+    case MODE_WGRAD_T: launch_shape<MN_WGRAD_X, MN_DENSE, false>(a, s); break;
     default:
-      if (a.a_kmajor && a.b_kmajor) igemm_kernel<MODE_GEMM, true, true><<<grid, NT, 0, s>>>(a);
-      else if (a.a_kmajor) igemm_kernel<MODE_GEMM, true, false><<<grid, NT, 0, s>>>(a);
-      else if (a.b_kmajor) igemm_kernel<MODE_GEMM, false, true><<<grid, NT, 0, s>>>(a);
-      else igemm_kernel<MODE_GEMM, false, false><<<grid, NT, 0, s>>>(a);
+      if (a.a_kmajor && a.b_kmajor) launch_t<KM_DENSE, KM_DENSE, 128, 128>(a, s);
+      else if (a.a_kmajor) launch_t<KM_DENSE, MN_DENSE, 128, 128>(a, s);
+      else if (a.b_kmajor) launch_t<MN_DENSE, KM_DENSE, 128, 128>(a, s);
+      else launch_t<MN_DENSE, MN_DENSE, 128, 128>(a, s);
   }
 }
 

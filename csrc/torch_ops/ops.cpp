@@ -47,6 +47,8 @@ ConvGeom geom(const std::vector<int64_t>& xs, const std::vector<int64_t>& ws, in
   g.P = (g.H + 2 * pad - dil * (g.R - 1) - 1) / st + 1;
   g.Q = (g.W + 2 * pad - dil * (g.S - 1) - 1) / st + 1;
   TORCH_CHECK(g.P > 0 && g.Q > 0, "conv output is empty");
+  TORCH_CHECK(g.N * std::max(g.H * g.W * g.C, g.P * g.Q * g.Ko) * 2 < (int64_t(1) << 31),
+              "conv tensors must be < 2 GiB (32-bit buffer offsets)");
   return g;
 }
 
@@ -68,6 +70,7 @@ Tensor conv_fwd_impl(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t di
   auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
   auto a = conv_args(g, stride, pad, dil);
   a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
+  a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
   a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
   a.out_mode = tfx::OUT_BF16;
   a.stats = stats;
@@ -94,6 +97,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
   auto dx = at::empty({g.N, g.H, g.W, g.C}, dy.options());
   auto a = conv_args(g, stride, pad, dil);
   a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
+  a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
   a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
   a.out_mode = tfx::OUT_BF16;
   tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
@@ -106,11 +110,22 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int
   auto g = geom(x.sizes().vec(), dw.sizes().vec(), stride, pad, dil);
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
   auto a = conv_args(g, stride, pad, dil);
-  a.A = bf(dy); a.B = bf(x); a.Cp = dw.data_ptr();
-  a.M = g.Ko; a.N = g.R * g.S * g.C; a.K = g.N * g.P * g.Q; a.lda = g.Ko; a.ldc = a.N;
+  const int64_t RSC = g.R * g.S * g.C;
+  a.K = g.N * g.P * g.Q;
   a.out_mode = tfx::OUT_F32_ATOMIC;
   a.zero_out = accumulate ? 0 : 1;
-  tfx::igemm_launch(a, tfx::MODE_WGRAD, cur_stream());
+  a.Cp = dw.data_ptr();
+  a.ldc = RSC;
+  if (g.Ko < 128 && RSC > g.Ko) {
+    // narrow Ko: compute dW^T = Xcol^T dY (M = R*S*C on the 256-row tile side), store transposed
+    a.A = bf(x); a.B = bf(dy); a.a_bytes = x.nbytes(); a.b_bytes = dy.nbytes();
+    a.M = RSC; a.N = g.Ko; a.ldb = g.Ko; a.trans_out = 1;
+    tfx::igemm_launch(a, tfx::MODE_WGRAD_T, cur_stream());
+  } else {
+    a.A = bf(dy); a.B = bf(x); a.a_bytes = dy.nbytes(); a.b_bytes = x.nbytes();
+    a.M = g.Ko; a.N = RSC; a.lda = g.Ko;
+    tfx::igemm_launch(a, tfx::MODE_WGRAD, cur_stream());
+  }
 }
 
 // ------------------------------------------------------------------ dense bf16 GEMM
@@ -127,6 +142,9 @@ void gemm_setup(tfx::IgemmArgs& g, const Tensor& a, const Tensor& b, bool ta, bo
   check_aligned16(a, "a");
   check_aligned16(b, "b");
   g.A = bf(a); g.B = bf(b);
+  // buffer-resource extents: from the view's start to the end of its storage
+  g.a_bytes = (a.storage().nbytes() - a.storage_offset() * a.element_size());
+  g.b_bytes = (b.storage().nbytes() - b.storage_offset() * b.element_size());
   g.M = M; g.N = N; g.K = K;
   g.lda = a.stride(0); g.ldb = b.stride(0);
   g.a_kmajor = ta ? 0 : 1;

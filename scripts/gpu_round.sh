@@ -23,6 +23,9 @@ for s in $STEPS; do
     torch)
       timeout -k 10 400 python bench.py --impl torch --steps 20 --warmup 5 > gpurun_out/bench_torch.log 2>&1
       rc=$?; echo "torch rc=$rc"; tail -3 gpurun_out/bench_torch.log; [ $rc -eq 0 ] || exit $rc ;;
+    convbench)
+      timeout -k 10 400 python scripts/conv_bench.py > gpurun_out/conv_bench.log 2>&1
+      rc=$?; echo "convbench rc=$rc"; tail -3 gpurun_out/conv_bench.log; [ $rc -eq 0 ] || exit $rc ;;
     prof)
       export TMPDIR=/tmp
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 2 > gpurun_out/prof.log 2>&1
