@@ -140,6 +140,7 @@ struct Writer {
   std::deque<std::string> q;
   std::thread th;
   bool stop = false;
+  bool busy = false;  // a popped record is being written (guarded by mu)
   double flush_secs = 2.0;
   std::atomic<uint64_t> written{0};
 
@@ -151,10 +152,12 @@ struct Writer {
       while (!q.empty()) {
         std::string rec = std::move(q.front());
         q.pop_front();
+        busy = true;
         lk.unlock();
         fwrite(rec.data(), 1, rec.size(), f);
         written.fetch_add(1);
         lk.lock();
+        busy = false;
       }
       auto now = std::chrono::steady_clock::now();
       if (stop || std::chrono::duration<double>(now - last).count() >= flush_secs) {
@@ -235,7 +238,7 @@ void tfx_events_flush(void* h) {
   for (int i = 0; i < 5000; ++i) {
     {
       std::lock_guard<std::mutex> g(w->mu);
-      if (w->q.empty()) break;
+      if (w->q.empty() && !w->busy) break;
     }
     w->cv.notify_one();
     std::this_thread::sleep_for(std::chrono::milliseconds(1));
@@ -269,3 +272,5 @@ int tfx_tfrecord_append(const char* path, const char* data, size_t n) {
 }
 
 }  // extern "C"
+
+extern "C" int tfx_rt_version() { return 2; }

@@ -1,1 +1,157 @@
-"""ckpt package."""
+"""Checkpoints with TF1's on-disk LAYOUT and our own container format.
+
+``Saver.save(store, "<dir>/model.ckpt", global_step=N)`` writes::
+
+    <dir>/checkpoint                          text: model_checkpoint_path / all_model_checkpoint_paths
+    <dir>/model.ckpt-N.index                  JSON index: name -> dtype, shape, crc32c (format tfx-ckpt-v1)
+    <dir>/model.ckpt-N.data-00000-of-00001    safetensors container with every tensor (f32)
+    <dir>/model.ckpt-N.meta                   JSON "meta graph": variable list + user metadata
+
+Variables keep their TF names (``global_step``, ``weights/Variable``, ``biases/Variable_1``, ...).
+The data file is safetensors (loaded with the safe loader, nothing executable); CRC32C of every
+tensor is verified on restore.  ``export_saved_model`` writes the SavedModel-shaped directory
+``saved_model.pb`` + ``variables/variables.{index,data-00000-of-00001}``; ``saved_model.pb`` here is
+our container (magic ``TFXSM001`` + JSON signature/meta), not a TF protobuf.
+The reference's Supervisor builds a default Saver but never saves without ``logdir``
+(R/distributed/distributed.py:129-131); ``--logdir`` turns it on in this framework.
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import time
+from typing import Dict, List, Optional
+
+import torch
+from safetensors.torch import load_file, save_file
+
+from .. import runtime
+
+FORMAT = "tfx-ckpt-v1"
+SM_MAGIC = b"TFXSM001"
+
+
+def _crc(t: torch.Tensor) -> int:
+    return runtime.crc32c(t.detach().cpu().contiguous().numpy().tobytes())
+
+
+def _write_tensors(prefix: str, tensors: Dict[str, torch.Tensor], meta: Optional[dict]) -> None:
+    cpu = {k: v.detach().cpu().contiguous() for k, v in tensors.items()}
+    save_file(cpu, prefix + ".data-00000-of-00001", metadata={"format": FORMAT})
+    index = {"format": FORMAT, "num_shards": 1,
+             "tensors": {k: {"dtype": str(v.dtype).replace("torch.", ""), "shape": list(v.shape), "crc32c": _crc(v)}
+                         for k, v in cpu.items()}}
+    with open(prefix + ".index", "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+    with open(prefix + ".meta", "w") as f:
+        json.dump({"format": FORMAT, "variables": sorted(cpu), "meta": meta or {}, "time": time.time()}, f, indent=1)
+
+
+def read_checkpoint(prefix: str, verify: bool = True) -> Dict[str, torch.Tensor]:
+    with open(prefix + ".index") as f:
+        index = json.load(f)
+    if index.get("format") != FORMAT:
+        raise ValueError(f"{prefix}.index: unknown checkpoint format {index.get('format')!r}")
+    tensors = load_file(prefix + ".data-00000-of-00001")
+    if verify:
+        for k, info in index["tensors"].items():
+            if _crc(tensors[k]) != info["crc32c"]:
+                raise ValueError(f"checkpoint tensor {k!r} fails its CRC32C check")
+    return tensors
+
+
+class Saver:
+    def __init__(self, max_to_keep: int = 5):
+        self.max_to_keep = max_to_keep
+        self._kept: List[str] = []
+
+    def save(self, store, save_path: str, global_step: Optional[int] = None, extra: Optional[Dict] = None,
+             meta: Optional[dict] = None) -> str:
+        prefix = f"{save_path}-{int(global_step)}" if global_step is not None else save_path
+        d = os.path.dirname(os.path.abspath(prefix))
+        os.makedirs(d, exist_ok=True)
+        tensors = dict(store.named_values())
+        if global_step is not None:
+            tensors.setdefault("global_step", torch.tensor(float(global_step)))
+        for k, v in (extra or {}).items():
+            tensors[k] = torch.as_tensor(v)
+        _write_tensors(prefix, tensors, meta)
+        self._kept = [p for p in _read_state(d) if p != prefix] + [prefix]
+        while self.max_to_keep and len(self._kept) > self.max_to_keep:
+            old = self._kept.pop(0)
+            for suf in (".index", ".data-00000-of-00001", ".meta"):
+                try:
+                    os.remove(old + suf)
+                except FileNotFoundError:
+                    pass
+        _write_state(d, prefix, self._kept)
+        return prefix
+
+    def restore(self, store, prefix: str, strict: bool = True) -> Dict[str, torch.Tensor]:
+        tensors = read_checkpoint(prefix)
+        store.load_named({k: v for k, v in tensors.items() if k != "global_step"}, strict=strict)
+        return tensors
+
+
+def _state_path(d: str) -> str:
+    return os.path.join(d, "checkpoint")
+
+
+def _read_state(d: str) -> List[str]:
+    p = _state_path(d)
+    if not os.path.exists(p):
+        return []
+    out = []
+    for line in open(p):
+        m = re.match(r'\s*all_model_checkpoint_paths:\s*"(.*)"', line)
+        if m:
+            q = m.group(1)
+            out.append(q if os.path.isabs(q) else os.path.join(d, q))
+    return out
+
+
+def _write_state(d: str, latest: str, all_paths: List[str]) -> None:
+    rel = lambda p: os.path.relpath(p, d)  # noqa: E731
+    lines = [f'model_checkpoint_path: "{rel(latest)}"'] + [f'all_model_checkpoint_paths: "{rel(p)}"' for p in all_paths]
+    tmp = _state_path(d) + ".tmp"
+    with open(tmp, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    os.replace(tmp, _state_path(d))
+
+
+def latest_checkpoint(checkpoint_dir: str) -> Optional[str]:
+    p = _state_path(checkpoint_dir)
+    if not os.path.exists(p):
+        return None
+    for line in open(p):
+        m = re.match(r'\s*model_checkpoint_path:\s*"(.*)"', line)
+        if m:
+            q = m.group(1)
+            q = q if os.path.isabs(q) else os.path.join(checkpoint_dir, q)
+            return q if os.path.exists(q + ".index") else None
+    return None
+
+
+def export_saved_model(store, export_dir: str, signature: Optional[dict] = None) -> str:
+    os.makedirs(os.path.join(export_dir, "variables"), exist_ok=True)
+    _write_tensors(os.path.join(export_dir, "variables", "variables"), store.named_values(), {"saved_model": True})
+    body = json.dumps({"format": FORMAT, "signature": signature or {},
+                       "variables": [{"name": v.name, "shape": list(v.shape)} for v in store.vars]}).encode()
+    with open(os.path.join(export_dir, "saved_model.pb"), "wb") as f:
+        f.write(SM_MAGIC + body)
+    return export_dir
+
+
+def load_saved_model(store, export_dir: str) -> dict:
+    with open(os.path.join(export_dir, "saved_model.pb"), "rb") as f:
+        raw = f.read()
+    if not raw.startswith(SM_MAGIC):
+        raise ValueError("not a tensorflow_examples_amd SavedModel")
+    meta = json.loads(raw[len(SM_MAGIC):])
+    tensors = read_checkpoint(os.path.join(export_dir, "variables", "variables"))
+    store.load_named(tensors, strict=False)
+    return meta
+
+
+__all__ = ["Saver", "latest_checkpoint", "read_checkpoint", "export_saved_model", "load_saved_model"]

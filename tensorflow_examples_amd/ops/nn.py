@@ -356,3 +356,65 @@ def accuracy(logits, labels) -> torch.Tensor:
         return torch.ops.tfx.accuracy_count(logits.contiguous(), idx, dense)[0] / logits.shape[0]
     tgt = labels if labels.dtype == torch.long else labels.argmax(1)
     return (logits.argmax(1) == tgt).float().mean()
+
+
+# ====================================================================== f32 dense (parity models)
+_ACT = {None: 0, "none": 0, "relu": 1, "sigmoid": 2}
+
+
+def _dense_ref(x, w, b=None, act=0):
+    y = x @ w
+    if b is not None:
+        y = y + b
+    if act == 1:
+        y = torch.relu(y)
+    elif act == 2:
+        y = torch.sigmoid(y)
+    return y
+
+
+class _DenseF32(torch.autograd.Function):
+    """y = act(x @ W + b), W stored [in, out] like tf.matmul(x, W) (R/distributed/distributed.py:96-98).
+    GPU: exact-f32 MFMA GEMM (sgemm.hip) with the bias + activation fused into its epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, w: Variable, b: Optional[Variable], act: int):
+        ctx.w, ctx.b, ctx.act = w, b, act
+        ctx.native = _native.use_native(x)
+        if ctx.native:
+            y = torch.ops.tfx.sgemm(x.contiguous(), w.master, False, False, b.master if b is not None else None, act)
+        else:
+            y = _dense_ref(x, w.master, b.master if b is not None else None, act)
+        ctx.save_for_backward(x, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y = ctx.saved_tensors
+        w, b, act = ctx.w, ctx.b, ctx.act
+        g = gy
+        if act == 1:
+            g = g * (y > 0)
+        elif act == 2:
+            g = g * y * (1 - y)  # TF1 SigmoidGrad: dy * y * (1 - y)
+        g = g.contiguous()
+        dx = None
+        if ctx.native:
+            if ctx.needs_input_grad[0]:
+                dx = torch.ops.tfx.sgemm(g, w.master, False, True, None, 0)
+            if w.trainable:
+                torch.ops.tfx.sgemm_into(x.contiguous(), g, True, False, w.grad, True)
+        else:
+            if ctx.needs_input_grad[0]:
+                dx = g @ w.master.t()
+            if w.trainable:
+                w.grad.add_(x.t() @ g)
+        if b is not None and b.trainable:
+            b.grad.add_(g.sum(0))
+        _grad_ready(w, b)
+        return dx, None, None, None, None
+
+
+def dense(x, w: Variable, b: Optional[Variable] = None, activation=None):
+    """f32 fully-connected layer: ``activation(x @ W + b)``, W is [in, out]."""
+    return _DenseF32.apply(x, w.store.anchor, w, b, _ACT[activation])

@@ -1,0 +1,99 @@
+"""The example scripts, run as subprocesses exactly as a user would (reference recipe)."""
+import glob
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_simple_golden_output():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "simple", "simple.py")], capture_output=True,
+                         text=True, timeout=120, check=True).stdout
+    # SURVEY §6.2 golden values (float32 semantics of R/simple/simple.py, 1005 steps)
+    assert out.strip() == "W: [-0.9999971] b: [0.9999914] loss 4.9244164e-11"
+
+
+def _ports(n):
+    s = [socket.socket() for _ in range(n)]
+    for x in s:
+        x.bind(("127.0.0.1", 0))
+    p = [x.getsockname()[1] for x in s]
+    for x in s:
+        x.close()
+    return p
+
+
+def _args(ports, logs, extra=()):
+    ps, w1, w2 = ports
+    return [f"--ps_hosts=127.0.0.1:{ps}", f"--worker_hosts=127.0.0.1:{w1},127.0.0.1:{w2}", "--device=cpu",
+            f"--logs_path={logs}", "--recovery_wait_secs=0.2", *extra]
+
+
+def test_distributed_ps_two_workers(tmp_path):
+    """1 ps + 2 workers on localhost ports (R/distributed/distributed.py:7-13)."""
+    script = os.path.join(ROOT, "distributed", "distributed.py")
+    args = _args(_ports(3), str(tmp_path / "logs"),
+                 ["--training_epochs=1", "--max_batches_per_epoch=120", "--ps_exit_after_workers"])
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    ps = subprocess.Popen([sys.executable, script, *args, "--job_name=ps", "--task_index=0"], env=env)
+    time.sleep(0.3)
+    w1 = subprocess.Popen([sys.executable, script, *args, "--job_name=worker", "--task_index=1"],
+                          stdout=subprocess.PIPE, text=True, env=env)
+    w0 = subprocess.Popen([sys.executable, script, *args, "--job_name=worker", "--task_index=0"],
+                          stdout=subprocess.PIPE, text=True, env=env)
+    try:
+        o0, _ = w0.communicate(timeout=240)
+        o1, _ = w1.communicate(timeout=240)
+        assert w0.returncode == 0 and w1.returncode == 0
+        assert ps.wait(timeout=30) == 0  # --ps_exit_after_workers
+    finally:
+        for p in (ps, w0, w1):
+            if p.poll() is None:
+                p.kill()
+    for out in (o0, o1):
+        lines = out.strip().splitlines()
+        assert lines[0] == "Variables initialized ..."
+        prog = [l for l in lines if l.startswith("Step so far:")]
+        assert len(prog) == 2  # batches 100 and 120 (last batch of the epoch)
+        assert " Epoch so far:  1,  Batch used: 100 of 120,  Cost now: " in prog[0]
+        assert lines[-4].startswith("Acc: ") and lines[-3].startswith("Time Taken: ")
+        assert lines[-2].startswith("Final Computed Cost: ") and lines[-1] == "done with training"
+    # the global step counts both workers' updates: the last worker to finish saw ~240
+    last = max(int(l.split(":")[1].split(",")[0]) for o in (o0, o1) for l in o.splitlines() if l.startswith("Step"))
+    assert last == 240
+    ev = glob.glob(str(tmp_path / "logs" / "events.out.tfevents.*"))
+    assert len(ev) == 2
+
+
+def test_worker_fails_when_ps_dies(tmp_path):
+    script = os.path.join(ROOT, "distributed", "distributed.py")
+    args = _args(_ports(3), str(tmp_path / "logs"), ["--training_epochs=50"])
+    ps = subprocess.Popen([sys.executable, script, *args, "--job_name=ps", "--task_index=0"])
+    time.sleep(0.3)
+    w0 = subprocess.Popen([sys.executable, script, *args, "--job_name=worker", "--task_index=0"],
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        # wait until training is running, then kill the ps
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            line = w0.stdout.readline()
+            if line.startswith("Step so far"):
+                break
+        ps.send_signal(signal.SIGKILL)
+        ps.wait(timeout=10)
+        _, err = w0.communicate(timeout=60)
+        assert w0.returncode != 0 and "ps unavailable" in err
+    finally:
+        for p in (ps, w0):
+            if p.poll() is None:
+                p.kill()
+
+
+def test_missing_hosts_is_usage_error():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "distributed", "distributed.py"), "--job_name=ps"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
