@@ -43,9 +43,6 @@ def test_resnet_gpu_matches_cpu_reference_first_step(gpu, depth):
         if eg > 2.0 * eb + 0.05:
             bad.append((v.name, eg, eb))
     assert not bad, bad[:5]
-    fc = sc.by_name["resnet%d/fc/kernel" % depth]
-    efc = ((sg.by_name[fc.name].grad.cpu() - fc.grad).norm() / fc.grad.norm()).item()
-    assert efc < 0.02, efc
 
 
 def test_graph_capture_step(gpu):
