@@ -68,15 +68,17 @@ void sgemm_launch(const float* A, const float* B, float* C, const float* bias, i
                   int ldb, int ldc, bool transA, bool transB, int act, bool accumulate, hipStream_t s);
 
 // ---------------------------------------------------------------- batch norm (NHWC)
-void bn_stats(const uint16_t* x, int64_t M, int C, float* sums, hipStream_t s);
-void bn_finalize(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
+// slots: persistent per-layer workspace [NSLOT][2][C] f32, zero between uses (consumers re-zero it)
+void bn_stats(const uint16_t* x, int64_t M, int C, float* slots, hipStream_t s);
+void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float* beta, float eps,
                  float momentum, float* run_mean, float* run_var, float* save, hipStream_t s);
 void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
                   const float* run_var, float* save, hipStream_t s);
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
               uint16_t* y, hipStream_t s);
 void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const float* save, int64_t M,
-                 int C, bool relu, float* red, uint16_t* dx, uint16_t* dres, hipStream_t s);
+                 int C, bool relu, float* slots, float* red, float* dgamma, float* dbeta, uint16_t* dx,
+                 uint16_t* dres, hipStream_t s);
 
 // ---------------------------------------------------------------- loss / pooling
 void softmax_xent(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,

@@ -1,43 +1,46 @@
-// Batch normalisation for NHWC bf16 activations (f32 statistics), with ReLU and the
-// residual add of a ResNet bottleneck fused into the apply pass.
+// Batch normalisation for NHWC bf16 activations (f32 statistics), with ReLU and the residual add
+// of a ResNet bottleneck fused into the apply pass.
 //
 // Layout: x is [M][C] with M = N*H*W rows (channels-last), C contiguous.
 // Forward  : stats -> finalize (mean, invstd, scale = gamma*invstd, shift = beta - mean*scale,
 //            running-stat update) -> apply  y = relu?(x*scale + shift (+ res)).
-//            The stats usually come for free from the producing conv's epilogue
-//            (igemm.hip, MODE_FWD with a stats buffer); bn_stats is the standalone pass.
+//            The stats normally come for free from the producing conv's epilogue
+//            (igemm.hip with a stats workspace); bn_stats is the standalone pass.
 // Backward : reduce (sum g', sum g'*xhat with g' = g * [z > 0] recomputed from x/res)
-//            -> apply  dx = scale*(g' - sum_g/M - xhat*sum_gx/M), dres = g'.
-// Cross-block reductions go through NSLOT=64 slot rows [NSLOT][2][C]: block b adds its partial
-// into slot b % NSLOT (<= ~32 adders per address instead of every block on one address, which
-// serialises at the memory side: MI355X_MICROARCH.md "Global float atomics", contention row),
-// and the finalize/reduce kernel sums the 64 slots.
-// Memory-bound: every pass moves 16 B per lane (8 channels), grid-stride.
+//            -> apply  dx = A*g' + B*x + D per channel (BN backward folded into 3 coefficients),
+//            dres = g'.  dgamma / dbeta are accumulated straight into the parameter gradients.
+//
+// Cross-block reductions go through a PERSISTENT slot workspace [NSLOT][2][C] (one per BN layer):
+// block b adds its partial into slot b % NSLOT (<= ~32 adders per address instead of every block
+// on one address, which serialises at the memory side: MI355X_MICROARCH.md "Global float
+// atomics", contention row).  The consumer (finalize / slot-reduce) zeroes the slots after reading
+// them, so the workspace is always zero between uses: no memset launches.
+// Elementwise passes give every thread a FIXED 8-channel vector (grid stride is a multiple of
+// C/8), so per-channel parameters live in registers; 16 B per lane per access.
 #include "tfx_common.h"
 #include "tfx_kernels.h"
 
 namespace tfx {
 
+namespace {
+
 // ------------------------------------------------------------------ stats (vector)
 // TPR threads per row (C/8), RPB = 256/TPR rows per block-iteration.
-__global__ void __launch_bounds__(256) bn_stats_vec_kernel(const uint16_t* __restrict__ x, int64_t M,
-                                                           int C, float* __restrict__ sums) {
+__global__ void __launch_bounds__(256) bn_stats_vec_kernel(const uint16_t* __restrict__ x, int64_t M, int C,
+                                                           float* __restrict__ slots) {
   const int tpr = C >> 3;
   const int rpb = 256 / tpr;
   const int t = threadIdx.x;
-  const int cv = t % tpr;       // which 8-channel vector
-  const int r0 = t / tpr;       // row lane
+  const int cv = t % tpr, r0 = t / tpr;
   float s[8] = {0}, q[8] = {0};
   const int64_t stride = (int64_t)gridDim.x * rpb;
   for (int64_t r = (int64_t)blockIdx.x * rpb + r0; r < M; r += stride) {
-    U4 v = *reinterpret_cast<const U4*>(x + r * C + cv * 8);
     float f[8];
-    unpack8(v, f);
+    unpack8(*reinterpret_cast<const U4*>(x + r * C + cv * 8), f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s[i] += f[i]; q[i] = fmaf(f[i], f[i], q[i]); }
   }
-  // reduce across the rpb row lanes sharing a channel vector (LDS tree)
-  __shared__ float red[256 * 8 + 8];
+  __shared__ float red[256 * 8];
   for (int pass = 0; pass < 2; ++pass) {
     float* v = pass ? q : s;
 #pragma unroll
@@ -51,23 +54,22 @@ __global__ void __launch_bounds__(256) bn_stats_vec_kernel(const uint16_t* __res
       __syncthreads();
     }
     if (r0 == 0) {
+      float* slot = slots + (size_t)(blockIdx.x % NSLOT) * 2 * C + pass * C + cv * 8;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        atomicAdd(&sums[(blockIdx.x % NSLOT) * 2 * C + pass * C + cv * 8 + i], red[i * 256 + t]);
+      for (int i = 0; i < 8; ++i) atomicAdd(slot + i, red[i * 256 + t]);
     }
     __syncthreads();
   }
 }
 
-// ------------------------------------------------------------------ stats (generic C)
-__global__ void __launch_bounds__(256) bn_stats_gen_kernel(const uint16_t* __restrict__ x, int64_t M,
-                                                           int C, float* __restrict__ sums) {
+__global__ void __launch_bounds__(256) bn_stats_gen_kernel(const uint16_t* __restrict__ x, int64_t M, int C,
+                                                           float* __restrict__ slots) {
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   float s = 0.f, q = 0.f;
   if (c < C) {
     for (int64_t r = (int64_t)blockIdx.y * 4 + ty; r < M; r += (int64_t)gridDim.y * 4) {
-      float f = bf16_to_f32(x[r * C + c]);
+      const float f = bf16_to_f32(x[r * C + c]);
       s += f;
       q = fmaf(f, f, q);
     }
@@ -77,25 +79,23 @@ __global__ void __launch_bounds__(256) bn_stats_gen_kernel(const uint16_t* __res
   rq[threadIdx.x] = q;
   __syncthreads();
   if (ty == 0 && c < C) {
-    s = rs[tx] + rs[tx + 64] + rs[tx + 128] + rs[tx + 192];
-    q = rq[tx] + rq[tx + 64] + rq[tx + 128] + rq[tx + 192];
-    float* slot = sums + (size_t)((blockIdx.y % NSLOT) * 2) * C;
-    atomicAdd(&slot[c], s);
-    atomicAdd(&slot[C + c], q);
+    float* slot = slots + (size_t)((blockIdx.y % NSLOT) * 2) * C;
+    atomicAdd(&slot[c], rs[tx] + rs[tx + 64] + rs[tx + 128] + rs[tx + 192]);
+    atomicAdd(&slot[C + c], rq[tx] + rq[tx + 64] + rq[tx + 128] + rq[tx + 192]);
   }
 }
 
-// ------------------------------------------------------------------ finalize
-// sums[0:C]=Σx, sums[C:2C]=Σx²  ->  save[0:C]=mean, save[C:2C]=invstd, save[2C:3C]=scale,
-// save[3C:4C]=shift; running stats updated in place (unbiased variance, PyTorch/TF momentum form).
-// Sum the NSLOT slot rows of slots[NSLOT][2][C] into out[2][C] (64 channels x 4 slot-lanes per block)
-__device__ __forceinline__ void slot_sum(const float* __restrict__ slots, int C, int c, int ty, float& s, float& q) {
+// Sum the NSLOT slot rows for channel c (64 channels x 4 slot-lanes per block) and zero them.
+__device__ __forceinline__ void slot_sum_consume(float* __restrict__ slots, int C, int c, int ty, float& s, float& q) {
   s = 0.f;
   q = 0.f;
   if (c < C) {
     for (int k = ty; k < NSLOT; k += 4) {
-      s += slots[(size_t)k * 2 * C + c];
-      q += slots[(size_t)k * 2 * C + C + c];
+      float* p = slots + (size_t)k * 2 * C;
+      s += p[c];
+      q += p[C + c];
+      p[c] = 0.f;  // keep the workspace zero for its next use
+      p[C + c] = 0.f;
     }
   }
   __shared__ float rs[256], rq[256];
@@ -107,26 +107,24 @@ __device__ __forceinline__ void slot_sum(const float* __restrict__ slots, int C,
   q = rq[tx] + rq[tx + 64] + rq[tx + 128] + rq[tx + 192];
 }
 
-__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ slots, int64_t M, int C,
+__global__ void __launch_bounds__(256) bn_finalize_kernel(float* __restrict__ slots, int64_t M, int C,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           float eps, float momentum, float* __restrict__ run_mean,
                                                           float* __restrict__ run_var, float* __restrict__ save) {
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   float sum, sq;
-  slot_sum(slots, C, c, ty, sum, sq);
+  slot_sum_consume(slots, C, c, ty, sum, sq);
   if (ty != 0 || c >= C) return;
   const float inv_m = 1.f / (float)M;
   const float mean = sum * inv_m;
   const float var = fmaxf(sq * inv_m - mean * mean, 0.f);
   const float invstd = rsqrtf(var + eps);
-  const float g = gamma ? gamma[c] : 1.f;
-  const float b = beta ? beta[c] : 0.f;
-  const float scale = g * invstd;
+  const float scale = (gamma ? gamma[c] : 1.f) * invstd;
   save[c] = mean;
   save[C + c] = invstd;
   save[2 * C + c] = scale;
-  save[3 * C + c] = b - mean * scale;
+  save[3 * C + c] = (beta ? beta[c] : 0.f) - mean * scale;
   if (run_mean) {
     const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
@@ -134,20 +132,22 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   }
 }
 
-// backward: slots -> red[2][C]
-__global__ void __launch_bounds__(256) bn_slot_reduce_kernel(const float* __restrict__ slots, int C,
-                                                             float* __restrict__ red) {
+// backward: slots -> red[2][C] (= [dbeta | dgamma]); accumulate into the parameter grads
+__global__ void __launch_bounds__(256) bn_slot_reduce_kernel(float* __restrict__ slots, int C,
+                                                             float* __restrict__ red, float* __restrict__ dgamma,
+                                                             float* __restrict__ dbeta) {
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   float s, q;
-  slot_sum(slots, C, c, ty, s, q);
+  slot_sum_consume(slots, C, c, ty, s, q);
   if (ty == 0 && c < C) {
     red[c] = s;
     red[C + c] = q;
+    if (dbeta) dbeta[c] += s;
+    if (dgamma) dgamma[c] += q;
   }
 }
 
-// inference: scale/shift from running statistics
 __global__ void bn_eval_prep_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
                                     float eps, const float* __restrict__ run_mean,
                                     const float* __restrict__ run_var, float* __restrict__ save) {
@@ -161,27 +161,41 @@ __global__ void bn_eval_prep_kernel(int C, const float* __restrict__ gamma, cons
   save[3 * C + c] = (beta ? beta[c] : 0.f) - run_mean[c] * scale;
 }
 
-// ------------------------------------------------------------------ apply
+// ------------------------------------------------------------------ apply (fixed channel vector)
+// grid * 256 is a multiple of C/8 (host), so vector i = tid + k*stride always has channel vector
+// (tid0 % (C/8)).  Two vectors per iteration for memory-level parallelism.
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(256) bn_apply_vec_kernel(const uint16_t* __restrict__ x,
                                                            const uint16_t* __restrict__ res,
-                                                           const float* __restrict__ save, int64_t nvec,
-                                                           int C, uint16_t* __restrict__ y) {
-  const float* scale = save + 2 * C;
-  const float* shift = save + 3 * C;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)((i * 8) % C);
+                                                           const float* __restrict__ save, int64_t nvec, int C,
+                                                           uint16_t* __restrict__ y) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int c0 = (int)(i0 % (C >> 3)) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = save[2 * C + c0 + k];
+    sh[k] = save[3 * C + c0 + k];
+  }
+  auto one = [&](int64_t i) {
     float f[8], r[8];
     unpack8(reinterpret_cast<const U4*>(x)[i], f);
     if (RES) unpack8(reinterpret_cast<const U4*>(res)[i], r);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float z = fmaf(f[k], scale[c0 + k], shift[c0 + k]);
+      float z = fmaf(f[k], sc[k], sh[k]);
       if (RES) z += r[k];
       f[k] = RELU ? fmaxf(z, 0.f) : z;
     }
     reinterpret_cast<U4*>(y)[i] = pack8(f);
+  };
+  int64_t i = i0;
+  for (; i + stride < nvec; i += 2 * stride) {
+    one(i);
+    one(i + stride);
   }
+  if (i < nvec) one(i);
 }
 
 template <bool RES, bool RELU>
@@ -200,28 +214,23 @@ __global__ void __launch_bounds__(256) bn_apply_gen_kernel(const uint16_t* __res
 }
 
 // ------------------------------------------------------------------ backward reduce
-// red[0:C] = Σ g', red[C:2C] = Σ g'·xhat
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* __restrict__ g,
                                                                 const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ res,
-                                                                const float* __restrict__ save, int64_t M,
-                                                                int C, float* __restrict__ red) {
+                                                                const float* __restrict__ save, int64_t M, int C,
+                                                                float* __restrict__ slots) {
   const int tpr = C >> 3;
   const int rpb = 256 / tpr;
   const int t = threadIdx.x;
   const int cv = t % tpr, r0 = t / tpr;
-  const float* mean = save;
-  const float* invstd = save + C;
-  const float* scale = save + 2 * C;
-  const float* shift = save + 3 * C;
   float mu[8], is[8], sc[8], sh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    mu[k] = mean[cv * 8 + k];
-    is[k] = invstd[cv * 8 + k];
-    sc[k] = scale[cv * 8 + k];
-    sh[k] = shift[cv * 8 + k];
+    mu[k] = save[cv * 8 + k];
+    is[k] = save[C + cv * 8 + k];
+    sc[k] = save[2 * C + cv * 8 + k];
+    sh[k] = save[3 * C + cv * 8 + k];
   }
   float sg[8] = {0}, sx[8] = {0};
   const int64_t stride = (int64_t)gridDim.x * rpb;
@@ -243,7 +252,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* 
       sx[k] = fmaf(gg, (xf[k] - mu[k]) * is[k], sx[k]);
     }
   }
-  __shared__ float lds[256 * 8 + 8];
+  __shared__ float lds[256 * 8];
   for (int pass = 0; pass < 2; ++pass) {
     float* v = pass ? sx : sg;
 #pragma unroll
@@ -257,9 +266,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* 
       __syncthreads();
     }
     if (r0 == 0) {
+      float* slot = slots + (size_t)(blockIdx.x % NSLOT) * 2 * C + pass * C + cv * 8;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        atomicAdd(&red[(blockIdx.x % NSLOT) * 2 * C + pass * C + cv * 8 + i], lds[i * 256 + t]);
+      for (int i = 0; i < 8; ++i) atomicAdd(slot + i, lds[i * 256 + t]);
     }
     __syncthreads();
   }
@@ -269,8 +278,8 @@ template <bool RES, bool RELU>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_gen_kernel(const uint16_t* __restrict__ g,
                                                                 const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ res,
-                                                                const float* __restrict__ save, int64_t M,
-                                                                int C, float* __restrict__ red) {
+                                                                const float* __restrict__ save, int64_t M, int C,
+                                                                float* __restrict__ slots) {
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   float sg = 0.f, sx = 0.f;
@@ -294,42 +303,53 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_gen_kernel(const uint16_t* 
   b[threadIdx.x] = sx;
   __syncthreads();
   if (ty == 0 && c < C) {
-    float* slot = red + (size_t)((blockIdx.y % NSLOT) * 2) * C;
+    float* slot = slots + (size_t)((blockIdx.y % NSLOT) * 2) * C;
     atomicAdd(&slot[c], a[tx] + a[tx + 64] + a[tx + 128] + a[tx + 192]);
     atomicAdd(&slot[C + c], b[tx] + b[tx + 64] + b[tx + 128] + b[tx + 192]);
   }
 }
 
-// ------------------------------------------------------------------ backward apply
-// dx = scale * (g' - Σg'/M - xhat * Σg'xhat/M); dres = g' (residual branch gradient)
+// ------------------------------------------------------------------ backward apply (fixed channel)
+// dx = scale*(g' - sum_g/M - (x-mu)*is*sum_gx/M) = A*g' + B*x + D
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* __restrict__ g,
                                                                const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ res,
                                                                const float* __restrict__ save,
-                                                               const float* __restrict__ red, int64_t nvec,
-                                                               int64_t M, int C, uint16_t* __restrict__ dx,
+                                                               const float* __restrict__ red, int64_t nvec, int64_t M,
+                                                               int C, uint16_t* __restrict__ dx,
                                                                uint16_t* __restrict__ dres) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int c0 = (int)(i0 % (C >> 3)) * 8;
   const float inv_m = 1.f / (float)M;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)((i * 8) % C);
+  float A[8], B[8], D[8], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + k;
+    const float mu = save[c], is = save[C + c];
+    sc[k] = save[2 * C + c];
+    sh[k] = save[3 * C + c];
+    const float kg = red[c] * inv_m, kx = red[C + c] * inv_m * is;
+    A[k] = sc[k];
+    B[k] = -sc[k] * kx;
+    D[k] = sc[k] * (kx * mu - kg);
+  }
+  for (int64_t i = i0; i < nvec; i += stride) {
     float gf[8], xf[8], rf[8], o[8];
     unpack8(reinterpret_cast<const U4*>(g)[i], gf);
     unpack8(reinterpret_cast<const U4*>(x)[i], xf);
     if (RES && RELU) unpack8(reinterpret_cast<const U4*>(res)[i], rf);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
-      const float mu = save[c], is = save[C + c], sc = save[2 * C + c], sh = save[3 * C + c];
       float gg = gf[k];
       if (RELU) {
-        float z = fmaf(xf[k], sc, sh);
+        float z = fmaf(xf[k], sc[k], sh[k]);
         if (RES) z += rf[k];
         gg = z > 0.f ? gg : 0.f;
       }
       gf[k] = gg;
-      const float xh = (xf[k] - mu) * is;
-      o[k] = sc * (gg - red[c] * inv_m - xh * red[C + c] * inv_m);
+      o[k] = fmaf(A[k], gg, fmaf(B[k], xf[k], D[k]));
     }
     reinterpret_cast<U4*>(dx)[i] = pack8(o);
     if (RES) reinterpret_cast<U4*>(dres)[i] = pack8(gf);
@@ -341,8 +361,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_gen_kernel(const uint16_t* _
                                                                const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ res,
                                                                const float* __restrict__ save,
-                                                               const float* __restrict__ red, int64_t n,
-                                                               int64_t M, int C, uint16_t* __restrict__ dx,
+                                                               const float* __restrict__ red, int64_t n, int64_t M,
+                                                               int C, uint16_t* __restrict__ dx,
                                                                uint16_t* __restrict__ dres) {
   const float inv_m = 1.f / (float)M;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -361,30 +381,48 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_gen_kernel(const uint16_t* _
   }
 }
 
-// ================================================================== launchers
-static inline bool vec_ok(int C) { return (C % 8 == 0) && (C / 8) <= 256 && (256 % (C / 8) == 0); }
-static inline int grid_for(int64_t work, int per_block) {
+// ================================================================== launch helpers
+bool vec_ok(int C) { return (C % 8 == 0) && (C / 8) <= 256 && (256 % (C / 8) == 0); }
+int grid_for(int64_t work, int per_block, int cap = 2048) {
   int64_t g = (work + per_block - 1) / per_block;
-  if (g > 2048) g = 2048;
+  if (g > cap) g = cap;
   return (int)(g < 1 ? 1 : g);
 }
+int gcd(int a, int b) { return b ? gcd(b, a % b) : a; }
+// elementwise grid whose stride (grid*256 vectors) is a multiple of C/8
+int fixed_channel_grid(int64_t nvec, int C) {
+  const int cv = C / 8;
+  const int mult = cv / gcd(cv, 256);  // blocks per channel period
+  int g = grid_for(nvec, 256 * 4, 4096);
+  g = (g + mult - 1) / mult * mult;
+  return g;
+}
 
-void bn_stats(const uint16_t* x, int64_t M, int C, float* sums, hipStream_t s) {
-  TFX_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * NSLOT, s));
+#define TFX_DISPATCH_RR(RES, RELU, ...)                              \
+  if (RES) {                                                         \
+    if (RELU) { constexpr bool R_ = true, L_ = true; __VA_ARGS__; }   \
+    else { constexpr bool R_ = true, L_ = false; __VA_ARGS__; }       \
+  } else {                                                           \
+    if (RELU) { constexpr bool R_ = false, L_ = true; __VA_ARGS__; }  \
+    else { constexpr bool R_ = false, L_ = false; __VA_ARGS__; }      \
+  }
+
+}  // namespace
+
+void bn_stats(const uint16_t* x, int64_t M, int C, float* slots, hipStream_t s) {
   if (vec_ok(C)) {
     const int rpb = 256 / (C / 8);
-    int g = grid_for(M, rpb * 8);  // >= 8 rows per row-lane
-    bn_stats_vec_kernel<<<g, 256, 0, s>>>(x, M, C, sums);
+    bn_stats_vec_kernel<<<grid_for(M, rpb * 8), 256, 0, s>>>(x, M, C, slots);
   } else {
     dim3 grid((C + 63) / 64, grid_for(M, 64));
-    bn_stats_gen_kernel<<<grid, 256, 0, s>>>(x, M, C, sums);
+    bn_stats_gen_kernel<<<grid, 256, 0, s>>>(x, M, C, slots);
   }
 }
 
-void bn_finalize(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
-                 float momentum, float* run_mean, float* run_var, float* save, hipStream_t s) {
-  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, s>>>(sums, M, C, gamma, beta, eps, momentum, run_mean,
-                                                   run_var, save);
+void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float* beta, float eps, float momentum,
+                 float* run_mean, float* run_var, float* save, hipStream_t s) {
+  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, s>>>(slots, M, C, gamma, beta, eps, momentum, run_mean, run_var,
+                                                   save);
 }
 
 void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
@@ -392,39 +430,28 @@ void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const
   bn_eval_prep_kernel<<<(C + 255) / 256, 256, 0, s>>>(C, gamma, beta, eps, run_mean, run_var, save);
 }
 
-#define TFX_DISPATCH_RR(RES, RELU, ...)            \
-  if (RES) {                                       \
-    if (RELU) { constexpr bool R_ = true, L_ = true; __VA_ARGS__; }   \
-    else { constexpr bool R_ = true, L_ = false; __VA_ARGS__; }       \
-  } else {                                         \
-    if (RELU) { constexpr bool R_ = false, L_ = true; __VA_ARGS__; }  \
-    else { constexpr bool R_ = false, L_ = false; __VA_ARGS__; }      \
-  }
-
-void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
-              uint16_t* y, hipStream_t s) {
+void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu, uint16_t* y,
+              hipStream_t s) {
   const int64_t n = M * C;
   const bool has_res = res != nullptr;
   if (C % 8 == 0) {
     const int64_t nvec = n / 8;
-    int g = grid_for(nvec, 256 * 4);
+    const int g = fixed_channel_grid(nvec, C);
     TFX_DISPATCH_RR(has_res, relu, (bn_apply_vec_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, nvec, C, y)));
   } else {
-    int g = grid_for(n, 256 * 4);
+    const int g = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_apply_gen_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, n, C, y)));
   }
 }
 
-void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const float* save, int64_t M,
-                 int C, bool relu, float* red, uint16_t* dx, uint16_t* dres, hipStream_t s) {
-  // red: [2C] result followed by the [NSLOT][2][C] slot workspace
-  float* slots = red + 2 * C;
-  TFX_HIP_CHECK(hipMemsetAsync(slots, 0, sizeof(float) * 2 * C * NSLOT, s));
-  const bool has_res = res != nullptr;  // only meaningful for the ReLU mask recompute
+void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C,
+                 bool relu, float* slots, float* red, float* dgamma, float* dbeta, uint16_t* dx, uint16_t* dres,
+                 hipStream_t s) {
+  const bool has_res = res != nullptr;
   const int64_t n = M * C;
   if (vec_ok(C)) {
     const int rpb = 256 / (C / 8);
-    int gr = grid_for(M, rpb * 8);
+    const int gr = grid_for(M, rpb * 8);
     TFX_DISPATCH_RR(has_res, relu,
                     (bn_bwd_reduce_vec_kernel<R_, L_><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
   } else {
@@ -432,16 +459,15 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
     TFX_DISPATCH_RR(has_res, relu,
                     (bn_bwd_reduce_gen_kernel<R_, L_><<<grid, 256, 0, s>>>(g, x, res, save, M, C, slots)));
   }
-  bn_slot_reduce_kernel<<<(C + 63) / 64, 256, 0, s>>>(slots, C, red);
-  // With a residual input (bottleneck output BN) dres = g' is always produced: the identity /
-  // projection branch needs it.  The host wrapper guarantees dres != nullptr when res != nullptr.
+  bn_slot_reduce_kernel<<<(C + 63) / 64, 256, 0, s>>>(slots, C, red, dgamma, dbeta);
+  // with a residual input dres = g' is produced (the host guarantees dres != nullptr then)
   if (C % 8 == 0) {
     const int64_t nvec = n / 8;
-    int ga = grid_for(nvec, 256 * 4);
+    const int ga = fixed_channel_grid(nvec, C);
     TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_vec_kernel<R_, L_><<<ga, 256, 0, s>>>(
                                        g, x, res, save, red, nvec, M, C, dx, dres)));
   } else {
-    int ga = grid_for(n, 256 * 4);
+    const int ga = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_gen_kernel<R_, L_><<<ga, 256, 0, s>>>(
                                        g, x, res, save, red, n, M, C, dx, dres)));
   }

@@ -82,12 +82,12 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil) {
   return conv_fwd_impl(x, w, stride, pad, dil, nullptr);
 }
 
-// conv forward + the per-channel BN statistics of its output, fused into the GEMM epilogue.
-// Returns (y, slots) where slots is the [NSLOT][2][Ko] partial-sum workspace bn_fwd_train consumes.
-std::tuple<Tensor, Tensor> conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil) {
-  auto slots = at::zeros({tfx::NSLOT * 2 * w.size(0)}, x.options().dtype(at::kFloat));
-  auto y = conv_fwd_impl(x, w, stride, pad, dil, slots.data_ptr<float>());
-  return {y, slots};
+// conv forward + the per-channel BN statistics of its output, fused into the GEMM epilogue and
+// accumulated into the BN layer's persistent slot workspace ([NSLOT][2][Ko], zero on entry).
+Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor slots) {
+  CHECK_F32(slots);
+  TORCH_CHECK(slots.numel() == tfx::NSLOT * 2 * w.size(0), "stat slots size");
+  return conv_fwd_impl(x, w, stride, pad, dil, slots.data_ptr<float>());
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil) {
@@ -201,16 +201,15 @@ void sgemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor out, bool accumulat
 }
 
 // ------------------------------------------------------------------ batch norm
+// slots: the layer's persistent [NSLOT][2][C] workspace; have_stats = the producer (conv epilogue)
+// already accumulated this batch's statistics into it.
 std::tuple<Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
                                         optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
-                                        double eps, optional<Tensor> res, bool relu, optional<Tensor> slots) {
+                                        double eps, optional<Tensor> res, bool relu, Tensor slots, bool have_stats) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
-  auto opts = x.options().dtype(at::kFloat);
-  const bool have = slots.has_value() && slots->defined();
-  if (have) TORCH_CHECK(slots->numel() == tfx::NSLOT * 2 * C && slots->scalar_type() == at::kFloat, "stat slots");
-  Tensor sums = have ? *slots : at::empty({tfx::NSLOT * 2 * C}, opts);
-  auto save = at::empty({4 * C}, opts);
+  TORCH_CHECK(slots.numel() == tfx::NSLOT * 2 * C && slots.scalar_type() == at::kFloat, "stat slots");
+  auto save = at::empty({4 * C}, x.options().dtype(at::kFloat));
   auto y = at::empty_like(x);
   const uint16_t* r = nullptr;
   if (res.has_value() && res->defined()) {
@@ -219,8 +218,9 @@ std::tuple<Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma, option
     r = bf(*res);
   }
   auto s = cur_stream();
-  if (!have) tfx::bn_stats(bf(x), M, C, sums.data_ptr<float>(), s);
-  tfx::bn_finalize(sums.data_ptr<float>(), M, C, fp(gamma), fp(beta), eps, momentum, fpm(run_mean), fpm(run_var),
+  float* sl = slots.data_ptr<float>();
+  if (!have_stats) tfx::bn_stats(bf(x), M, C, sl, s);
+  tfx::bn_finalize(sl, M, C, fp(gamma), fp(beta), eps, momentum, fpm(run_mean), fpm(run_var),
                    save.data_ptr<float>(), s);
   tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y), s);
   return {y, save};
@@ -240,12 +240,15 @@ std::tuple<Tensor, Tensor> bn_fwd_eval(Tensor x, optional<Tensor> gamma, optiona
   return {y, save};
 }
 
-// returns dx, dres (undefined unless res given), red = [dbeta(C) | dgamma(C)]
-std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> res, Tensor save, bool relu) {
+// returns dx, dres (undefined unless res given), red = [dbeta(C) | dgamma(C)]; when dgamma/dbeta
+// are given the parameter gradients are accumulated in place by the reduce kernel.
+std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> res, Tensor save, bool relu,
+                                          Tensor slots, optional<Tensor> dgamma, optional<Tensor> dbeta) {
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd grad shape");
-  auto red = at::empty({2 * C + tfx::NSLOT * 2 * C}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(slots.numel() == tfx::NSLOT * 2 * C && slots.scalar_type() == at::kFloat, "stat slots");
+  auto red = at::empty({2 * C}, x.options().dtype(at::kFloat));
   auto dx = at::empty_like(x);
   Tensor dres;
   const uint16_t* r = nullptr;
@@ -254,9 +257,9 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
     r = bf(*res);
     dres = at::empty_like(x);
   }
-  tfx::bn_backward(bf(g), bf(x), r, save.data_ptr<float>(), M, C, relu, red.data_ptr<float>(), bfm(dx),
-                   r ? bfm(dres) : nullptr, cur_stream());
-  return {dx, dres, red.narrow(0, 0, 2 * C)};
+  tfx::bn_backward(bf(g), bf(x), r, save.data_ptr<float>(), M, C, relu, slots.data_ptr<float>(),
+                   red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), bfm(dx), r ? bfm(dres) : nullptr, cur_stream());
+  return {dx, dres, red};
 }
 
 // ------------------------------------------------------------------ loss / metrics / pooling

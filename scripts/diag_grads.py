@@ -17,7 +17,7 @@ def run(depth, fused, batch=8):
     sg.master.copy_(sc.master.cuda()); sg.refresh_shadow()
     if not fused:
         orig = resnet._Conv.__call__
-        resnet._Conv.__call__ = lambda self, x, training=True: ops.conv2d(x, self.w, self.stride, self.pad, stats=False)
+        resnet._Conv.__call__ = lambda self, x, ws=None: ops.conv2d(x, self.w, self.stride, self.pad)
     g = torch.Generator().manual_seed(1)
     img = torch.randint(0, 256, (batch, 32, 32, 3), dtype=torch.uint8, generator=g)
     lab = torch.randint(0, 10, (batch,), generator=g)

@@ -17,6 +17,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from .. import ops
+from ..ops.nn import BNWorkspace
 from ..variables import Constant, HeNormal, VariableStore, Zeros
 
 STAGES = {
@@ -36,13 +37,18 @@ class _BN:
             self.beta = store.variable([c], Zeros(), name="beta")
             self.mean = store.add_state("moving_mean", torch.zeros(c))
             self.var = store.add_state("moving_variance", torch.ones(c))
+        self.ws = BNWorkspace(c)
 
-    def __call__(self, x, training, relu=False, residual=None):
-        slots = None
-        if isinstance(x, tuple):  # (conv output, fused BN statistics)
-            x, slots = x
+    def __call__(self, x, training, relu=False, residual=None, stats_ready=False):
+        ws = self.ws.get(x.device) if x.device.type == "cuda" else None
         return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
-                              eps=1e-5, residual=residual, relu=relu, slots=slots)
+                              eps=1e-5, residual=residual, relu=relu, workspace=ws, stats_ready=stats_ready)
+
+    def after_conv(self, conv, x, training, relu=False, residual=None):
+        """conv -> BN with the BN statistics produced by the conv's epilogue (GPU, training)."""
+        fused = training and x.device.type == "cuda"
+        y = conv(x, self.ws.get(x.device) if fused else None)
+        return self(y, training, relu=relu, residual=residual, stats_ready=fused)
 
 
 class _Conv:
@@ -50,9 +56,8 @@ class _Conv:
         self.w = store.variable([cout, k, k, cin], HeNormal(), name=name)
         self.stride, self.pad = stride, k // 2
 
-    def __call__(self, x, training=True):
-        # every conv of the network feeds a BN: let its epilogue produce the BN statistics
-        return ops.conv2d(x, self.w, self.stride, self.pad, stats=training)
+    def __call__(self, x, bn_stats_into=None):
+        return ops.conv2d(x, self.w, self.stride, self.pad, bn_stats_into=bn_stats_into)
 
 
 class Bottleneck:
@@ -73,10 +78,10 @@ class Bottleneck:
                 self.bp = _BN(store, cout, "shortcut_bn")
 
     def __call__(self, x, training):
-        o = self.b1(self.c1(x, training), training, relu=True)
-        o = self.b2(self.c2(o, training), training, relu=True)
-        sc = x if self.proj is None else self.bp(self.proj(x, training), training)
-        return self.b3(self.c3(o, training), training, relu=True, residual=sc)
+        o = self.b1.after_conv(self.c1, x, training, relu=True)
+        o = self.b2.after_conv(self.c2, o, training, relu=True)
+        sc = x if self.proj is None else self.bp.after_conv(self.proj, x, training)
+        return self.b3.after_conv(self.c3, o, training, relu=True, residual=sc)
 
 
 class Basic:
@@ -94,9 +99,9 @@ class Basic:
                 self.bp = _BN(store, width, "shortcut_bn")
 
     def __call__(self, x, training):
-        o = self.b1(self.c1(x, training), training, relu=True)
-        sc = x if self.proj is None else self.bp(self.proj(x, training), training)
-        return self.b2(self.c2(o, training), training, relu=True, residual=sc)
+        o = self.b1.after_conv(self.c1, x, training, relu=True)
+        sc = x if self.proj is None else self.bp.after_conv(self.proj, x, training)
+        return self.b2.after_conv(self.c2, o, training, relu=True, residual=sc)
 
 
 class ResNetCifar:
@@ -129,7 +134,7 @@ class ResNetCifar:
         self.store.refresh_shadow()
 
     def __call__(self, x: torch.Tensor, training: bool = True) -> torch.Tensor:
-        o = self.stem_bn(self.stem(x, training), training, relu=True)
+        o = self.stem_bn.after_conv(self.stem, x, training, relu=True)
         for blk in self.blocks:
             o = blk(o, training)
         f = ops.global_avg_pool(o)

@@ -59,22 +59,15 @@ def _conv_ref(x, w, stride=1, pad=0, dil=1):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats):
+    def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into):
         ctx.w, ctx.cfg = w, (stride, pad, dil)
         ctx.native = _native.use_native(x)
         ctx.save_for_backward(x)
         if ctx.native:
-            if stats:
-                y, slots = torch.ops.tfx.conv_fwd_stats(x.contiguous(), w.value, stride, pad, dil)
-                ctx.mark_non_differentiable(slots)
-                return y, slots
+            if stats_into is not None:
+                return torch.ops.tfx.conv_fwd_stats(x.contiguous(), w.value, stride, pad, dil, stats_into)
             return torch.ops.tfx.conv_fwd(x.contiguous(), w.value, stride, pad, dil)
-        y = _conv_ref(x, w.value.to(x.dtype), stride, pad, dil)
-        if stats:
-            empty = torch.empty(0)
-            ctx.mark_non_differentiable(empty)
-            return y, empty
-        return y
+        return _conv_ref(x, w.value.to(x.dtype), stride, pad, dil)
 
     @staticmethod
     def backward(ctx, gy, *unused):
@@ -93,13 +86,30 @@ class _Conv2d(torch.autograd.Function):
         return dx, None, None, None, None, None, None
 
 
-def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int = 1, stats: bool = False):
+def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int = 1,
+           bn_stats_into: Optional[torch.Tensor] = None):
     """NHWC conv, weight stored [Ko, R, S, C]. GPU: implicit-GEMM MFMA kernels (igemm.hip).
 
-    ``stats=True`` returns ``(y, bn_slots)``: the per-channel sum / sum-of-squares of ``y`` are
-    produced by the conv's GEMM epilogue, so a following :func:`batch_norm` (``slots=``) skips
-    its own statistics pass over ``y`` (on CPU the slots are empty and BN computes them)."""
-    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, stats)
+    ``bn_stats_into`` = the following BN layer's slot workspace (:class:`BNWorkspace`): the
+    per-channel sum / sum-of-squares of ``y`` are then produced by the conv's GEMM epilogue and the
+    BN (``stats_ready=True``) skips its own statistics pass over ``y``.  Ignored on CPU."""
+    ws = bn_stats_into if (bn_stats_into is not None and x.device.type == "cuda") else None
+    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, ws)
+
+
+class BNWorkspace:
+    """Per-BN-layer persistent [NSLOT][2][C] f32 statistics workspace (always zero between uses:
+    the finalize / reduce kernels re-zero what they consume), so no per-step memsets."""
+    NSLOT = 64
+
+    def __init__(self, channels: int):
+        self.c = channels
+        self.buf = None
+
+    def get(self, device) -> torch.Tensor:
+        if self.buf is None or self.buf.device != device:
+            self.buf = torch.zeros(self.NSLOT * 2 * self.c, dtype=torch.float32, device=device)
+        return self.buf
 
 
 # ====================================================================== batch norm (+res, +relu)
@@ -129,7 +139,7 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
-                training, slots):
+                training, ws, stats_ready):
         ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
         ctx.native = _native.use_native(x)
         ctx.has_res = res is not None
@@ -137,9 +147,13 @@ class _BatchNorm(torch.autograd.Function):
         b_t = beta.master if beta is not None else None
         if ctx.native:
             x = x.contiguous()
+            if ws is None:
+                ws = torch.zeros(64 * 2 * x.shape[-1], dtype=torch.float32, device=x.device)
+                stats_ready = False
+            ctx.ws = ws
             if training:
-                sl = slots if (slots is not None and slots.numel() > 0) else None
-                y, save = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu, sl)
+                y, save = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu, ws,
+                                                     bool(stats_ready))
             else:
                 y, save = torch.ops.tfx.bn_fwd_eval(x, g_t, b_t, rm, rv, eps, res, relu)
             ctx.save_for_backward(x, res, save)
@@ -156,13 +170,12 @@ class _BatchNorm(torch.autograd.Function):
             x, res, save = ctx.saved_tensors
             if not training:
                 raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
-            dx, dres, red = torch.ops.tfx.bn_bwd(gy.contiguous(), x, res, save, relu)
-            C = x.shape[-1]
-            if gamma is not None and gamma.trainable:
-                gamma.grad.add_(red[C:])
-                beta.grad.add_(red[:C])
+            train_p = gamma is not None and gamma.trainable
+            dx, dres, red = torch.ops.tfx.bn_bwd(gy.contiguous(), x, res, save, relu, ctx.ws,
+                                                 gamma.grad if train_p else None, beta.grad if train_p else None)
+            if train_p:
                 _grad_ready(gamma, beta)
-            return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None
+            return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None
         x, res = ctx.saved_tensors
         with torch.enable_grad():
             xs = x.detach().requires_grad_(True)
@@ -177,19 +190,19 @@ class _BatchNorm(torch.autograd.Function):
             gamma.grad.add_(grads[0])
             beta.grad.add_(grads[1])
             _grad_ready(gamma, beta)
-        return dx, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
                momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False,
-               slots: Optional[torch.Tensor] = None):
+               workspace: Optional[torch.Tensor] = None, stats_ready: bool = False):
     """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
     ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass)."""
     anchor = gamma.store.anchor if gamma is not None else None
-    if not training:
-        slots = None
+    if x.device.type != "cuda":
+        workspace = None
     return _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
-                            slots)
+                            workspace, stats_ready and training and workspace is not None)
 
 
 # ====================================================================== dense

@@ -116,7 +116,9 @@ def test_batchnorm_train(gpu, C, res, relu):
     gamma = torch.rand(C, device=gpu) + 0.5
     beta = torch.randn(C, device=gpu)
     rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
-    y, save = torch.ops.tfx.bn_fwd_train(x, gamma, beta, rm, rv, 0.1, 1e-5, r, relu, None)
+    ws = torch.zeros(64 * 2 * C, device=gpu)
+    y, save = torch.ops.tfx.bn_fwd_train(x, gamma, beta, rm, rv, 0.1, 1e-5, r, relu, ws, False)
+    assert ws.abs().max().item() == 0.0  # consumed workspace is re-zeroed
     xr = x.float().requires_grad_(True)
     gr = gamma.clone().requires_grad_(True)
     br = beta.clone().requires_grad_(True)
@@ -132,9 +134,12 @@ def test_batchnorm_train(gpu, C, res, relu):
     assert torch.allclose(rv, 0.9 + 0.1 * var.detach() * M / (M - 1), atol=1e-3)
     g = _bf(torch.randn(M, C, device=gpu))
     yr.backward(g.float())
-    dx, dres, red = torch.ops.tfx.bn_bwd(g, x, r, save, relu)
+    dgam, dbet = torch.ones(C, device=gpu), torch.zeros(C, device=gpu)
+    dx, dres, red = torch.ops.tfx.bn_bwd(g, x, r, save, relu, ws, dgam, dbet)
+    assert ws.abs().max().item() == 0.0
     assert _rel(dx, xr.grad) < 2e-2
     assert _rel(red[C:], gr.grad) < 1e-3 and _rel(red[:C], br.grad) < 1e-3
+    assert _rel(dgam - 1, gr.grad) < 1e-3 and _rel(dbet, br.grad) < 1e-3  # accumulated in place
     if res:
         assert _rel(dres, rr.grad) < 1e-2
 
@@ -206,12 +211,13 @@ def test_conv_fwd_fused_bn_stats(gpu, shape):
     N, H, W, C, Ko, R, st, pad = shape
     x = _bf(torch.randn(N, H, W, C, device=gpu))
     w = _bf(torch.randn(Ko, R, R, C, device=gpu) * 0.1)
-    y, slots = torch.ops.tfx.conv_fwd_stats(x, w, st, pad, 1)
+    slots = torch.zeros(64 * 2 * Ko, device=gpu)
+    y = torch.ops.tfx.conv_fwd_stats(x, w, st, pad, 1, slots)
     s = slots.view(64, 2, Ko).sum(0)
     yf = y.float().reshape(-1, Ko)
     assert torch.allclose(s[0], yf.sum(0), rtol=1e-4, atol=1e-3)
     assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
     gamma, beta = torch.ones(Ko, device=gpu), torch.zeros(Ko, device=gpu)
-    y1, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots)
-    y2, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, None)
+    y1, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots, True)
+    y2, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots, False)
     assert _rel(y1, y2) < 1e-3
