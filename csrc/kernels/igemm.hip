@@ -211,7 +211,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64
 
 }  // namespace
 
-template <int AKIND, int BKIND, int BM, int BN>
+// SWAP: compute the transposed tile (MFMA operands exchanged) so each lane holds 4 CONSECUTIVE
+// output columns of one row: bf16 outputs leave as one 8-byte store per 16x16 tile per lane, and
+// transposed f32 outputs (dW^T) as 16-lane contiguous runs.  Plain f32 atomics keep SWAP=false
+// (4 rows x 16 contiguous columns per instruction).
+template <int AKIND, int BKIND, int BM, int BN, bool SWAP>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BKT * 2, STAGE = (BM + BN) * BKT * 2;
@@ -274,7 +278,10 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
     }
   };
 
@@ -306,40 +313,76 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
     }
   }
 
-  // ---------------- fused BN statistics of the bf16-rounded output (per column, this tile's rows)
+  // Element (m, n) of lane's acc[i][j][r]:
+  //   SWAP : m = mb + i*16 + (lane&15),        n = nb + j*16 + (lane>>4)*4 + r
+  //   !SWAP: m = mb + i*16 + (lane>>4)*4 + r,  n = nb + j*16 + (lane&15)
+  const int mb = m0 + wm * WM, nb = n0 + wn * WN;
+
+  // ---------------- fused BN statistics of the bf16-rounded output (per column n, this tile's rows)
   if (a.stats) {
-    float cs[TN], cq[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      cs[j] = 0.f;
-      cq[j] = 0.f;
-      const int n = n0 + wn * WN + j * 16 + (lane & 15);
-      const float bias = (a.bias && n < a.N) ? a.bias[n] : 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-          float v = acc[i][j][r] + bias;
-          if (a.relu) v = fmaxf(v, 0.f);
-          v = bf16_to_f32(f32_to_bf16(v));
-          if (m < a.M) {
-            cs[j] += v;
-            cq[j] = fmaf(v, v, cq[j]);
-          }
-        }
-      cs[j] += __shfl_xor(cs[j], 16, 64);
-      cs[j] += __shfl_xor(cs[j], 32, 64);
-      cq[j] += __shfl_xor(cq[j], 16, 64);
-      cq[j] += __shfl_xor(cq[j], 32, 64);
-    }
     float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN cols][2]; LDS is free after the loop
-    if (lane < 16) {
+    if constexpr (SWAP) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = wn * WN + j * 16 + lane;
-        red[(wm * BN + col) * 2 + 0] = cs[j];
-        red[(wm * BN + col) * 2 + 1] = cq[j];
+        float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = nb + j * 16 + (lane >> 4) * 4 + r;
+          const float bias = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const int m = mb + i * 16 + (lane & 15);
+            float v = acc[i][j][r] + bias;
+            if (a.relu) v = fmaxf(v, 0.f);
+            v = bf16_to_f32(f32_to_bf16(v));
+            if (m < a.M) {
+              cs[r] += v;
+              cq[r] = fmaf(v, v, cq[r]);
+            }
+          }
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            cs[r] += __shfl_xor(cs[r], o, 64);
+            cq[r] += __shfl_xor(cq[r], o, 64);
+          }
+        }
+        if ((lane & 15) == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int col = wn * WN + j * 16 + (lane >> 4) * 4 + r;
+            red[(wm * BN + col) * 2 + 0] = cs[r];
+            red[(wm * BN + col) * 2 + 1] = cq[r];
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float cs = 0.f, cq = 0.f;
+        const int n = nb + j * 16 + (lane & 15);
+        const float bias = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = mb + i * 16 + (lane >> 4) * 4 + r;
+            float v = acc[i][j][r] + bias;
+            if (a.relu) v = fmaxf(v, 0.f);
+            v = bf16_to_f32(f32_to_bf16(v));
+            if (m < a.M) {
+              cs += v;
+              cq = fmaf(v, v, cq);
+            }
+          }
+        cs += __shfl_xor(cs, 16, 64);
+        cs += __shfl_xor(cs, 32, 64);
+        cq += __shfl_xor(cq, 16, 64);
+        cq += __shfl_xor(cq, 32, 64);
+        if (lane < 16) {
+          const int col = wn * WN + j * 16 + lane;
+          red[(wm * BN + col) * 2 + 0] = cs;
+          red[(wm * BN + col) * 2 + 1] = cq;
+        }
       }
     }
     __syncthreads();
@@ -353,26 +396,111 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
     }
   }
 
-  // ---------------- epilogue: lane holds rows (lane>>4)*4 + r, column lane&15 of each 16x16 tile
-  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  // ---------------- epilogue (mode tested once per block, bias preloaded: no loads in the store loops)
+  if constexpr (SWAP) {
+    float bias[TN][4];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + col_l;
-    if (n >= a.N) continue;
-    const float bias = a.bias ? a.bias[n] : 0.f;
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+      for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
+    if (a.bias) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + i * 16 + row_l + r;
-        if (m >= a.M) continue;
-        float v = acc[i][j][r] + bias;
-        if (a.relu) v = fmaxf(v, 0.f);
-        const int64_t o = a.trans_out ? (int64_t)n * a.ldc + m : (int64_t)m * a.ldc + n;
-        if (a.out_mode == OUT_BF16) reinterpret_cast<uint16_t*>(a.Cp)[o] = f32_to_bf16(v);
-        else if (a.out_mode == OUT_F32) reinterpret_cast<float*>(a.Cp)[o] = v;
-        else if (a.out_mode == OUT_F32_ADD) reinterpret_cast<float*>(a.Cp)[o] += v;
-        else atomicAdd(reinterpret_cast<float*>(a.Cp) + o, v);
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = nb + j * 16 + (lane >> 4) * 4 + r;
+          bias[j][r] = a.bias[min(n, a.N - 1)];
+        }
+    }
+    const bool relu = a.relu != 0;
+    if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 3) == 0 && (a.N & 3) == 0) {
+      uint16_t* Cb = reinterpret_cast<uint16_t*>(a.Cp);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = nb + j * 16 + (lane >> 4) * 4;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = acc[i][j][r] + bias[j][r];
+            if (relu) v[r] = fmaxf(v[r], 0.f);
+          }
+          uint2 w2;
+          w2.x = pack_bf16x2(v[0], v[1]);
+          w2.y = pack_bf16x2(v[2], v[3]);
+          if (m < a.M && n < a.N) *reinterpret_cast<uint2*>(Cb + (int64_t)m * a.ldc + n) = w2;
+        }
+      }
+    } else if (a.out_mode == OUT_F32_ATOMIC && a.trans_out) {
+      float* Cf = reinterpret_cast<float*>(a.Cp);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = nb + j * 16 + (lane >> 4) * 4 + r;
+            if (m < a.M && n < a.N) atomicAdd(Cf + (int64_t)n * a.ldc + m, acc[i][j][r]);
+          }
+      }
+    } else {  // generic (ragged N, other modes): element stores
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = nb + j * 16 + (lane >> 4) * 4 + r;
+            if (m >= a.M || n >= a.N) continue;
+            float v = acc[i][j][r] + bias[j][r];
+            if (relu) v = fmaxf(v, 0.f);
+            const int64_t o = a.trans_out ? (int64_t)n * a.ldc + m : (int64_t)m * a.ldc + n;
+            if (a.out_mode == OUT_BF16) reinterpret_cast<uint16_t*>(a.Cp)[o] = f32_to_bf16(v);
+            else if (a.out_mode == OUT_F32) reinterpret_cast<float*>(a.Cp)[o] = v;
+            else if (a.out_mode == OUT_F32_ADD) reinterpret_cast<float*>(a.Cp)[o] += v;
+            else atomicAdd(reinterpret_cast<float*>(a.Cp) + o, v);
+          }
+      }
+    }
+  } else {
+    float bias[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bias[j] = a.bias ? a.bias[min(nb + j * 16 + (lane & 15), a.N - 1)] : 0.f;
+    if (a.out_mode == OUT_F32_ATOMIC && !a.trans_out) {
+      float* Cf = reinterpret_cast<float*>(a.Cp);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = nb + j * 16 + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = mb + i * 16 + (lane >> 4) * 4 + r;
+            if (m < a.M && n < a.N) atomicAdd(Cf + (int64_t)m * a.ldc + n, acc[i][j][r] + bias[j]);
+          }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = nb + j * 16 + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = mb + i * 16 + (lane >> 4) * 4 + r;
+            if (m >= a.M || n >= a.N) continue;
+            float v = acc[i][j][r] + bias[j];
+            if (a.relu) v = fmaxf(v, 0.f);
+            const int64_t o = a.trans_out ? (int64_t)n * a.ldc + m : (int64_t)m * a.ldc + n;
+            if (a.out_mode == OUT_BF16) reinterpret_cast<uint16_t*>(a.Cp)[o] = f32_to_bf16(v);
+            else if (a.out_mode == OUT_F32) reinterpret_cast<float*>(a.Cp)[o] = v;
+            else if (a.out_mode == OUT_F32_ADD) reinterpret_cast<float*>(a.Cp)[o] += v;
+            else atomicAdd(reinterpret_cast<float*>(a.Cp) + o, v);
+          }
       }
     }
   }
@@ -401,7 +529,9 @@ void launch_t(IgemmArgs& a, hipStream_t s) {
   splits = (nkt + a.kps - 1) / a.kps;
   const int grid = tiles * splits;
   if (grid == 0) return;
-  igemm_kernel<AK, BK, BM, BN><<<grid, NT, 0, s>>>(a);
+  // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
+  if (a.out_mode == OUT_BF16 || a.trans_out) igemm_kernel<AK, BK, BM, BN, true><<<grid, NT, 0, s>>>(a);
+  else igemm_kernel<AK, BK, BM, BN, false><<<grid, NT, 0, s>>>(a);
 }
 
 // tile choice: narrow N -> 256x64 (if M is large) or 128x64; otherwise 128x128
