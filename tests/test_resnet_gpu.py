@@ -61,7 +61,7 @@ def test_graph_capture_step(gpu):
 def test_resnet50_steps_reduce_loss(gpu):
     store, model = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=0)
     assert 23_000_000 < store.num_params() < 24_000_000
-    opt = MomentumOptimizer(store, 0.01, momentum=0.9)
+    opt = MomentumOptimizer(store, 0.002, momentum=0.9)  # CPU fp32 reference: 3.05 -> 1.93
     tr = ClassifierTrainer(store, model, opt)
     g = torch.Generator().manual_seed(0)
     img = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, generator=g).to(gpu)
