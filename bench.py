@@ -48,6 +48,7 @@ def parse(argv=None):
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph (N=1 only)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--backend", default=None, help="process-group backend (default nccl = RCCL)")
     return ap.parse_args(argv)
 
 
@@ -63,7 +64,7 @@ def synthetic_batches(n, batch, device, seed):
 
 def main(argv=None):
     a = parse(argv)
-    dev = init_distributed(device="cuda")
+    dev = init_distributed(backend=a.backend, device="cuda")
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     torch.manual_seed(1234 + rank)

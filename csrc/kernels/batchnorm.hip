@@ -34,7 +34,20 @@ __global__ void __launch_bounds__(256) bn_stats_vec_kernel(const uint16_t* __res
   const int cv = t % tpr, r0 = t / tpr;
   float s[8] = {0}, q[8] = {0};
   const int64_t stride = (int64_t)gridDim.x * rpb;
-  for (int64_t r = (int64_t)blockIdx.x * rpb + r0; r < M; r += stride) {
+  int64_t r = (int64_t)blockIdx.x * rpb + r0;
+  for (; r + 3 * stride < M; r += 4 * stride) {
+    U4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const U4*>(x + (r + u * stride) * C + cv * 8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s[i] += f[i]; q[i] = fmaf(f[i], f[i], q[i]); }
+    }
+  }
+  for (; r < M; r += stride) {
     float f[8];
     unpack8(*reinterpret_cast<const U4*>(x + r * C + cv * 8), f);
 #pragma unroll
@@ -234,12 +247,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* 
   }
   float sg[8] = {0}, sx[8] = {0};
   const int64_t stride = (int64_t)gridDim.x * rpb;
-  for (int64_t r = (int64_t)blockIdx.x * rpb + r0; r < M; r += stride) {
-    const int64_t off = r * C + cv * 8;
+  auto accum = [&](const U4& gv, const U4& xv, const U4& rv) {
     float gf[8], xf[8], rf[8];
-    unpack8(*reinterpret_cast<const U4*>(g + off), gf);
-    unpack8(*reinterpret_cast<const U4*>(x + off), xf);
-    if (RES && RELU) unpack8(*reinterpret_cast<const U4*>(res + off), rf);
+    unpack8(gv, gf);
+    unpack8(xv, xf);
+    if (RES && RELU) unpack8(rv, rf);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float gg = gf[k];
@@ -251,6 +263,27 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* 
       sg[k] += gg;
       sx[k] = fmaf(gg, (xf[k] - mu[k]) * is[k], sx[k]);
     }
+  };
+  // 4 independent rows in flight per thread (the loop is load-latency bound otherwise)
+  constexpr int U = 4;
+  int64_t r = (int64_t)blockIdx.x * rpb + r0;
+  for (; r + (U - 1) * stride < M; r += U * stride) {
+    U4 gv[U], xv[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (r + u * stride) * C + cv * 8;
+      gv[u] = *reinterpret_cast<const U4*>(g + off);
+      xv[u] = *reinterpret_cast<const U4*>(x + off);
+      if (RES && RELU) rv[u] = *reinterpret_cast<const U4*>(res + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) accum(gv[u], xv[u], rv[u]);
+  }
+  for (; r < M; r += stride) {
+    const int64_t off = r * C + cv * 8;
+    U4 rv = {0u, 0u, 0u, 0u};
+    if (RES && RELU) rv = *reinterpret_cast<const U4*>(res + off);
+    accum(*reinterpret_cast<const U4*>(g + off), *reinterpret_cast<const U4*>(x + off), rv);
   }
   __shared__ float lds[256 * 8];
   for (int pass = 0; pass < 2; ++pass) {
@@ -451,7 +484,7 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
   const int64_t n = M * C;
   if (vec_ok(C)) {
     const int rpb = 256 / (C / 8);
-    const int gr = grid_for(M, rpb * 8);
+    const int gr = grid_for(M, rpb * 4);
     TFX_DISPATCH_RR(has_res, relu,
                     (bn_bwd_reduce_vec_kernel<R_, L_><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
   } else {
