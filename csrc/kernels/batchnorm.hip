@@ -98,15 +98,28 @@ __global__ void __launch_bounds__(256) bn_stats_gen_kernel(const uint16_t* __res
   }
 }
 
-// Sum the NSLOT slot rows for channel c (64 channels x 4 slot-lanes per block) and zero them.
-__device__ __forceinline__ void slot_sum_consume(float* __restrict__ slots, int C, int c, int ty, float& s, float& q) {
+// Sum the NSLOT slot rows for 16 channels per block (16 slot-lanes x 4 slots each, all loads in
+// flight before any store), then zero the consumed slots.  Returns the sums in lanes ty == 0.
+__device__ __forceinline__ void slot_sum_consume(float* __restrict__ slots, int C, int c, float& s, float& q) {
+  const int ty = threadIdx.x >> 4;  // 0..15
+  float vs[NSLOT / 16], vq[NSLOT / 16];
   s = 0.f;
   q = 0.f;
   if (c < C) {
-    for (int k = ty; k < NSLOT; k += 4) {
-      float* p = slots + (size_t)k * 2 * C;
-      s += p[c];
-      q += p[C + c];
+#pragma unroll
+    for (int i = 0; i < NSLOT / 16; ++i) {
+      const float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
+      vs[i] = p[c];
+      vq[i] = p[C + c];
+    }
+#pragma unroll
+    for (int i = 0; i < NSLOT / 16; ++i) {
+      s += vs[i];
+      q += vq[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NSLOT / 16; ++i) {
+      float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
       p[c] = 0.f;  // keep the workspace zero for its next use
       p[C + c] = 0.f;
     }
@@ -115,20 +128,23 @@ __device__ __forceinline__ void slot_sum_consume(float* __restrict__ slots, int 
   rs[threadIdx.x] = s;
   rq[threadIdx.x] = q;
   __syncthreads();
-  const int tx = threadIdx.x & 63;
-  s = rs[tx] + rs[tx + 64] + rs[tx + 128] + rs[tx + 192];
-  q = rq[tx] + rq[tx + 64] + rq[tx + 128] + rq[tx + 192];
+  if (ty == 0) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      s += rs[threadIdx.x + 16 * k];
+      q += rq[threadIdx.x + 16 * k];
+    }
+  }
 }
 
 __global__ void __launch_bounds__(256) bn_finalize_kernel(float* __restrict__ slots, int64_t M, int C,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           float eps, float momentum, float* __restrict__ run_mean,
                                                           float* __restrict__ run_var, float* __restrict__ save) {
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   float sum, sq;
-  slot_sum_consume(slots, C, c, ty, sum, sq);
-  if (ty != 0 || c >= C) return;
+  slot_sum_consume(slots, C, c, sum, sq);
+  if ((threadIdx.x >> 4) != 0 || c >= C) return;
   const float inv_m = 1.f / (float)M;
   const float mean = sum * inv_m;
   const float var = fmaxf(sq * inv_m - mean * mean, 0.f);
@@ -149,11 +165,10 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(float* __restrict__ sl
 __global__ void __launch_bounds__(256) bn_slot_reduce_kernel(float* __restrict__ slots, int C,
                                                              float* __restrict__ red, float* __restrict__ dgamma,
                                                              float* __restrict__ dbeta) {
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   float s, q;
-  slot_sum_consume(slots, C, c, ty, s, q);
-  if (ty == 0 && c < C) {
+  slot_sum_consume(slots, C, c, s, q);
+  if ((threadIdx.x >> 4) == 0 && c < C) {
     red[c] = s;
     red[C + c] = q;
     if (dbeta) dbeta[c] += s;
@@ -227,7 +242,7 @@ __global__ void __launch_bounds__(256) bn_apply_gen_kernel(const uint16_t* __res
 }
 
 // ------------------------------------------------------------------ backward reduce
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, int U>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* __restrict__ g,
                                                                 const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ res,
@@ -264,8 +279,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* 
       sx[k] = fmaf(gg, (xf[k] - mu[k]) * is[k], sx[k]);
     }
   };
-  // 4 independent rows in flight per thread (the loop is load-latency bound otherwise)
-  constexpr int U = 4;
+  // U independent rows in flight per thread
   int64_t r = (int64_t)blockIdx.x * rpb + r0;
   for (; r + (U - 1) * stride < M; r += U * stride) {
     U4 gv[U], xv[U], rv[U];
@@ -454,7 +468,7 @@ void bn_stats(const uint16_t* x, int64_t M, int C, float* slots, hipStream_t s) 
 
 void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float* beta, float eps, float momentum,
                  float* run_mean, float* run_var, float* save, hipStream_t s) {
-  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, s>>>(slots, M, C, gamma, beta, eps, momentum, run_mean, run_var,
+  bn_finalize_kernel<<<(C + 15) / 16, 256, 0, s>>>(slots, M, C, gamma, beta, eps, momentum, run_mean, run_var,
                                                    save);
 }
 
@@ -484,15 +498,27 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
   const int64_t n = M * C;
   if (vec_ok(C)) {
     const int rpb = 256 / (C / 8);
-    const int gr = grid_for(M, rpb * 4);
-    TFX_DISPATCH_RR(has_res, relu,
-                    (bn_bwd_reduce_vec_kernel<R_, L_><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
+    static const int U = [] {
+      const char* e = getenv("TFX_BN_RED_U");
+      return e ? atoi(e) : 1;
+    }();
+    const int gr = grid_for(M, rpb * (U >= 4 ? 4 : 8));
+    if (U >= 4) {
+      TFX_DISPATCH_RR(has_res, relu,
+                      (bn_bwd_reduce_vec_kernel<R_, L_, 4><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
+    } else if (U == 2) {
+      TFX_DISPATCH_RR(has_res, relu,
+                      (bn_bwd_reduce_vec_kernel<R_, L_, 2><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
+    } else {
+      TFX_DISPATCH_RR(has_res, relu,
+                      (bn_bwd_reduce_vec_kernel<R_, L_, 1><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
+    }
   } else {
     dim3 grid((C + 63) / 64, grid_for(M, 64));
     TFX_DISPATCH_RR(has_res, relu,
                     (bn_bwd_reduce_gen_kernel<R_, L_><<<grid, 256, 0, s>>>(g, x, res, save, M, C, slots)));
   }
-  bn_slot_reduce_kernel<<<(C + 63) / 64, 256, 0, s>>>(slots, C, red, dgamma, dbeta);
+  bn_slot_reduce_kernel<<<(C + 15) / 16, 256, 0, s>>>(slots, C, red, dgamma, dbeta);
   // with a residual input dres = g' is produced (the host guarantees dres != nullptr then)
   if (C % 8 == 0) {
     const int64_t nvec = n / 8;

@@ -26,6 +26,9 @@ for s in $STEPS; do
     convbench)
       timeout -k 10 400 python scripts/conv_bench.py > gpurun_out/conv_bench.log 2>&1
       rc=$?; echo "convbench rc=$rc"; tail -3 gpurun_out/conv_bench.log; [ $rc -eq 0 ] || exit $rc ;;
+    bnbench)
+      for u in 1; do TFX_BN_RED_U=$u timeout -k 10 200 python scripts/bn_bench.py > gpurun_out/bn_bench_u$u.log 2>&1 || exit 1; done
+      echo bnbench done; tail -1 gpurun_out/bn_bench_u*.log ;;
     prof)
       export TMPDIR=/tmp
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 2 > gpurun_out/prof.log 2>&1
