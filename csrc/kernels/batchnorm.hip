@@ -66,11 +66,11 @@ __global__ void __launch_bounds__(256) bn_stats_vec_kernel(const uint16_t* __res
       }
       __syncthreads();
     }
-    if (r0 == 0) {
-      float* slot = slots + (size_t)(blockIdx.x % NSLOT) * 2 * C + pass * C + cv * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) atomicAdd(slot + i, red[i * 256 + t]);
-    }
+    __syncthreads();
+    // coalesced atomics: consecutive lanes -> consecutive channels (channel c = cv*8 + i lives at
+    // red[i*256 + cv]); a lane-per-8-channel pattern would be a 32-B-strided scatter per instruction
+    float* slot = slots + (size_t)(blockIdx.x % NSLOT) * 2 * C + pass * C;
+    for (int c = t; c < C; c += 256) atomicAdd(slot + c, red[(c & 7) * 256 + (c >> 3)]);
     __syncthreads();
   }
 }
@@ -312,11 +312,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* 
       }
       __syncthreads();
     }
-    if (r0 == 0) {
-      float* slot = slots + (size_t)(blockIdx.x % NSLOT) * 2 * C + pass * C + cv * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) atomicAdd(slot + i, lds[i * 256 + t]);
-    }
+    __syncthreads();
+    float* slot = slots + (size_t)(blockIdx.x % NSLOT) * 2 * C + pass * C;
+    for (int c = t; c < C; c += 256) atomicAdd(slot + c, lds[(c & 7) * 256 + (c >> 3)]);
     __syncthreads();
   }
 }
