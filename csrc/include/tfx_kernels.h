@@ -42,6 +42,7 @@ struct IgemmArgs {
   const uint16_t* B = nullptr;
   int64_t a_bytes = 0, b_bytes = 0;  // extents of A/B (buffer-resource bounds; must be < 2 GiB)
   int trans_out = 0;                 // store C[m][n] at Cp[n*ldc + m]
+  const uint16_t* addend = nullptr;  // bf16 outputs: C = acc + addend (same layout as C; may alias Cp)
   void* Cp = nullptr;
   const float* bias = nullptr;
   int M = 0, N = 0, K = 0;

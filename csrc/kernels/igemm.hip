@@ -427,10 +427,19 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
             v[r] = acc[i][j][r] + bias[j][r];
             if (relu) v[r] = fmaxf(v[r], 0.f);
           }
-          uint2 w2;
-          w2.x = pack_bf16x2(v[0], v[1]);
-          w2.y = pack_bf16x2(v[2], v[3]);
-          if (m < a.M && n < a.N) *reinterpret_cast<uint2*>(Cb + (int64_t)m * a.ldc + n) = w2;
+          if (m < a.M && n < a.N) {
+            if (a.addend) {  // fused residual-branch gradient sum (dX = dgrad + other branch)
+              const uint2 o2 = *reinterpret_cast<const uint2*>(a.addend + (int64_t)m * a.ldc + n);
+              v[0] += __uint_as_float(o2.x << 16);
+              v[1] += __uint_as_float(o2.x & 0xffff0000u);
+              v[2] += __uint_as_float(o2.y << 16);
+              v[3] += __uint_as_float(o2.y & 0xffff0000u);
+            }
+            uint2 w2;
+            w2.x = pack_bf16x2(v[0], v[1]);
+            w2.y = pack_bf16x2(v[2], v[3]);
+            *reinterpret_cast<uint2*>(Cb + (int64_t)m * a.ldc + n) = w2;
+          }
         }
       }
     } else if (a.out_mode == OUT_F32_ATOMIC && a.trans_out) {
@@ -459,6 +468,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
             float v = acc[i][j][r] + bias[j][r];
             if (relu) v = fmaxf(v, 0.f);
             const int64_t o = a.trans_out ? (int64_t)n * a.ldc + m : (int64_t)m * a.ldc + n;
+            if (a.addend) v += bf16_to_f32(a.addend[o]);
             if (a.out_mode == OUT_BF16) reinterpret_cast<uint16_t*>(a.Cp)[o] = f32_to_bf16(v);
             else if (a.out_mode == OUT_F32) reinterpret_cast<float*>(a.Cp)[o] = v;
             else if (a.out_mode == OUT_F32_ADD) reinterpret_cast<float*>(a.Cp)[o] += v;

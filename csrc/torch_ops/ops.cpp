@@ -90,16 +90,25 @@ Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t d
   return conv_fwd_impl(x, w, stride, pad, dil, slots.data_ptr<float>());
 }
 
-Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil) {
+// dX = dgrad(dy) (+ addend: the gradient of x's other consumer, summed in the epilogue; the
+// result is written in place into addend's storage when given)
+Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil,
+                  optional<Tensor> addend) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
-  auto dx = at::empty({g.N, g.H, g.W, g.C}, dy.options());
+  const bool acc = addend.has_value() && addend->defined();
+  if (acc) {
+    CHECK_BF16(*addend); CHECK_CONTIG(*addend);
+    TORCH_CHECK(addend->sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "addend shape");
+  }
+  auto dx = acc ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
   auto a = conv_args(g, stride, pad, dil);
   a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
   a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
   a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
   a.out_mode = tfx::OUT_BF16;
+  if (acc) a.addend = bf(*addend);
   tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
   return dx;
 }

@@ -71,7 +71,7 @@ def main():
         r = {"shape": [N, H, W, C, K, R, st], "count": cnt, "gflop": flops / 1e9}
         slots = torch.zeros(64 * 2 * K, device=dev)
         r["fwd_us"] = timeit(lambda: torch.ops.tfx.conv_fwd_stats(x, w, st, pad, 1, slots), a.iters)
-        r["dgrad_us"] = timeit(lambda: torch.ops.tfx.conv_dgrad(gy, w, list(x.shape), st, pad, 1), a.iters)
+        r["dgrad_us"] = timeit(lambda: torch.ops.tfx.conv_dgrad(gy, w, list(x.shape), st, pad, 1, None), a.iters)
         r["wgrad_us"] = timeit(lambda: torch.ops.tfx.conv_wgrad(gy, x, dw, st, pad, 1, True), a.iters)
         r["mi_fwd_us"] = timeit(lambda: F.conv2d(xc, wc, stride=st, padding=pad), a.iters)
         r["mi_dgrad_us"] = timeit(lambda: torch.nn.grad.conv2d_input(xc.shape, wc, gyc, stride=st, padding=pad), a.iters)

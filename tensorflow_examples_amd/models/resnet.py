@@ -39,16 +39,17 @@ class _BN:
             self.var = store.add_state("moving_variance", torch.ones(c))
         self.ws = BNWorkspace(c)
 
-    def __call__(self, x, training, relu=False, residual=None, stats_ready=False):
+    def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None):
         ws = self.ws.get(x.device) if x.device.type == "cuda" else None
         return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
-                              eps=1e-5, residual=residual, relu=relu, workspace=ws, stats_ready=stats_ready)
+                              eps=1e-5, residual=residual, relu=relu, workspace=ws, stats_ready=stats_ready,
+                              residual_grad_sink=residual_sink)
 
-    def after_conv(self, conv, x, training, relu=False, residual=None):
+    def after_conv(self, conv, x, training, relu=False, residual=None, sink=None, residual_sink=None):
         """conv -> BN with the BN statistics produced by the conv's epilogue (GPU, training)."""
         fused = training and x.device.type == "cuda"
-        y = conv(x, self.ws.get(x.device) if fused else None)
-        return self(y, training, relu=relu, residual=residual, stats_ready=fused)
+        y = conv(x, self.ws.get(x.device) if fused else None, sink)
+        return self(y, training, relu=relu, residual=residual, stats_ready=fused, residual_sink=residual_sink)
 
 
 class _Conv:
@@ -56,8 +57,8 @@ class _Conv:
         self.w = store.variable([cout, k, k, cin], HeNormal(), name=name)
         self.stride, self.pad = stride, k // 2
 
-    def __call__(self, x, bn_stats_into=None):
-        return ops.conv2d(x, self.w, self.stride, self.pad, bn_stats_into=bn_stats_into)
+    def __call__(self, x, bn_stats_into=None, grad_sink=None):
+        return ops.conv2d(x, self.w, self.stride, self.pad, bn_stats_into=bn_stats_into, grad_sink=grad_sink)
 
 
 class Bottleneck:
@@ -78,9 +79,14 @@ class Bottleneck:
                 self.bp = _BN(store, cout, "shortcut_bn")
 
     def __call__(self, x, training):
-        o = self.b1.after_conv(self.c1, x, training, relu=True)
+        # x feeds conv1 and the shortcut: the shortcut's input-gradient is folded into conv1's
+        # dgrad epilogue (GradSink) instead of an autograd add kernel
+        prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda") else (None, None)
+        o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons)
         o = self.b2.after_conv(self.c2, o, training, relu=True)
-        sc = x if self.proj is None else self.bp.after_conv(self.proj, x, training)
+        if self.proj is None:
+            return self.b3.after_conv(self.c3, o, training, relu=True, residual=x, residual_sink=prod)
+        sc = self.bp.after_conv(self.proj, x, training, sink=prod)
         return self.b3.after_conv(self.c3, o, training, relu=True, residual=sc)
 
 
@@ -99,8 +105,11 @@ class Basic:
                 self.bp = _BN(store, width, "shortcut_bn")
 
     def __call__(self, x, training):
-        o = self.b1.after_conv(self.c1, x, training, relu=True)
-        sc = x if self.proj is None else self.bp.after_conv(self.proj, x, training)
+        prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda") else (None, None)
+        o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons)
+        if self.proj is None:
+            return self.b2.after_conv(self.c2, o, training, relu=True, residual=x, residual_sink=prod)
+        sc = self.bp.after_conv(self.proj, x, training, sink=prod)
         return self.b2.after_conv(self.c2, o, training, relu=True, residual=sc)
 
 

@@ -59,8 +59,8 @@ def _conv_ref(x, w, stride=1, pad=0, dil=1):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into):
-        ctx.w, ctx.cfg = w, (stride, pad, dil)
+    def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into, sink):
+        ctx.w, ctx.cfg, ctx.sink = w, (stride, pad, dil), sink
         ctx.native = _native.use_native(x)
         ctx.save_for_backward(x)
         if ctx.native:
@@ -77,24 +77,67 @@ class _Conv2d(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         if ctx.native:
             gy = gy.contiguous()
-            dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil) if need_dx else None
+            sink = ctx.sink
+            dx = None
+            if need_dx:
+                if sink is not None and sink.mode == "consume":
+                    # last consumer of x in backward order: fold the other branch's gradient in
+                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, sink.take())
+                else:
+                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, None)
+                    if sink is not None:  # mode "produce": park it for the last consumer
+                        sink.put(dx)
+                        dx = None
             if w.trainable:
                 torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
                 _grad_ready(w)
-            return dx, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None
         dx = _ref_param_grads(lambda xx, ww: _conv_ref(xx, ww, stride, pad, dil), x, [w], gy, need_dx)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
 def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int = 1,
-           bn_stats_into: Optional[torch.Tensor] = None):
+           bn_stats_into: Optional[torch.Tensor] = None, grad_sink: Optional["GradSink"] = None):
     """NHWC conv, weight stored [Ko, R, S, C]. GPU: implicit-GEMM MFMA kernels (igemm.hip).
 
     ``bn_stats_into`` = the following BN layer's slot workspace (:class:`BNWorkspace`): the
     per-channel sum / sum-of-squares of ``y`` are then produced by the conv's GEMM epilogue and the
     BN (``stats_ready=True``) skips its own statistics pass over ``y``.  Ignored on CPU."""
-    ws = bn_stats_into if (bn_stats_into is not None and x.device.type == "cuda") else None
-    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, ws)
+    gpu = x.device.type == "cuda"
+    ws = bn_stats_into if (bn_stats_into is not None and gpu) else None
+    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, ws, grad_sink if gpu else None)
+
+
+class GradSink:
+    """Fuses the gradient sum of a tensor with two consumers (a ResNet block input feeds conv1 and
+    the residual / projection branch).  The branch that runs FIRST in backward ("produce") parks
+    its input-gradient here instead of returning it to autograd; the consumer that runs LAST
+    ("consume", conv1's data-gradient) adds it in its GEMM epilogue -- no separate add kernel.
+    Backward order is fixed by autograd's sequence numbers: conv1 is created first in the block,
+    so it runs last (the ``take`` assertion guards this)."""
+
+    def __init__(self, mode: str):
+        assert mode in ("produce", "consume")
+        self.mode = mode
+        self.buf = None
+        self.peer: Optional["GradSink"] = None
+
+    @staticmethod
+    def pair():
+        prod, cons = GradSink("produce"), GradSink("consume")
+        prod.peer = cons
+        cons.peer = prod
+        return prod, cons
+
+    def put(self, g):
+        tgt = self.peer if self.peer is not None else self
+        assert tgt.buf is None, "gradient sink already holds a gradient"
+        tgt.buf = g
+
+    def take(self):
+        g, self.buf = self.buf, None
+        assert g is not None, "gradient sink consumed before its producer ran"
+        return g
 
 
 class BNWorkspace:
@@ -139,8 +182,9 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
-                training, ws, stats_ready):
+                training, ws, stats_ready, res_sink):
         ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
+        ctx.res_sink = res_sink
         ctx.native = _native.use_native(x)
         ctx.has_res = res is not None
         g_t = gamma.master if gamma is not None else None
@@ -175,7 +219,11 @@ class _BatchNorm(torch.autograd.Function):
                                                  gamma.grad if train_p else None, beta.grad if train_p else None)
             if train_p:
                 _grad_ready(gamma, beta)
-            return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None
+            if ctx.has_res and ctx.res_sink is not None:
+                ctx.res_sink.put(dres)
+                dres = None
+            return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None, \
+                None
         x, res = ctx.saved_tensors
         with torch.enable_grad():
             xs = x.detach().requires_grad_(True)
@@ -190,19 +238,21 @@ class _BatchNorm(torch.autograd.Function):
             gamma.grad.add_(grads[0])
             beta.grad.add_(grads[1])
             _grad_ready(gamma, beta)
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
                momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False,
-               workspace: Optional[torch.Tensor] = None, stats_ready: bool = False):
+               workspace: Optional[torch.Tensor] = None, stats_ready: bool = False,
+               residual_grad_sink: Optional[GradSink] = None):
     """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
     ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass)."""
     anchor = gamma.store.anchor if gamma is not None else None
     if x.device.type != "cuda":
         workspace = None
+    sink = residual_grad_sink if (x.device.type == "cuda" and residual is not None) else None
     return _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
-                            workspace, stats_ready and training and workspace is not None)
+                            workspace, stats_ready and training and workspace is not None, sink)
 
 
 # ====================================================================== dense

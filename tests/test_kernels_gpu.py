@@ -46,8 +46,12 @@ def test_conv_fwd_dgrad_wgrad(gpu, shape):
     assert _rel(y, yr.permute(0, 2, 3, 1)) < 1e-2
     gy = _bf(torch.randn_like(y.float()))
     yr.backward(gy.float().permute(0, 3, 1, 2))
-    dx = torch.ops.tfx.conv_dgrad(gy, w, list(x.shape), st, pad, 1)
+    dx = torch.ops.tfx.conv_dgrad(gy, w, list(x.shape), st, pad, 1, None)
     assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    add = _bf(torch.randn_like(dx.float()))
+    ref_sum = dx.float() + add.float()
+    dx2 = torch.ops.tfx.conv_dgrad(gy, w, list(x.shape), st, pad, 1, add)  # epilogue-fused sum, in place
+    assert dx2.data_ptr() == add.data_ptr() and _rel(dx2, ref_sum) < 1e-2
     dw = torch.zeros(Ko, R, R, C, device=gpu)
     torch.ops.tfx.conv_wgrad(gy, x, dw, st, pad, 1, False)
     assert _rel(dw, wr.grad.permute(0, 2, 3, 1)) < 5e-3
