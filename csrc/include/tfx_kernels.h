@@ -96,4 +96,31 @@ void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, f
 void sumsq_flat(const void* g, bool g_bf16, int64_t n, float* out, hipStream_t s);
 void cast_f32_bf16(const float* x, int64_t n, uint16_t* y, hipStream_t s);
 
+// ---------------------------------------------------------------- pooling (NHWC bf16)
+void maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, uint16_t* y,
+                 uint8_t* arg, hipStream_t st);
+void maxpool_bwd(const uint16_t* dy, const uint8_t* arg, int N, int H, int W, int C, int k, int s, int pad, int P,
+                 int Q, uint16_t* dx, hipStream_t st);
+void avgpool_fwd(const uint16_t* x, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, uint16_t* y,
+                 hipStream_t st);
+void avgpool_bwd(const uint16_t* dy, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, uint16_t* dx,
+                 hipStream_t st);
+
+// ---------------------------------------------------------------- sparse (word2vec) / recurrent (LSTM)
+void embedding_gather(const float* table, int64_t V, int D, const int64_t* ids, int64_t n, void* out, bool out_bf16,
+                      hipStream_t s);
+void embedding_scatter_add(float* table, int64_t V, int D, const int64_t* ids, int64_t n, const float* rows,
+                           float alpha, hipStream_t s);
+void log_uniform_sample(int64_t n, int64_t range, uint64_t seed, const int64_t* seed_dev, const int64_t* ids_in,
+                        int64_t* out, float* logq, int num_expected, hipStream_t s);
+void skipgram_batch(const int32_t* corpus, int64_t N, int B, int window, uint64_t seed, const int64_t* seed_dev,
+                    int64_t* centers, int64_t* labels, hipStream_t s);
+void sampled_loss(bool softmax, const float* E, const float* Wt, const float* bt, const float* nl, int B, int S, int D,
+                  const float* logq_t, const float* logq_n, const int64_t* tid, const int64_t* sid, float gscale,
+                  float* loss, float* dn, float* dE, float* dWt, float* dbt, hipStream_t s);
+void lstm_cell_fwd(const float* gx, const float* gh, const float* bias, const float* c_prev, int B, int H,
+                   float* act, float* c, float* h, uint16_t* h16, hipStream_t s);
+void lstm_cell_bwd(const float* act, const float* c, const float* c_prev, const float* dh, const float* dc_next,
+                   int B, int H, float* dgates, uint16_t* dg16, float* dc_prev, hipStream_t s);
+
 }  // namespace tfx

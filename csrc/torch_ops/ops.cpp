@@ -362,9 +362,204 @@ void cast_f32_bf16(Tensor x, Tensor y) {
   tfx::cast_f32_bf16(x.data_ptr<float>(), x.numel(), bfm(y), cur_stream());
 }
 
+// ------------------------------------------------------------------ pooling (NHWC bf16)
+int64_t pool_out(int64_t H, int64_t k, int64_t s, int64_t pad) { return (H + 2 * pad - k) / s + 1; }
+
+std::tuple<Tensor, Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 4 && k >= 1 && k <= 15 && s >= 1 && pad >= 0 && pad < k, "maxpool args");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t P = pool_out(H, k, s, pad), Q = pool_out(W, k, s, pad);
+  TORCH_CHECK(P > 0 && Q > 0, "maxpool output is empty");
+  auto y = at::empty({N, P, Q, C}, x.options());
+  auto arg = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  tfx::maxpool_fwd(bf(x), N, H, W, C, k, s, pad, P, Q, bfm(y), arg.data_ptr<uint8_t>(), cur_stream());
+  return {y, arg};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor arg, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(arg);
+  TORCH_CHECK(arg.scalar_type() == at::kByte && arg.sizes() == dy.sizes(), "argmax shape");
+  const int64_t N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  TORCH_CHECK(P == pool_out(H, k, s, pad) && Q == pool_out(W, k, s, pad), "maxpool_bwd geometry");
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  tfx::maxpool_bwd(bf(dy), arg.data_ptr<uint8_t>(), N, H, W, C, k, s, pad, P, Q, bfm(dx), cur_stream());
+  return dx;
+}
+
+Tensor avgpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 4 && k >= 1 && s >= 1 && pad >= 0 && pad < k, "avgpool args");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t P = pool_out(H, k, s, pad), Q = pool_out(W, k, s, pad);
+  TORCH_CHECK(P > 0 && Q > 0, "avgpool output is empty");
+  auto y = at::empty({N, P, Q, C}, x.options());
+  tfx::avgpool_fwd(bf(x), N, H, W, C, k, s, pad, P, Q, bfm(y), cur_stream());
+  return y;
+}
+
+Tensor avgpool_bwd(Tensor dy, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy);
+  const int64_t N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  TORCH_CHECK(P == pool_out(H, k, s, pad) && Q == pool_out(W, k, s, pad), "avgpool_bwd geometry");
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  tfx::avgpool_bwd(bf(dy), N, H, W, C, k, s, pad, P, Q, bfm(dx), cur_stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------ sparse embedding / sampled loss
+void check_table(const Tensor& table) {
+  CHECK_DEV(table); CHECK_F32(table); CHECK_CONTIG(table);
+  TORCH_CHECK(table.dim() == 2 && table.size(1) % 4 == 0, "embedding table must be [V, D] with D % 4 == 0");
+  check_aligned16(table, "table");
+}
+
+Tensor embedding_gather(Tensor table, Tensor ids, bool out_bf16) {
+  check_table(table);
+  CHECK_DEV(ids); CHECK_CONTIG(ids);
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "ids must be int64");
+  const int64_t n = ids.numel(), D = table.size(1);
+  auto out = at::empty({n, D}, table.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  if (n) tfx::embedding_gather(table.data_ptr<float>(), table.size(0), D, ids.data_ptr<int64_t>(), n, out.data_ptr(),
+                               out_bf16, cur_stream());
+  return out;
+}
+
+void embedding_scatter_add(Tensor table, Tensor ids, Tensor rows, double alpha) {
+  check_table(table);
+  CHECK_DEV(ids); CHECK_CONTIG(ids); CHECK_CONTIG(rows); CHECK_F32(rows);
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "ids must be int64");
+  const int64_t n = ids.numel(), D = table.size(1);
+  TORCH_CHECK(rows.numel() == n * D, "rows must be [n, D]");
+  if (n) tfx::embedding_scatter_add(table.data_ptr<float>(), table.size(0), D, ids.data_ptr<int64_t>(), n,
+                                    rows.data_ptr<float>(), alpha, cur_stream());
+}
+
+std::tuple<Tensor, Tensor> log_uniform_sample(int64_t n, int64_t range, int64_t seed, int64_t num_expected,
+                                              at::Device device, optional<Tensor> seed_t) {
+  TORCH_CHECK(n > 0 && range > 0, "sampler args");
+  const int64_t* sd = nullptr;
+  if (seed_t.has_value() && seed_t->defined()) {
+    TORCH_CHECK(seed_t->scalar_type() == at::kLong && seed_t->is_cuda() && seed_t->numel() >= 1, "seed tensor");
+    sd = seed_t->data_ptr<int64_t>();
+  }
+  auto opts = at::TensorOptions().device(device);
+  auto ids = at::empty({n}, opts.dtype(at::kLong));
+  auto logq = at::empty({n}, opts.dtype(at::kFloat));
+  tfx::log_uniform_sample(n, range, (uint64_t)seed, sd, nullptr, ids.data_ptr<int64_t>(), logq.data_ptr<float>(),
+                          (int)num_expected, cur_stream());
+  return {ids, logq};
+}
+
+Tensor log_uniform_logq(Tensor ids, int64_t range, int64_t num_expected) {
+  CHECK_DEV(ids); CHECK_CONTIG(ids);
+  TORCH_CHECK(ids.scalar_type() == at::kLong && range > 0, "log_uniform_logq args");
+  auto logq = at::empty({ids.numel()}, ids.options().dtype(at::kFloat));
+  if (ids.numel())
+    tfx::log_uniform_sample(ids.numel(), range, 0, nullptr, ids.data_ptr<int64_t>(), nullptr, logq.data_ptr<float>(),
+                            (int)num_expected, cur_stream());
+  return logq;
+}
+
+std::tuple<Tensor, Tensor> skipgram_batch(Tensor corpus, int64_t B, int64_t window, int64_t seed,
+                                          optional<Tensor> seed_t) {
+  CHECK_DEV(corpus); CHECK_CONTIG(corpus);
+  TORCH_CHECK(corpus.scalar_type() == at::kInt, "corpus must be int32");
+  TORCH_CHECK(B > 0 && window >= 1 && corpus.numel() > 2 * window, "skipgram_batch args");
+  const int64_t* sd = nullptr;
+  if (seed_t.has_value() && seed_t->defined()) {
+    TORCH_CHECK(seed_t->scalar_type() == at::kLong && seed_t->is_cuda(), "seed tensor");
+    sd = seed_t->data_ptr<int64_t>();
+  }
+  auto c = at::empty({B}, corpus.options().dtype(at::kLong)), l = at::empty({B}, corpus.options().dtype(at::kLong));
+  tfx::skipgram_batch(corpus.data_ptr<int32_t>(), corpus.numel(), B, window, (uint64_t)seed, sd, c.data_ptr<int64_t>(),
+                      l.data_ptr<int64_t>(), cur_stream());
+  return {c, l};
+}
+
+// E, Wt: [B, D] f32 (gathered input / true-class rows); bt: [B] true-class biases (optional);
+// neg_logits: [B, S] = E Ws^T + bs.  Returns (loss_rows [B], dneg [B,S], dE [B,D], dWt [B,D], dbt [B]).
+std::vector<Tensor> sampled_loss(Tensor E, Tensor Wt, optional<Tensor> bt, Tensor neg_logits, optional<Tensor> logq_t,
+                                 optional<Tensor> logq_n, optional<Tensor> true_ids, optional<Tensor> sampled_ids,
+                                 double gscale, bool softmax) {
+  CHECK_DEV(E); CHECK_F32(E); CHECK_CONTIG(E); CHECK_F32(Wt); CHECK_CONTIG(Wt);
+  CHECK_F32(neg_logits); CHECK_CONTIG(neg_logits);
+  TORCH_CHECK(E.dim() == 2 && Wt.sizes() == E.sizes() && neg_logits.dim() == 2, "sampled_loss shapes");
+  const int64_t B = E.size(0), D = E.size(1), S = neg_logits.size(1);
+  TORCH_CHECK(neg_logits.size(0) == B, "neg_logits must be [B, S]");
+  if (fp(bt)) TORCH_CHECK(bt->numel() == B && bt->is_contiguous(), "bt");
+  if (fp(logq_t)) TORCH_CHECK(logq_t->numel() == B, "logq_true");
+  if (fp(logq_n)) TORCH_CHECK(logq_n->numel() == S, "logq_sampled");
+  const bool hits = true_ids.has_value() && true_ids->defined() && sampled_ids.has_value() && sampled_ids->defined();
+  if (hits) TORCH_CHECK(true_ids->numel() == B && sampled_ids->numel() == S && true_ids->scalar_type() == at::kLong &&
+                        sampled_ids->scalar_type() == at::kLong, "accidental-hit ids");
+  auto opts = E.options();
+  auto loss = at::empty({B}, opts), dn = at::empty({B, S}, opts), dE = at::empty({B, D}, opts),
+       dWt = at::empty({B, D}, opts), dbt = at::empty({B}, opts);
+  tfx::sampled_loss(softmax, E.data_ptr<float>(), Wt.data_ptr<float>(), fp(bt), neg_logits.data_ptr<float>(), B, S, D,
+                    fp(logq_t), fp(logq_n), hits ? true_ids->data_ptr<int64_t>() : nullptr,
+                    hits ? sampled_ids->data_ptr<int64_t>() : nullptr, gscale, loss.data_ptr<float>(),
+                    dn.data_ptr<float>(), dE.data_ptr<float>(), dWt.data_ptr<float>(), dbt.data_ptr<float>(),
+                    cur_stream());
+  return {loss, dn, dE, dWt, dbt};
+}
+
+// ------------------------------------------------------------------ LSTM cell
+// gx, gh: [B, 4H] f32 (gh optional); bias [4H] optional; c_prev [B, H] optional
+// outputs written into act [B, 4H], c [B, H], h [B, H] (+ optional bf16 copy of h)
+void lstm_cell_fwd(Tensor gx, optional<Tensor> gh, optional<Tensor> bias, optional<Tensor> c_prev, Tensor act,
+                   Tensor c, Tensor h, optional<Tensor> h16) {
+  CHECK_DEV(gx); CHECK_F32(gx); CHECK_CONTIG(gx); CHECK_CONTIG(act); CHECK_CONTIG(c); CHECK_CONTIG(h);
+  const int64_t B = c.size(0), H = c.size(1);
+  TORCH_CHECK(gx.numel() == B * 4 * H && act.numel() == B * 4 * H && h.numel() == B * H, "lstm shapes");
+  if (fp(gh)) TORCH_CHECK(gh->numel() == B * 4 * H && gh->is_contiguous(), "gh shape");
+  if (fp(bias)) TORCH_CHECK(bias->numel() == 4 * H, "bias shape");
+  if (fp(c_prev)) TORCH_CHECK(c_prev->numel() == B * H && c_prev->is_contiguous(), "c_prev shape");
+  uint16_t* hb = nullptr;
+  if (h16.has_value() && h16->defined()) {
+    CHECK_BF16(*h16);
+    TORCH_CHECK(h16->numel() == B * H && h16->is_contiguous(), "h16 shape");
+    hb = bfm(*h16);
+  }
+  tfx::lstm_cell_fwd(gx.data_ptr<float>(), fp(gh), fp(bias), fp(c_prev), B, H, act.data_ptr<float>(),
+                     c.data_ptr<float>(), h.data_ptr<float>(), hb, cur_stream());
+}
+
+// dgates (f32) and/or dg16 (bf16 copy for the MFMA GEMMs); dc_prev may alias dc_next (in place)
+void lstm_cell_bwd(Tensor act, Tensor c, optional<Tensor> c_prev, optional<Tensor> dh, optional<Tensor> dc_next,
+                   optional<Tensor> dgates, optional<Tensor> dg16, optional<Tensor> dc_prev) {
+  CHECK_DEV(act); CHECK_F32(act); CHECK_CONTIG(act); CHECK_CONTIG(c);
+  const int64_t B = c.size(0), H = c.size(1);
+  TORCH_CHECK(act.numel() == B * 4 * H, "lstm bwd shapes");
+  if (fp(dgates)) TORCH_CHECK(dgates->numel() == B * 4 * H && dgates->is_contiguous(), "dgates shape");
+  uint16_t* d16 = nullptr;
+  if (dg16.has_value() && dg16->defined()) {
+    CHECK_BF16(*dg16);
+    TORCH_CHECK(dg16->numel() == B * 4 * H && dg16->is_contiguous(), "dg16 shape");
+    d16 = bfm(*dg16);
+  }
+  TORCH_CHECK(fp(dgates) || d16, "lstm_cell_bwd needs an output");
+  for (const auto* t : {&c_prev, &dh, &dc_next, &dc_prev})
+    if (fp(*t)) TORCH_CHECK((*t)->numel() == B * H && (*t)->is_contiguous(), "lstm bwd state shape");
+  tfx::lstm_cell_bwd(act.data_ptr<float>(), c.data_ptr<float>(), fp(c_prev), fp(dh), fp(dc_next), B, H,
+                     fpm(dgates), d16, fpm(dc_prev), cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tfx, m) {
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("embedding_gather", &embedding_gather);
+  m.def("embedding_scatter_add", &embedding_scatter_add);
+  m.def("log_uniform_sample", &log_uniform_sample);
+  m.def("log_uniform_logq", &log_uniform_logq);
+  m.def("sampled_loss", &sampled_loss);
+  m.def("skipgram_batch", &skipgram_batch);
+  m.def("lstm_cell_fwd", &lstm_cell_fwd);
+  m.def("lstm_cell_bwd", &lstm_cell_bwd);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("conv_dgrad", &conv_dgrad);

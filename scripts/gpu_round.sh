@@ -17,6 +17,12 @@ for s in $STEPS; do
     bench)
       timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_native.log 2>&1
       rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench_native.log; [ $rc -eq 0 ] || exit $rc ;;
+    ab)
+      for i in 1 2; do
+        TFX_NO_GRADSINK=1 timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/ab_off_$i.log 2>&1 || exit 1
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/ab_on_$i.log 2>&1 || exit 1
+      done
+      grep -ho '"ms_per_step": [0-9.]*' gpurun_out/ab_*.log ;;
     graph)
       timeout -k 10 400 python bench.py --steps 20 --warmup 5 --graph > gpurun_out/bench_graph.log 2>&1
       rc=$?; echo "graph rc=$rc"; tail -3 gpurun_out/bench_graph.log; [ $rc -eq 0 ] || exit $rc ;;

@@ -12,6 +12,7 @@ the 16-byte vector-load granularity; its weights for channels 3..7 stay exactly 
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -28,6 +29,7 @@ STAGES = {
     152: ("bottleneck", [3, 8, 36, 3]),
 }
 IN_CH_PAD = 8
+_SINK = os.environ.get("TFX_NO_GRADSINK", "0") != "1"  # A/B switch for the fused residual-gradient sum
 
 
 class _BN:
@@ -81,7 +83,7 @@ class Bottleneck:
     def __call__(self, x, training):
         # x feeds conv1 and the shortcut: the shortcut's input-gradient is folded into conv1's
         # dgrad epilogue (GradSink) instead of an autograd add kernel
-        prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda") else (None, None)
+        prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
         o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons)
         o = self.b2.after_conv(self.c2, o, training, relu=True)
         if self.proj is None:
@@ -105,7 +107,7 @@ class Basic:
                 self.bp = _BN(store, width, "shortcut_bn")
 
     def __call__(self, x, training):
-        prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda") else (None, None)
+        prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
         o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons)
         if self.proj is None:
             return self.b2.after_conv(self.c2, o, training, relu=True, residual=x, residual_sink=prod)

@@ -362,6 +362,61 @@ def global_avg_pool(x):
     return _GlobalAvgPool.apply(x)
 
 
+def _pool_ref(x, k, s, pad, kind):
+    xc = x.permute(0, 3, 1, 2)
+    if kind == "max":
+        y = F.max_pool2d(xc, k, s, pad)
+    else:
+        y = F.avg_pool2d(xc, k, s, pad, count_include_pad=False)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+class _Pool2d(torch.autograd.Function):
+    """NHWC k x k pooling (pool.hip). Max pool keeps a uint8 in-window argmax so the backward is a
+    deterministic gather (no atomics); avg pool divides by the in-bounds window size."""
+
+    @staticmethod
+    def forward(ctx, x, k, s, pad, kind):
+        ctx.cfg, ctx.shape = (k, s, pad, kind), x.shape
+        ctx.native = _native.use_native(x) and x.dtype == torch.bfloat16
+        if ctx.native:
+            xc = x.contiguous()
+            if kind == "max":
+                y, arg = torch.ops.tfx.maxpool_fwd(xc, k, s, pad)
+                ctx.save_for_backward(arg)
+                return y
+            ctx.save_for_backward()
+            return torch.ops.tfx.avgpool_fwd(xc, k, s, pad)
+        ctx.save_for_backward(x)
+        return _pool_ref(x, k, s, pad, kind)
+
+    @staticmethod
+    def backward(ctx, gy):
+        k, s, pad, kind = ctx.cfg
+        _, H, W, _ = ctx.shape
+        if ctx.native:
+            g = gy.to(torch.bfloat16).contiguous()
+            if kind == "max":
+                (arg,) = ctx.saved_tensors
+                return torch.ops.tfx.maxpool_bwd(g, arg, H, W, k, s, pad), None, None, None, None
+            return torch.ops.tfx.avgpool_bwd(g, H, W, k, s, pad), None, None, None, None
+        (x,) = ctx.saved_tensors
+        with torch.enable_grad():
+            xx = x.detach().requires_grad_(True)
+            (dx,) = torch.autograd.grad(_pool_ref(xx, k, s, pad, kind), [xx], gy)
+        return dx, None, None, None, None
+
+
+def max_pool2d(x, ksize: int = 2, stride: Optional[int] = None, pad: int = 0):
+    """tf.nn.max_pool on NHWC (``pad`` explicit; SAME for k=2,s=2 on even sizes is pad=0)."""
+    return _Pool2d.apply(x, ksize, stride or ksize, pad, "max")
+
+
+def avg_pool2d(x, ksize: int = 2, stride: Optional[int] = None, pad: int = 0):
+    """tf.nn.avg_pool on NHWC; padded taps are excluded from the mean (TF semantics)."""
+    return _Pool2d.apply(x, ksize, stride or ksize, pad, "avg")
+
+
 # ====================================================================== losses / metrics
 class _SoftmaxXent(torch.autograd.Function):
     @staticmethod

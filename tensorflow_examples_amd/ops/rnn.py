@@ -1,0 +1,143 @@
+"""GEMM-stacked LSTM layer (char-LSTM, BASELINE.json config 5).
+
+TF1 equivalent: ``tf.contrib.rnn.BasicLSTMCell`` / ``LSTMBlockCell`` unrolled by
+``tf.nn.dynamic_rnn`` -- one [B, In+H] x [In+H, 4H] MatMul per step followed by the gate
+nonlinearities.  MI355X design (one autograd node for the whole sequence):
+
+forward, T steps, batch B, hidden H:
+    GX  = X[T*B, In] @ W_ih^T + b           ONE bf16 MFMA GEMM for all time steps (f32 out)
+    for t:  GX[t] += h16[t-1] @ W_hh^T       bf16 MFMA GEMM accumulating in place (4 gates stacked)
+            act[t], c[t], h16[t] = cell(GX[t], c[t-1])   fused pointwise kernel, f32 cell state
+backward:
+    for t = T-1 .. 0:
+            dg16[t], dc = cell_bwd(act[t], c[t], c[t-1], dH[t], dc)   fused, dc carried in place
+            dH[t-1] += dg16[t] @ W_hh                                 GEMM accumulating in place
+    dW_hh += dG^T @ H_prev,  dW_ih += dG^T @ X,  dX = dG @ W_ih     three GEMMs over ALL steps
+so only the inherently sequential part (one small GEMM + one pointwise kernel per step and
+direction) runs T times; the weight gradients are batched over time into large GEMMs.
+Gate order: i, f, g, o (f gets ``forget_bias`` added in the pointwise kernel through ``b``).
+The whole step is HIP-graph capturable (no host syncs), which removes the per-step launch cost.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _native
+from .nn import _grad_ready
+from ..variables import Variable
+
+
+def _lstm_ref(x, w_ih, w_hh, b, h0, c0):
+    """PyTorch reference (f32): x [T,B,In] -> (out [T,B,H], h_T, c_T)."""
+    T = x.shape[0]
+    H = w_hh.shape[1]
+    h, c = h0, c0
+    outs = []
+    gx = x.float() @ w_ih.t() + b
+    for t in range(T):
+        z = gx[t] + h @ w_hh.t()
+        i, f, g, o = z.split(H, dim=1)
+        i, f, g, o = torch.sigmoid(i), torch.sigmoid(f), torch.tanh(g), torch.sigmoid(o)
+        c = f * c + i * g
+        h = o * torch.tanh(c)
+        outs.append(h)
+    return torch.stack(outs), h, c
+
+
+class _LSTMLayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, w_ih: Variable, w_hh: Variable, b: Variable, h0, c0):
+        T, B, In = x.shape
+        H = w_hh.shape[1]
+        ctx.vars = (w_ih, w_hh, b)
+        ctx.native = _native.use_native(x) and x.dtype == torch.bfloat16
+        if not ctx.native:
+            ctx.save_for_backward(x, h0, c0)
+            with torch.no_grad():
+                out, hT, cT = _lstm_ref(x, w_ih.master, w_hh.master, b.master, h0, c0)
+            return out.to(x.dtype), hT, cT
+        dev = x.device
+        xf = x.reshape(T * B, In).contiguous()
+        gx = torch.ops.tfx.gemm(xf, w_ih.value, False, True, b.master, False, True)  # [T*B, 4H] f32
+        hbuf = torch.empty(T + 1, B, H, dtype=torch.bfloat16, device=dev)
+        cbuf = torch.empty(T + 1, B, H, dtype=torch.float32, device=dev)
+        hbuf[0].copy_(h0)
+        cbuf[0].copy_(c0)
+        act = torch.empty(T, B, 4 * H, dtype=torch.float32, device=dev)
+        hT = torch.empty(B, H, dtype=torch.float32, device=dev)
+        gx = gx.view(T, B, 4 * H)
+        for t in range(T):
+            torch.ops.tfx.gemm_into(hbuf[t], w_hh.value, False, True, gx[t], True)
+            torch.ops.tfx.lstm_cell_fwd(gx[t], None, None, cbuf[t], act[t], cbuf[t + 1], hT, hbuf[t + 1])
+        ctx.save_for_backward(xf, hbuf, cbuf, act)
+        return hbuf[1:], hT, cbuf[T].clone()
+
+    @staticmethod
+    def backward(ctx, gout, g_hT, g_cT):
+        w_ih, w_hh, b = ctx.vars
+        if not ctx.native:
+            x, h0, c0 = ctx.saved_tensors
+            with torch.enable_grad():
+                xs = x.detach().float().requires_grad_(True)
+                ps = [v.master.detach().clone().requires_grad_(True) for v in (w_ih, w_hh, b)]
+                out, hT, cT = _lstm_ref(xs, *ps, h0, c0)
+                outs, grads_in = [out], [gout.float()]
+                if g_hT is not None:
+                    outs.append(hT)
+                    grads_in.append(g_hT)
+                if g_cT is not None:
+                    outs.append(cT)
+                    grads_in.append(g_cT)
+                gr = torch.autograd.grad(outs, [xs] + ps, grads_in, allow_unused=True)
+            for v, g in zip((w_ih, w_hh, b), gr[1:]):
+                if v.trainable and g is not None:
+                    v.grad.add_(g)
+            _grad_ready(w_ih, w_hh, b)
+            return gr[0].to(x.dtype), None, None, None, None, None, None
+        xf, hbuf, cbuf, act = ctx.saved_tensors
+        T = act.shape[0]
+        B, H = cbuf.shape[1], cbuf.shape[2]
+        dH = gout.float().contiguous().clone() if gout is not None else \
+            torch.zeros(T, B, H, dtype=torch.float32, device=xf.device)
+        if g_hT is not None:
+            dH[T - 1].add_(g_hT)
+        dc = g_cT.float().contiguous().clone() if g_cT is not None else \
+            torch.zeros(B, H, dtype=torch.float32, device=xf.device)
+        dg = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=xf.device)
+        for t in range(T - 1, -1, -1):
+            torch.ops.tfx.lstm_cell_bwd(act[t], cbuf[t + 1], cbuf[t], dH[t], dc, None, dg[t], dc)
+            if t > 0:
+                torch.ops.tfx.gemm_into(dg[t], w_hh.value, False, False, dH[t - 1], True)
+        dgf = dg.view(T * B, 4 * H)
+        if w_hh.trainable:
+            torch.ops.tfx.gemm_into(dgf, hbuf[:T].reshape(T * B, H), True, False, w_hh.grad, True)
+        if w_ih.trainable:
+            torch.ops.tfx.gemm_into(dgf, xf, True, False, w_ih.grad, True)
+        if b.trainable:
+            b.grad.add_(dgf.float().sum(0))
+        _grad_ready(w_ih, w_hh, b)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.tfx.gemm(dgf, w_ih.value, False, False, None, False, False).view(T, B, -1)
+        return dx, None, None, None, None, None, None
+
+
+def lstm_layer(x: torch.Tensor, w_ih: Variable, w_hh: Variable, b: Variable,
+               state: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+    """Run one LSTM layer over a whole sequence. ``x`` [T,B,In] (bf16 on GPU), weights
+    ``w_ih`` [4H,In], ``w_hh`` [4H,H], ``b`` [4H].  ``state`` = (h0, c0) f32 [B,H] (zeros if None);
+    it is treated as a constant (truncated BPTT).  Returns (out [T,B,H], (h_T, c_T))."""
+    T, B, _ = x.shape
+    H = w_hh.shape[1]
+    if state is None:
+        h0 = torch.zeros(B, H, dtype=torch.float32, device=x.device)
+        c0 = torch.zeros(B, H, dtype=torch.float32, device=x.device)
+    else:
+        h0, c0 = (s.detach().float().contiguous() for s in state)
+    out, hT, cT = _LSTMLayer.apply(x, w_ih.store.anchor, w_ih, w_hh, b, h0, c0)
+    return out, (hT.detach(), cT.detach())
+
+
+__all__ = ["lstm_layer"]

@@ -26,6 +26,7 @@ class Optimizer:
         self.wd, self.b1, self.b2, self.eps = float(weight_decay), float(beta1), float(beta2), float(eps)
         dev = store.device
         self.lr_t = torch.tensor([float(learning_rate)], dtype=torch.float32, device=dev)
+        self._lr = float(learning_rate)  # host copy for the sparse (IndexedSlices) updates
         self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
         self.m = torch.zeros_like(store.master) if self.kind >= MOMENTUM else None
         self.v = torch.zeros_like(store.master) if self.kind >= ADAM else None
@@ -33,10 +34,28 @@ class Optimizer:
 
     @property
     def learning_rate(self) -> float:
-        return float(self.lr_t.item())
+        return self._lr
 
     def set_learning_rate(self, lr: float) -> None:
+        self._lr = float(lr)
         self.lr_t.fill_(float(lr))
+
+    def apply_sparse(self, grad_scale: float = 1.0) -> None:
+        """Apply and clear the pending IndexedSlices gradients of every :class:`SparseVariable`:
+        ``table[ids] -= lr * grad_scale * rows`` (scatter-add kernel, duplicates summed, TF sparse
+        ``ApplyGradientDescent`` semantics).  Only plain SGD has a sparse form here."""
+        for sv in self.store.sparse:
+            if not sv.pending:
+                continue
+            if self.kind != SGD:
+                raise NotImplementedError("sparse (embedding) variables need GradientDescentOptimizer")
+            alpha = -self._lr * grad_scale
+            for ids, rows in sv.pending:
+                if _native.use_native(sv.table):
+                    torch.ops.tfx.embedding_scatter_add(sv.table, ids, rows, alpha)
+                else:
+                    sv.table.index_add_(0, ids, rows, alpha=alpha)
+            sv.clear()
 
     def apply_gradients(self, grad_scale: float = 1.0, sumsq: Optional[torch.Tensor] = None,
                         max_norm: float = 0.0) -> None:
@@ -45,6 +64,10 @@ class Optimizer:
         st = self.store
         self.iterations += 1
         self.step_t.add_(1.0)
+        if st.sparse:
+            self.apply_sparse(grad_scale)
+        if not st.vars:
+            return
         if _native.use_native(st.master):
             torch.ops.tfx.optimizer_apply(self.kind, st.master, st.grad, self.m, self.v, self.lr_t, grad_scale,
                                           self.wd, self.b1, self.b2, self.eps, self.step_t, sumsq, max_norm,

@@ -107,6 +107,24 @@ class GlorotUniform(Initializer):
         return (torch.rand(shape, generator=gen, dtype=torch.float32) * 2 - 1) * lim
 
 
+@dataclass
+class Padded(Initializer):
+    """Initialise the leading ``real_shape`` corner with ``inner`` and zero the padding.
+
+    Used for layers whose channel counts are padded to the 8-element (16-B) granularity of the
+    MFMA kernels (LeNet-5's 1 -> 6 -> 16 channels are carried as 8 -> 8 -> 16): padded weights,
+    BN scales and shifts start at exactly zero and, because every gradient that reaches them is
+    exactly zero too, stay zero under SGD / momentum / Adam -- the padded network computes the
+    same function as the unpadded one."""
+    inner: Initializer = field(default_factory=Zeros)
+    real_shape: tuple = ()
+
+    def __call__(self, shape, gen):
+        out = torch.zeros(shape, dtype=torch.float32)
+        out[tuple(slice(0, r) for r in self.real_shape)] = self.inner(tuple(self.real_shape), gen)
+        return out
+
+
 # ---------------------------------------------------------------- variables
 @dataclass
 class Variable:
@@ -140,6 +158,60 @@ class Variable:
             self.value.copy_(self.master)
 
 
+class SparseVariable:
+    """A large, sparsely-updated table (word2vec embeddings, NCE weights/biases).
+
+    Lives OUTSIDE the flat store: a 1M x 128 f32 table is 512 MB, and only the ~B rows a step
+    touches change, so it has no dense gradient buffer and no dense optimizer pass.  Backward
+    ops append ``(ids, rows)`` pairs to :attr:`pending` (TF's ``IndexedSlices``); the optimizer
+    applies them with the scatter-add kernel (TF ``ScatterSub`` / sparse ``ApplyGradientDescent``
+    semantics: duplicates are summed).  Initialised on the device (no host round trip)."""
+
+    def __init__(self, name, shape, initializer: Initializer, store: "VariableStore", trainable=True, index=0):
+        self.name, self.shape, self.initializer = name, tuple(int(s) for s in shape), initializer
+        self.store, self.trainable, self.index = store, trainable, index
+        self.table: Optional[torch.Tensor] = None
+        self.pending: List[tuple] = []
+
+    def materialize(self) -> None:
+        dev = self.store.device
+        g = torch.Generator(device=dev).manual_seed(self.store.seed * 1000003 + 7919 + self.index)
+        t = torch.empty(self.shape, dtype=torch.float32, device=dev)
+        ini = self.initializer
+        if isinstance(ini, Uniform):
+            t.uniform_(ini.low, ini.high, generator=g)
+        elif isinstance(ini, (RandomNormal, TruncatedNormal)):
+            t.normal_(ini.mean, ini.stddev, generator=g)
+            if isinstance(ini, TruncatedNormal):
+                lo, hi = ini.mean - 2 * ini.stddev, ini.mean + 2 * ini.stddev
+                bad = (t < lo) | (t > hi)
+                while bool(bad.any()):
+                    t[bad] = torch.empty(int(bad.sum()), device=dev).normal_(ini.mean, ini.stddev, generator=g)
+                    bad = (t < lo) | (t > hi)
+        elif isinstance(ini, Constant):
+            t.fill_(float(ini.value))
+        elif isinstance(ini, Zeros):
+            t.zero_()
+        else:
+            t.copy_(ini(self.shape, torch.Generator().manual_seed(self.store.seed * 1000003 + 7919 + self.index)))
+        self.table = t
+
+    @property
+    def master(self) -> torch.Tensor:
+        return self.table
+
+    value = master
+
+    def add_sparse_grad(self, ids: torch.Tensor, rows: torch.Tensor) -> None:
+        self.pending.append((ids.reshape(-1), rows.reshape(ids.numel(), -1).float().contiguous()))
+
+    def clear(self) -> None:
+        self.pending.clear()
+
+    def assign(self, t: torch.Tensor) -> None:
+        self.table.copy_(t.to(self.table.dtype).view(self.shape))
+
+
 class VariableStore:
     """Creates variables (TF naming, creation order preserved) and lays them out flat."""
 
@@ -148,6 +220,7 @@ class VariableStore:
         self.compute_dtype = compute_dtype
         self.seed = seed
         self.vars: List[Variable] = []
+        self.sparse: List[SparseVariable] = []
         self.by_name: Dict[str, Variable] = {}
         self.state: Dict[str, torch.Tensor] = {}  # non-trainable state (BN running stats, global_step)
         self.master: Optional[torch.Tensor] = None
@@ -191,6 +264,17 @@ class VariableStore:
         self.by_name[full] = v
         return v
 
+    def sparse_variable(self, shape, initializer: Initializer, name: str = "Variable",
+                        trainable=True) -> SparseVariable:
+        """A table updated through sparse (IndexedSlices) gradients -- see :class:`SparseVariable`."""
+        if self.master is not None:
+            raise RuntimeError("VariableStore already finalized")
+        full = self.unique_name(name)
+        v = SparseVariable(full, shape, initializer, self, trainable, index=len(self.vars) + len(self.sparse))
+        self.sparse.append(v)
+        self.by_name[full] = v
+        return v
+
     def add_state(self, name: str, t: torch.Tensor) -> torch.Tensor:
         full = self.unique_name(name)
         t = t.to(self.device)
@@ -211,6 +295,9 @@ class VariableStore:
             self.shadow = torch.zeros(self.total, dtype=self.compute_dtype, device=self.device)
         if init:
             self.initialize()
+        else:
+            for sv in self.sparse:
+                sv.table = torch.zeros(sv.shape, dtype=torch.float32, device=self.device)
         return self
 
     def initialize(self) -> None:
@@ -221,6 +308,8 @@ class VariableStore:
             host[v.offset:v.offset + v.numel] = v.initializer(v.shape, g).reshape(-1)
         self.master.copy_(host)
         self.refresh_shadow()
+        for sv in self.sparse:
+            sv.materialize()
 
     def refresh_shadow(self) -> None:
         if self.shadow is not None:
@@ -233,11 +322,13 @@ class VariableStore:
         return [v for v in self.vars if v.trainable]
 
     def num_params(self) -> int:
-        return sum(v.numel for v in self.vars if v.trainable)
+        return sum(v.numel for v in self.vars if v.trainable) + \
+            sum(int(math.prod(v.shape)) for v in self.sparse if v.trainable)
 
     # -- checkpoint helpers (name -> f32 tensor)
     def named_values(self) -> Dict[str, torch.Tensor]:
         out = {v.name: v.master.detach() for v in self.vars}
+        out.update({v.name: v.table.detach() for v in self.sparse})
         out.update({k: t.detach() for k, t in self.state.items()})
         return out
 
@@ -245,6 +336,11 @@ class VariableStore:
         for v in self.vars:
             if v.name in values:
                 v.master.copy_(values[v.name].to(self.device, torch.float32).view(v.shape))
+            elif strict:
+                raise KeyError(f"missing variable {v.name}")
+        for v in self.sparse:
+            if v.name in values:
+                v.table.copy_(values[v.name].to(self.device, torch.float32).view(v.shape))
             elif strict:
                 raise KeyError(f"missing variable {v.name}")
         for k, t in self.state.items():

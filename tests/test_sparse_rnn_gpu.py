@@ -1,0 +1,269 @@
+"""HIP kernels of the LeNet-5 / word2vec / char-LSTM workloads against PyTorch fp32 references:
+pooling (pool.hip), embedding gather / scatter-add, log-uniform sampler, fused sampled losses,
+skip-gram batch generator and the LSTM cell + whole-sequence layer (sparse_rnn.hip)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tensorflow_examples_amd import ops
+from tensorflow_examples_amd.ops import rnn as rnn_ops
+from tensorflow_examples_amd.ops import sparse as sp
+from tensorflow_examples_amd.variables import Uniform, VariableStore, Zeros
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+# ---------------------------------------------------------------- pooling
+@pytest.mark.parametrize("shape", [(2, 28, 28, 8, 2, 2, 0), (3, 10, 10, 16, 2, 2, 0), (2, 9, 7, 8, 3, 2, 1),
+                                   (1, 8, 8, 24, 3, 1, 1)])
+def test_maxpool_fwd_bwd(gpu, shape):
+    N, H, W, C, k, s, pad = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device=gpu).to(torch.bfloat16)
+    y, arg = torch.ops.tfx.maxpool_fwd(x, k, s, pad)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, pad)
+    assert torch.equal(y.float(), yr.detach().permute(0, 2, 3, 1))
+    dy = torch.randn_like(y)
+    dx = torch.ops.tfx.maxpool_bwd(dy, arg, H, W, k, s, pad)
+    (gx,) = torch.autograd.grad(yr, [xr], dy.float().permute(0, 3, 1, 2))
+    # bf16 output rounding of overlapping-window sums only
+    assert _rel(dx, gx.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 8, 8, 2, 2, 0), (2, 9, 7, 16, 3, 2, 1)])
+def test_avgpool_fwd_bwd(gpu, shape):
+    N, H, W, C, k, s, pad = shape
+    torch.manual_seed(1)
+    x = torch.randn(N, H, W, C, device=gpu).to(torch.bfloat16)
+    y = torch.ops.tfx.avgpool_fwd(x, k, s, pad)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.avg_pool2d(xr, k, s, pad, count_include_pad=False)
+    assert _rel(y, yr.detach().permute(0, 2, 3, 1)) < 1e-2
+    dy = torch.randn_like(y)
+    dx = torch.ops.tfx.avgpool_bwd(dy, H, W, k, s, pad)
+    (gx,) = torch.autograd.grad(yr, [xr], dy.float().permute(0, 3, 1, 2))
+    assert _rel(dx, gx.permute(0, 2, 3, 1)) < 1e-2
+
+
+# ---------------------------------------------------------------- embedding
+@pytest.mark.parametrize("D", [128, 6, 1])
+def test_embedding_gather_scatter(gpu, D):
+    torch.manual_seed(0)
+    V, n = 1000, 777
+    table = torch.randn(V, D, device=gpu)
+    ids = torch.randint(0, V, (n,), device=gpu)
+    ids[:50] = 3  # heavy duplicates
+    out = torch.ops.tfx.embedding_gather(table, ids, False)
+    assert torch.equal(out, table[ids])
+    outb = torch.ops.tfx.embedding_gather(table, ids, True)
+    assert torch.equal(outb, table[ids].to(torch.bfloat16))
+    rows = torch.randn(n, D, device=gpu)
+    ref = table.clone().index_add_(0, ids, rows, alpha=-0.5)
+    torch.ops.tfx.embedding_scatter_add(table, ids, rows, -0.5)
+    assert (table - ref).abs().max().item() < 1e-4
+
+
+def test_log_uniform_sampler(gpu):
+    V, S = 1_000_000, 1 << 20
+    ids, logq = torch.ops.tfx.log_uniform_sample(S, V, 1234, 64, gpu, None)
+    assert ids.min().item() >= 0 and ids.max().item() < V
+    # empirical frequency of the first ranks vs P(k) = log((k+2)/(k+1)) / log(V+1)
+    cnt = torch.bincount(ids[ids < 8], minlength=8).float().cpu() / S
+    p = torch.tensor([math.log((k + 2) / (k + 1)) / math.log(V + 1) for k in range(8)])
+    assert ((cnt - p).abs() / p).max().item() < 0.02
+    ref = torch.log(64 * torch.log((ids.double() + 2) / (ids.double() + 1)) / math.log(V + 1)).float()
+    assert (logq - ref).abs().max().item() < 1e-4
+    lq = torch.ops.tfx.log_uniform_logq(ids[:100].contiguous(), V, 64)
+    assert torch.allclose(lq, logq[:100])
+    # device seed counter: different draws per counter value, same draws for the same value
+    c = torch.zeros(1, dtype=torch.long, device=gpu)
+    a1, _ = torch.ops.tfx.log_uniform_sample(64, V, 7, 64, gpu, c)
+    a2, _ = torch.ops.tfx.log_uniform_sample(64, V, 7, 64, gpu, c)
+    c += 1
+    a3, _ = torch.ops.tfx.log_uniform_sample(64, V, 7, 64, gpu, c)
+    assert torch.equal(a1, a2) and not torch.equal(a1, a3)
+
+
+@pytest.mark.parametrize("softmax", [False, True])
+def test_sampled_loss_grads(gpu, softmax):
+    torch.manual_seed(0)
+    B, S, D, V = 300, 64, 128, 5000
+    E, Wt, Ws = (torch.randn(n, D, device=gpu) * 0.3 for n in (B, B, S))
+    bt, bs = torch.randn(B, device=gpu) * 0.1, torch.randn(S, device=gpu) * 0.1
+    tid = torch.randint(0, V, (B,), device=gpu)
+    sid = torch.randint(0, V, (S,), device=gpu)
+    tid[:5] = sid[:5]  # force accidental hits
+    lt, ls = sp.log_uniform_logq(tid, V, S), sp.log_uniform_logq(sid, V, S)
+    hits = (tid, sid) if softmax else (None, None)
+    got = sp.sampled_loss_grads(E, Wt, bt, Ws, bs, lt, ls, *hits, softmax=softmax, gscale=1.0 / B)
+    ref = sp._sampled_ref(E, Wt, bt, Ws, bs, lt, ls, *hits, softmax, 1.0 / B)
+    for g, r in zip(got, ref):
+        assert _rel(g, r) < 2e-5, (softmax, _rel(g, r))
+
+
+def test_skipgram_batch(gpu):
+    corpus = torch.arange(100000, dtype=torch.int32, device=gpu)
+    c, l = torch.ops.tfx.skipgram_batch(corpus, 4096, 2, 99, None)
+    d = (l - c).cpu()
+    assert set(d.unique().tolist()) <= {-2, -1, 1, 2}
+    assert c.min().item() >= 2 and c.max().item() < 100000 - 2
+    assert len(set(d.unique().tolist())) == 4
+
+
+def test_embedding_lookup_autograd_dense_and_sparse(gpu):
+    store = VariableStore(device=gpu, seed=3)
+    dense = store.variable([50, 16], Uniform(-1, 1), name="dense")
+    table = store.sparse_variable([50, 16], Uniform(-1, 1), name="table")
+    store.finalize()
+    ids = torch.randint(0, 50, (7, 9), device=gpu)
+    store.zero_grad()
+    y = ops.embedding_lookup(dense, ids) * 2 + ops.embedding_lookup(table, ids)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref = torch.zeros(50, 16, device=gpu).index_add_(0, ids.reshape(-1), 2 * g.reshape(-1, 16))
+    assert (dense.grad - ref).abs().max().item() < 1e-5
+    (pids, prows), = table.pending
+    got = torch.zeros(50, 16, device=gpu).index_add_(0, pids, prows)
+    assert (got - ref / 2).abs().max().item() < 1e-5
+
+
+# ---------------------------------------------------------------- LSTM
+def test_lstm_cell_kernels(gpu):
+    torch.manual_seed(0)
+    B, H = 37, 64
+    gx, gh = torch.randn(B, 4 * H, device=gpu), torch.randn(B, 4 * H, device=gpu)
+    bias, cp = torch.randn(4 * H, device=gpu), torch.randn(B, H, device=gpu)
+    act, c, h = torch.empty(B, 4 * H, device=gpu), torch.empty(B, H, device=gpu), torch.empty(B, H, device=gpu)
+    h16 = torch.empty(B, H, device=gpu, dtype=torch.bfloat16)
+    torch.ops.tfx.lstm_cell_fwd(gx, gh, bias, cp, act, c, h, h16)
+    z = (gx + gh + bias).requires_grad_(True)
+    cpr = cp.clone().requires_grad_(True)
+    i, f, g, o = z.split(H, 1)
+    cr = torch.sigmoid(f) * cpr + torch.sigmoid(i) * torch.tanh(g)
+    hr = torch.sigmoid(o) * torch.tanh(cr)
+    assert _rel(c, cr) < 1e-5 and _rel(h, hr) < 1e-5 and _rel(h16, hr) < 5e-3
+    dh, dcn = torch.randn(B, H, device=gpu), torch.randn(B, H, device=gpu)
+    dg, dg16, dcp = torch.empty(B, 4 * H, device=gpu), torch.empty(B, 4 * H, device=gpu, dtype=torch.bfloat16), \
+        torch.empty(B, H, device=gpu)
+    torch.ops.tfx.lstm_cell_bwd(act, c, cp, dh, dcn, dg, dg16, dcp)
+    gz, gc = torch.autograd.grad([hr, cr], [z, cpr], [dh, dcn])
+    assert _rel(dg, gz) < 1e-5 and _rel(dcp, gc) < 1e-5 and _rel(dg16, gz) < 5e-3
+
+
+def test_lstm_layer_vs_reference(gpu):
+    torch.manual_seed(0)
+    T, B, In, H = 12, 16, 64, 128
+    store = VariableStore(device=gpu, compute_dtype=torch.bfloat16, seed=1)
+    w_ih = store.variable([4 * H, In], Uniform(-0.1, 0.1), name="w_ih")
+    w_hh = store.variable([4 * H, H], Uniform(-0.1, 0.1), name="w_hh")
+    b = store.variable([4 * H], Uniform(-0.1, 0.1), name="b")
+    store.finalize()
+    x = torch.randn(T, B, In, device=gpu).to(torch.bfloat16).requires_grad_(True)
+    h0, c0 = torch.randn(B, H, device=gpu) * 0.5, torch.randn(B, H, device=gpu) * 0.5
+    store.zero_grad()
+    out, (hT, cT) = ops.lstm_layer(x, w_ih, w_hh, b, (h0, c0))
+    gout = torch.randn(T, B, H, device=gpu)
+    out.backward(gout.to(out.dtype))
+    # fp32 reference with the same bf16-rounded weights
+    ps = [v.value.float().clone().requires_grad_(True) for v in (w_ih, w_hh)] + [b.master.clone().requires_grad_(True)]
+    xr = x.detach().float().requires_grad_(True)
+    outr, hr, cr = rnn_ops._lstm_ref(xr, *ps, h0, c0)
+    gr = torch.autograd.grad(outr, [xr] + ps, gout.to(torch.bfloat16).float())
+    assert _rel(out, outr) < 1e-2 and _rel(hT, hr) < 1e-2 and _rel(cT, cr) < 1e-2
+    assert _rel(x.grad, gr[0]) < 3e-2
+    for v, g in zip((w_ih, w_hh, b), gr[1:]):
+        assert _rel(v.grad, g) < 3e-2, v.name
+
+
+# ---------------------------------------------------------------- models
+def test_lenet5_trains(gpu):
+    from tensorflow_examples_amd.models.lenet import build_lenet5, to_model_input
+    from tensorflow_examples_amd.optim import MomentumOptimizer
+    from tensorflow_examples_amd.train import ClassifierTrainer
+    store, m = build_lenet5(device=gpu)
+    tr = ClassifierTrainer(store, m, MomentumOptimizer(store, 0.05, 0.9))
+    torch.manual_seed(0)
+    x = to_model_input(torch.rand(128, 784, device=gpu))
+    y = torch.randint(0, 10, (128,), device=gpu)
+    first = float(tr.step(x, y))
+    for _ in range(40):
+        last = float(tr.step(x, y))
+    assert last < 0.2 * first
+    # padded channels stay exactly zero
+    assert m.c1.w.master[6:].abs().sum().item() == 0 and m.c1.w.master[..., 1:].abs().sum().item() == 0
+    assert m.c1.gamma.master[6:].abs().sum().item() == 0 and m.c1.beta.master[6:].abs().sum().item() == 0
+    assert m.c2.w.master[..., 6:].abs().sum().item() == 0
+
+
+def test_lenet5_matches_cpu_fp32(gpu):
+    """One step of the bf16 GPU LeNet vs the fp32 CPU reference path (same init)."""
+    from tensorflow_examples_amd.models.lenet import build_lenet5, to_model_input
+    torch.manual_seed(0)
+    x = torch.rand(64, 784)
+    y = torch.randint(0, 10, (64,))
+    grads = []
+    for dev, dt in ((gpu, torch.bfloat16), (torch.device("cpu"), torch.float32)):
+        store, m = build_lenet5(device=dev, dtype=dt, seed=5)
+        store.zero_grad()
+        loss = ops.softmax_cross_entropy(m(to_model_input(x.to(dev), dt), training=True), y.to(dev))
+        loss.backward()
+        grads.append((float(loss), store.grad.float().cpu()))
+    assert abs(grads[0][0] - grads[1][0]) < 0.05 * abs(grads[1][0])
+    assert _rel(grads[0][1], grads[1][1]) < 0.1
+
+
+def test_word2vec_fused_step_matches_autograd(gpu):
+    from tensorflow_examples_amd.models.word2vec import build_skipgram
+    from tensorflow_examples_amd.optim import GradientDescentOptimizer
+    for kind in ("nce", "sampled_softmax"):
+        sa, ma = build_skipgram(gpu, vocab_size=20000, embedding_size=64, num_sampled=32, loss=kind, seed=1)
+        sb, mb = build_skipgram(gpu, vocab_size=20000, embedding_size=64, num_sampled=32, loss=kind, seed=1)
+        opt = GradientDescentOptimizer(sb, 1.0)
+        c = torch.randint(0, 20000, (256,), device=gpu)
+        l = torch.randint(0, 20000, (256,), device=gpu)
+        la = ma.train_step(c, l, 1.0, seed=11)
+        sb.zero_grad()
+        lb = mb.loss(c, l, seed=11)
+        lb.backward()
+        opt.apply_gradients()
+        assert abs(float(la) - float(lb)) < 1e-4 * abs(float(lb))
+        for va, vb in zip(sa.sparse, sb.sparse):
+            assert (va.table - vb.table).abs().max().item() < 1e-5, (kind, va.name)
+
+
+def test_word2vec_learns(gpu):
+    from tensorflow_examples_amd.data.text import device_skipgram_batch, synthetic_zipf_corpus
+    from tensorflow_examples_amd.models.word2vec import build_skipgram
+    store, m = build_skipgram(gpu, vocab_size=50000, embedding_size=128, num_sampled=64)
+    corpus = torch.from_numpy(synthetic_zipf_corpus(1_000_000, 50000, 0)).to(gpu)
+    losses = []
+    for i in range(300):
+        c, l = device_skipgram_batch(corpus, 512, 1, seed=i)
+        losses.append(float(m.train_step(c, l, 1.0, seed=i)))
+    assert np.mean(losses[-20:]) < 0.5 * np.mean(losses[:5])
+
+
+def test_char_lstm_learns_and_graph(gpu):
+    from tensorflow_examples_amd.models.char_lstm import LMTrainer, build_char_lstm
+    from tensorflow_examples_amd.optim import AdamOptimizer
+    rng = np.random.default_rng(0)
+    pat = torch.from_numpy(rng.integers(0, 64, 50))
+    ids = pat.repeat(200)
+    store, m = build_char_lstm(gpu, vocab_size=64, embed=64, hidden=128, layers=2)
+    tr = LMTrainer(m, AdamOptimizer(store, 0.01), max_grad_norm=5.0)
+    from tensorflow_examples_amd.data.text import ptb_batches
+    st, losses = None, []
+    for ep in range(3):
+        for x, y in ptb_batches(ids.numpy(), 16, 25):
+            l, st = tr.step(torch.from_numpy(x).to(gpu), torch.from_numpy(y).to(gpu), st)
+            losses.append(float(l))
+    assert losses[-1] < 0.3 * losses[0]
