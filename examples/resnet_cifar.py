@@ -1,0 +1,106 @@
+"""ResNet on CIFAR-10 (BASELINE.json config 3: "CIFAR-10 ResNet-50 bf16 DP on 8xMI355X").
+
+One process per GPU (launch with torchrun), RCCL bucketed all-reduce overlapped with backward,
+fused momentum SGD with weight decay and a step-wise LR schedule, on-device augmentation
+(pad-4 random crop + flip), host->HBM double-buffered prefetch, per-epoch test accuracy and
+checkpoints (rank 0).  CIFAR-10 binary files from ``--data_dir`` when present, else synthetic.
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/resnet_cifar.py --depth=50 --batch_size=256
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from tensorflow_examples_amd import app, ops  # noqa: E402
+from tensorflow_examples_amd.ckpt import Saver, latest_checkpoint  # noqa: E402
+from tensorflow_examples_amd.data.cifar import augment, load_cifar10  # noqa: E402
+from tensorflow_examples_amd.data.pipeline import DevicePrefetcher, batches  # noqa: E402
+from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
+from tensorflow_examples_amd.optim import MomentumOptimizer  # noqa: E402
+from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed  # noqa: E402
+from tensorflow_examples_amd.train import ClassifierTrainer  # noqa: E402
+
+flags = app.flags
+flags.DEFINE_string("data_dir", "", "directory with the CIFAR-10 binary batches (synthetic if absent)")
+flags.DEFINE_integer("depth", 50, "ResNet depth: 18, 34, 50, 101, 152")
+flags.DEFINE_integer("batch_size", 256, "images per GPU")
+flags.DEFINE_integer("epochs", 1, "training epochs")
+flags.DEFINE_integer("max_steps", 0, "stop after N steps (0 = full epochs)")
+flags.DEFINE_float("learning_rate", 0.1, "base LR (scaled by the number of GPUs)")
+flags.DEFINE_float("weight_decay", 5e-4, "L2 weight decay")
+flags.DEFINE_string("lr_boundaries", "0.5,0.75", "fractions of training where the LR drops 10x")
+flags.DEFINE_float("bucket_mb", 32.0, "all-reduce bucket size (MB)")
+flags.DEFINE_string("logdir", "", "checkpoint directory (resume from the latest checkpoint in it)")
+flags.DEFINE_integer("synthetic_train", 50000, "synthetic training-set size when no data is found")
+flags.DEFINE_integer("eval_examples", 0, "evaluate on the first N test images (0 = all)")
+FLAGS = flags.FLAGS
+
+
+def main(_):
+    dev = init_distributed(device="cuda" if torch.cuda.is_available() else "cpu")
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    xtr, ytr, xte, yte, synth = load_cifar10(FLAGS.data_dir or None, synthetic_train=FLAGS.synthetic_train)
+    if rank == 0:
+        print("CIFAR-10 %s: %d train / %d test" % ("synthetic" if synth else "binary", len(xtr), len(xte)))
+    store, model = build_resnet_cifar(device=dev, depth=FLAGS.depth, dtype=dtype, seed=0)
+    opt = MomentumOptimizer(store, FLAGS.learning_rate * world, momentum=0.9, weight_decay=FLAGS.weight_decay)
+    start_step = 0
+    if FLAGS.logdir and latest_checkpoint(FLAGS.logdir):
+        tensors = Saver().restore(store, latest_checkpoint(FLAGS.logdir))
+        start_step = int(float(tensors["global_step"])) if "global_step" in tensors else 0
+    broadcast_variables(store)
+    dp = GradAllReduce(store, bucket_bytes=int(FLAGS.bucket_mb * (1 << 20))) if world > 1 else None
+    trainer = ClassifierTrainer(store, model, opt, dp)
+    shard = np.arange(rank, len(xtr), world)
+    steps_per_epoch = len(shard) // FLAGS.batch_size
+    total = FLAGS.max_steps or steps_per_epoch * FLAGS.epochs
+    bounds = [int(float(f) * total) for f in FLAGS.lr_boundaries.split(",") if f]
+    step, t0, seen = start_step, time.time(), 0
+    for ep in range(FLAGS.epochs):
+        src = batches([xtr[shard], ytr[shard]], FLAGS.batch_size, seed=ep * 1000 + rank)
+        for img, lab in DevicePrefetcher(src, dev):
+            lr = FLAGS.learning_rate * world * (0.1 ** sum(step >= b for b in bounds))
+            opt.set_learning_rate(lr)
+            loss = trainer.step(to_model_input(augment(img), dtype), lab)
+            step += 1
+            seen += img.shape[0]
+            if rank == 0 and step % 50 == 0:
+                print("epoch %d step %d lr %.4f loss %.4f" % (ep + 1, step, lr, float(loss)), flush=True)
+            if step - start_step >= total:
+                break
+        if step - start_step >= total:
+            break
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.time() - t0
+    ips = torch.tensor([seen / dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(ips)
+    if FLAGS.eval_examples:
+        xte, yte = xte[:FLAGS.eval_examples], yte[:FLAGS.eval_examples]
+    correct = 0.0
+    with torch.no_grad():
+        for i in range(0, len(xte), 500):
+            x = to_model_input(torch.as_tensor(xte[i:i + 500], device=dev), dtype)
+            y = torch.as_tensor(yte[i:i + 500], device=dev)
+            correct += float(ops.accuracy(model(x, training=False), y)) * len(y)
+    if rank == 0:
+        print("test accuracy %.4f" % (correct / len(xte)))
+        print("images/sec (all GPUs) %.1f" % float(ips))
+        if FLAGS.logdir:
+            print("saved", Saver().save(store, os.path.join(FLAGS.logdir, "model.ckpt"), global_step=step))
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    app.run(main)

@@ -35,6 +35,22 @@ for s in $STEPS; do
     bnbench)
       for u in 1; do TFX_BN_RED_U=$u timeout -k 10 200 python scripts/bn_bench.py > gpurun_out/bn_bench_u$u.log 2>&1 || exit 1; done
       echo bnbench done; tail -1 gpurun_out/bn_bench_u*.log ;;
+    newtests)
+      timeout -k 10 600 python -m pytest tests/test_sparse_rnn_gpu.py -q -p no:cacheprovider > gpurun_out/pytest_new.log 2>&1
+      rc=$?; echo "newtests rc=$rc"; tail -8 gpurun_out/pytest_new.log
+      ok_or_testfail $rc || exit $rc ;;
+    models)
+      : > gpurun_out/bench_models.jsonl
+      for spec in "lenet5 native" "lenet5 native --graph" "lenet5 torch" "lenet5 torch --graph" \
+                  "word2vec native" "word2vec native --graph" "word2vec torch" \
+                  "word2vec native --batch 128 --graph" "word2vec torch --batch 128" \
+                  "char_lstm native" "char_lstm native --graph" "char_lstm torch"; do
+        set -- $spec
+        m=$1; impl=$2; shift 2
+        timeout -k 10 300 python scripts/bench_models.py --model $m --impl $impl "$@" >> gpurun_out/bench_models.jsonl 2> gpurun_out/bench_models_err.log
+        rc=$?; echo "$spec rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_models_err.log; [ $rc -eq 1 ] || exit $rc; }
+      done
+      cat gpurun_out/bench_models.jsonl ;;
     prof)
       export TMPDIR=/tmp
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 2 > gpurun_out/prof.log 2>&1

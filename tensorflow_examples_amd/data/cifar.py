@@ -1,0 +1,69 @@
+"""CIFAR-10 input: the binary distribution (``data_batch_{1..5}.bin``, ``test_batch.bin``: records
+of 1 label byte + 3072 image bytes in CHW order) read with numpy only -- no pickle -- and a
+deterministic synthetic fallback of the same shape (there is no dataset download on the box).
+
+Images are returned NHWC uint8 [N,32,32,3]; :func:`augment` does the standard CIFAR training
+augmentation (4-pixel pad + random 32x32 crop + horizontal flip) on the device, batched.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+RECORD = 1 + 3 * 32 * 32
+TRAIN_FILES = ["data_batch_%d.bin" % i for i in range(1, 6)]
+TEST_FILE = "test_batch.bin"
+
+
+def read_cifar_bin(path: str) -> Tuple[np.ndarray, np.ndarray]:
+    raw = np.fromfile(path, dtype=np.uint8)
+    if raw.size % RECORD:
+        raise ValueError(f"{path}: size {raw.size} is not a multiple of {RECORD}")
+    rec = raw.reshape(-1, RECORD)
+    labels = rec[:, 0].astype(np.int64)
+    images = rec[:, 1:].reshape(-1, 3, 32, 32).transpose(0, 2, 3, 1).copy()
+    return images, labels
+
+
+def synthetic_cifar(n: int, seed: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """Learnable CIFAR-shaped data: per-class random colour/texture prototypes plus noise."""
+    rng = np.random.RandomState(seed)
+    protos = np.random.RandomState(4321).randint(0, 256, size=(10, 8, 8, 3)).astype(np.float32)
+    labels = rng.randint(0, 10, size=n).astype(np.int64)
+    base = np.repeat(np.repeat(protos[labels], 4, axis=1), 4, axis=2)
+    imgs = np.clip(base + rng.normal(0, 40, size=base.shape), 0, 255).astype(np.uint8)
+    return imgs, labels
+
+
+def load_cifar10(data_dir: Optional[str], synthetic_train: int = 50000, synthetic_test: int = 10000):
+    """(train_images, train_labels, test_images, test_labels, is_synthetic)."""
+    if data_dir:
+        for sub in ("", "cifar-10-batches-bin"):
+            d = os.path.join(data_dir, sub)
+            if all(os.path.exists(os.path.join(d, f)) for f in TRAIN_FILES + [TEST_FILE]):
+                parts = [read_cifar_bin(os.path.join(d, f)) for f in TRAIN_FILES]
+                xtr = np.concatenate([p[0] for p in parts])
+                ytr = np.concatenate([p[1] for p in parts])
+                xte, yte = read_cifar_bin(os.path.join(d, TEST_FILE))
+                return xtr, ytr, xte, yte, False
+    xtr, ytr = synthetic_cifar(synthetic_train, 0)
+    xte, yte = synthetic_cifar(synthetic_test, 1)
+    return xtr, ytr, xte, yte, True
+
+
+def augment(images: torch.Tensor, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """Random 4-pixel-padded crop + horizontal flip of an NHWC uint8 batch (on its device)."""
+    n = images.shape[0]
+    dev = images.device
+    padded = torch.nn.functional.pad(images.permute(0, 3, 1, 2), (4, 4, 4, 4)).permute(0, 2, 3, 1)
+    ox = torch.randint(0, 9, (n,), device=dev, generator=generator)
+    oy = torch.randint(0, 9, (n,), device=dev, generator=generator)
+    flip = torch.randint(0, 2, (n,), device=dev, generator=generator).bool()
+    ar = torch.arange(32, device=dev)
+    rows = (oy[:, None] + ar[None, :])                                  # [n,32]
+    cols = ox[:, None] + torch.where(flip[:, None], 31 - ar[None, :], ar[None, :])
+    bidx = torch.arange(n, device=dev)[:, None, None]
+    return padded[bidx, rows[:, :, None], cols[:, None, :]]

@@ -124,6 +124,8 @@ def broadcast_variables(store: VariableStore, src: int = 0, group=None) -> None:
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
     dist.broadcast(store.master, src=src, group=group)
+    for sv in store.sparse:
+        dist.broadcast(sv.table, src=src, group=group)
     for t in store.state.values():
         dist.broadcast(t, src=src, group=group)
     store.refresh_shadow()

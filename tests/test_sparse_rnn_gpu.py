@@ -29,12 +29,12 @@ def test_maxpool_fwd_bwd(gpu, shape):
     torch.manual_seed(0)
     x = torch.randn(N, H, W, C, device=gpu).to(torch.bfloat16)
     y, arg = torch.ops.tfx.maxpool_fwd(x, k, s, pad)
-    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    xr = x.float().cpu().permute(0, 3, 1, 2).contiguous().requires_grad_(True)  # CPU fp32 reference
     yr = F.max_pool2d(xr, k, s, pad)
-    assert torch.equal(y.float(), yr.detach().permute(0, 2, 3, 1))
+    assert torch.equal(y.float().cpu(), yr.detach().permute(0, 2, 3, 1))
     dy = torch.randn_like(y)
     dx = torch.ops.tfx.maxpool_bwd(dy, arg, H, W, k, s, pad)
-    (gx,) = torch.autograd.grad(yr, [xr], dy.float().permute(0, 3, 1, 2))
+    (gx,) = torch.autograd.grad(yr, [xr], dy.float().cpu().permute(0, 3, 1, 2))
     # bf16 output rounding of overlapping-window sums only
     assert _rel(dx, gx.permute(0, 2, 3, 1)) < 1e-2
 
@@ -45,12 +45,12 @@ def test_avgpool_fwd_bwd(gpu, shape):
     torch.manual_seed(1)
     x = torch.randn(N, H, W, C, device=gpu).to(torch.bfloat16)
     y = torch.ops.tfx.avgpool_fwd(x, k, s, pad)
-    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    xr = x.float().cpu().permute(0, 3, 1, 2).contiguous().requires_grad_(True)  # CPU fp32 reference
     yr = F.avg_pool2d(xr, k, s, pad, count_include_pad=False)
     assert _rel(y, yr.detach().permute(0, 2, 3, 1)) < 1e-2
     dy = torch.randn_like(y)
     dx = torch.ops.tfx.avgpool_bwd(dy, H, W, k, s, pad)
-    (gx,) = torch.autograd.grad(yr, [xr], dy.float().permute(0, 3, 1, 2))
+    (gx,) = torch.autograd.grad(yr, [xr], dy.float().cpu().permute(0, 3, 1, 2))
     assert _rel(dx, gx.permute(0, 2, 3, 1)) < 1e-2
 
 
@@ -79,7 +79,7 @@ def test_log_uniform_sampler(gpu):
     # empirical frequency of the first ranks vs P(k) = log((k+2)/(k+1)) / log(V+1)
     cnt = torch.bincount(ids[ids < 8], minlength=8).float().cpu() / S
     p = torch.tensor([math.log((k + 2) / (k + 1)) / math.log(V + 1) for k in range(8)])
-    assert ((cnt - p).abs() / p).max().item() < 0.02
+    assert ((cnt - p).abs() / p).max().item() < 0.05  # ~5 sigma at S = 2^20
     ref = torch.log(64 * torch.log((ids.double() + 2) / (ids.double() + 1)) / math.log(V + 1)).float()
     assert (logq - ref).abs().max().item() < 1e-4
     lq = torch.ops.tfx.log_uniform_logq(ids[:100].contiguous(), V, 64)
