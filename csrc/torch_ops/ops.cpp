@@ -544,9 +544,18 @@ void lstm_cell_bwd(Tensor act, Tensor c, optional<Tensor> c_prev, optional<Tenso
                      fpm(dgates), d16, fpm(dc_prev), cur_stream());
 }
 
+void philox_fill(Tensor out, int64_t seed, int64_t subseq, int64_t dist, double a, double b) {
+  CHECK_DEV(out); CHECK_F32(out); CHECK_CONTIG(out);
+  TORCH_CHECK(dist >= 0 && dist <= 2, "philox dist");
+  if (out.numel())
+    tfx::philox_fill(out.data_ptr<float>(), out.numel(), (uint64_t)seed, (uint64_t)subseq, (int)dist, (float)a,
+                     (float)b, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tfx, m) {
+  m.def("philox_fill", &philox_fill);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -37,6 +37,10 @@ class Initializer:
     def __call__(self, shape: Sequence[int], gen: torch.Generator) -> torch.Tensor:  # pragma: no cover
         raise NotImplementedError
 
+    def philox_spec(self, shape) -> Optional[tuple]:
+        """(dist, a, b) for the Philox generator (random.py), or None for a host-side initializer."""
+        return None
+
 
 @dataclass
 class Zeros(Initializer):
@@ -61,6 +65,9 @@ class RandomNormal(Initializer):
     def __call__(self, shape, gen):
         return torch.randn(shape, generator=gen, dtype=torch.float32) * self.stddev + self.mean
 
+    def philox_spec(self, shape):
+        return (1, self.mean, self.stddev)
+
 
 @dataclass
 class TruncatedNormal(Initializer):
@@ -75,6 +82,9 @@ class TruncatedNormal(Initializer):
             bad = t.abs() > 2
         return t * self.stddev + self.mean
 
+    def philox_spec(self, shape):
+        return (2, self.mean, self.stddev)
+
 
 @dataclass
 class Uniform(Initializer):
@@ -83,6 +93,9 @@ class Uniform(Initializer):
 
     def __call__(self, shape, gen):
         return torch.rand(shape, generator=gen, dtype=torch.float32) * (self.high - self.low) + self.low
+
+    def philox_spec(self, shape):
+        return (0, self.low, self.high)
 
 
 @dataclass
@@ -94,17 +107,29 @@ class HeNormal(Initializer):
         fan_in = int(math.prod(shape[1:])) if len(shape) > 1 else int(shape[0])
         return torch.randn(shape, generator=gen, dtype=torch.float32) * (self.gain / math.sqrt(fan_in))
 
+    def philox_spec(self, shape):
+        fan_in = int(math.prod(shape[1:])) if len(shape) > 1 else int(shape[0])
+        return (1, 0.0, self.gain / math.sqrt(fan_in))
+
 
 @dataclass
 class GlorotUniform(Initializer):
-    def __call__(self, shape, gen):
+    @staticmethod
+    def _lim(shape):
         if len(shape) == 2:
             fan_out, fan_in = shape[0], shape[1]
         else:
             rf = int(math.prod(shape[1:-1])) if len(shape) > 2 else 1
             fan_out, fan_in = shape[0] * rf, shape[-1] * rf
-        lim = math.sqrt(6.0 / (fan_in + fan_out))
+        return math.sqrt(6.0 / (fan_in + fan_out))
+
+    def __call__(self, shape, gen):
+        lim = self._lim(shape)
         return (torch.rand(shape, generator=gen, dtype=torch.float32) * 2 - 1) * lim
+
+    def philox_spec(self, shape):
+        lim = self._lim(shape)
+        return (0, -lim, lim)
 
 
 @dataclass
@@ -175,6 +200,16 @@ class SparseVariable:
 
     def materialize(self) -> None:
         dev = self.store.device
+        spec = self.initializer.philox_spec(self.shape)
+        if self.store.init_mode == "philox" and (spec is not None or isinstance(self.initializer, (Zeros, Constant))):
+            from .random import philox_fill
+            t = torch.empty(self.shape, dtype=torch.float32, device=dev)
+            if spec is None:
+                t.fill_(float(getattr(self.initializer, "value", 0.0)))
+            else:
+                philox_fill(t, self.store.seed, (1 << 40) + self.index, *spec)
+            self.table = t
+            return
         g = torch.Generator(device=dev).manual_seed(self.store.seed * 1000003 + 7919 + self.index)
         t = torch.empty(self.shape, dtype=torch.float32, device=dev)
         ini = self.initializer
@@ -215,7 +250,11 @@ class SparseVariable:
 class VariableStore:
     """Creates variables (TF naming, creation order preserved) and lays them out flat."""
 
-    def __init__(self, device="cpu", compute_dtype=torch.float32, seed: int = 0):
+    def __init__(self, device="cpu", compute_dtype=torch.float32, seed: int = 0, init: str = "philox"):
+        """``init``: "philox" (default) runs every random initializer through the Philox4x32-10
+        generator of random.py -- on the device for GPU stores, identical streams on CPU and GPU;
+        "torch" uses host torch.Generator draws (kept for reproducing older runs)."""
+        self.init_mode = init
         self.device = torch.device(device)
         self.compute_dtype = compute_dtype
         self.seed = seed
@@ -302,14 +341,38 @@ class VariableStore:
 
     def initialize(self) -> None:
         """Run every initializer (TF global_variables_initializer). Deterministic per (seed, index)."""
-        host = torch.zeros(self.total, dtype=torch.float32)
-        for v in self.vars:
-            g = torch.Generator().manual_seed(self.seed * 1000003 + v.index)
-            host[v.offset:v.offset + v.numel] = v.initializer(v.shape, g).reshape(-1)
-        self.master.copy_(host)
+        if self.init_mode == "philox":
+            self._initialize_philox()
+        else:
+            host = torch.zeros(self.total, dtype=torch.float32)
+            for v in self.vars:
+                g = torch.Generator().manual_seed(self.seed * 1000003 + v.index)
+                host[v.offset:v.offset + v.numel] = v.initializer(v.shape, g).reshape(-1)
+            self.master.copy_(host)
         self.refresh_shadow()
         for sv in self.sparse:
             sv.materialize()
+
+    def _initialize_philox(self) -> None:
+        from .random import philox_fill
+        self.master.zero_()
+        for v in self.vars:
+            ini, view, shape = v.initializer, self.master[v.offset:v.offset + v.numel], v.shape
+            if isinstance(ini, Padded):
+                inner = ini.inner.philox_spec(tuple(ini.real_shape))
+                if inner is None:
+                    src = ini.inner(tuple(ini.real_shape), torch.Generator().manual_seed(self.seed * 1000003 + v.index))
+                else:
+                    src = torch.empty(tuple(ini.real_shape), dtype=torch.float32, device=self.device)
+                    philox_fill(src, self.seed, v.index, *inner)
+                view.view(shape)[tuple(slice(0, r) for r in ini.real_shape)] = src.to(self.device)
+                continue
+            spec = ini.philox_spec(shape)
+            if spec is not None:
+                philox_fill(view, self.seed, v.index, *spec)
+            else:
+                g = torch.Generator().manual_seed(self.seed * 1000003 + v.index)
+                view.copy_(ini(shape, g).reshape(-1).to(self.device))
 
     def refresh_shadow(self) -> None:
         if self.shadow is not None:

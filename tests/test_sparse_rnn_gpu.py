@@ -267,3 +267,15 @@ def test_char_lstm_learns_and_graph(gpu):
             l, st = tr.step(torch.from_numpy(x).to(gpu), torch.from_numpy(y).to(gpu), st)
             losses.append(float(l))
     assert losses[-1] < 0.3 * losses[0]
+
+
+def test_philox_kernel_matches_numpy_twin(gpu):
+    from tensorflow_examples_amd.random import philox_numpy
+    for dist, a, b in ((0, -0.5, 0.5), (1, 0.0, 1.0), (2, 0.1, 2.0)):
+        t = torch.empty(100003, device=gpu)
+        torch.ops.tfx.philox_fill(t, 1234567, 42, dist, a, b)
+        ref = torch.from_numpy(philox_numpy(100003, 1234567, 42, dist, a, b))
+        if dist == 0:
+            assert torch.equal(t.cpu(), ref)
+        else:  # device vs libm log/cos/sin rounding only
+            assert (t.cpu() - ref).abs().max().item() < 1e-4 * max(1.0, b)
