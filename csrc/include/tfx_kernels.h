@@ -75,10 +75,12 @@ void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float
                  float momentum, float* run_mean, float* run_var, float* save, hipStream_t s);
 void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
                   const float* run_var, float* save, hipStream_t s);
+// mask (optional, residual + ReLU on the C % 8 == 0 path): 1 bit per element, the ReLU mask of y
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
-              uint16_t* y, hipStream_t s);
-void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const float* save, int64_t M,
-                 int C, bool relu, float* slots, float* red, float* dgamma, float* dbeta, uint16_t* dx,
+              uint16_t* y, uint8_t* mask, hipStream_t s);
+// residual + ReLU: pass the forward's mask (vector path) or res (generic path) for the ReLU mask
+void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask, const float* save,
+                 int64_t M, int C, bool relu, float* slots, float* red, float* dgamma, float* dbeta, uint16_t* dx,
                  uint16_t* dres, hipStream_t s);
 
 // ---------------------------------------------------------------- loss / pooling

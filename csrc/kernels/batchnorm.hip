@@ -192,11 +192,14 @@ __global__ void bn_eval_prep_kernel(int C, const float* __restrict__ gamma, cons
 // ------------------------------------------------------------------ apply (fixed channel vector)
 // grid * 256 is a multiple of C/8 (host), so vector i = tid + k*stride always has channel vector
 // (tid0 % (C/8)).  Two vectors per iteration for memory-level parallelism.
+// With RES && RELU the ReLU mask of the output is also stored, one bit per element (one byte per
+// 8-channel vector): the backward then reads 1/16 of the residual tensor's bytes instead of the
+// residual itself (twice: reduce and apply).
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(256) bn_apply_vec_kernel(const uint16_t* __restrict__ x,
                                                            const uint16_t* __restrict__ res,
                                                            const float* __restrict__ save, int64_t nvec, int C,
-                                                           uint16_t* __restrict__ y) {
+                                                           uint16_t* __restrict__ y, uint8_t* __restrict__ mask) {
   const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int c0 = (int)(i0 % (C >> 3)) * 8;
@@ -210,13 +213,16 @@ __global__ void __launch_bounds__(256) bn_apply_vec_kernel(const uint16_t* __res
     float f[8], r[8];
     unpack8(reinterpret_cast<const U4*>(x)[i], f);
     if (RES) unpack8(reinterpret_cast<const U4*>(res)[i], r);
+    uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float z = fmaf(f[k], sc[k], sh[k]);
       if (RES) z += r[k];
+      bits |= (z > 0.f ? 1u : 0u) << k;
       f[k] = RELU ? fmaxf(z, 0.f) : z;
     }
     reinterpret_cast<U4*>(y)[i] = pack8(f);
+    if (RES && RELU && mask) mask[i] = (uint8_t)bits;
   };
   int64_t i = i0;
   for (; i + stride < nvec; i += 2 * stride) {
@@ -242,10 +248,11 @@ __global__ void __launch_bounds__(256) bn_apply_gen_kernel(const uint16_t* __res
 }
 
 // ------------------------------------------------------------------ backward reduce
+// RES && RELU: the ReLU mask comes from the forward's mask bits (``mask``, one byte per vector)
 template <bool RES, bool RELU, int U>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* __restrict__ g,
                                                                 const uint16_t* __restrict__ x,
-                                                                const uint16_t* __restrict__ res,
+                                                                const uint8_t* __restrict__ mask,
                                                                 const float* __restrict__ save, int64_t M, int C,
                                                                 float* __restrict__ slots) {
   const int tpr = C >> 3;
@@ -262,42 +269,42 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(const uint16_t* 
   }
   float sg[8] = {0}, sx[8] = {0};
   const int64_t stride = (int64_t)gridDim.x * rpb;
-  auto accum = [&](const U4& gv, const U4& xv, const U4& rv) {
-    float gf[8], xf[8], rf[8];
+  auto accum = [&](const U4& gv, const U4& xv, uint32_t mb) {
+    float gf[8], xf[8];
     unpack8(gv, gf);
     unpack8(xv, xf);
-    if (RES && RELU) unpack8(rv, rf);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float gg = gf[k];
-      if (RELU) {
-        float z = fmaf(xf[k], sc[k], sh[k]);
-        if (RES) z += rf[k];
-        gg = z > 0.f ? gg : 0.f;
+      if (RES && RELU) {
+        gg = ((mb >> k) & 1u) ? gg : 0.f;
+      } else if (RELU) {
+        gg = fmaf(xf[k], sc[k], sh[k]) > 0.f ? gg : 0.f;
       }
       sg[k] += gg;
       sx[k] = fmaf(gg, (xf[k] - mu[k]) * is[k], sx[k]);
     }
   };
   // U independent rows in flight per thread
+  const int tprv = C >> 3;
   int64_t r = (int64_t)blockIdx.x * rpb + r0;
   for (; r + (U - 1) * stride < M; r += U * stride) {
-    U4 gv[U], xv[U], rv[U];
+    U4 gv[U], xv[U];
+    uint32_t mv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t off = (r + u * stride) * C + cv * 8;
       gv[u] = *reinterpret_cast<const U4*>(g + off);
       xv[u] = *reinterpret_cast<const U4*>(x + off);
-      if (RES && RELU) rv[u] = *reinterpret_cast<const U4*>(res + off);
+      mv[u] = (RES && RELU) ? mask[(r + u * stride) * tprv + cv] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) accum(gv[u], xv[u], rv[u]);
+    for (int u = 0; u < U; ++u) accum(gv[u], xv[u], mv[u]);
   }
   for (; r < M; r += stride) {
     const int64_t off = r * C + cv * 8;
-    U4 rv = {0u, 0u, 0u, 0u};
-    if (RES && RELU) rv = *reinterpret_cast<const U4*>(res + off);
-    accum(*reinterpret_cast<const U4*>(g + off), *reinterpret_cast<const U4*>(x + off), rv);
+    const uint32_t mb = (RES && RELU) ? mask[r * tprv + cv] : 0u;
+    accum(*reinterpret_cast<const U4*>(g + off), *reinterpret_cast<const U4*>(x + off), mb);
   }
   __shared__ float lds[256 * 8];
   for (int pass = 0; pass < 2; ++pass) {
@@ -359,7 +366,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_gen_kernel(const uint16_t* 
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* __restrict__ g,
                                                                const uint16_t* __restrict__ x,
-                                                               const uint16_t* __restrict__ res,
+                                                               const uint8_t* __restrict__ mask,
                                                                const float* __restrict__ save,
                                                                const float* __restrict__ red, int64_t nvec, int64_t M,
                                                                int C, uint16_t* __restrict__ dx,
@@ -381,17 +388,17 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* _
     D[k] = sc[k] * (kx * mu - kg);
   }
   for (int64_t i = i0; i < nvec; i += stride) {
-    float gf[8], xf[8], rf[8], o[8];
+    float gf[8], xf[8], o[8];
     unpack8(reinterpret_cast<const U4*>(g)[i], gf);
     unpack8(reinterpret_cast<const U4*>(x)[i], xf);
-    if (RES && RELU) unpack8(reinterpret_cast<const U4*>(res)[i], rf);
+    const uint32_t mb = (RES && RELU) ? mask[i] : 0u;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float gg = gf[k];
-      if (RELU) {
-        float z = fmaf(xf[k], sc[k], sh[k]);
-        if (RES) z += rf[k];
-        gg = z > 0.f ? gg : 0.f;
+      if (RES && RELU) {
+        gg = ((mb >> k) & 1u) ? gg : 0.f;
+      } else if (RELU) {
+        gg = fmaf(xf[k], sc[k], sh[k]) > 0.f ? gg : 0.f;
       }
       gf[k] = gg;
       o[k] = fmaf(A[k], gg, fmaf(B[k], xf[k], D[k]));
@@ -476,25 +483,26 @@ void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const
 }
 
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu, uint16_t* y,
-              hipStream_t s) {
+              uint8_t* mask, hipStream_t s) {
   const int64_t n = M * C;
   const bool has_res = res != nullptr;
   if (C % 8 == 0) {
     const int64_t nvec = n / 8;
     const int g = fixed_channel_grid(nvec, C);
-    TFX_DISPATCH_RR(has_res, relu, (bn_apply_vec_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, nvec, C, y)));
+    TFX_DISPATCH_RR(has_res, relu, (bn_apply_vec_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, nvec, C, y, mask)));
   } else {
     const int g = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_apply_gen_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, n, C, y)));
   }
 }
 
-void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C,
-                 bool relu, float* slots, float* red, float* dgamma, float* dbeta, uint16_t* dx, uint16_t* dres,
-                 hipStream_t s) {
-  const bool has_res = res != nullptr;
+void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask, const float* save,
+                 int64_t M, int C, bool relu, float* slots, float* red, float* dgamma, float* dbeta, uint16_t* dx,
+                 uint16_t* dres, hipStream_t s) {
+  const bool has_res = res != nullptr || mask != nullptr;
   const int64_t n = M * C;
-  if (vec_ok(C)) {
+  // the vector kernels take the residual ReLU mask from the forward's mask bits
+  if (vec_ok(C) && (!has_res || !relu || mask)) {
     const int rpb = 256 / (C / 8);
     static const int U = [] {
       const char* e = getenv("TFX_BN_RED_U");
@@ -503,13 +511,13 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
     const int gr = grid_for(M, rpb * (U >= 4 ? 4 : 8));
     if (U >= 4) {
       TFX_DISPATCH_RR(has_res, relu,
-                      (bn_bwd_reduce_vec_kernel<R_, L_, 4><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
+                      (bn_bwd_reduce_vec_kernel<R_, L_, 4><<<gr, 256, 0, s>>>(g, x, mask, save, M, C, slots)));
     } else if (U == 2) {
       TFX_DISPATCH_RR(has_res, relu,
-                      (bn_bwd_reduce_vec_kernel<R_, L_, 2><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
+                      (bn_bwd_reduce_vec_kernel<R_, L_, 2><<<gr, 256, 0, s>>>(g, x, mask, save, M, C, slots)));
     } else {
       TFX_DISPATCH_RR(has_res, relu,
-                      (bn_bwd_reduce_vec_kernel<R_, L_, 1><<<gr, 256, 0, s>>>(g, x, res, save, M, C, slots)));
+                      (bn_bwd_reduce_vec_kernel<R_, L_, 1><<<gr, 256, 0, s>>>(g, x, mask, save, M, C, slots)));
     }
   } else {
     dim3 grid((C + 63) / 64, grid_for(M, 64));
@@ -518,11 +526,11 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
   }
   bn_slot_reduce_kernel<<<(C + 15) / 16, 256, 0, s>>>(slots, C, red, dgamma, dbeta);
   // with a residual input dres = g' is produced (the host guarantees dres != nullptr then)
-  if (C % 8 == 0) {
+  if (vec_ok(C) && (!has_res || !relu || mask)) {
     const int64_t nvec = n / 8;
     const int ga = fixed_channel_grid(nvec, C);
     TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_vec_kernel<R_, L_><<<ga, 256, 0, s>>>(
-                                       g, x, res, save, red, nvec, M, C, dx, dres)));
+                                       g, x, mask, save, red, nvec, M, C, dx, dres)));
   } else {
     const int ga = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_gen_kernel<R_, L_><<<ga, 256, 0, s>>>(

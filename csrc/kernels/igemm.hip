@@ -215,11 +215,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64
 // output columns of one row: bf16 outputs leave as one 8-byte store per 16x16 tile per lane, and
 // transposed f32 outputs (dW^T) as 16-lane contiguous runs.  Plain f32 atomics keep SWAP=false
 // (4 rows x 16 contiguous columns per instruction).
-template <int AKIND, int BKIND, int BM, int BN, bool SWAP>
-__global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
+// STG = LDS stages: 2 for the pipelined K loop; 1 for single-k-tile GEMMs (K <= 64: the 1x1 convs
+// of 64-channel layers), which then fit 4 blocks per CU -- those are memory-bound, and occupancy is
+// what keeps enough loads and stores in flight.
+template <int AKIND, int BKIND, int BM, int BN, bool SWAP, int STG>
+__global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4) : 2) igemm_kernel(IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BKT * 2, STAGE = (BM + BN) * BKT * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[STG * STAGE];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -285,6 +288,12 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
     }
   };
 
+  if constexpr (STG == 1) {  // host guarantees a single k-tile
+    issue(kt0, sa0, sb0);
+    stage_store(0, sa0, sb0);
+    __syncthreads();
+    compute(0);
+  } else {
   // prologue: tile kt0 -> stage 0, tile kt0+1 in flight in set 1
   issue(kt0, sa0, sb0);
   issue(kt0 + 1, sa1, sb1);
@@ -311,6 +320,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
       stage_store(0, sa0, sb0);
       __syncthreads();
     }
+  }
   }
 
   // Element (m, n) of lane's acc[i][j][r]:
@@ -413,7 +423,49 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmArgs a) {
         }
     }
     const bool relu = a.relu != 0;
-    if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 3) == 0 && (a.N & 3) == 0) {
+    if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0 && (TN % 2) == 0) {
+      // 16-byte stores: lanes l and l^16 hold 4-column halves of the same row in tiles j and j+1;
+      // swapping one half (4 floats over __shfl_xor 16) gives each lane 8 consecutive columns --
+      // the even lane of tile j, the odd lane of tile j+1 -- i.e. half the store instructions.
+      uint16_t* Cb = reinterpret_cast<uint16_t*>(a.Cp);
+      const bool odd = (lane >> 4) & 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < TN; j += 2) {
+          float v0[4], v1[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v0[r] = acc[i][j][r] + bias[j][r];
+            v1[r] = acc[i][j + 1][r] + bias[j + 1][r];
+            if (relu) {
+              v0[r] = fmaxf(v0[r], 0.f);
+              v1[r] = fmaxf(v1[r], 0.f);
+            }
+          }
+          float o[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float send = odd ? v0[r] : v1[r];
+            const float recv = __shfl_xor(send, 16, 64);
+            o[r] = odd ? recv : v0[r];
+            o[4 + r] = odd ? v1[r] : recv;
+          }
+          const int n = nb + (j + (odd ? 1 : 0)) * 16 + ((lane >> 5) << 3);
+          if (m < a.M && n < a.N) {
+            uint16_t* dst = Cb + (int64_t)m * a.ldc + n;
+            if (a.addend) {  // fused residual-branch gradient sum (dX = dgrad + other branch)
+              float ad[8];
+              unpack8(*reinterpret_cast<const U4*>(a.addend + (int64_t)m * a.ldc + n), ad);
+#pragma unroll
+              for (int r = 0; r < 8; ++r) o[r] += ad[r];
+            }
+            *reinterpret_cast<U4*>(dst) = pack8(o);
+          }
+        }
+      }
+    } else if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 3) == 0 && (a.N & 3) == 0) {
       uint16_t* Cb = reinterpret_cast<uint16_t*>(a.Cp);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -540,11 +592,27 @@ void launch_t(IgemmArgs& a, hipStream_t s) {
   const int grid = tiles * splits;
   if (grid == 0) return;
   // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
-  if (a.out_mode == OUT_BF16 || a.trans_out) igemm_kernel<AK, BK, BM, BN, true><<<grid, NT, 0, s>>>(a);
-  else igemm_kernel<AK, BK, BM, BN, false><<<grid, NT, 0, s>>>(a);
+  const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
+  if (nkt == 1 && splits == 1) {
+    if (swap) igemm_kernel<AK, BK, BM, BN, true, 1><<<grid, NT, 0, s>>>(a);
+    else igemm_kernel<AK, BK, BM, BN, false, 1><<<grid, NT, 0, s>>>(a);
+  } else {
+    if (swap) igemm_kernel<AK, BK, BM, BN, true, 2><<<grid, NT, 0, s>>>(a);
+    else igemm_kernel<AK, BK, BM, BN, false, 2><<<grid, NT, 0, s>>>(a);
+  }
 }
 
-// tile choice: narrow N -> 256x64 (if M is large) or 128x64; otherwise 128x128
+// tile choice: narrow N -> 256x64 (if M is large) or 128x64; otherwise 128x128, unless that leaves
+// the chip under-filled (fewer than 2 blocks per CU: the small late-stage convs), then 128x64 --
+// twice the blocks for the same K loop.  TFX_TILE_POLICY=0 disables the under-fill rule (A/B).
+int tile_policy() {
+  static const int p = [] {
+    const char* e = getenv("TFX_TILE_POLICY");
+    return e ? atoi(e) : 1;
+  }();
+  return p;
+}
+
 template <int AK, int BK, bool ALLOW256 = true>
 void launch_shape(IgemmArgs& a, hipStream_t s) {
   if (a.N <= 64) {
@@ -553,6 +621,10 @@ void launch_shape(IgemmArgs& a, hipStream_t s) {
     }
     launch_t<AK, BK, 128, 64>(a, s);
   } else {
+    const long tiles128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
+    if constexpr (ALLOW256) {
+      if (tile_policy() >= 1 && tiles128 < 512) return launch_t<AK, BK, 128, 64>(a, s);
+    }
     launch_t<AK, BK, 128, 128>(a, s);
   }
 }

@@ -212,9 +212,12 @@ void sgemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor out, bool accumulat
 // ------------------------------------------------------------------ batch norm
 // slots: the layer's persistent [NSLOT][2][C] workspace; have_stats = the producer (conv epilogue)
 // already accumulated this batch's statistics into it.
-std::tuple<Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
-                                        optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
-                                        double eps, optional<Tensor> res, bool relu, Tensor slots, bool have_stats) {
+// returns (y, save, mask): mask = 1-bit ReLU mask of y (uint8 per 8 channels) for residual + ReLU
+// layers on the vector path (what the backward reads instead of the residual), else undefined.
+std::tuple<Tensor, Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
+                                                optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
+                                                double eps, optional<Tensor> res, bool relu, Tensor slots,
+                                                bool have_stats) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(slots.numel() == tfx::NSLOT * 2 * C && slots.scalar_type() == at::kFloat, "stat slots");
@@ -231,8 +234,12 @@ std::tuple<Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma, option
   if (!have_stats) tfx::bn_stats(bf(x), M, C, sl, s);
   tfx::bn_finalize(sl, M, C, fp(gamma), fp(beta), eps, momentum, fpm(run_mean), fpm(run_var),
                    save.data_ptr<float>(), s);
-  tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y), s);
-  return {y, save};
+  Tensor mask;
+  if (r && relu && C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0)
+    mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y),
+                mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, s);
+  return {y, save, mask};
 }
 
 std::tuple<Tensor, Tensor> bn_fwd_eval(Tensor x, optional<Tensor> gamma, optional<Tensor> beta, Tensor run_mean,
@@ -245,14 +252,16 @@ std::tuple<Tensor, Tensor> bn_fwd_eval(Tensor x, optional<Tensor> gamma, optiona
   tfx::bn_eval_prep(C, fp(gamma), fp(beta), eps, run_mean.data_ptr<float>(), run_var.data_ptr<float>(),
                     save.data_ptr<float>(), s);
   const uint16_t* r = (res.has_value() && res->defined()) ? bf(*res) : nullptr;
-  tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y), s);
+  tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y), nullptr, s);
   return {y, save};
 }
 
 // returns dx, dres (undefined unless res given), red = [dbeta(C) | dgamma(C)]; when dgamma/dbeta
 // are given the parameter gradients are accumulated in place by the reduce kernel.
+// residual layers: pass the forward's ``mask`` (vector path; then ``res`` may be omitted) or ``res``.
 std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> res, Tensor save, bool relu,
-                                          Tensor slots, optional<Tensor> dgamma, optional<Tensor> dbeta) {
+                                          Tensor slots, optional<Tensor> dgamma, optional<Tensor> dbeta,
+                                          optional<Tensor> mask) {
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd grad shape");
@@ -261,13 +270,20 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
   auto dx = at::empty_like(x);
   Tensor dres;
   const uint16_t* r = nullptr;
+  const uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() * 8 == x.numel(), "relu mask size");
+    mk = mask->data_ptr<uint8_t>();
+  }
   if (res.has_value() && res->defined()) {
     CHECK_CONTIG(*res);
     r = bf(*res);
-    dres = at::empty_like(x);
   }
-  tfx::bn_backward(bf(g), bf(x), r, save.data_ptr<float>(), M, C, relu, slots.data_ptr<float>(),
-                   red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), bfm(dx), r ? bfm(dres) : nullptr, cur_stream());
+  if (r || mk) dres = at::empty_like(x);
+  TORCH_CHECK(!(relu && mk == nullptr && r == nullptr && dres.defined()), "residual bn_bwd needs res or mask");
+  tfx::bn_backward(bf(g), bf(x), r, mk, save.data_ptr<float>(), M, C, relu, slots.data_ptr<float>(),
+                   red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), bfm(dx), dres.defined() ? bfm(dres) : nullptr,
+                   cur_stream());
   return {dx, dres, red};
 }
 

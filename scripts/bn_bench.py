@@ -45,11 +45,12 @@ def main():
         r = torch.randn(M, C, device="cuda").bfloat16() if res else None
         gam, bet = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
         ws = torch.zeros(64 * 2 * C, device="cuda")
-        y, save = torch.ops.tfx.bn_fwd_train(x, gam, bet, None, None, 0.1, 1e-5, r, True, ws, False)
+        y, save, mask = torch.ops.tfx.bn_fwd_train(x, gam, bet, None, None, 0.1, 1e-5, r, True, ws, False)
+        mask = mask if (mask is not None and mask.numel()) else None
         tf = t(lambda: torch.ops.tfx.bn_fwd_train(x, gam, bet, None, None, 0.1, 1e-5, r, True, ws, False))
-        tb = t(lambda: torch.ops.tfx.bn_bwd(g, x, r, save, True, ws, None, None))
+        tb = t(lambda: torch.ops.tfx.bn_bwd(g, x, None if mask is not None else r, save, True, ws, None, None, mask))
         nb = M * C * 2
-        bf, bb = nb * (4 if res else 3), nb * (8 if res else 4)
+        bf, bb = nb * (4 if res else 3) + (nb // 16 if res else 0), nb * (6 if res else 4) + (nb // 8 if res else 0)
         print(f"M={M:7d} C={C:5d} res={int(res)} x{cnt}: fwd {tf:7.1f}us ({bf / tf / 1e3:5.2f} GB/s)  "
               f"bwd {tb:7.1f}us ({bb / tb / 1e3:5.2f} GB/s)")
         tot_f += cnt * tf

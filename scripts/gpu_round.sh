@@ -23,6 +23,16 @@ for s in $STEPS; do
         timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/ab_on_$i.log 2>&1 || exit 1
       done
       grep -ho '"ms_per_step": [0-9.]*' gpurun_out/ab_*.log ;;
+    abtile)
+      for i in 1 2; do
+        TFX_TILE_POLICY=0 timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/abt_off_$i.log 2>&1 || exit 1
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/abt_on_$i.log 2>&1 || exit 1
+      done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/abt_*.log ;;
+    kerneltests)
+      timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py tests/test_resnet_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1
+      rc=$?; echo "kerneltests rc=$rc"; tail -5 gpurun_out/pytest_kernels.log
+      [ $rc -eq 0 ] || exit $rc ;;
     graph)
       timeout -k 10 400 python bench.py --steps 20 --warmup 5 --graph > gpurun_out/bench_graph.log 2>&1
       rc=$?; echo "graph rc=$rc"; tail -3 gpurun_out/bench_graph.log; [ $rc -eq 0 ] || exit $rc ;;

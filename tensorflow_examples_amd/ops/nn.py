@@ -195,12 +195,16 @@ class _BatchNorm(torch.autograd.Function):
                 ws = torch.zeros(64 * 2 * x.shape[-1], dtype=torch.float32, device=x.device)
                 stats_ready = False
             ctx.ws = ws
+            mask = None
             if training:
-                y, save = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu, ws,
-                                                     bool(stats_ready))
+                y, save, mask = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu, ws,
+                                                           bool(stats_ready))
             else:
                 y, save = torch.ops.tfx.bn_fwd_eval(x, g_t, b_t, rm, rv, eps, res, relu)
-            ctx.save_for_backward(x, res, save)
+            if mask is not None and mask.numel() == 0:
+                mask = None
+            # residual + ReLU: the backward needs only the 1-bit ReLU mask, not the residual tensor
+            ctx.save_for_backward(x, None if mask is not None else res, save, mask)
             return y
         ctx.save_for_backward(x, res)
         with torch.no_grad():
@@ -211,12 +215,13 @@ class _BatchNorm(torch.autograd.Function):
         rm, rv, momentum, eps, relu, training = ctx.cfg
         gamma, beta = ctx.gamma, ctx.beta
         if ctx.native:
-            x, res, save = ctx.saved_tensors
+            x, res, save, mask = ctx.saved_tensors
             if not training:
                 raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
             train_p = gamma is not None and gamma.trainable
             dx, dres, red = torch.ops.tfx.bn_bwd(gy.contiguous(), x, res, save, relu, ctx.ws,
-                                                 gamma.grad if train_p else None, beta.grad if train_p else None)
+                                                 gamma.grad if train_p else None, beta.grad if train_p else None,
+                                                 mask)
             if train_p:
                 _grad_ready(gamma, beta)
             if ctx.has_res and ctx.res_sink is not None:

@@ -121,8 +121,13 @@ def test_batchnorm_train(gpu, C, res, relu):
     beta = torch.randn(C, device=gpu)
     rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
     ws = torch.zeros(64 * 2 * C, device=gpu)
-    y, save = torch.ops.tfx.bn_fwd_train(x, gamma, beta, rm, rv, 0.1, 1e-5, r, relu, ws, False)
+    y, save, mask = torch.ops.tfx.bn_fwd_train(x, gamma, beta, rm, rv, 0.1, 1e-5, r, relu, ws, False)
     assert ws.abs().max().item() == 0.0  # consumed workspace is re-zeroed
+    if res and relu and C % 8 == 0 and 256 % (C // 8) == 0:  # 1-bit ReLU mask of y, one byte per 8 channels
+        bits = torch.stack([(mask.long() >> k) & 1 for k in range(8)], 1).reshape(M, C)
+        assert torch.equal(bits.bool(), y.float() > 0)
+    else:
+        assert mask is None or mask.numel() == 0
     xr = x.float().requires_grad_(True)
     gr = gamma.clone().requires_grad_(True)
     br = beta.clone().requires_grad_(True)
@@ -139,8 +144,13 @@ def test_batchnorm_train(gpu, C, res, relu):
     g = _bf(torch.randn(M, C, device=gpu))
     yr.backward(g.float())
     dgam, dbet = torch.ones(C, device=gpu), torch.zeros(C, device=gpu)
-    dx, dres, red = torch.ops.tfx.bn_bwd(g, x, r, save, relu, ws, dgam, dbet)
+    has_mask = mask is not None and mask.numel() > 0
+    dx, dres, red = torch.ops.tfx.bn_bwd(g, x, None if has_mask else r, save, relu, ws, dgam, dbet,
+                                         mask if has_mask else None)
     assert ws.abs().max().item() == 0.0
+    if has_mask:  # the residual-tensor path (generic kernels) gives the same gradients
+        dx2, dres2, _ = torch.ops.tfx.bn_bwd(g, x, r, save, relu, ws, None, None, None)
+        assert _rel(dx2, dx) < 1e-2 and _rel(dres2, dres) < 1e-2
     assert _rel(dx, xr.grad) < 2e-2
     assert _rel(red[C:], gr.grad) < 1e-3 and _rel(red[:C], br.grad) < 1e-3
     assert _rel(dgam - 1, gr.grad) < 1e-3 and _rel(dbet, br.grad) < 1e-3  # accumulated in place
@@ -222,6 +232,6 @@ def test_conv_fwd_fused_bn_stats(gpu, shape):
     assert torch.allclose(s[0], yf.sum(0), rtol=1e-4, atol=1e-3)
     assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
     gamma, beta = torch.ones(Ko, device=gpu), torch.zeros(Ko, device=gpu)
-    y1, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots, True)
-    y2, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots, False)
+    y1, _, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots, True)
+    y2, _, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots, False)
     assert _rel(y1, y2) < 1e-3
