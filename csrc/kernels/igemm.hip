@@ -585,7 +585,11 @@ void launch_t(IgemmArgs& a, hipStream_t s) {
   const int nkt = (a.K + BKT - 1) / BKT;
   const int tiles = a.tiles_m * a.tiles_n;
   int splits = 1;
-  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, 512);
+  static const int want = [] {
+    const char* e = getenv("TFX_SPLITK_BLOCKS");
+    return e ? atoi(e) : 256;  // one block per CU: measured best (fewer f32 atomic partials)
+  }();
+  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, want);
   a.kps = (nkt + splits - 1) / splits;
   if (splits > 1) a.kps += a.kps & 1;  // even k-tiles per split: no zero step in the loop
   splits = (nkt + a.kps - 1) / a.kps;

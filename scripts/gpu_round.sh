@@ -29,6 +29,14 @@ for s in $STEPS; do
         timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/abt_on_$i.log 2>&1 || exit 1
       done
       grep -o '"ms_per_step": [0-9.]*' gpurun_out/abt_*.log ;;
+    absplit)
+      for v in 128 192 256; do
+        TFX_SPLITK_BLOCKS=$v timeout -k 10 400 python bench.py --steps 40 --warmup 5 > gpurun_out/abs_$v.log 2>&1 || exit 1
+      done
+      for v in 128 192 256; do
+        TFX_SPLITK_BLOCKS=$v timeout -k 10 400 python bench.py --steps 40 --warmup 5 > gpurun_out/abs2_$v.log 2>&1 || exit 1
+      done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/abs*.log ;;
     kerneltests)
       timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py tests/test_resnet_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1
       rc=$?; echo "kerneltests rc=$rc"; tail -5 gpurun_out/pytest_kernels.log
