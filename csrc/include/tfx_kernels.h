@@ -22,9 +22,10 @@ struct FastDiv {
     m = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
   }
 #ifdef __HIPCC__
+  // valid for n < 2^31 (then t + n < 2^32): every index the kernels divide is < 2^31
   __device__ __forceinline__ uint32_t div(uint32_t n) const {
     const uint32_t t = __umulhi(n, m);
-    return (uint32_t)(((uint64_t)t + n) >> s);
+    return (t + n) >> s;
   }
 #endif
   uint32_t div_host(uint32_t n) const {

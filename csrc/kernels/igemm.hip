@@ -76,51 +76,70 @@ __device__ __forceinline__ bf16x8_t lds_read_mn(const char* img, int cb, int kk,
 
 // ------------------------------------------------------------------ operand loaders
 // ROWS = tile extent of this operand (BM for A, BN for B).  K-major: thread covers chunk t&7 of rows
-// (t>>3) + 32*i.  MN-major: chunk t % (ROWS/8) of k-rows t / (ROWS/8) + (2048/ROWS)*i.
+// (t>>3) + 32*i.  MN-major: thread covers ONE k-row, t>>2, and chunks (t&3) + 4*j of it -- the k
+// decode (pixel n,p,q for the weight gradient, (r,s,ko) for the data gradient's weights) is done once
+// per k-tile, not once per load; the 4-apart chunks keep the swizzled ds_write_b128 conflict-free.
+// Address math is split into a per-row part precomputed once (init) and a per-k-tile part shared by
+// all of a thread's rows, with 24-bit multiplies (v_mul_u32_u24, full rate; the host guarantees
+// pixel counts < 2^24) instead of quarter-rate 32-bit ones: the K loop's VALU issue competes with
+// the MFMAs for the SIMD (MI355X_MICROARCH.md 'vector-instruction ISSUE cost').
+__device__ __forceinline__ int mul24(int a, int b) { return (int)__umul24((unsigned)a, (unsigned)b); }
+
 template <int KIND, int ROWS>
 struct Loader {
   static constexpr bool KM = is_kmaj(KIND);
   static constexpr int NP = ROWS / 32;          // 16-B loads per thread per tile
   static constexpr int CH = ROWS / 8;           // MN-major chunks per k-row
-  static constexpr int RSTEP = NT / CH;         // MN-major k-row step between passes
-  int c0;        // K-major: element offset of chunk in k (8*kc); MN-major: column of the chunk
-  int r0;        // K-major: first row; MN-major: first k-row
-  bool col_ok;   // MN-major column validity
-  int ctx0[NP], ctx1[NP], ctx2[NP];
-  int cr, cs, cc;  // MN_WGRAD_X column decode
+  static_assert(KM || CH == 4 * NP, "MN-major: 4 threads per k-row");
+  int c0;        // K-major: element offset of chunk in k (8*kc)
+  int r0;        // K-major: first row; MN-major: the k-row
+  int ctx0[NP], ctx1[NP], ctx2[NP], base[NP];
+  int col[NP];                     // MN-major: column of chunk j (-1: out of range)
+  int cr[NP], cs[NP], cc[NP];      // MN_WGRAD_X column decode per chunk
+  int t3_;                         // MN-major: first chunk (t & 3) of the k-row
 
-  __device__ __forceinline__ void init(const IgemmArgs& a, int base, int lim, int t) {
+  __device__ __forceinline__ void init(const IgemmArgs& a, int base0, int lim, int ld, int t) {
     if constexpr (KM) {
       c0 = 8 * (t & 7);
       r0 = t >> 3;
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
-        const int row = base + r0 + 32 * i;
+        const int row = base0 + r0 + 32 * i;
         const bool ok = row < lim;
         if constexpr (KIND == KM_DENSE) {
-          ctx0[i] = ok ? row : -1;
+          ctx0[i] = ok ? 0 : -1;
+          base[i] = row * ld;
         } else {
           const int GY = KIND == KM_FWD_X ? a.P : a.H, GX = KIND == KM_FWD_X ? a.Q : a.W;
           int n = row / (GY * GX), yx = row - n * GY * GX, y = yx / GX, x = yx - y * GX;
-          ctx0[i] = ok ? n : -1;
+          // rows past M get a y far out of range: every bounds test below then fails (no flag register)
+          constexpr int FAR = -(1 << 28);
           if constexpr (KIND == KM_FWD_X) {
-            ctx1[i] = y * a.sh - a.ph;
+            ctx1[i] = ok ? y * a.sh - a.ph : FAR;
             ctx2[i] = x * a.sw - a.pw;
+            // element offset of (n, iy0, ix0, 0): may be negative (padding), only used when in range
+            base[i] = ((n * a.H + y * a.sh - a.ph) * a.W + ctx2[i]) * a.C;
           } else {
-            ctx1[i] = y + a.ph;
+            ctx1[i] = ok ? y + a.ph : FAR;
             ctx2[i] = x + a.pw;
+            base[i] = n * a.P;
           }
         }
       }
     } else {
-      c0 = base + 8 * (t % CH);
-      r0 = t / CH;
-      col_ok = c0 < lim;
-      if constexpr (KIND == MN_WGRAD_X) {
-        const int rs = col_ok ? c0 / a.C : 0;
-        cc = c0 - rs * a.C;
-        cr = rs / a.S;
-        cs = rs - cr * a.S;
+      r0 = t >> 2;
+      t3_ = t & 3;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const int cj = base0 + 8 * ((t & 3) + 4 * j);
+        col[j] = cj < lim ? cj : -1;
+        if constexpr (KIND == MN_DENSE) base[j] = r0 * ld + cj;
+        if constexpr (KIND == MN_WGRAD_X) {
+          const int rs = cj < lim ? cj / a.C : 0;
+          cc[j] = cj - rs * a.C;
+          cr[j] = rs / a.S;
+          cs[j] = rs - cr[j] * a.S;
+        }
       }
     }
   }
@@ -135,49 +154,56 @@ struct Loader {
       if constexpr (KIND == KM_DENSE) {
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
-          const uint32_t o = (uint32_t)(ctx0[i] * ld + k) * 2u;
+          const uint32_t o = (uint32_t)(base[i] + k) * 2u;
           off[i] = (kok & (ctx0[i] >= 0)) ? o : BAD;
         }
       } else if constexpr (KIND == KM_FWD_X) {
-        const int rs = a.fd_C.div(k), c = k - rs * a.C, r = a.fd_S.div(rs), s = rs - r * a.S;
+        const int rs = a.fd_C.div(k), c = k - mul24(rs, a.C), r = a.fd_S.div(rs), s = rs - mul24(r, a.S);
+        const int rdh = mul24(r, a.dh), sdw = mul24(s, a.dw);
+        const int dk = mul24(mul24(rdh, a.W) + sdw, a.C) + c;  // (r*dh*W + s*dw)*C + c
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
-          const int iy = ctx1[i] + r * a.dh, ix = ctx2[i] + s * a.dw;
-          const bool ok = kok & (ctx0[i] >= 0) & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
-          const uint32_t o = (uint32_t)(((ctx0[i] * a.H + iy) * a.W + ix) * a.C + c) * 2u;
+          const int iy = ctx1[i] + rdh, ix = ctx2[i] + sdw;
+          const bool ok = kok & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
+          const uint32_t o = (uint32_t)(base[i] + dk) * 2u;
           off[i] = ok ? o : BAD;
         }
       } else {  // KM_DGRAD_DY: k = (r, s, ko)
-        const int rs = a.fd_Ko.div(k), ko = k - rs * a.Ko, r = a.fd_S.div(rs), s = rs - r * a.S;
+        const int rs = a.fd_Ko.div(k), ko = k - mul24(rs, a.Ko), r = a.fd_S.div(rs), s = rs - mul24(r, a.S);
+        const int rdh = mul24(r, a.dh), sdw = mul24(s, a.dw);
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
-          const int ty = ctx1[i] - r * a.dh, tx = ctx2[i] - s * a.dw;
+          const int ty = ctx1[i] - rdh, tx = ctx2[i] - sdw;
           const int p = ty >> a.sh_log2, q = tx >> a.sw_log2;
-          const bool ok = kok & (ctx0[i] >= 0) & (ty >= 0) & (tx >= 0) & ((p << a.sh_log2) == ty) &
+          const bool ok = kok & (ty >= 0) & (tx >= 0) & ((p << a.sh_log2) == ty) &
                           ((q << a.sw_log2) == tx) & (p < a.P) & (q < a.Q);
-          const uint32_t o = (uint32_t)(((ctx0[i] * a.P + p) * a.Q + q) * a.Ko + ko) * 2u;
+          const uint32_t o = (uint32_t)(mul24(mul24(base[i] + p, a.Q) + q, a.Ko) + ko) * 2u;
           off[i] = ok ? o : BAD;
         }
       }
     } else {
+      const int k = k0 + r0;  // this thread's k-row: decoded once per k-tile
+      const bool kok = k < kend;
+      if constexpr (KIND == MN_DENSE) {
+        const int k0ld = k0 * ld;
 #pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int k = k0 + r0 + RSTEP * i;
-        bool ok = col_ok & (k < kend);
-        int e = 0;
-        if constexpr (KIND == MN_DENSE) {
-          e = k * ld + c0;
-        } else if constexpr (KIND == MN_DGRAD_W) {
-          const int rs = a.fd_Ko.div(k), ko = k - rs * a.Ko, r = a.fd_S.div(rs), s = rs - r * a.S;
-          e = ((ko * a.R + r) * a.S + s) * a.C + c0;
-        } else {  // MN_WGRAD_X
-          const int PQ = a.P * a.Q;
-          const int n = a.fd_PQ.div(k), pq = k - n * PQ, p = a.fd_Q.div(pq), q = pq - p * a.Q;
-          const int iy = p * a.sh - a.ph + cr * a.dh, ix = q * a.sw - a.pw + cs * a.dw;
-          ok = ok & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
-          e = ((n * a.H + iy) * a.W + ix) * a.C + cc;
+        for (int j = 0; j < NP; ++j) off[j] = (kok & (col[j] >= 0)) ? (uint32_t)(k0ld + base[j]) * 2u : BAD;
+      } else if constexpr (KIND == MN_DGRAD_W) {
+        const int rs = a.fd_Ko.div(k), ko = k - mul24(rs, a.Ko);
+        const int e0 = mul24(ko, a.R * a.S * a.C) + mul24(rs, a.C);  // ((ko*R + r)*S + s)*C
+#pragma unroll
+        for (int j = 0; j < NP; ++j) off[j] = (kok & (col[j] >= 0)) ? (uint32_t)(e0 + col[j]) * 2u : BAD;
+      } else {  // MN_WGRAD_X: pixel (n, p, q) of k, then per chunk its (r, s, c) tap
+        const int PQ = a.P * a.Q;
+        const int n = a.fd_PQ.div(k), pq = k - mul24(n, PQ), p = a.fd_Q.div(pq), q = pq - mul24(p, a.Q);
+        const int iy0 = mul24(p, a.sh) - a.ph, ix0 = mul24(q, a.sw) - a.pw, nH = mul24(n, a.H);
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+          const int iy = iy0 + mul24(cr[j], a.dh), ix = ix0 + mul24(cs[j], a.dw);
+          const bool ok = kok & (col[j] >= 0) & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
+          const int e = mul24(mul24(nH + iy, a.W) + ix, a.C) + cc[j];
+          off[j] = ok ? (uint32_t)e * 2u : BAD;
         }
-        off[i] = ok ? (uint32_t)e * 2u : BAD;
       }
     }
   }
@@ -192,7 +218,7 @@ struct Loader {
     for (int i = 0; i < NP; ++i) {
       int o;
       if constexpr (KM) o = kmaj_off(r0 + 32 * i, c0 >> 3);
-      else o = mn_off<ROWS>(r0 + RSTEP * i, (c0 & (ROWS - 1)) >> 3);
+      else o = mn_off<ROWS>(r0, (t3_ + 4 * i));
       *reinterpret_cast<u32x4_t*>(img + o) = r[i];
     }
   }
@@ -238,8 +264,8 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
 
   Loader<AKIND, BM> la;
   Loader<BKIND, BN> lb;
-  la.init(a, m0, a.M, t);
-  lb.init(a, n0, a.N, t);
+  la.init(a, m0, a.M, a.lda, t);
+  lb.init(a, n0, a.N, a.ldb, t);
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a.a_bytes), rb = make_rsrc(a.B, a.b_bytes);
 
   u32x4_t sa0[Loader<AKIND, BM>::NP], sb0[Loader<BKIND, BN>::NP];
@@ -639,6 +665,30 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
   if (a.out_mode == OUT_F32_ATOMIC && a.zero_out) {
     const size_t rows = a.trans_out ? a.N : a.M;
     TFX_HIP_CHECK(hipMemsetAsync(a.Cp, 0, sizeof(float) * rows * a.ldc, s));
+  }
+  // 1x1 stride-1 unpadded convs (two thirds of ResNet-50's) are plain GEMMs over the NHWC rows:
+  // dense loaders instead of the im2col / parity gathers -- no per-row address decode at all.
+  const bool pointwise = mode != MODE_GEMM && a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 &&
+                         a.pw == 0;
+  if (pointwise) {
+    switch (mode) {
+      case MODE_FWD:  // X[M][C] . W[Ko][C]^T
+        a.lda = a.C; a.ldb = a.C;
+        launch_shape<KM_DENSE, KM_DENSE>(a, s);
+        return;
+      case MODE_DGRAD:  // dY[M][Ko] . W[Ko][C]
+        a.lda = a.Ko; a.ldb = a.C;
+        launch_shape<KM_DENSE, MN_DENSE>(a, s);
+        return;
+      case MODE_WGRAD:  // dY^T[Ko][pix] . X[pix][C]
+        a.lda = a.Ko; a.ldb = a.C;
+        launch_shape<MN_DENSE, MN_DENSE, false>(a, s);
+        return;
+      case MODE_WGRAD_T:  // X^T[C][pix] . dY[pix][Ko]
+        a.lda = a.C; a.ldb = a.Ko;
+        launch_shape<MN_DENSE, MN_DENSE, false>(a, s);
+        return;
+    }
   }
   switch (mode) {
     case MODE_FWD: launch_shape<KM_FWD_X, KM_DENSE>(a, s); break;

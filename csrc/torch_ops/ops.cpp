@@ -49,6 +49,9 @@ ConvGeom geom(const std::vector<int64_t>& xs, const std::vector<int64_t>& ws, in
   TORCH_CHECK(g.P > 0 && g.Q > 0, "conv output is empty");
   TORCH_CHECK(g.N * std::max(g.H * g.W * g.C, g.P * g.Q * g.Ko) * 2 < (int64_t(1) << 31),
               "conv tensors must be < 2 GiB (32-bit buffer offsets)");
+  TORCH_CHECK(g.N * g.H * g.W < (int64_t(1) << 24) && g.N * g.P * g.Q < (int64_t(1) << 24) &&
+                  g.R * g.S * g.C < (int64_t(1) << 24),
+              "conv pixel counts must be < 2^24 (24-bit address multiplies): split the batch");
   return g;
 }
 
