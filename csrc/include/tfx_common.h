@@ -43,6 +43,21 @@ __device__ __forceinline__ U4 pack8(const float* f) {
   return r;
 }
 
+// Sum over each 16-lane DPP row (lanes 16k..16k+15), result in every lane of the row: 4 VALU
+// adds with DPP source modifiers (quad_perm xor 1, xor 2, row_half_mirror, row_mirror) instead of
+// ds_bpermute round trips through the LDS crossbar.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -35,7 +35,7 @@ struct FastDiv {
 };
 
 // ---------------------------------------------------------------- implicit GEMM
-enum { MODE_GEMM = 0, MODE_FWD = 1, MODE_DGRAD = 2, MODE_WGRAD = 3, MODE_WGRAD_T = 4 };
+enum { MODE_GEMM = 0, MODE_FWD = 1, MODE_DGRAD = 2, MODE_WGRAD = 3, MODE_WGRAD_T = 4, MODE_DGRAD_CLS = 5 };
 enum { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ADD = 2, OUT_F32_ATOMIC = 3 };
 
 struct IgemmArgs {
@@ -59,6 +59,12 @@ struct IgemmArgs {
   float* stats = nullptr;
   FastDiv fd_C, fd_S, fd_Ko, fd_PQ, fd_Q;
   int zero_out = 1;
+  // MODE_DGRAD_CLS: one output-parity class (cph, cpw) of a stride-2 data gradient.  The GEMM rows
+  // are the class's sub-grid pixels (H x W above = the class grid), its k = (ri, si, ko) runs over
+  // the taps r = cr0 + 2 ri, s = cs0 + 2 si of the full wR x wS filter only, and row m is stored at
+  // pixel (n, 2y + cph, 2x + cpw) of the out_H x out_W gradient (fd_cHW / fd_cW decode m).
+  int cls = 0, cph = 0, cpw = 0, cr0 = 0, cs0 = 0, wR = 1, wS = 1, out_H = 0, out_W = 0;
+  FastDiv fd_cHW, fd_cW;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;
 };

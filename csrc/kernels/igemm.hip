@@ -31,7 +31,8 @@ namespace tfx {
 
 namespace {
 
-enum { KM_DENSE = 0, KM_FWD_X = 1, KM_DGRAD_DY = 2, MN_DENSE = 10, MN_DGRAD_W = 11, MN_WGRAD_X = 12 };
+enum { KM_DENSE = 0, KM_FWD_X = 1, KM_DGRAD_DY = 2, MN_DENSE = 10, MN_DGRAD_W = 11, MN_WGRAD_X = 12,
+       MN_DGRAD_W2 = 13 };
 constexpr uint32_t BAD = 0x80000000u;  // byte offset beyond any num_records -> loads return 0
 constexpr int NT = 256, BKT = 64;
 
@@ -191,6 +192,14 @@ struct Loader {
       } else if constexpr (KIND == MN_DGRAD_W) {
         const int rs = a.fd_Ko.div(k), ko = k - mul24(rs, a.Ko);
         const int e0 = mul24(ko, a.R * a.S * a.C) + mul24(rs, a.C);  // ((ko*R + r)*S + s)*C
+#pragma unroll
+        for (int j = 0; j < NP; ++j) off[j] = (kok & (col[j] >= 0)) ? (uint32_t)(e0 + col[j]) * 2u : BAD;
+      } else if constexpr (KIND == MN_DGRAD_W2) {
+        // parity-class taps: k = (ri, si, ko) -> full-filter tap (cr0 + 2 ri, cs0 + 2 si)
+        const int rs = a.fd_Ko.div(k), ko = k - mul24(rs, a.Ko);
+        const int ri = a.fd_S.div(rs), si = rs - mul24(ri, a.S);
+        const int tap = mul24(a.cr0 + 2 * ri, a.wS) + a.cs0 + 2 * si;
+        const int e0 = mul24(ko, a.wR * a.wS * a.C) + mul24(tap, a.C);
 #pragma unroll
         for (int j = 0; j < NP; ++j) off[j] = (kok & (col[j] >= 0)) ? (uint32_t)(e0 + col[j]) * 2u : BAD;
       } else {  // MN_WGRAD_X: pixel (n, p, q) of k, then per chunk its (r, s, c) tap
@@ -358,29 +367,30 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
   if (a.stats) {
     float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN cols][2]; LDS is free after the loop
     if constexpr (SWAP) {
+      // lane holds rows mb + i*16 + (lane&15), columns nb + j*16 + (lane>>4)*4 + r: sum its TM rows
+      // in registers, then the 16 rows of the DPP row (row16_sum: no LDS, no branches)
+      float rv[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) rv[i] = (mb + i * 16 + (lane & 15)) < a.M ? 1.f : 0.f;
+      const bool relu = a.relu != 0;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+        float cs[4], cq[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = nb + j * 16 + (lane >> 4) * 4 + r;
-          const float bias = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+          const float bias = a.bias ? a.bias[min(n, a.N - 1)] : 0.f;
+          float s1 = 0.f, s2 = 0.f;
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
-            const int m = mb + i * 16 + (lane & 15);
             float v = acc[i][j][r] + bias;
-            if (a.relu) v = fmaxf(v, 0.f);
-            v = bf16_to_f32(f32_to_bf16(v));
-            if (m < a.M) {
-              cs[r] += v;
-              cq[r] = fmaf(v, v, cq[r]);
-            }
+            if (relu) v = fmaxf(v, 0.f);
+            v = bf16_to_f32(f32_to_bf16(v)) * rv[i];
+            s1 += v;
+            s2 = fmaf(v, v, s2);
           }
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            cs[r] += __shfl_xor(cs[r], o, 64);
-            cq[r] += __shfl_xor(cq[r], o, 64);
-          }
+          cs[r] = row16_sum(s1);
+          cq[r] = row16_sum(s2);
         }
         if ((lane & 15) == 0) {
 #pragma unroll
@@ -449,6 +459,18 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
         }
     }
     const bool relu = a.relu != 0;
+    // element offset of output row m (MODE_DGRAD_CLS: class sub-grid pixel -> full-grid pixel)
+    int64_t rowoff[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = min(mb + i * 16 + (lane & 15), a.M - 1);
+      int row = m;
+      if (a.cls) {
+        const int n = a.fd_cHW.div(m), yx = m - n * a.H * a.W, y = a.fd_cW.div(yx), x = yx - y * a.W;
+        row = (n * a.out_H + 2 * y + a.cph) * a.out_W + 2 * x + a.cpw;
+      }
+      rowoff[i] = (int64_t)row * a.ldc;
+    }
     if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0 && (TN % 2) == 0) {
       // 16-byte stores: lanes l and l^16 hold 4-column halves of the same row in tiles j and j+1;
       // swapping one half (4 floats over __shfl_xor 16) gives each lane 8 consecutive columns --
@@ -473,17 +495,19 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
           float o[8];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float send = odd ? v0[r] : v1[r];
-            const float recv = __shfl_xor(send, 16, 64);
-            o[r] = odd ? recv : v0[r];
-            o[4 + r] = odd ? v1[r] : recv;
+            // v_permlane16_swap: odd 16-lane rows of v0 <-> even rows of v1.  Even lanes end with
+            // [own v0 | partner v0], odd lanes with [partner v1 | own v1] (no LDS round trip)
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v0[r]), __float_as_uint(v1[r]),
+                                                             false, false);
+            o[r] = __uint_as_float(sw[0]);
+            o[4 + r] = __uint_as_float(sw[1]);
           }
           const int n = nb + (j + (odd ? 1 : 0)) * 16 + ((lane >> 5) << 3);
           if (m < a.M && n < a.N) {
-            uint16_t* dst = Cb + (int64_t)m * a.ldc + n;
+            uint16_t* dst = Cb + rowoff[i] + n;
             if (a.addend) {  // fused residual-branch gradient sum (dX = dgrad + other branch)
               float ad[8];
-              unpack8(*reinterpret_cast<const U4*>(a.addend + (int64_t)m * a.ldc + n), ad);
+              unpack8(*reinterpret_cast<const U4*>(a.addend + rowoff[i] + n), ad);
 #pragma unroll
               for (int r = 0; r < 8; ++r) o[r] += ad[r];
             }
@@ -507,7 +531,7 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
           }
           if (m < a.M && n < a.N) {
             if (a.addend) {  // fused residual-branch gradient sum (dX = dgrad + other branch)
-              const uint2 o2 = *reinterpret_cast<const uint2*>(a.addend + (int64_t)m * a.ldc + n);
+              const uint2 o2 = *reinterpret_cast<const uint2*>(a.addend + rowoff[i] + n);
               v[0] += __uint_as_float(o2.x << 16);
               v[1] += __uint_as_float(o2.x & 0xffff0000u);
               v[2] += __uint_as_float(o2.y << 16);
@@ -516,7 +540,7 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
             uint2 w2;
             w2.x = pack_bf16x2(v[0], v[1]);
             w2.y = pack_bf16x2(v[2], v[3]);
-            *reinterpret_cast<uint2*>(Cb + (int64_t)m * a.ldc + n) = w2;
+            *reinterpret_cast<uint2*>(Cb + rowoff[i] + n) = w2;
           }
         }
       }
@@ -545,7 +569,7 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
             if (m >= a.M || n >= a.N) continue;
             float v = acc[i][j][r] + bias[j][r];
             if (relu) v = fmaxf(v, 0.f);
-            const int64_t o = a.trans_out ? (int64_t)n * a.ldc + m : (int64_t)m * a.ldc + n;
+            const int64_t o = a.trans_out ? (int64_t)n * a.ldc + m : rowoff[i] + n;
             if (a.addend) v += bf16_to_f32(a.addend[o]);
             if (a.out_mode == OUT_BF16) reinterpret_cast<uint16_t*>(a.Cp)[o] = f32_to_bf16(v);
             else if (a.out_mode == OUT_F32) reinterpret_cast<float*>(a.Cp)[o] = v;
@@ -688,11 +712,24 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
         a.lda = a.C; a.ldb = a.Ko;
         launch_shape<MN_DENSE, MN_DENSE, false>(a, s);
         return;
+      case MODE_DGRAD_CLS:
+        // single-tap class aligned with dY (1x1 stride-2 even pixels, 3x3 stride-2 (even, even)):
+        // dY[M][Ko] . W[:, tap, :] -- dense operands, the tap folded into B's base; rows remapped
+        if (a.H == a.P && a.W == a.Q) {
+          const int64_t tap_off = (int64_t)(a.cr0 * a.wS + a.cs0) * a.C;
+          a.B += tap_off;
+          a.b_bytes -= tap_off * 2;
+          a.lda = a.Ko; a.ldb = a.wR * a.wS * a.C;
+          launch_shape<KM_DENSE, MN_DENSE>(a, s);
+          return;
+        }
+        break;
     }
   }
   switch (mode) {
     case MODE_FWD: launch_shape<KM_FWD_X, KM_DENSE>(a, s); break;
     case MODE_DGRAD: launch_shape<KM_DGRAD_DY, MN_DGRAD_W>(a, s); break;
+    case MODE_DGRAD_CLS: launch_shape<KM_DGRAD_DY, MN_DGRAD_W2>(a, s); break;
     case MODE_WGRAD: launch_shape<MN_DENSE, MN_WGRAD_X, false>(a, s); break;
     case MODE_WGRAD_T: launch_shape<MN_WGRAD_X, MN_DENSE, false>(a, s); break;
     default:

@@ -7,6 +7,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <cstdlib>
 #include <tuple>
 #include <vector>
 
@@ -93,6 +94,14 @@ Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t d
   return conv_fwd_impl(x, w, stride, pad, dil, slots.data_ptr<float>());
 }
 
+bool dgrad_classes_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("TFX_DGRAD_CLASSES");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 // dX = dgrad(dy) (+ addend: the gradient of x's other consumer, summed in the epilogue; the
 // result is written in place into addend's storage when given)
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil,
@@ -104,6 +113,41 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
   if (acc) {
     CHECK_BF16(*addend); CHECK_CONTIG(*addend);
     TORCH_CHECK(addend->sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "addend shape");
+  }
+  if (stride == 2 && dil == 1 && dgrad_classes_enabled()) {
+    // Stride-2 data gradient by output-parity class: pixel (h, w) only receives taps with
+    // r = h + pad (mod 2), s = w + pad (mod 2), so each of the 4 classes is a dense stride-1
+    // implicit GEMM over its own taps -- a quarter of the MACs of the zero-filled single GEMM.
+    bool empty_class = false;
+    for (int cph = 0; cph < 2; ++cph)
+      for (int cpw = 0; cpw < 2; ++cpw)
+        if ((g.R - (cph + pad) % 2 + 1) / 2 <= 0 || (g.S - (cpw + pad) % 2 + 1) / 2 <= 0) empty_class = true;
+    auto dx = acc ? *addend : (empty_class ? at::zeros({g.N, g.H, g.W, g.C}, dy.options())
+                                           : at::empty({g.N, g.H, g.W, g.C}, dy.options()));
+    for (int cph = 0; cph < 2; ++cph) {
+      for (int cpw = 0; cpw < 2; ++cpw) {
+        const int r0 = (cph + pad) % 2, s0 = (cpw + pad) % 2;
+        const int Rc = (int)(g.R - r0 + 1) / 2, Sc = (int)(g.S - s0 + 1) / 2;
+        const int Hc = (int)(g.H - cph + 1) / 2, Wc = (int)(g.W - cpw + 1) / 2;
+        if (Rc <= 0 || Sc <= 0 || Hc <= 0 || Wc <= 0) continue;  // dx keeps addend / zeros there
+        tfx::IgemmArgs a;
+        a.Nb = g.N; a.H = Hc; a.W = Wc; a.C = g.C; a.Ko = g.Ko; a.R = Rc; a.S = Sc; a.P = g.P; a.Q = g.Q;
+        a.sh = a.sw = 1; a.sh_log2 = a.sw_log2 = 0; a.dh = a.dw = 1;
+        a.ph = (cph + pad - r0) / 2; a.pw = (cpw + pad - s0) / 2;  // p = y + ph - ri
+        a.fd_C = tfx::FastDiv(g.C); a.fd_S = tfx::FastDiv(Sc); a.fd_Ko = tfx::FastDiv(g.Ko);
+        a.fd_PQ = tfx::FastDiv(g.P * g.Q); a.fd_Q = tfx::FastDiv(g.Q);
+        a.cls = 1; a.cph = cph; a.cpw = cpw; a.cr0 = r0; a.cs0 = s0; a.wR = g.R; a.wS = g.S;
+        a.out_H = g.H; a.out_W = g.W;
+        a.fd_cHW = tfx::FastDiv(Hc * Wc); a.fd_cW = tfx::FastDiv(Wc);
+        a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
+        a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
+        a.M = g.N * Hc * Wc; a.N = g.C; a.K = Rc * Sc * g.Ko; a.ldc = g.C;
+        a.out_mode = tfx::OUT_BF16;
+        if (acc) a.addend = bf(*addend);
+        tfx::igemm_launch(a, tfx::MODE_DGRAD_CLS, cur_stream());
+      }
+    }
+    return dx;
   }
   auto dx = acc ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
   auto a = conv_args(g, stride, pad, dil);

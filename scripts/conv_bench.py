@@ -71,6 +71,7 @@ def main():
         r = {"shape": [N, H, W, C, K, R, st], "count": cnt, "gflop": flops / 1e9}
         slots = torch.zeros(64 * 2 * K, device=dev)
         r["fwd_us"] = timeit(lambda: torch.ops.tfx.conv_fwd_stats(x, w, st, pad, 1, slots), a.iters)
+        r["fwd_nostats_us"] = timeit(lambda: torch.ops.tfx.conv_fwd(x, w, st, pad, 1), a.iters)
         r["dgrad_us"] = timeit(lambda: torch.ops.tfx.conv_dgrad(gy, w, list(x.shape), st, pad, 1, None), a.iters)
         r["wgrad_us"] = timeit(lambda: torch.ops.tfx.conv_wgrad(gy, x, dw, st, pad, 1, True), a.iters)
         r["mi_fwd_us"] = timeit(lambda: F.conv2d(xc, wc, stride=st, padding=pad), a.iters)
@@ -84,7 +85,8 @@ def main():
         rows.append(r)
         print(f"{str(r['shape']):34s} x{cnt} {r['gflop']:6.2f}GF | ours fwd {r['fwd_tflops']:6.1f} dgr {r['dgrad_tflops']:6.1f} "
               f"wgr {r['wgrad_tflops']:6.1f} | miopen fwd {r['mi_fwd_tflops']:6.1f} dgr {r['mi_dgrad_tflops']:6.1f} "
-              f"wgr {r['mi_wgrad_tflops']:6.1f} TF/s", flush=True)
+              f"wgr {r['mi_wgrad_tflops']:6.1f} TF/s | fwd {r['fwd_us']:.1f}us (no stats {r['fwd_nostats_us']:.1f}) "
+              f"dgr {r['dgrad_us']:.1f}us wgr {r['wgrad_us']:.1f}us", flush=True)
     print(f"TOTAL per step (all convs, fwd+dgrad+wgrad): ours {tot['ours']/1e3:.2f} ms, miopen {tot['miopen']/1e3:.2f} ms")
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump({"rows": rows, "total_us": tot}, open(a.out, "w"), indent=1)

@@ -34,7 +34,7 @@ from ..variables import Variable, VariableStore
 
 class GradAllReduce:
     def __init__(self, store: VariableStore, bucket_bytes: int = 32 << 20, group=None, overlap: bool = True,
-                 compress_bf16: bool = False):
+                 compress_bf16: bool = False, tail_bytes: int = 2 << 20):
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -42,19 +42,37 @@ class GradAllReduce:
         self.compress = compress_bf16
         elem = store.grad.element_size()
         cap = max(1, bucket_bytes // elem)
+        tail_cap = max(1, tail_bytes // elem)
         self.buckets: List[List[int]] = []  # [lo, hi) element ranges of the flat grad buffer
         self.members: List[List[Variable]] = []
         self.var_bucket: Dict[int, int] = {}
+        groups: List[List[Variable]] = []
         cur: List[Variable] = []
         size = 0
         for v in reversed(store.trainable()):
             cur.append(v)
             size += v.numel
             if size >= cap:
-                self._close(cur)
+                groups.append(cur)
                 cur, size = [], 0
         if cur:
-            self._close(cur)
+            groups.append(cur)
+        # The LAST bucket holds the first layers' gradients, which are ready only when backward
+        # ends: its all-reduce is the one part that cannot overlap compute.  Cut it down to a tail of
+        # at most ``tail_bytes`` (ResNet-50: the stem + stage-1 grads, ~1 MB) so the exposed
+        # collective is short; the rest of that group still overlaps the early layers' backward.
+        if tail_bytes > 0 and groups and sum(v.numel for v in groups[-1]) > tail_cap:
+            last = groups.pop()
+            acc, k = 0, len(last)
+            while k > 0 and acc + last[k - 1].numel <= tail_cap:
+                k -= 1
+                acc += last[k].numel
+            if 0 < k < len(last):
+                groups.extend([last[:k], last[k:]])
+            else:
+                groups.append(last)
+        for g in groups:
+            self._close(g)
         self._pending: List[int] = []
         self._launched: List[bool] = []
         self._works = []

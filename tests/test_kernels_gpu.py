@@ -29,6 +29,11 @@ CONV_SHAPES = [
     (2, 8, 8, 64, 256, 1, 2, 0),
     (2, 32, 32, 8, 64, 3, 1, 1),  # padded-RGB stem
     (1, 5, 5, 16, 24, 3, 1, 1),   # ragged M / N
+    # stride-2 data gradients run as 4 output-parity-class GEMMs (even / odd grids, empty classes)
+    (2, 16, 16, 128, 128, 3, 2, 1),
+    (2, 10, 10, 64, 32, 5, 2, 2),
+    (2, 7, 9, 32, 64, 1, 2, 0),
+    (2, 16, 16, 64, 128, 1, 2, 0),
 ]
 
 
