@@ -37,6 +37,14 @@ for s in $STEPS; do
         TFX_SPLITK_BLOCKS=$v timeout -k 10 400 python bench.py --steps 40 --warmup 5 > gpurun_out/abs2_$v.log 2>&1 || exit 1
       done
       grep -o '"ms_per_step": [0-9.]*' gpurun_out/abs*.log ;;
+    abwg)
+      for v in 128 64; do
+        TFX_WGRAD_TILE=$v timeout -k 10 300 python scripts/conv_bench.py --out gpurun_out/conv_bench_wg$v.json > gpurun_out/conv_bench_wg$v.log 2>&1 || exit 1
+      done
+      for i in 1 2; do for v in 128 64; do
+        TFX_WGRAD_TILE=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/abwg_${v}_$i.log 2>&1 || exit 1
+      done; done
+      tail -1 gpurun_out/conv_bench_wg*.log; grep -o '"ms_per_step": [0-9.]*' gpurun_out/abwg_*.log ;;
     kerneltests)
       timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py tests/test_resnet_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1
       rc=$?; echo "kerneltests rc=$rc"; tail -5 gpurun_out/pytest_kernels.log

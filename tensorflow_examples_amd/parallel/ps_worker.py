@@ -50,3 +50,56 @@ class AsyncPSWorker:
             x, y = self._to_dev(images[s:s + batch]), self._to_dev(labels[s:s + batch])
             hits += float(ops.accuracy(self.model.logits(x), y)) * x.shape[0]
         return hits / len(images)
+
+
+class SyncReplicasPSWorker(AsyncPSWorker):
+    """Synchronous replicas over the parameter server (``--sync_replicas``).
+
+    The reference only carries a commented-out ``tf.train.SyncReplicasOptimizer`` with
+    ``replicas_to_aggregate = total_num_replicas = len(workers)`` (R/distributed/distributed.py:
+    109-112).  Its semantics realised here: every global step aggregates the gradients of ALL
+    workers.  Each worker pulls the same parameters, computes its gradient, the gradients are
+    averaged across workers with one all-reduce of the flat f32 grad buffer (a gloo process group
+    over the worker hosts -- the payload is the 318 KB MLP gradient, host-resident anyway for the
+    PS push), the chief pushes the average once (the ps applies SGD and bumps ``global_step`` once
+    per aggregated step) and broadcasts the new step, which doubles as the barrier that keeps the
+    next pull behind the update.
+    """
+
+    def __init__(self, model, client, learning_rate: float, group, is_chief: bool, naive_xent: bool = True):
+        super().__init__(model, client, learning_rate, naive_xent)
+        import torch.distributed as dist
+        self.dist, self.group, self.is_chief = dist, group, is_chief
+        self.world = dist.get_world_size(group)
+        self._host = torch.zeros(self.store.total, dtype=torch.float32)
+        self._step_t = torch.zeros(1, dtype=torch.float64)
+
+    def step(self, batch_x, batch_y):
+        x, y = self._to_dev(batch_x), self._to_dev(batch_y)
+        self.client.pull()
+        self.store.zero_grad()
+        logits = self.model.logits(x)
+        loss = ops.softmax_cross_entropy(logits, y, naive=self.naive)
+        acc = ops.accuracy(logits.detach(), y)
+        loss.backward()
+        self._host.copy_(self.store.grad)
+        self.dist.all_reduce(self._host, group=self.group)
+        self._host.mul_(1.0 / self.world)
+        if self.is_chief:
+            self.store.grad.copy_(self._host)
+            self._step_t[0] = self.client.push(self.lr)
+        self.dist.broadcast(self._step_t, src=0, group=self.group)
+        return float(loss.item()), float(acc.item()), int(self._step_t[0]) - 1
+
+
+def init_worker_group(worker_hosts, task_index: int, port_offset: int = 1000, timeout_s: float = 120.0):
+    """gloo process group over the worker tasks: rank = task_index, rendezvous on worker 0's host at
+    its port + ``port_offset`` (the worker's own port is the reference's server address)."""
+    import datetime
+
+    import torch.distributed as dist
+    host, port = worker_hosts[0].rsplit(":", 1)
+    dist.init_process_group("gloo", init_method=f"tcp://{host}:{int(port) + port_offset}",
+                            rank=task_index, world_size=len(worker_hosts),
+                            timeout=datetime.timedelta(seconds=timeout_s))
+    return dist.group.WORLD

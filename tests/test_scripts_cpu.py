@@ -69,6 +69,42 @@ def test_distributed_ps_two_workers(tmp_path):
     assert len(ev) == 2
 
 
+def test_distributed_sync_replicas(tmp_path):
+    """--sync_replicas: every global step aggregates both workers' gradients (SyncReplicasOptimizer
+    semantics of the reference's commented-out rep_op, R/distributed/distributed.py:109-112), so
+    the global step advances once per aggregated step and both replicas see the same parameters."""
+    script = os.path.join(ROOT, "distributed", "distributed.py")
+    ports = _ports(4)
+    args = _args(ports[:3], str(tmp_path / "logs"),
+                 ["--training_epochs=1", "--max_batches_per_epoch=120", "--ps_exit_after_workers", "--sync_replicas",
+                  f"--sync_port_offset={ports[3] - ports[1]}"])
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    ps = subprocess.Popen([sys.executable, script, *args, "--job_name=ps", "--task_index=0"], env=env)
+    time.sleep(0.3)
+    w1 = subprocess.Popen([sys.executable, script, *args, "--job_name=worker", "--task_index=1"],
+                          stdout=subprocess.PIPE, text=True, env=env)
+    w0 = subprocess.Popen([sys.executable, script, *args, "--job_name=worker", "--task_index=0"],
+                          stdout=subprocess.PIPE, text=True, env=env)
+    try:
+        o0, _ = w0.communicate(timeout=240)
+        o1, _ = w1.communicate(timeout=240)
+        assert w0.returncode == 0 and w1.returncode == 0
+        assert ps.wait(timeout=30) == 0
+    finally:
+        for p in (ps, w0, w1):
+            if p.poll() is None:
+                p.kill()
+    steps = []
+    for out in (o0, o1):
+        prog = [l for l in out.splitlines() if l.startswith("Step so far:")]
+        assert len(prog) == 2
+        steps.append([int(l.split(":")[1].split(",")[0]) for l in prog])
+    # one global step per aggregated step (not 240 as in async mode), identical on both replicas
+    assert steps[0] == steps[1] == [100, 120]
+    acc = [l for o in (o0, o1) for l in o.splitlines() if l.startswith("Acc: ")]
+    assert len(acc) == 2 and acc[0] == acc[1]
+
+
 def test_worker_fails_when_ps_dies(tmp_path):
     script = os.path.join(ROOT, "distributed", "distributed.py")
     args = _args(_ports(3), str(tmp_path / "logs"), ["--training_epochs=50"])
