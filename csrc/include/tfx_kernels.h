@@ -11,6 +11,7 @@ namespace tfx {
 
 // Cross-block reduction slots for per-channel statistics ([NSLOT][2][C] f32, see batchnorm.hip)
 constexpr int NSLOT = 64;
+constexpr int BN_CNT = 64;  // per-column-tile counters after the slots (N <= 64 * 64 columns)
 
 // Division by a runtime-invariant divisor via multiply-high (valid for n < 2^31).
 struct FastDiv {
@@ -65,6 +66,31 @@ struct IgemmArgs {
   // pixel (n, 2y + cph, 2x + cpw) of the out_H x out_W gradient (fd_cHW / fd_cW decode m).
   int cls = 0, cph = 0, cpw = 0, cr0 = 0, cs0 = 0, wR = 1, wS = 1, out_H = 0, out_W = 0;
   FastDiv fd_cHW, fd_cW;
+  // ---- fused batch-norm epilogues (per output column c; the BN layer's workspace holds the
+  // [NSLOT][2][N] slots and, after them, BN_CNT per-column-tile arrival counters, zero between uses)
+  // bn_final: the LAST block to finish each column tile (agent-scope release / acquire on its
+  //   counter) reduces that tile's slots -- forward (stats != nullptr): BN finalize into bn_save
+  //   [mean | invstd | scale | shift] + running stats; backward (bnb_x != nullptr): red = [sum g' |
+  //   sum g' xhat] and dbeta / dgamma += -- so no separate finalize / slot-reduce launch.
+  unsigned* bn_cnt = nullptr;
+  int bn_final = 0;
+  const float* bn_gamma = nullptr;
+  const float* bn_beta = nullptr;
+  float* bn_rmean = nullptr;
+  float* bn_rvar = nullptr;
+  float* bn_save = nullptr;
+  float bn_eps = 1e-5f, bn_momentum = 0.1f;
+  // backward partials of the BN whose OUTPUT gradient this dgrad produces: g' = bf16(out) * relu
+  // mask (from x*scale+shift > 0, or the residual layer's mask bits), accumulated per column:
+  // sum g' and sum g' * (x - mean) * invstd into bnb_slots
+  const uint16_t* bnb_x = nullptr;
+  const float* bnb_save = nullptr;
+  const uint8_t* bnb_mask = nullptr;
+  int bnb_relu = 0;
+  float* bnb_slots = nullptr;
+  float* bnb_red = nullptr;
+  float* bnb_dgamma = nullptr;
+  float* bnb_dbeta = nullptr;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;
 };
@@ -80,12 +106,17 @@ void sgemm_launch(const float* A, const float* B, float* C, const float* bias, i
 void bn_stats(const uint16_t* x, int64_t M, int C, float* slots, hipStream_t s);
 void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float* beta, float eps,
                  float momentum, float* run_mean, float* run_var, float* save, hipStream_t s);
+// slots -> red = [sum g' | sum g' xhat] (+= into dbeta / dgamma when given), slots re-zeroed
+void bn_slot_reduce(float* slots, int C, float* red, float* dgamma, float* dbeta, hipStream_t s);
 void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
                   const float* run_var, float* save, hipStream_t s);
 // mask (optional, residual + ReLU on the C % 8 == 0 path): 1 bit per element, the ReLU mask of y
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
               uint16_t* y, uint8_t* mask, hipStream_t s);
 // residual + ReLU: pass the forward's mask (vector path) or res (generic path) for the ReLU mask
+void bn_backward_apply(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask,
+                       const float* save, const float* red, int64_t M, int C, bool relu, uint16_t* dx,
+                       uint16_t* dres, hipStream_t s);
 void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask, const float* save,
                  int64_t M, int C, bool relu, float* slots, float* red, float* dgamma, float* dbeta, uint16_t* dx,
                  uint16_t* dres, hipStream_t s);

@@ -524,7 +524,20 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
     TFX_DISPATCH_RR(has_res, relu,
                     (bn_bwd_reduce_gen_kernel<R_, L_><<<grid, 256, 0, s>>>(g, x, res, save, M, C, slots)));
   }
+  bn_slot_reduce(slots, C, red, dgamma, dbeta, s);
+  bn_backward_apply(g, x, res, mask, save, red, M, C, relu, dx, dres, s);
+}
+
+void bn_slot_reduce(float* slots, int C, float* red, float* dgamma, float* dbeta, hipStream_t s) {
   bn_slot_reduce_kernel<<<(C + 15) / 16, 256, 0, s>>>(slots, C, red, dgamma, dbeta);
+}
+
+// the apply half of bn_backward, for a red[] produced elsewhere (a conv dgrad epilogue)
+void bn_backward_apply(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask,
+                       const float* save, const float* red, int64_t M, int C, bool relu, uint16_t* dx,
+                       uint16_t* dres, hipStream_t s) {
+  const bool has_res = res != nullptr || mask != nullptr;
+  const int64_t n = M * C;
   // with a residual input dres = g' is produced (the host guarantees dres != nullptr then)
   if (vec_ok(C) && (!has_res || !relu || mask)) {
     const int64_t nvec = n / 8;

@@ -27,12 +27,16 @@
 #include "tfx_common.h"
 #include "tfx_kernels.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace tfx {
 
 namespace {
 
 enum { KM_DENSE = 0, KM_FWD_X = 1, KM_DGRAD_DY = 2, MN_DENSE = 10, MN_DGRAD_W = 11, MN_WGRAD_X = 12,
        MN_DGRAD_W2 = 13 };
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_BNB = 2 };
 constexpr uint32_t BAD = 0x80000000u;  // byte offset beyond any num_records -> loads return 0
 constexpr int NT = 256, BKT = 64;
 
@@ -244,6 +248,88 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, n, 0x00020000);
 }
 
+// ------------------------------------------------------------------ fused-BN last arriver
+// Every block of column tile tn has added its per-column partials into the slots.  The payload is
+// written ONLY by agent-scope atomics (performed past the XCD L2, which drops the line), so the
+// hand-off needs no L2 writeback (MI355X_MICROARCH.md "Correctness boundaries", sc1 table row 1):
+// every wave drains vmcnt, barrier, ONE lane bumps the tile's counter; the block whose add returns
+// tiles_m - 1 is last and its waves read the slots with sc1 loads after a barrier.  An agent release
+// (buffer_wbl2) per block here would write back the freshly stored output tile of every block on the
+// XCD: measured 2-6x slower conv kernels.  The host only fuses when the tile's slot columns are whole
+// 128-B lines (N % 32 == 0), so no block ever loads a line holding another tile's pending sums.
+// The last arriver sums the NSLOT slot rows of the tile's columns, re-zeroes them (sc1 stores: the
+// lines leave the L2 again) and resets the counter, so the workspace is zero between uses.
+// FWD: finalize the BN of the columns (bn_finalize_kernel's math); BWD: red + dgamma / dbeta.
+template <int BN, bool BWD>
+__device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n0, char* smem, int t) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* flag = reinterpret_cast<unsigned*>(smem + 8192);  // past the [2][BN][2] f32 partials
+  if (t == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.bn_cnt + tn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = prev == (unsigned)(a.tiles_m - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*flag == 0) return;
+  constexpr int NPH = 256 / BN;  // slot phases per column
+  const int cl = t % BN, ph = t / BN, c = n0 + cl;
+  float* slots = BWD ? a.bnb_slots : a.stats;
+  float s = 0.f, q = 0.f;
+  if (c < a.N) {
+    float vs[NSLOT / NPH], vq[NSLOT / NPH];
+#pragma unroll
+    for (int k = 0; k < NSLOT / NPH; ++k) {
+      float* row = slots + (size_t)(ph + k * NPH) * 2 * a.N;
+      vs[k] = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      vq[k] = __hip_atomic_load(row + a.N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int k = 0; k < NSLOT / NPH; ++k) {
+      s += vs[k];
+      q += vq[k];
+      float* row = slots + (size_t)(ph + k * NPH) * 2 * a.N;
+      __hip_atomic_store(row + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(row + a.N + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  float* part = reinterpret_cast<float*>(smem);
+  part[(ph * BN + cl) * 2] = s;
+  part[(ph * BN + cl) * 2 + 1] = q;
+  __syncthreads();
+  if (t < BN && c < a.N) {
+    s = 0.f;
+    q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NPH; ++k) {
+      s += part[(k * BN + t) * 2];
+      q += part[(k * BN + t) * 2 + 1];
+    }
+    const int C = a.N;
+    if constexpr (BWD) {
+      a.bnb_red[c] = s;
+      a.bnb_red[C + c] = q;
+      if (a.bnb_dbeta) a.bnb_dbeta[c] += s;
+      if (a.bnb_dgamma) a.bnb_dgamma[c] += q;
+    } else {
+      const float inv_m = 1.f / (float)a.M;
+      const float mean = s * inv_m;
+      const float var = fmaxf(q * inv_m - mean * mean, 0.f);
+      const float invstd = rsqrtf(var + a.bn_eps);
+      const float scale = (a.bn_gamma ? a.bn_gamma[c] : 1.f) * invstd;
+      a.bn_save[c] = mean;
+      a.bn_save[C + c] = invstd;
+      a.bn_save[2 * C + c] = scale;
+      a.bn_save[3 * C + c] = (a.bn_beta ? a.bn_beta[c] : 0.f) - mean * scale;
+      if (a.bn_rmean) {
+        const float unb = a.M > 1 ? var * (float)a.M / (float)(a.M - 1) : var;
+        a.bn_rmean[c] = (1.f - a.bn_momentum) * a.bn_rmean[c] + a.bn_momentum * mean;
+        a.bn_rvar[c] = (1.f - a.bn_momentum) * a.bn_rvar[c] + a.bn_momentum * unb;
+      }
+    }
+  }
+  if (t == 0) __hip_atomic_store(a.bn_cnt + tn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 // SWAP: compute the transposed tile (MFMA operands exchanged) so each lane holds 4 CONSECUTIVE
@@ -253,8 +339,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64
 // STG = LDS stages: 2 for the pipelined K loop; 1 for single-k-tile GEMMs (K <= 64: the 1x1 convs
 // of 64-channel layers), which then fit 4 blocks per CU -- those are memory-bound, and occupancy is
 // what keeps enough loads and stores in flight.
-template <int AKIND, int BKIND, int BM, int BN, bool SWAP, int STG>
-__global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4) : 2) igemm_kernel(IgemmArgs a) {
+// EPI: compile-time epilogue extras (so the plain GEMM / wgrad kernels carry none of their code or
+// registers): EPI_STATS = fused BN statistics (+ last-arriver finalize) of a conv forward,
+// EPI_BNB = fused BN-backward partials (+ last-arriver reduce) of a conv data gradient.
+template <int AKIND, int BKIND, int BM, int BN, bool SWAP, int STG, int EPI>
+__global__ void __launch_bounds__(256, (STG == 1 && EPI == EPI_PLAIN) ? (BM * BN >= 128 * 128 ? 3 : 4) : 2) igemm_kernel(IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BKT * 2, STAGE = (BM + BN) * BKT * 2;
   __shared__ __attribute__((aligned(16))) char smem[STG * STAGE];
@@ -364,7 +453,12 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
   const int mb = m0 + wm * WM, nb = n0 + wn * WN;
 
   // ---------------- fused BN statistics of the bf16-rounded output (per column n, this tile's rows)
-  if (a.stats) {
+  if constexpr (STG == 1) {
+    // single-k-tile variant: no barrier after compute(0) -- other waves may still be reading the
+    // stage that the epilogue's LDS partials overwrite
+    if constexpr (EPI != EPI_PLAIN) __syncthreads();
+  }
+  if constexpr (EPI == EPI_STATS) {
     float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN cols][2]; LDS is free after the loop
     if constexpr (SWAP) {
       // lane holds rows mb + i*16 + (lane&15), columns nb + j*16 + (lane>>4)*4 + r: sum its TM rows
@@ -471,49 +565,133 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
       }
       rowoff[i] = (int64_t)row * a.ldc;
     }
-    if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0 && (TN % 2) == 0) {
+    // fused-BN variants only ever take the 16-byte path (igemm_launch checks): compile only that one
+    if (EPI != EPI_PLAIN ||
+        (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0 && (TN % 2) == 0)) {
       // 16-byte stores: lanes l and l^16 hold 4-column halves of the same row in tiles j and j+1;
       // swapping one half (4 floats over __shfl_xor 16) gives each lane 8 consecutive columns --
       // the even lane of tile j, the odd lane of tile j+1 -- i.e. half the store instructions.
       uint16_t* Cb = reinterpret_cast<uint16_t*>(a.Cp);
       const bool odd = (lane >> 4) & 1;
+      constexpr bool bnb = EPI == EPI_BNB;  // fused BN-backward partials of this output
+      float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN cols][2] partials (LDS free after the loop)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = mb + i * 16 + (lane & 15);
+      for (int j = 0; j < TN; j += 2) {
+        const int n = nb + (j + (odd ? 1 : 0)) * 16 + ((lane >> 5) << 3);
+        // per-column BN parameters of this lane's 8 columns (mean, invstd, scale, shift)
+        float mu[8], is[8], sc[8], sh[8], bs[8], bq[8];
+        if constexpr (bnb) {
+          const int nc = min(n, a.N - 8);
 #pragma unroll
-        for (int j = 0; j < TN; j += 2) {
-          float v0[4], v1[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v0[r] = acc[i][j][r] + bias[j][r];
-            v1[r] = acc[i][j + 1][r] + bias[j + 1][r];
-            if (relu) {
-              v0[r] = fmaxf(v0[r], 0.f);
-              v1[r] = fmaxf(v1[r], 0.f);
-            }
-          }
-          float o[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            // v_permlane16_swap: odd 16-lane rows of v0 <-> even rows of v1.  Even lanes end with
-            // [own v0 | partner v0], odd lanes with [partner v1 | own v1] (no LDS round trip)
-            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v0[r]), __float_as_uint(v1[r]),
-                                                             false, false);
-            o[r] = __uint_as_float(sw[0]);
-            o[4 + r] = __uint_as_float(sw[1]);
-          }
-          const int n = nb + (j + (odd ? 1 : 0)) * 16 + ((lane >> 5) << 3);
-          if (m < a.M && n < a.N) {
-            uint16_t* dst = Cb + rowoff[i] + n;
-            if (a.addend) {  // fused residual-branch gradient sum (dX = dgrad + other branch)
-              float ad[8];
-              unpack8(*reinterpret_cast<const U4*>(a.addend + rowoff[i] + n), ad);
-#pragma unroll
-              for (int r = 0; r < 8; ++r) o[r] += ad[r];
-            }
-            *reinterpret_cast<U4*>(dst) = pack8(o);
+          for (int k = 0; k < 8; ++k) {
+            mu[k] = a.bnb_save[nc + k];
+            is[k] = a.bnb_save[a.N + nc + k];
+            sc[k] = a.bnb_save[2 * a.N + nc + k];
+            sh[k] = a.bnb_save[3 * a.N + nc + k];
+            bs[k] = 0.f;
+            bq[k] = 0.f;
           }
         }
+        // The epilogue's global reads (addend, BN input, ReLU mask bits) of IC rows are issued
+        // together BEFORE the rows' stores: the compiler cannot hoist a load over a store it may
+        // alias (the addend IS the output when summed in place), so a row-by-row loop would run one
+        // full memory latency per row.  Loads use an in-range column; out-of-range rows / columns
+        // are dropped at the store.
+        constexpr int IC = TM < 4 ? TM : 4;
+        const int nl = min(n, a.N - 8);
+#pragma unroll
+        for (int i0 = 0; i0 < TM; i0 += IC) {
+          U4 adv[IC], xvv[IC];
+          uint32_t mbv[IC];
+#pragma unroll
+          for (int ii = 0; ii < IC; ++ii) {
+            const int64_t o = rowoff[i0 + ii] + nl;
+            if (a.addend) adv[ii] = *reinterpret_cast<const U4*>(a.addend + o);
+            if constexpr (bnb) {
+              xvv[ii] = *reinterpret_cast<const U4*>(a.bnb_x + o);
+              mbv[ii] = a.bnb_mask ? a.bnb_mask[o >> 3] : 0xffu;
+            }
+          }
+#pragma unroll
+          for (int ii = 0; ii < IC; ++ii) {
+            const int i = i0 + ii;
+            const int m = mb + i * 16 + (lane & 15);
+            float v0[4], v1[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v0[r] = acc[i][j][r] + bias[j][r];
+              v1[r] = acc[i][j + 1][r] + bias[j + 1][r];
+              if (relu) {
+                v0[r] = fmaxf(v0[r], 0.f);
+                v1[r] = fmaxf(v1[r], 0.f);
+              }
+            }
+            float o[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              // v_permlane16_swap: odd 16-lane rows of v0 <-> even rows of v1.  Even lanes end with
+              // [own v0 | partner v0], odd lanes with [partner v1 | own v1] (no LDS round trip)
+              const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v0[r]), __float_as_uint(v1[r]),
+                                                               false, false);
+              o[r] = __uint_as_float(sw[0]);
+              o[4 + r] = __uint_as_float(sw[1]);
+            }
+            if (m < a.M && n < a.N) {
+              uint16_t* dst = Cb + rowoff[i] + n;
+              if (a.addend) {  // fused residual-branch gradient sum (dX = dgrad + other branch)
+                float ad[8];
+                unpack8(adv[ii], ad);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] += ad[r];
+              }
+              const U4 packed = pack8(o);
+              *reinterpret_cast<U4*>(dst) = packed;
+              if constexpr (bnb) {
+                // g' = bf16(out) * relu mask; xhat from the BN input x (same NHWC position)
+                float g[8], xv[8];
+                unpack8(packed, g);
+                unpack8(xvv[ii], xv);
+                const uint32_t mbits = mbv[ii];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                  bool on = true;
+                  if (a.bnb_relu) on = a.bnb_mask ? ((mbits >> k) & 1u) != 0 : fmaf(xv[k], sc[k], sh[k]) > 0.f;
+                  const float gg = on ? g[k] : 0.f;
+                  bs[k] += gg;
+                  bq[k] = fmaf(gg, (xv[k] - mu[k]) * is[k], bq[k]);
+                }
+              }
+            }
+          }
+        }
+        if constexpr (bnb) {
+          // the 16 rows of this DPP row share the lane's 8 columns: reduce them in registers
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            bs[k] = row16_sum(bs[k]);
+            bq[k] = row16_sum(bq[k]);
+          }
+          if ((lane & 15) == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const int col = n - n0 + k;
+              red[(wm * BN + col) * 2 + 0] = bs[k];
+              red[(wm * BN + col) * 2 + 1] = bq[k];
+            }
+          }
+        }
+      }
+      if constexpr (bnb) {
+        __syncthreads();
+        if (t < BN) {
+          const int nn = n0 + t;
+          if (nn < a.N) {
+            float* slot = a.bnb_slots + (size_t)(tm % NSLOT) * 2 * a.N;
+            atomicAdd(&slot[nn], red[t * 2] + red[(BN + t) * 2]);
+            atomicAdd(&slot[a.N + nn], red[t * 2 + 1] + red[(BN + t) * 2 + 1]);
+          }
+        }
+        if (a.bn_final) bn_tile_reduce<BN, true>(a, tn, n0, smem, t);
       }
     } else if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 3) == 0 && (a.N & 3) == 0) {
       uint16_t* Cb = reinterpret_cast<uint16_t*>(a.Cp);
@@ -616,6 +794,11 @@ __global__ void __launch_bounds__(256, STG == 1 ? (BM * BN >= 128 * 128 ? 3 : 4)
       }
     }
   }
+  // forward BN finalize by the last block of each column tile, after the stores (acc is dead here:
+  // the slot reads get the registers)
+  if constexpr (EPI == EPI_STATS) {
+    if (a.bn_final) bn_tile_reduce<BN, false>(a, tn, n0, smem, t);
+  }
 }
 
 // ============================================================ host launcher
@@ -631,7 +814,7 @@ int pick_splits(int tiles, int nkt, int want_blocks) {
   return std::max(1, std::min(s, max_s));
 }
 
-template <int AK, int BK, int BM, int BN>
+template <int AK, int BK, int BM, int BN, int EPI = EPI_PLAIN>
 void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1) {
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + BN - 1) / BN;
@@ -650,12 +833,15 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1) {
   if (grid == 0) return;
   // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
-  if (nkt == 1 && splits == 1) {
-    if (swap) igemm_kernel<AK, BK, BM, BN, true, 1><<<grid, NT, 0, s>>>(a);
-    else igemm_kernel<AK, BK, BM, BN, false, 1><<<grid, NT, 0, s>>>(a);
+  if constexpr (EPI != EPI_PLAIN) {  // fused-BN epilogues: bf16 outputs only (SWAP orientation)
+    if (nkt == 1 && splits == 1) igemm_kernel<AK, BK, BM, BN, true, 1, EPI><<<grid, NT, 0, s>>>(a);
+    else igemm_kernel<AK, BK, BM, BN, true, 2, EPI><<<grid, NT, 0, s>>>(a);
+  } else if (nkt == 1 && splits == 1) {
+    if (swap) igemm_kernel<AK, BK, BM, BN, true, 1, EPI><<<grid, NT, 0, s>>>(a);
+    else igemm_kernel<AK, BK, BM, BN, false, 1, EPI><<<grid, NT, 0, s>>>(a);
   } else {
-    if (swap) igemm_kernel<AK, BK, BM, BN, true, 2><<<grid, NT, 0, s>>>(a);
-    else igemm_kernel<AK, BK, BM, BN, false, 2><<<grid, NT, 0, s>>>(a);
+    if (swap) igemm_kernel<AK, BK, BM, BN, true, 2, EPI><<<grid, NT, 0, s>>>(a);
+    else igemm_kernel<AK, BK, BM, BN, false, 2, EPI><<<grid, NT, 0, s>>>(a);
   }
 }
 
@@ -682,32 +868,46 @@ int wgrad_tile() {
   return t;
 }
 
-template <int AK, int BK, bool ALLOW256 = true>
+template <int AK, int BK, bool ALLOW256 = true, int EPI = EPI_PLAIN>
 void launch_shape(IgemmArgs& a, hipStream_t s) {
   if constexpr (!ALLOW256) {
     const bool dense_pair = (AK == MN_DENSE && BK == MN_DENSE) || (a.R == 1 && a.S == 1);  // 1x1 (any stride)
-    if (a.N > 64 && (wgrad_tile() == 64 || (wgrad_tile() == 0 && dense_pair))) return launch_t<AK, BK, 128, 64>(a, s, 2);
+    if (a.N > 64 && (wgrad_tile() == 64 || (wgrad_tile() == 0 && dense_pair))) return launch_t<AK, BK, 128, 64, EPI>(a, s, 2);
   }
   if (a.N <= 64) {
     if constexpr (ALLOW256) {
-      if (a.M >= 256 * 256) return launch_t<AK, BK, 256, 64>(a, s);
+      if (a.M >= 256 * 256) return launch_t<AK, BK, 256, 64, EPI>(a, s);
     }
-    launch_t<AK, BK, 128, 64>(a, s);
+    launch_t<AK, BK, 128, 64, EPI>(a, s);
   } else {
     const long tiles128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
     if constexpr (ALLOW256) {
-      if (tile_policy() >= 1 && tiles128 < 512) return launch_t<AK, BK, 128, 64>(a, s);
+      if (tile_policy() >= 1 && tiles128 < 512) return launch_t<AK, BK, 128, 64, EPI>(a, s);
     }
-    launch_t<AK, BK, 128, 128>(a, s);
+    launch_t<AK, BK, 128, 128, EPI>(a, s);
   }
 }
 
 }  // namespace
 
+template <int AK, int BK, int EPI_ON>
+void launch_epi(IgemmArgs& a, hipStream_t s) {
+  if (a.stats || a.bnb_x) launch_shape<AK, BK, true, EPI_ON>(a, s);
+  else launch_shape<AK, BK, true, EPI_PLAIN>(a, s);
+}
+
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
   if (a.out_mode == OUT_F32_ATOMIC && a.zero_out) {
     const size_t rows = a.trans_out ? a.N : a.M;
     TFX_HIP_CHECK(hipMemsetAsync(a.Cp, 0, sizeof(float) * rows * a.ldc, s));
+  }
+  // fused-BN epilogues live in the bf16 16-byte-store path of the forward / data-gradient kernels
+  if (a.stats || a.bnb_x) {
+    if (!(a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0 &&
+          (mode == MODE_FWD || (a.bnb_x && mode == MODE_DGRAD)) && (a.stats == nullptr || a.bnb_x == nullptr))) {
+      fprintf(stderr, "igemm_launch: unsupported fused-BN epilogue configuration\n");
+      abort();
+    }
   }
   // 1x1 stride-1 unpadded convs (two thirds of ResNet-50's) are plain GEMMs over the NHWC rows:
   // dense loaders instead of the im2col / parity gathers -- no per-row address decode at all.
@@ -717,11 +917,11 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
     switch (mode) {
       case MODE_FWD:  // X[M][C] . W[Ko][C]^T
         a.lda = a.C; a.ldb = a.C;
-        launch_shape<KM_DENSE, KM_DENSE>(a, s);
+        launch_epi<KM_DENSE, KM_DENSE, EPI_STATS>(a, s);
         return;
       case MODE_DGRAD:  // dY[M][Ko] . W[Ko][C]
         a.lda = a.Ko; a.ldb = a.C;
-        launch_shape<KM_DENSE, MN_DENSE>(a, s);
+        launch_epi<KM_DENSE, MN_DENSE, EPI_BNB>(a, s);
         return;
       case MODE_WGRAD:  // dY^T[Ko][pix] . X[pix][C]
         a.lda = a.Ko; a.ldb = a.C;
@@ -746,8 +946,8 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
     }
   }
   switch (mode) {
-    case MODE_FWD: launch_shape<KM_FWD_X, KM_DENSE>(a, s); break;
-    case MODE_DGRAD: launch_shape<KM_DGRAD_DY, MN_DGRAD_W>(a, s); break;
+    case MODE_FWD: launch_epi<KM_FWD_X, KM_DENSE, EPI_STATS>(a, s); break;
+    case MODE_DGRAD: launch_epi<KM_DGRAD_DY, MN_DGRAD_W, EPI_BNB>(a, s); break;
     case MODE_DGRAD_CLS: launch_shape<KM_DGRAD_DY, MN_DGRAD_W2>(a, s); break;
     case MODE_WGRAD: launch_shape<MN_DENSE, MN_WGRAD_X, false>(a, s); break;
     case MODE_WGRAD_T: launch_shape<MN_WGRAD_X, MN_DENSE, false>(a, s); break;

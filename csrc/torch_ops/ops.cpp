@@ -90,7 +90,7 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil) {
 // accumulated into the BN layer's persistent slot workspace ([NSLOT][2][Ko], zero on entry).
 Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor slots) {
   CHECK_F32(slots);
-  TORCH_CHECK(slots.numel() == tfx::NSLOT * 2 * w.size(0), "stat slots size");
+  TORCH_CHECK(slots.numel() >= tfx::NSLOT * 2 * w.size(0), "stat slots size");
   return conv_fwd_impl(x, w, stride, pad, dil, slots.data_ptr<float>());
 }
 
@@ -158,6 +158,101 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
   if (acc) a.addend = bf(*addend);
   tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
   return dx;
+}
+
+// ---- fused BN epilogues.  ws = the BN layer's workspace: [NSLOT][2][C] f32 slots followed by
+// BN_CNT u32 column-tile counters (all zero between uses; the kernels restore that).
+unsigned* bn_counters(const Tensor& ws, int64_t C) {
+  CHECK_F32(ws); CHECK_CONTIG(ws);
+  TORCH_CHECK(ws.numel() >= tfx::NSLOT * 2 * C + tfx::BN_CNT, "BN workspace too small for the fused epilogue");
+  TORCH_CHECK(C <= 64 * tfx::BN_CNT, "fused BN epilogue: too many column tiles");
+  return reinterpret_cast<unsigned*>(ws.data_ptr<float>() + tfx::NSLOT * 2 * C);
+}
+
+// The in-kernel last-arriver reduce needs each column tile's slot columns to be whole 128-B lines
+// (igemm.hip bn_tile_reduce): C % 32 == 0 and a 128-B aligned workspace.  Otherwise the epilogue
+// only accumulates and a separate finalize / slot-reduce kernel follows.  OFF by default
+// (TFX_BN_LAST_ARRIVER=1 enables it): the counter round trip + the serial tail of the last block
+// cost more than the 5 us kernel they save -- ResNet-50 convs fwd 2.544 -> 2.651 ms, bwd 3.034 ->
+// 3.104 ms per step (profiles/r01_v9/epi_bench_la*.log).
+int bn_final_ok(const Tensor& ws, int64_t C) {
+  static const bool on = [] {
+    const char* e = getenv("TFX_BN_LAST_ARRIVER");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return (on && C % 32 == 0 && (reinterpret_cast<uintptr_t>(ws.data_ptr()) & 127) == 0) ? 1 : 0;
+}
+
+// conv forward whose epilogue produces the following BN's batch statistics AND, in the last block
+// of each column tile, finalizes them: returns (y, save = [mean | invstd | scale | shift]) and
+// updates the running statistics -- the BN then only applies (bn_apply_train).
+std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor ws,
+                                       optional<Tensor> gamma, optional<Tensor> beta, optional<Tensor> run_mean,
+                                       optional<Tensor> run_var, double momentum, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
+  auto g = geom(x.sizes().vec(), w.sizes().vec(), stride, pad, dil);
+  auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
+  auto save = at::empty({4 * g.Ko}, x.options().dtype(at::kFloat));
+  auto a = conv_args(g, stride, pad, dil);
+  a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
+  a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
+  a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
+  a.out_mode = tfx::OUT_BF16;
+  a.stats = ws.data_ptr<float>();
+  a.bn_cnt = bn_counters(ws, g.Ko);
+  a.bn_final = bn_final_ok(ws, g.Ko);
+  a.bn_gamma = fp(gamma); a.bn_beta = fp(beta); a.bn_rmean = fpm(run_mean); a.bn_rvar = fpm(run_var);
+  a.bn_save = save.data_ptr<float>();
+  a.bn_eps = (float)eps; a.bn_momentum = (float)momentum;
+  tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
+  if (!a.bn_final)
+    tfx::bn_finalize(a.stats, a.M, g.Ko, a.bn_gamma, a.bn_beta, a.bn_eps, a.bn_momentum, a.bn_rmean, a.bn_rvar,
+                     a.bn_save, cur_stream());
+  return {y, save};
+}
+
+// stride-1 conv data gradient whose epilogue also reduces the backward of the BN that produced
+// the conv's input (the gradient written here is that BN's complete output gradient): returns
+// (dx, red = [sum g' | sum g' xhat]) with dgamma / dbeta accumulated -- the BN then only applies
+// (bn_bwd_apply).  bn_mask: the residual + ReLU layer's forward mask bits (else the ReLU mask is
+// recomputed from bn_x).
+std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride,
+                                         int64_t pad, int64_t dil, optional<Tensor> addend, Tensor bn_x,
+                                         Tensor bn_save, optional<Tensor> bn_mask, bool relu, Tensor ws,
+                                         optional<Tensor> dgamma, optional<Tensor> dbeta) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
+  TORCH_CHECK(stride == 1, "conv_dgrad_bn: stride-1 convs only (stride 2 runs per parity class)");
+  auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
+  TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
+  CHECK_BF16(bn_x); CHECK_CONTIG(bn_x); CHECK_F32(bn_save);
+  TORCH_CHECK(bn_x.sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "bn_x shape");
+  TORCH_CHECK(bn_save.numel() == 4 * g.C, "bn_save size");
+  const bool acc = addend.has_value() && addend->defined();
+  if (acc) {
+    CHECK_BF16(*addend); CHECK_CONTIG(*addend);
+    TORCH_CHECK(addend->sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "addend shape");
+  }
+  auto dx = acc ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
+  auto red = at::empty({2 * g.C}, dy.options().dtype(at::kFloat));
+  auto a = conv_args(g, stride, pad, dil);
+  a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
+  a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
+  a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+  a.out_mode = tfx::OUT_BF16;
+  if (acc) a.addend = bf(*addend);
+  a.bnb_x = bf(bn_x); a.bnb_save = bn_save.data_ptr<float>();
+  if (bn_mask.has_value() && bn_mask->defined()) {
+    TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == bn_x.numel(), "bn_mask size");
+    a.bnb_mask = bn_mask->data_ptr<uint8_t>();
+  }
+  a.bnb_relu = relu ? 1 : 0;
+  a.bnb_slots = ws.data_ptr<float>();
+  a.bn_cnt = bn_counters(ws, g.C);
+  a.bn_final = bn_final_ok(ws, g.C);
+  a.bnb_red = red.data_ptr<float>(); a.bnb_dgamma = fpm(dgamma); a.bnb_dbeta = fpm(dbeta);
+  tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
+  if (!a.bn_final) tfx::bn_slot_reduce(a.bnb_slots, g.C, a.bnb_red, a.bnb_dgamma, a.bnb_dbeta, cur_stream());
+  return {dx, red};
 }
 
 // dW (f32, [Ko][R][S][C]) = or += conv weight gradient
@@ -267,7 +362,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma
                                                 bool have_stats) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(slots.numel() == tfx::NSLOT * 2 * C && slots.scalar_type() == at::kFloat, "stat slots");
+  TORCH_CHECK(slots.numel() >= tfx::NSLOT * 2 * C && slots.scalar_type() == at::kFloat, "stat slots");
   auto save = at::empty({4 * C}, x.options().dtype(at::kFloat));
   auto y = at::empty_like(x);
   const uint16_t* r = nullptr;
@@ -287,6 +382,26 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma
   tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y),
                 mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, s);
   return {y, save, mask};
+}
+
+// forward apply only, with save from conv_fwd_bn: returns (y, mask) (mask as in bn_fwd_train)
+std::tuple<Tensor, Tensor> bn_apply_train(Tensor x, optional<Tensor> res, Tensor save, bool relu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(save);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(save.numel() == 4 * C, "save size");
+  auto y = at::empty_like(x);
+  const uint16_t* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    CHECK_BF16(*res); CHECK_CONTIG(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+    r = bf(*res);
+  }
+  Tensor mask;
+  if (r && relu && C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0)
+    mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y),
+                mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return {y, mask};
 }
 
 std::tuple<Tensor, Tensor> bn_fwd_eval(Tensor x, optional<Tensor> gamma, optional<Tensor> beta, Tensor run_mean,
@@ -312,7 +427,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd grad shape");
-  TORCH_CHECK(slots.numel() == tfx::NSLOT * 2 * C && slots.scalar_type() == at::kFloat, "stat slots");
+  TORCH_CHECK(slots.numel() >= tfx::NSLOT * 2 * C && slots.scalar_type() == at::kFloat, "stat slots");
   auto red = at::empty({2 * C}, x.options().dtype(at::kFloat));
   auto dx = at::empty_like(x);
   Tensor dres;
@@ -332,6 +447,31 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
                    red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), bfm(dx), dres.defined() ? bfm(dres) : nullptr,
                    cur_stream());
   return {dx, dres, red};
+}
+
+// backward apply only, with red from conv_dgrad_bn: returns (dx, dres)
+std::tuple<Tensor, Tensor> bn_bwd_apply(Tensor g, Tensor x, optional<Tensor> res, Tensor save, Tensor red,
+                                        bool relu, optional<Tensor> mask) {
+  CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(red);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd_apply grad shape");
+  TORCH_CHECK(red.numel() == 2 * C && save.numel() == 4 * C, "red / save size");
+  auto dx = at::empty_like(x);
+  Tensor dres;
+  const uint16_t* r = nullptr;
+  const uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() * 8 == x.numel(), "relu mask size");
+    mk = mask->data_ptr<uint8_t>();
+  }
+  if (res.has_value() && res->defined()) {
+    CHECK_CONTIG(*res);
+    r = bf(*res);
+  }
+  if (r || mk) dres = at::empty_like(x);
+  tfx::bn_backward_apply(bf(g), bf(x), r, mk, save.data_ptr<float>(), red.data_ptr<float>(), M, C, relu, bfm(dx),
+                         dres.defined() ? bfm(dres) : nullptr, cur_stream());
+  return {dx, dres};
 }
 
 // ------------------------------------------------------------------ loss / metrics / pooling
@@ -640,6 +780,10 @@ TORCH_LIBRARY(tfx, m) {
   m.def("sgemm", &sgemm);
   m.def("sgemm_into", &sgemm_into);
   m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_apply_train", &bn_apply_train);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("conv_fwd_bn", &conv_fwd_bn);
+  m.def("conv_dgrad_bn", &conv_dgrad_bn);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd", &bn_bwd);
   m.def("softmax_xent", &softmax_xent);

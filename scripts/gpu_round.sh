@@ -23,6 +23,17 @@ for s in $STEPS; do
         timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/ab_on_$i.log 2>&1 || exit 1
       done
       grep -ho '"ms_per_step": [0-9.]*' gpurun_out/ab_*.log ;;
+    epibench)
+      for v in 1 0; do
+        TFX_BN_LAST_ARRIVER=$v timeout -k 10 300 python scripts/epi_bench.py --out gpurun_out/epi_bench_la$v.json > gpurun_out/epi_bench_la$v.log 2>&1 || exit 1
+      done
+      tail -1 gpurun_out/epi_bench_la*.log ;;
+    abfuse)
+      for i in 1 2; do
+        TFX_FUSE_BN=0 timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/abf_off_$i.log 2>&1 || exit 1
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/abf_on_$i.log 2>&1 || exit 1
+      done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/abf_*.log ;;
     abtile)
       for i in 1 2; do
         TFX_TILE_POLICY=0 timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/abt_off_$i.log 2>&1 || exit 1

@@ -30,6 +30,9 @@ STAGES = {
 }
 IN_CH_PAD = 8
 _SINK = os.environ.get("TFX_NO_GRADSINK", "0") != "1"  # A/B switch for the fused residual-gradient sum
+# A/B switch for the conv<->BN epilogue fusions: BN finalize in the producing conv's epilogue, BN
+# backward reduction in the consuming conv's data-gradient epilogue (igemm.hip EPI_STATS / EPI_BNB)
+_FUSE_BN = os.environ.get("TFX_FUSE_BN", "1") != "0"
 
 
 class _BN:
@@ -41,15 +44,23 @@ class _BN:
             self.var = store.add_state("moving_variance", torch.ones(c))
         self.ws = BNWorkspace(c)
 
-    def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None):
-        ws = self.ws.get(x.device) if x.device.type == "cuda" else None
+    def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None, ws_obj=False):
+        ws = (self.ws if ws_obj else self.ws.get(x.device)) if x.device.type == "cuda" else None
         return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
                               eps=1e-5, residual=residual, relu=relu, workspace=ws, stats_ready=stats_ready,
                               residual_grad_sink=residual_sink)
 
-    def after_conv(self, conv, x, training, relu=False, residual=None, sink=None, residual_sink=None):
-        """conv -> BN with the BN statistics produced by the conv's epilogue (GPU, training)."""
+    def after_conv(self, conv, x, training, relu=False, residual=None, sink=None, residual_sink=None,
+                   fuse_input_bn_backward=False):
+        """conv -> BN with the BN statistics produced (and, with _FUSE_BN, finalized) by the conv's
+        epilogue (GPU, training).  ``fuse_input_bn_backward``: the conv's data gradient is the
+        complete gradient of ``x`` -- reduce x's producing BN's backward in its epilogue."""
         fused = training and x.device.type == "cuda"
+        if fused and _FUSE_BN:
+            self.ws.finalize_args = (self.gamma.master, self.beta.master, self.mean, self.var, 0.1, 1e-5)
+            y = conv(x, self.ws, sink, fuse_input_bn_backward and _FUSE_BN)
+            return self(y, training, relu=relu, residual=residual, stats_ready=True, residual_sink=residual_sink,
+                        ws_obj=True)
         y = conv(x, self.ws.get(x.device) if fused else None, sink)
         return self(y, training, relu=relu, residual=residual, stats_ready=fused, residual_sink=residual_sink)
 
@@ -59,8 +70,9 @@ class _Conv:
         self.w = store.variable([cout, k, k, cin], HeNormal(), name=name)
         self.stride, self.pad = stride, k // 2
 
-    def __call__(self, x, bn_stats_into=None, grad_sink=None):
-        return ops.conv2d(x, self.w, self.stride, self.pad, bn_stats_into=bn_stats_into, grad_sink=grad_sink)
+    def __call__(self, x, bn_stats_into=None, grad_sink=None, fuse_input_bn_backward=False):
+        return ops.conv2d(x, self.w, self.stride, self.pad, bn_stats_into=bn_stats_into, grad_sink=grad_sink,
+                          fuse_input_bn_backward=fuse_input_bn_backward)
 
 
 class Bottleneck:
@@ -84,12 +96,15 @@ class Bottleneck:
         # x feeds conv1 and the shortcut: the shortcut's input-gradient is folded into conv1's
         # dgrad epilogue (GradSink) instead of an autograd add kernel
         prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
-        o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons)
-        o = self.b2.after_conv(self.c2, o, training, relu=True)
+        # conv1 is x's last consumer in backward only when the GradSink carries the other branch
+        o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons, fuse_input_bn_backward=cons is not None)
+        o = self.b2.after_conv(self.c2, o, training, relu=True, fuse_input_bn_backward=True)
+        o3_fuse = True
         if self.proj is None:
-            return self.b3.after_conv(self.c3, o, training, relu=True, residual=x, residual_sink=prod)
+            return self.b3.after_conv(self.c3, o, training, relu=True, residual=x, residual_sink=prod,
+                                      fuse_input_bn_backward=o3_fuse)
         sc = self.bp.after_conv(self.proj, x, training, sink=prod)
-        return self.b3.after_conv(self.c3, o, training, relu=True, residual=sc)
+        return self.b3.after_conv(self.c3, o, training, relu=True, residual=sc, fuse_input_bn_backward=o3_fuse)
 
 
 class Basic:

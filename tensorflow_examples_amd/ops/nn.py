@@ -14,6 +14,7 @@ launch a bucket's all-reduce as soon as its last gradient lands.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -57,13 +58,26 @@ def _conv_ref(x, w, stride=1, pad=0, dil=1):
     return y.permute(0, 2, 3, 1).contiguous()
 
 
+# Largest BN input (bytes) whose backward reduction runs in the consumer conv's dgrad epilogue.
+# Above it the separate reduce kernel wins: the 128 MB block inputs of ResNet-50 stage 1 measured
+# 204 -> 229 us per dgrad + BN backward fused, while every <= 64 MB layer gains 2-8 us
+# (scripts/epi_bench.py, profiles/r01_v9).
+_BNB_MAX_BYTES = int(os.environ.get("TFX_BNB_MAX_MB", "64")) << 20
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into, sink):
-        ctx.w, ctx.cfg, ctx.sink = w, (stride, pad, dil), sink
+    def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into, sink, bnb):
+        ctx.w, ctx.cfg, ctx.sink, ctx.bnb = w, (stride, pad, dil), sink, bnb
         ctx.native = _native.use_native(x)
         ctx.save_for_backward(x)
         if ctx.native:
+            if isinstance(stats_into, BNWorkspace):
+                # epilogue statistics + last-arriver finalize: the BN only applies
+                ws = stats_into
+                y, ws.pending_save = torch.ops.tfx.conv_fwd_bn(x.contiguous(), w.value, stride, pad, dil,
+                                                               ws.get(x.device), *ws.finalize_args)
+                return y
             if stats_into is not None:
                 return torch.ops.tfx.conv_fwd_stats(x.contiguous(), w.value, stride, pad, dil, stats_into)
             return torch.ops.tfx.conv_fwd(x.contiguous(), w.value, stride, pad, dil)
@@ -80,7 +94,16 @@ class _Conv2d(torch.autograd.Function):
             sink = ctx.sink
             dx = None
             if need_dx:
-                if sink is not None and sink.mode == "consume":
+                bnb = ctx.bnb
+                if bnb is not None and stride == 1 and (sink is None or sink.mode == "consume") \
+                        and x.numel() * x.element_size() <= _BNB_MAX_BYTES:
+                    # dx is the complete gradient of the BN output x: the epilogue also reduces
+                    # that BN's backward (sum g', sum g' xhat, dgamma, dbeta) -- see BNBackwardFusion
+                    add = sink.take() if sink is not None else None
+                    dx, bnb.red = torch.ops.tfx.conv_dgrad_bn(
+                        gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
+                        bnb.ws, bnb.dgamma, bnb.dbeta)
+                elif sink is not None and sink.mode == "consume":
                     # last consumer of x in backward order: fold the other branch's gradient in
                     dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, sink.take())
                 else:
@@ -91,21 +114,26 @@ class _Conv2d(torch.autograd.Function):
             if w.trainable:
                 torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
                 _grad_ready(w)
-            return dx, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None
         dx = _ref_param_grads(lambda xx, ww: _conv_ref(xx, ww, stride, pad, dil), x, [w], gy, need_dx)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int = 1,
-           bn_stats_into: Optional[torch.Tensor] = None, grad_sink: Optional["GradSink"] = None):
+           bn_stats_into=None, grad_sink: Optional["GradSink"] = None, fuse_input_bn_backward: bool = False):
     """NHWC conv, weight stored [Ko, R, S, C]. GPU: implicit-GEMM MFMA kernels (igemm.hip).
 
-    ``bn_stats_into`` = the following BN layer's slot workspace (:class:`BNWorkspace`): the
-    per-channel sum / sum-of-squares of ``y`` are then produced by the conv's GEMM epilogue and the
-    BN (``stats_ready=True``) skips its own statistics pass over ``y``.  Ignored on CPU."""
+    ``bn_stats_into`` = the following BN layer's workspace: a raw slot tensor (the epilogue
+    produces the per-channel sum / sum-of-squares of ``y``; the BN finalizes) or a
+    :class:`BNWorkspace` with ``finalize_args`` set (the epilogue's last-arriving blocks also
+    finalize; the BN only applies).  ``fuse_input_bn_backward``: the caller guarantees this conv's
+    data gradient is the COMPLETE gradient of ``x`` (sole consumer, or the GradSink consumer); if
+    ``x`` came from :func:`batch_norm` its backward reduction then runs in the dgrad epilogue.
+    Ignored on CPU."""
     gpu = x.device.type == "cuda"
     ws = bn_stats_into if (bn_stats_into is not None and gpu) else None
-    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, ws, grad_sink if gpu else None)
+    bnb = getattr(x, "_tfx_bnb", None) if (gpu and fuse_input_bn_backward) else None
+    return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, ws, grad_sink if gpu else None, bnb)
 
 
 class GradSink:
@@ -141,18 +169,38 @@ class GradSink:
 
 
 class BNWorkspace:
-    """Per-BN-layer persistent [NSLOT][2][C] f32 statistics workspace (always zero between uses:
-    the finalize / reduce kernels re-zero what they consume), so no per-step memsets."""
+    """Per-BN-layer persistent f32 workspace: [NSLOT][2][C] statistics slots followed by BN_CNT
+    column-tile arrival counters (always zero between uses: whoever consumes the slots re-zeroes
+    them and resets the counters), so no per-step memsets.
+
+    ``finalize_args`` (gamma, beta, running mean, running var, momentum, eps) are set by the model
+    when the producing conv may finalize the BN in its epilogue; the conv then leaves the
+    [mean | invstd | scale | shift] vector in ``pending_save`` for the BN forward to consume."""
     NSLOT = 64
+    BN_CNT = 64
 
     def __init__(self, channels: int):
         self.c = channels
         self.buf = None
+        self.finalize_args = None
+        self.pending_save = None
 
     def get(self, device) -> torch.Tensor:
         if self.buf is None or self.buf.device != device:
-            self.buf = torch.zeros(self.NSLOT * 2 * self.c, dtype=torch.float32, device=device)
+            self.buf = torch.zeros(self.NSLOT * 2 * self.c + self.BN_CNT, dtype=torch.float32, device=device)
         return self.buf
+
+
+class BNBackwardFusion:
+    """What a consumer conv's data-gradient epilogue needs to reduce a BN's backward (attached to
+    the BN output as ``_tfx_bnb``): the BN input, its [mean|invstd|scale|shift], the residual
+    layer's ReLU mask bits, the slot workspace and the parameter-gradient views.  The conv fills
+    ``red`` ([sum g' | sum g' xhat]); the BN backward then runs only its apply pass."""
+    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red")
+
+    def __init__(self, x, save, mask, relu, ws, dgamma, dbeta):
+        self.x, self.save, self.mask, self.relu, self.ws = x, save, mask, relu, ws
+        self.dgamma, self.dbeta, self.red = dgamma, dbeta, None
 
 
 # ====================================================================== batch norm (+res, +relu)
@@ -182,21 +230,27 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
-                training, ws, stats_ready, res_sink):
+                training, ws, stats_ready, res_sink, wsobj, bnb_out):
         ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
         ctx.res_sink = res_sink
         ctx.native = _native.use_native(x)
         ctx.has_res = res is not None
+        ctx.bnb = None
         g_t = gamma.master if gamma is not None else None
         b_t = beta.master if beta is not None else None
         if ctx.native:
             x = x.contiguous()
             if ws is None:
-                ws = torch.zeros(64 * 2 * x.shape[-1], dtype=torch.float32, device=x.device)
+                ws = torch.zeros(BNWorkspace.NSLOT * 2 * x.shape[-1] + BNWorkspace.BN_CNT, dtype=torch.float32,
+                                 device=x.device)
                 stats_ready = False
             ctx.ws = ws
             mask = None
-            if training:
+            if training and wsobj is not None and wsobj.pending_save is not None:
+                # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
+                save, wsobj.pending_save = wsobj.pending_save, None
+                y, mask = torch.ops.tfx.bn_apply_train(x, res, save, relu)
+            elif training:
                 y, save, mask = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu, ws,
                                                            bool(stats_ready))
             else:
@@ -205,6 +259,12 @@ class _BatchNorm(torch.autograd.Function):
                 mask = None
             # residual + ReLU: the backward needs only the 1-bit ReLU mask, not the residual tensor
             ctx.save_for_backward(x, None if mask is not None else res, save, mask)
+            if training and bnb_out is not None and (res is None or not relu or mask is not None) \
+                    and x.shape[-1] % 8 == 0:
+                train_p = gamma is not None and gamma.trainable
+                ctx.bnb = BNBackwardFusion(x, save, mask, relu, ws, gamma.grad if train_p else None,
+                                           beta.grad if train_p else None)
+                bnb_out.append(ctx.bnb)
             return y
         ctx.save_for_backward(x, res)
         with torch.no_grad():
@@ -219,16 +279,21 @@ class _BatchNorm(torch.autograd.Function):
             if not training:
                 raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
             train_p = gamma is not None and gamma.trainable
-            dx, dres, red = torch.ops.tfx.bn_bwd(gy.contiguous(), x, res, save, relu, ctx.ws,
-                                                 gamma.grad if train_p else None, beta.grad if train_p else None,
-                                                 mask)
+            if ctx.bnb is not None and ctx.bnb.red is not None:
+                # the consumer conv's dgrad epilogue reduced this backward (and dgamma / dbeta)
+                dx, dres = torch.ops.tfx.bn_bwd_apply(gy.contiguous(), x, res, save, ctx.bnb.red, relu, mask)
+                ctx.bnb.red = None
+            else:
+                dx, dres, red = torch.ops.tfx.bn_bwd(gy.contiguous(), x, res, save, relu, ctx.ws,
+                                                     gamma.grad if train_p else None,
+                                                     beta.grad if train_p else None, mask)
             if train_p:
                 _grad_ready(gamma, beta)
             if ctx.has_res and ctx.res_sink is not None:
                 ctx.res_sink.put(dres)
                 dres = None
             return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None, \
-                None
+                None, None, None
         x, res = ctx.saved_tensors
         with torch.enable_grad():
             xs = x.detach().requires_grad_(True)
@@ -243,21 +308,33 @@ class _BatchNorm(torch.autograd.Function):
             gamma.grad.add_(grads[0])
             beta.grad.add_(grads[1])
             _grad_ready(gamma, beta)
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
                momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False,
-               workspace: Optional[torch.Tensor] = None, stats_ready: bool = False,
+               workspace=None, stats_ready: bool = False,
                residual_grad_sink: Optional[GradSink] = None):
     """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
-    ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass)."""
+    ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass).
+
+    ``workspace``: the layer's slot tensor or :class:`BNWorkspace` (then a statistics finalize
+    done by the producing conv is picked up).  On the GPU in training mode the output carries a
+    :class:`BNBackwardFusion` (``_tfx_bnb``) for a consumer conv that opts into reducing this
+    BN's backward in its data-gradient epilogue."""
     anchor = gamma.store.anchor if gamma is not None else None
+    wsobj = workspace if isinstance(workspace, BNWorkspace) else None
+    if wsobj is not None:
+        workspace = wsobj.get(x.device) if x.device.type == "cuda" else None
     if x.device.type != "cuda":
         workspace = None
     sink = residual_grad_sink if (x.device.type == "cuda" and residual is not None) else None
-    return _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
-                            workspace, stats_ready and training and workspace is not None, sink)
+    bnb_out = [] if (x.device.type == "cuda" and training) else None
+    y = _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
+                         workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out)
+    if bnb_out:
+        y._tfx_bnb = bnb_out[0]
+    return y
 
 
 # ====================================================================== dense

@@ -240,3 +240,90 @@ def test_conv_fwd_fused_bn_stats(gpu, shape):
     y1, _, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots, True)
     y2, _, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, slots, False)
     assert _rel(y1, y2) < 1e-3
+
+
+FUSED_BN_SHAPES = [
+    # N, H, W, C, Ko, R, stride, pad: 1x1 pointwise (dense loaders), 3x3 im2col, stride 2, ragged M
+    (4, 8, 8, 64, 64, 1, 1, 0),
+    (2, 8, 8, 64, 128, 3, 1, 1),
+    (3, 9, 7, 32, 136, 3, 2, 1),
+    (64, 16, 16, 64, 256, 1, 1, 0),  # many row tiles per column tile: the last-arriver path
+]
+
+
+@pytest.mark.parametrize("shape", FUSED_BN_SHAPES)
+def test_conv_fwd_bn_finalize(gpu, shape):
+    """conv_fwd_bn: the epilogue's last block per column tile finalizes the BN ([mean | invstd |
+    scale | shift] + running stats) and leaves the workspace (slots + counters) zero."""
+    N, H, W, C, Ko, R, st, pad = shape
+    torch.manual_seed(5)
+    x = _bf(torch.randn(N, H, W, C, device=gpu))
+    w = _bf(torch.randn(Ko, R, R, C, device=gpu) * 0.1)
+    gamma = torch.rand(Ko, device=gpu) + 0.5
+    beta = torch.randn(Ko, device=gpu)
+    rm, rv = torch.zeros(Ko, device=gpu), torch.ones(Ko, device=gpu)
+    ws = torch.zeros(64 * 2 * Ko + 64, device=gpu)
+    for it in range(2):  # twice: the counters must have been reset by the first launch
+        y, save = torch.ops.tfx.conv_fwd_bn(x, w, st, pad, 1, ws, gamma, beta, rm, rv, 0.1, 1e-5)
+        torch.cuda.synchronize()
+        assert ws.abs().max().item() == 0.0, "workspace not restored to zero"
+        assert _rel(y, torch.ops.tfx.conv_fwd(x, w, st, pad, 1)) < 1e-3
+        yf = y.float().reshape(-1, Ko)
+        mean, var = yf.mean(0), yf.var(0, unbiased=False)
+        invstd = torch.rsqrt(var + 1e-5)
+        assert torch.allclose(save[:Ko], mean, rtol=1e-4, atol=1e-4)
+        assert torch.allclose(save[Ko:2 * Ko], invstd, rtol=1e-3, atol=1e-4)
+        assert torch.allclose(save[2 * Ko:3 * Ko], gamma * invstd, rtol=1e-3, atol=1e-4)
+        assert torch.allclose(save[3 * Ko:], beta - mean * gamma * invstd, rtol=1e-3, atol=1e-3)
+    M = yf.shape[0]
+    unb = var * M / (M - 1)
+    assert torch.allclose(rm, 0.19 * mean, atol=1e-4, rtol=1e-3)  # two momentum-0.1 updates from 0
+    assert torch.allclose(rv, 0.81 + 0.19 * unb, atol=1e-3, rtol=1e-3)
+    # the BN apply over the conv's save == the unfused BN forward
+    y1, _ = torch.ops.tfx.bn_apply_train(y, None, save, True)
+    ws2 = torch.zeros(64 * 2 * Ko, device=gpu)
+    y2, _, _ = torch.ops.tfx.bn_fwd_train(y, gamma, beta, None, None, 0.1, 1e-5, None, True, ws2, False)
+    assert _rel(y1, y2) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [s for s in FUSED_BN_SHAPES if s[6] == 1])
+@pytest.mark.parametrize("variant", ["relu", "res_mask", "plain", "addend"])
+def test_conv_dgrad_bn_reduce(gpu, shape, variant):
+    """conv_dgrad_bn: dx of the conv + the backward reduction of the BN that produced the conv's
+    input (sum g', sum g' xhat, dgamma / dbeta), vs the unfused conv_dgrad -> bn_bwd."""
+    N, H, W, C, Ko, R, st, pad = shape
+    torch.manual_seed(6)
+    xb = _bf(torch.randn(N, H, W, C, device=gpu) * 1.5 + 0.3)  # BN input
+    res = _bf(torch.randn(N, H, W, C, device=gpu)) if variant == "res_mask" else None
+    relu = variant != "plain"
+    gamma = torch.rand(C, device=gpu) + 0.5
+    beta = torch.randn(C, device=gpu)
+    ws = torch.zeros(64 * 2 * C + 64, device=gpu)
+    y, save, mask = torch.ops.tfx.bn_fwd_train(xb, gamma, beta, None, None, 0.1, 1e-5, res, relu, ws, False)
+    if mask is not None and mask.numel() == 0:
+        mask = None
+    assert (mask is not None) == (variant == "res_mask")
+    w = _bf(torch.randn(Ko, R, R, C, device=gpu) * 0.1)
+    P = (H + 2 * pad - R) // st + 1
+    Q = (W + 2 * pad - R) // st + 1
+    dy = _bf(torch.randn(N, P, Q, Ko, device=gpu))
+    add = _bf(torch.randn(N, H, W, C, device=gpu)) if variant == "addend" else None
+    ref_dx = torch.ops.tfx.conv_dgrad(dy, w, list(y.shape), st, pad, 1, add.clone() if add is not None else None)
+    wsr = torch.zeros(64 * 2 * C, device=gpu)
+    dgr, dbr = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+    ref_bx, ref_dres, ref_red = torch.ops.tfx.bn_bwd(ref_dx, xb, None if mask is not None else res, save, relu, wsr,
+                                                     dgr, dbr, mask)
+    dg, db = torch.ones(C, device=gpu), torch.zeros(C, device=gpu)
+    for it in range(2):
+        dx, red = torch.ops.tfx.conv_dgrad_bn(dy, w, list(y.shape), st, pad, 1,
+                                              add.clone() if add is not None else None, xb, save, mask, relu, ws,
+                                              dg, db)
+        torch.cuda.synchronize()
+        assert ws.abs().max().item() == 0.0, "workspace not restored to zero"
+        assert _rel(dx, ref_dx) < 1e-3
+        assert _rel(red, ref_red) < 1e-3
+    assert _rel(dg - 1, 2 * dgr) < 1e-3 and _rel(db, 2 * dbr) < 1e-3  # accumulated in place, twice
+    bx, dres = torch.ops.tfx.bn_bwd_apply(dx, xb, None if mask is not None else res, save, red, relu, mask)
+    assert _rel(bx, ref_bx) < 1e-2
+    if mask is not None:
+        assert _rel(dres, ref_dres) < 1e-2
