@@ -342,12 +342,22 @@ __device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n
 // EPI: compile-time epilogue extras (so the plain GEMM / wgrad kernels carry none of their code or
 // registers): EPI_STATS = fused BN statistics (+ last-arriver finalize) of a conv forward,
 // EPI_BNB = fused BN-backward partials (+ last-arriver reduce) of a conv data gradient.
-template <int AKIND, int BKIND, int BM, int BN, bool SWAP, int STG, int EPI>
-__global__ void __launch_bounds__(256, (STG == 1 && EPI == EPI_PLAIN) ? (BM * BN >= 128 * 128 ? 3 : 4) : 2) igemm_kernel(IgemmArgs a) {
+// KS = 2: in-block split-K for the f32-atomic weight gradients.  512 threads = two 4-wave groups
+// on the SAME output tile, each running the pipelined K loop over half of the block's k-tiles in its
+// own LDS stages; group 1 hands its accumulators to group 0 through LDS and only group 0 issues the
+// atomics.  Twice the loads in flight per CU (these GEMMs are latency-bound at one 4-wave block per
+// CU) for the SAME atomic bytes -- splitting across blocks instead doubles the f32 atomic traffic,
+// which runs at ~1.3 TB/s chip-wide (MI355X_MICROARCH.md "Global float atomics").
+template <int AKIND, int BKIND, int BM, int BN, bool SWAP, int STG, int EPI, int KS = 1>
+__global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == EPI_PLAIN) ? (BM * BN >= 128 * 128 ? 3 : 4) : 2)) igemm_kernel(IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BKT * 2, STAGE = (BM + BN) * BKT * 2;
-  __shared__ __attribute__((aligned(16))) char smem[STG * STAGE];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
+  static_assert(KS == 1 || (KS == 2 && EPI == EPI_PLAIN && STG == 2), "in-block split-K: plain pipelined kernels");
+  static_assert(KS == 1 || TM * TN * 4 * 256 * 4 <= STG * STAGE, "accumulator hand-off must fit a group's stages");
+  __shared__ __attribute__((aligned(16))) char smem_all[KS * STG * STAGE];
+  const int grp = KS == 2 ? (int)(threadIdx.x >> 8) : 0;
+  char* smem = smem_all + grp * (STG * STAGE);
+  const int t = threadIdx.x & 255, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_mn = a.tiles_m * a.tiles_n;
@@ -356,9 +366,13 @@ __global__ void __launch_bounds__(256, (STG == 1 && EPI == EPI_PLAIN) ? (BM * BN
   const int tm = rem / a.tiles_n, tn = rem - tm * a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nkt = (a.K + BKT - 1) / BKT;
-  const int kt0 = split * a.kps;
-  const int kt1 = min(nkt, kt0 + a.kps);
-  if (kt0 >= kt1) return;
+  const int kt0_blk = split * a.kps;
+  const int kt1 = min(nkt, kt0_blk + a.kps);
+  if (kt0_blk >= kt1) return;
+  // this group's k-tiles [kt0, kt0 + kh): the SAME trip count for both groups (their barriers are
+  // block-wide); tiles past kt1 are zero-filled through kend
+  const int kh = KS == 2 ? (kt1 - kt0_blk + 1) / 2 : kt1 - kt0_blk;
+  const int kt0 = kt0_blk + grp * kh;
 
   Loader<AKIND, BM> la;
   Loader<BKIND, BN> lb;
@@ -372,7 +386,7 @@ __global__ void __launch_bounds__(256, (STG == 1 && EPI == EPI_PLAIN) ? (BM * BN
 
   // tiles at or past kt1 are zero-filled (every offset BAD), so an odd tile count can run the
   // even/odd loop to completion: the extra step multiplies zeros.
-  const int kend = min(a.K, kt1 * BKT);
+  const int kend = min(a.K, min(kt1, kt0 + kh) * BKT);
   auto issue = [&](int kt, u32x4_t* sa, u32x4_t* sb) {
     const int k0 = kt * BKT;
     la.offsets(a, a.lda, k0, kend, oa);
@@ -423,14 +437,15 @@ __global__ void __launch_bounds__(256, (STG == 1 && EPI == EPI_PLAIN) ? (BM * BN
   issue(kt0 + 1, sa1, sb1);
   stage_store(0, sa0, sb0);
   __syncthreads();
-  if (kt1 - kt0 == 1) {
+  if (kh == 1) {
     compute(0);
   } else {
     // single exit at the bottom: every path into the loop header has set 1 in flight and set 0
     // free, so the vmcnt bookkeeping is identical on both edges (no conservative vmcnt(0)).
     // sched_barrier(0) pins the order issue -> MFMAs -> LDS write: without it hipcc hoists the
     // stage write (and its vmcnt wait on the previous tile's loads) above the MFMAs.
-    for (int kt = kt0; kt < kt1; kt += 2) {
+    const int ktend = kt0 + kh;
+    for (int kt = kt0; kt < ktend; kt += 2) {
       issue(kt + 2, sa0, sb0);  // even: stage 0 holds kt, set 1 holds kt+1
       __builtin_amdgcn_sched_barrier(0);
       compute(0);
@@ -445,6 +460,29 @@ __global__ void __launch_bounds__(256, (STG == 1 && EPI == EPI_PLAIN) ? (BM * BN
       __syncthreads();
     }
   }
+  }
+
+  if constexpr (KS == 2) {
+    // group 1's accumulators -> its (now free) LDS stages -> summed into group 0's, conflict-free
+    // [element][thread] layout; group 1 is done after the hand-off
+    __syncthreads();  // kh == 1 leaves compute(0) without a trailing barrier
+    float* xch = reinterpret_cast<float*>(smem_all + STG * STAGE);
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xch[((i * TN + j) * 4 + r) * 256 + t] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += xch[((i * TN + j) * 4 + r) * 256 + t];
   }
 
   // Element (m, n) of lane's acc[i][j][r]:
@@ -814,7 +852,7 @@ int pick_splits(int tiles, int nkt, int want_blocks) {
   return std::max(1, std::min(s, max_s));
 }
 
-template <int AK, int BK, int BM, int BN, int EPI = EPI_PLAIN>
+template <int AK, int BK, int BM, int BN, int EPI = EPI_PLAIN, int KS = 1>
 void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1) {
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + BN - 1) / BN;
@@ -827,12 +865,25 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1) {
   }();
   if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, want * want_mult);
   a.kps = (nkt + splits - 1) / splits;
-  if (splits > 1) a.kps += a.kps & 1;  // even k-tiles per split: no zero step in the loop
+  if constexpr (KS == 2) {
+    // each 4-wave group takes kps/2 k-tiles: a multiple of 4 keeps both halves even (no zero step).
+    // An 8-wave block holds its CU's LDS alone, so more blocks than CUs would run a second wave
+    // (e.g. 144 tiles x 2 splits): the 4-wave form fits those at two blocks per CU.
+    if (a.kps < 4 || tiles * splits > want) return launch_t<AK, BK, BM, BN, EPI, 1>(a, s, want_mult);
+    a.kps = (a.kps + 3) & ~3;
+  } else if (splits > 1) {
+    a.kps += a.kps & 1;  // even k-tiles per split: no zero step in the loop
+  }
   splits = (nkt + a.kps - 1) / a.kps;
   const int grid = tiles * splits;
   if (grid == 0) return;
   // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
+  if constexpr (KS == 2) {
+    if (swap) igemm_kernel<AK, BK, BM, BN, true, 2, EPI_PLAIN, 2><<<grid, 2 * NT, 0, s>>>(a);
+    else igemm_kernel<AK, BK, BM, BN, false, 2, EPI_PLAIN, 2><<<grid, 2 * NT, 0, s>>>(a);
+    return;
+  }
   if constexpr (EPI != EPI_PLAIN) {  // fused-BN epilogues: bf16 outputs only (SWAP orientation)
     if (nkt == 1 && splits == 1) igemm_kernel<AK, BK, BM, BN, true, 1, EPI><<<grid, NT, 0, s>>>(a);
     else igemm_kernel<AK, BK, BM, BN, true, 2, EPI><<<grid, NT, 0, s>>>(a);
@@ -868,10 +919,26 @@ int wgrad_tile() {
   return t;
 }
 
+// in-block split-K for the weight gradients (TFX_WGRAD_KS=1 restores one 4-wave group per block)
+int wgrad_ks() {
+  static const int k = [] {
+    const char* e = getenv("TFX_WGRAD_KS");
+    return e ? atoi(e) : 2;
+  }();
+  return k;
+}
+
 template <int AK, int BK, bool ALLOW256 = true, int EPI = EPI_PLAIN>
 void launch_shape(IgemmArgs& a, hipStream_t s) {
   if constexpr (!ALLOW256) {
     const bool dense_pair = (AK == MN_DENSE && BK == MN_DENSE) || (a.R == 1 && a.S == 1);  // 1x1 (any stride)
+    if (wgrad_ks() == 2) {
+      // 8-wave blocks, one per CU: 128x64 tiles for the dense pair (half the atomic bytes of the
+      // 2-blocks-per-CU 128x64 form), 128x128 for the im2col-gathered ones
+      if (a.N <= 64 || (dense_pair && wgrad_tile() != 128) || wgrad_tile() == 64)
+        return launch_t<AK, BK, 128, 64, EPI, 2>(a, s);
+      return launch_t<AK, BK, 128, 128, EPI, 2>(a, s);
+    }
     if (a.N > 64 && (wgrad_tile() == 64 || (wgrad_tile() == 0 && dense_pair))) return launch_t<AK, BK, 128, 64, EPI>(a, s, 2);
   }
   if (a.N <= 64) {

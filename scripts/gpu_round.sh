@@ -28,6 +28,14 @@ for s in $STEPS; do
         TFX_BN_LAST_ARRIVER=$v timeout -k 10 300 python scripts/epi_bench.py --out gpurun_out/epi_bench_la$v.json > gpurun_out/epi_bench_la$v.log 2>&1 || exit 1
       done
       tail -1 gpurun_out/epi_bench_la*.log ;;
+    abks)
+      for v in 1 2; do
+        TFX_WGRAD_KS=$v timeout -k 10 300 python scripts/conv_bench.py --out gpurun_out/conv_bench_ks$v.json > gpurun_out/conv_bench_ks$v.log 2>&1 || exit 1
+      done
+      for i in 1 2; do for v in 1 2; do
+        TFX_WGRAD_KS=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/abks_${v}_$i.log 2>&1 || exit 1
+      done; done
+      grep TOTAL gpurun_out/conv_bench_ks*.log; grep -o '"ms_per_step": [0-9.]*' gpurun_out/abks_*.log ;;
     abfuse)
       for i in 1 2; do
         TFX_FUSE_BN=0 timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/abf_off_$i.log 2>&1 || exit 1
