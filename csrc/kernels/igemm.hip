@@ -276,20 +276,24 @@ __device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n
   float* slots = BWD ? a.bnb_slots : a.stats;
   float s = 0.f, q = 0.f;
   if (c < a.N) {
-    float vs[NSLOT / NPH], vq[NSLOT / NPH];
+    // 8 slot rows in flight per step (bounded registers: this runs in every fused-BN kernel)
+    constexpr int CH = NSLOT / NPH < 8 ? NSLOT / NPH : 8;
+    for (int k0 = 0; k0 < NSLOT / NPH; k0 += CH) {
+      float vs[CH], vq[CH];
 #pragma unroll
-    for (int k = 0; k < NSLOT / NPH; ++k) {
-      float* row = slots + (size_t)(ph + k * NPH) * 2 * a.N;
-      vs[k] = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      vq[k] = __hip_atomic_load(row + a.N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+      for (int k = 0; k < CH; ++k) {
+        float* row = slots + (size_t)(ph + (k0 + k) * NPH) * 2 * a.N;
+        vs[k] = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vq[k] = __hip_atomic_load(row + a.N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
 #pragma unroll
-    for (int k = 0; k < NSLOT / NPH; ++k) {
-      s += vs[k];
-      q += vq[k];
-      float* row = slots + (size_t)(ph + k * NPH) * 2 * a.N;
-      __hip_atomic_store(row + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(row + a.N + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < CH; ++k) {
+        s += vs[k];
+        q += vq[k];
+        float* row = slots + (size_t)(ph + (k0 + k) * NPH) * 2 * a.N;
+        __hip_atomic_store(row + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(row + a.N + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   float* part = reinterpret_cast<float*>(smem);
@@ -349,7 +353,7 @@ __device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n
 // CU) for the SAME atomic bytes -- splitting across blocks instead doubles the f32 atomic traffic,
 // which runs at ~1.3 TB/s chip-wide (MI355X_MICROARCH.md "Global float atomics").
 template <int AKIND, int BKIND, int BM, int BN, bool SWAP, int STG, int EPI, int KS = 1>
-__global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == EPI_PLAIN) ? (BM * BN >= 128 * 128 ? 3 : 4) : 2)) igemm_kernel(IgemmArgs a) {
+__global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI != EPI_BNB) ? (BM * BN >= 128 * 128 ? 3 : 4) : 2)) igemm_kernel(IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BKT * 2, STAGE = (BM + BN) * BKT * 2;
   static_assert(KS == 1 || (KS == 2 && EPI == EPI_PLAIN && STG == 2), "in-block split-K: plain pipelined kernels");
@@ -496,83 +500,7 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == E
     // stage that the epilogue's LDS partials overwrite
     if constexpr (EPI != EPI_PLAIN) __syncthreads();
   }
-  if constexpr (EPI == EPI_STATS) {
-    float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN cols][2]; LDS is free after the loop
-    if constexpr (SWAP) {
-      // lane holds rows mb + i*16 + (lane&15), columns nb + j*16 + (lane>>4)*4 + r: sum its TM rows
-      // in registers, then the 16 rows of the DPP row (row16_sum: no LDS, no branches)
-      float rv[TM];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) rv[i] = (mb + i * 16 + (lane & 15)) < a.M ? 1.f : 0.f;
-      const bool relu = a.relu != 0;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float cs[4], cq[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = nb + j * 16 + (lane >> 4) * 4 + r;
-          const float bias = a.bias ? a.bias[min(n, a.N - 1)] : 0.f;
-          float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            float v = acc[i][j][r] + bias;
-            if (relu) v = fmaxf(v, 0.f);
-            v = bf16_to_f32(f32_to_bf16(v)) * rv[i];
-            s1 += v;
-            s2 = fmaf(v, v, s2);
-          }
-          cs[r] = row16_sum(s1);
-          cq[r] = row16_sum(s2);
-        }
-        if ((lane & 15) == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int col = wn * WN + j * 16 + (lane >> 4) * 4 + r;
-            red[(wm * BN + col) * 2 + 0] = cs[r];
-            red[(wm * BN + col) * 2 + 1] = cq[r];
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float cs = 0.f, cq = 0.f;
-        const int n = nb + j * 16 + (lane & 15);
-        const float bias = (a.bias && n < a.N) ? a.bias[n] : 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = mb + i * 16 + (lane >> 4) * 4 + r;
-            float v = acc[i][j][r] + bias;
-            if (a.relu) v = fmaxf(v, 0.f);
-            v = bf16_to_f32(f32_to_bf16(v));
-            if (m < a.M) {
-              cs += v;
-              cq = fmaf(v, v, cq);
-            }
-          }
-        cs += __shfl_xor(cs, 16, 64);
-        cs += __shfl_xor(cs, 32, 64);
-        cq += __shfl_xor(cq, 16, 64);
-        cq += __shfl_xor(cq, 32, 64);
-        if (lane < 16) {
-          const int col = wn * WN + j * 16 + lane;
-          red[(wm * BN + col) * 2 + 0] = cs;
-          red[(wm * BN + col) * 2 + 1] = cq;
-        }
-      }
-    }
-    __syncthreads();
-    if (t < BN) {
-      const int n = n0 + t;
-      if (n < a.N) {
-        float* slot = a.stats + (size_t)(tm % NSLOT) * 2 * a.N;
-        atomicAdd(&slot[n], red[t * 2] + red[(BN + t) * 2]);
-        atomicAdd(&slot[a.N + n], red[t * 2 + 1] + red[(BN + t) * 2 + 1]);
-      }
-    }
-  }
+  static_assert(EPI == EPI_PLAIN || SWAP, "fused-BN epilogues use the SWAP (16-byte store) orientation");
 
   // ---------------- epilogue (mode tested once per block, bias preloaded: no loads in the store loops)
   if constexpr (SWAP) {
@@ -611,13 +539,21 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == E
       // the even lane of tile j, the odd lane of tile j+1 -- i.e. half the store instructions.
       uint16_t* Cb = reinterpret_cast<uint16_t*>(a.Cp);
       const bool odd = (lane >> 4) & 1;
-      constexpr bool bnb = EPI == EPI_BNB;  // fused BN-backward partials of this output
+      constexpr bool bnb = EPI == EPI_BNB;    // fused BN-backward partials of this output
+      constexpr bool sts = EPI == EPI_STATS;  // fused BN statistics of this (bf16-rounded) output
       float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN cols][2] partials (LDS free after the loop)
 #pragma unroll
       for (int j = 0; j < TN; j += 2) {
         const int n = nb + (j + (odd ? 1 : 0)) * 16 + ((lane >> 5) << 3);
         // per-column BN parameters of this lane's 8 columns (mean, invstd, scale, shift)
         float mu[8], is[8], sc[8], sh[8], bs[8], bq[8];
+        if constexpr (bnb || sts) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            bs[k] = 0.f;
+            bq[k] = 0.f;
+          }
+        }
         if constexpr (bnb) {
           const int nc = min(n, a.N - 8);
 #pragma unroll
@@ -626,8 +562,6 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == E
             is[k] = a.bnb_save[a.N + nc + k];
             sc[k] = a.bnb_save[2 * a.N + nc + k];
             sh[k] = a.bnb_save[3 * a.N + nc + k];
-            bs[k] = 0.f;
-            bq[k] = 0.f;
           }
         }
         // The epilogue's global reads (addend, BN input, ReLU mask bits) of IC rows are issued
@@ -684,6 +618,16 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == E
               }
               const U4 packed = pack8(o);
               *reinterpret_cast<U4*>(dst) = packed;
+              if constexpr (sts) {
+                // per-column sum / sum of squares of exactly the bf16 values the BN will read
+                float g[8];
+                unpack8(packed, g);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                  bs[k] += g[k];
+                  bq[k] = fmaf(g[k], g[k], bq[k]);
+                }
+              }
               if constexpr (bnb) {
                 // g' = bf16(out) * relu mask; xhat from the BN input x (same NHWC position)
                 float g[8], xv[8];
@@ -702,7 +646,7 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == E
             }
           }
         }
-        if constexpr (bnb) {
+        if constexpr (bnb || sts) {
           // the 16 rows of this DPP row share the lane's 8 columns: reduce them in registers
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
@@ -719,17 +663,17 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == E
           }
         }
       }
-      if constexpr (bnb) {
+      if constexpr (bnb || sts) {
         __syncthreads();
         if (t < BN) {
           const int nn = n0 + t;
           if (nn < a.N) {
-            float* slot = a.bnb_slots + (size_t)(tm % NSLOT) * 2 * a.N;
+            float* slot = (bnb ? a.bnb_slots : a.stats) + (size_t)(tm % NSLOT) * 2 * a.N;
             atomicAdd(&slot[nn], red[t * 2] + red[(BN + t) * 2]);
             atomicAdd(&slot[a.N + nn], red[t * 2 + 1] + red[(BN + t) * 2 + 1]);
           }
         }
-        if (a.bn_final) bn_tile_reduce<BN, true>(a, tn, n0, smem, t);
+        if (a.bn_final) bn_tile_reduce<BN, bnb>(a, tn, n0, smem, t);
       }
     } else if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 3) == 0 && (a.N & 3) == 0) {
       uint16_t* Cb = reinterpret_cast<uint16_t*>(a.Cp);
@@ -831,11 +775,6 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI == E
           }
       }
     }
-  }
-  // forward BN finalize by the last block of each column tile, after the stores (acc is dead here:
-  // the slot reads get the registers)
-  if constexpr (EPI == EPI_STATS) {
-    if (a.bn_final) bn_tile_reduce<BN, false>(a, tn, n0, smem, t);
   }
 }
 
