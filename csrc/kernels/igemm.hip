@@ -781,18 +781,18 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI != E
 // ============================================================ host launcher
 namespace {
 
-int pick_splits(int tiles, int nkt, int want_blocks) {
+int pick_splits(int tiles, int nkt, int want_blocks, int min_kps = 4) {
   if (tiles >= want_blocks) return 1;
   // floor: never more blocks than the target (1 or 2 per CU) -- a few CUs holding an extra block
   // would set the kernel's time (e.g. 36 tiles x 8 splits = 288 blocks on 256 CUs)
   int s = want_blocks / tiles;
   if (s * tiles < want_blocks * 3 / 4) s = (want_blocks + tiles - 1) / tiles;  // floor under-fills: round up
-  const int max_s = std::max(1, nkt / 4);  // keep >= 4 k-tiles per split
+  const int max_s = std::max(1, nkt / min_kps);  // keep >= min_kps (default 4) k-tiles per split
   return std::max(1, std::min(s, max_s));
 }
 
 template <int AK, int BK, int BM, int BN, int EPI = EPI_PLAIN, int KS = 1>
-void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1) {
+void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + BN - 1) / BN;
   const int nkt = (a.K + BKT - 1) / BKT;
@@ -802,13 +802,13 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1) {
     const char* e = getenv("TFX_SPLITK_BLOCKS");
     return e ? atoi(e) : 256;  // one block per CU: measured best (fewer f32 atomic partials)
   }();
-  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, want * want_mult);
+  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, want * want_mult, min_kps);
   a.kps = (nkt + splits - 1) / splits;
   if constexpr (KS == 2) {
     // each 4-wave group takes kps/2 k-tiles: a multiple of 4 keeps both halves even (no zero step).
     // An 8-wave block holds its CU's LDS alone, so more blocks than CUs would run a second wave
     // (e.g. 144 tiles x 2 splits): the 4-wave form fits those at two blocks per CU.
-    if (a.kps < 4 || tiles * splits > want) return launch_t<AK, BK, BM, BN, EPI, 1>(a, s, want_mult);
+    if (a.kps < 4 || tiles * splits > want) return launch_t<AK, BK, BM, BN, EPI, 1>(a, s, want_mult, min_kps);
     a.kps = (a.kps + 3) & ~3;
   } else if (splits > 1) {
     a.kps += a.kps & 1;  // even k-tiles per split: no zero step in the loop
@@ -862,6 +862,15 @@ int wgrad_tile() {
 int wgrad_ks() {
   static const int k = [] {
     const char* e = getenv("TFX_WGRAD_KS");
+    return e ? atoi(e) : 2;
+  }();
+  return k;
+}
+
+// min k-tiles per split for the skinny GEMM path (TFX_SKINNY_KPS; 0 disables the path)
+int skinny_min_kps() {
+  static const int k = [] {
+    const char* e = getenv("TFX_SKINNY_KPS");
     return e ? atoi(e) : 2;
   }();
   return k;
@@ -958,6 +967,17 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
     case MODE_WGRAD: launch_shape<MN_DENSE, MN_WGRAD_X, false>(a, s); break;
     case MODE_WGRAD_T: launch_shape<MN_WGRAD_X, MN_DENSE, false>(a, s); break;
     default:
+      // skinny f32-accumulated GEMMs (the recurrent h @ W_hh^T / dgates @ W_hh of an LSTM step:
+      // M = batch <= 128, a few thousand columns): latency-bound, so cut them into many short
+      // blocks -- 128x64 tiles, split-K down to min_kps k-tiles per block
+      if (a.out_mode == OUT_F32_ATOMIC && a.M <= 128 && skinny_min_kps() > 0) {
+        const int mk = skinny_min_kps();
+        if (a.a_kmajor && a.b_kmajor) launch_t<KM_DENSE, KM_DENSE, 128, 64>(a, s, 1, mk);
+        else if (a.a_kmajor) launch_t<KM_DENSE, MN_DENSE, 128, 64>(a, s, 1, mk);
+        else if (a.b_kmajor) launch_t<MN_DENSE, KM_DENSE, 128, 64>(a, s, 1, mk);
+        else launch_t<MN_DENSE, MN_DENSE, 128, 64>(a, s, 1, mk);
+        return;
+      }
       if (a.a_kmajor && a.b_kmajor) launch_t<KM_DENSE, KM_DENSE, 128, 128>(a, s);
       else if (a.a_kmajor) launch_t<KM_DENSE, MN_DENSE, 128, 128>(a, s);
       else if (a.b_kmajor) launch_t<MN_DENSE, KM_DENSE, 128, 128>(a, s);
