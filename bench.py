@@ -45,7 +45,9 @@ def parse(argv=None):
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph (N=1 only)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="capture the whole step in a HIP graph and replay it (N=1; default on)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager step launches")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--backend", default=None, help="process-group backend (default nccl = RCCL)")
@@ -70,6 +72,7 @@ def main(argv=None):
     torch.manual_seed(1234 + rank)
     data = synthetic_batches(a.nbatches, a.batch, dev, seed=1000 + rank)
 
+    graphed = False
     if a.impl == "native":
         store, model = build_resnet_cifar(device=dev, depth=a.depth, dtype=torch.bfloat16, seed=0)
         broadcast_variables(store)
@@ -81,9 +84,17 @@ def main(argv=None):
             img, lab = data[i % len(data)]
             return trainer.step(to_model_input(img), lab)
 
+        graphed = False
         if a.graph and world == 1:
+            # the captured step is the same work (forward, backward, fused optimizer) replayed with
+            # one launch; the per-step input batch is copied into the graph's static input
             img, lab = data[0]
-            trainer.capture(to_model_input(img), lab)
+            try:
+                trainer.capture(to_model_input(img), lab)
+                graphed = True
+            except Exception as e:  # pragma: no cover - capture is best effort, eager is the fallback
+                print("hip graph capture failed (%s); running eager" % e, file=sys.stderr)
+                trainer.graph = None
         nparams = store.num_params()
     else:
         from tensorflow_examples_amd.models.torch_baseline import TorchResNet50Cifar
@@ -151,7 +162,7 @@ def main(argv=None):
                 "impl": a.impl,
                 "optimizer": "momentum-SGD 0.9, wd 5e-4 (fused flat-buffer kernel)" if a.impl == "native" else "torch.optim.SGD foreach",
                 "allreduce_bucket_mb": a.bucket_mb,
-                "hip_graph": bool(a.graph and world == 1 and a.impl == "native"),
+                "hip_graph": bool(a.impl == "native" and graphed),
                 "params": nparams,
                 "final_loss": round(final_loss, 4),
             },
