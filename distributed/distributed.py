@@ -47,6 +47,8 @@ flags.DEFINE_boolean("ps_exit_after_workers", False, "ps exits once every worker
 flags.DEFINE_boolean("sync_replicas", False, "aggregate all workers' gradients per global step "
                      "(SyncReplicasOptimizer semantics, R/distributed/distributed.py:109-112)")
 flags.DEFINE_integer("sync_port_offset", 1000, "worker-group rendezvous port = worker 0 port + offset")
+flags.DEFINE_integer("save_checkpoint_steps", 0, "chief saves a checkpoint into --logdir every N local steps "
+                     "(0 = only at the end; TF1 Supervisor saves on a timer when logdir is set)")
 FLAGS = app.flags.FLAGS
 
 if not FLAGS.ps_hosts or not FLAGS.worker_hosts:
@@ -89,6 +91,7 @@ elif FLAGS.job_name == "worker":
     from tensorflow_examples_amd.data.mnist import read_data_sets
     from tensorflow_examples_amd.models.mnist_mlp import MnistMLP
     from tensorflow_examples_amd.parallel.ps_worker import AsyncPSWorker, SyncReplicasPSWorker, init_worker_group
+    from tensorflow_examples_amd.utils import fault
     from tensorflow_examples_amd.variables import VariableStore
 
     # load training examples, read with one_hot set to true
@@ -126,6 +129,7 @@ elif FLAGS.job_name == "worker":
 
     begin_time = time.time()
     frequency = 100
+    fault.before_init()  # TFX_FAULT hooks: recovery tests
     with sv.prepare_or_wait_for_session() as sess:
         if FLAGS.task_index == 0 and FLAGS.ps_exit_after_workers:
             import ctypes
@@ -142,6 +146,7 @@ elif FLAGS.job_name == "worker":
         start_time = time.time()
         cost = 0.0
         step = 0
+        local_steps = 0
         for epoch in range(training_epochs):
             batch_count = int(mnist.train.num_examples / batch_size)
             if FLAGS.max_batches_per_epoch:
@@ -154,6 +159,10 @@ elif FLAGS.job_name == "worker":
                 cost, acc, step = worker.step(batch_x, batch_y)
                 cost_v[0], acc_v[0] = cost, acc
                 writer.add_summary(summary_op(), step)
+                local_steps += 1
+                if FLAGS.logdir and FLAGS.save_checkpoint_steps and local_steps % FLAGS.save_checkpoint_steps == 0:
+                    sv.save(step + 1)
+                fault.after_step(local_steps)
 
                 count += 1
                 if count % frequency == 0 or i + 1 == batch_count:
