@@ -148,7 +148,11 @@ struct Writer {
     auto last = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> lk(mu);
     while (true) {
-      cv.wait_for(lk, std::chrono::milliseconds(200), [&] { return stop || !q.empty(); });
+      // system_clock deadline: libstdc++ maps it to pthread_cond_timedwait, which ThreadSanitizer
+      // intercepts (a steady_clock wait_for becomes pthread_cond_clockwait, which GCC 11's TSAN
+      // does not model -- it then reports the waiting mutex as held: tests/test_runtime_sanitizers.py)
+      cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(200),
+                    [&] { return stop || !q.empty(); });
       while (!q.empty()) {
         std::string rec = std::move(q.front());
         q.pop_front();
