@@ -45,6 +45,9 @@ struct IgemmArgs {
   int64_t a_bytes = 0, b_bytes = 0;  // extents of A/B (buffer-resource bounds; must be < 2 GiB)
   int trans_out = 0;                 // store C[m][n] at Cp[n*ldc + m]
   const uint16_t* addend = nullptr;  // bf16 outputs: C = acc + addend (same layout as C; may alias Cp)
+  // optional ReLU-mask bits of the addend (1 bit per element, one byte per 8 channels): C = acc +
+  // addend * mask -- a residual BN's masked output gradient consumed without materialising it
+  const uint8_t* addend_mask = nullptr;
   void* Cp = nullptr;
   const float* bias = nullptr;
   int M = 0, N = 0, K = 0;

@@ -422,7 +422,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* _
       o[k] = fmaf(A[k], gg, fmaf(B[k], xf[k], D[k]));
     }
     reinterpret_cast<U4*>(dx)[i] = pack8(o);
-    if (RES) reinterpret_cast<U4*>(dres)[i] = pack8(gf);
+    // dres == nullptr: the consumer reads g and the mask bits itself (masked conv addend)
+    if (RES && dres) reinterpret_cast<U4*>(dres)[i] = pack8(gf);
   }
 }
 
@@ -447,7 +448,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_gen_kernel(const uint16_t* _
     }
     const float xh = (xf - mu) * is;
     dx[i] = f32_to_bf16(sc * (gg - red[c] * inv_m - xh * red[C + c] * inv_m));
-    if (RES) dres[i] = f32_to_bf16(gg);
+    if (RES && dres) dres[i] = f32_to_bf16(gg);
   }
 }
 

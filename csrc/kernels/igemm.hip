@@ -574,11 +574,14 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI != E
 #pragma unroll
         for (int i0 = 0; i0 < TM; i0 += IC) {
           U4 adv[IC], xvv[IC];
-          uint32_t mbv[IC];
+          uint32_t mbv[IC], amv[IC];
 #pragma unroll
           for (int ii = 0; ii < IC; ++ii) {
             const int64_t o = rowoff[i0 + ii] + nl;
-            if (a.addend) adv[ii] = *reinterpret_cast<const U4*>(a.addend + o);
+            if (a.addend) {
+              adv[ii] = *reinterpret_cast<const U4*>(a.addend + o);
+              amv[ii] = a.addend_mask ? a.addend_mask[o >> 3] : 0xffu;
+            }
             if constexpr (bnb) {
               xvv[ii] = *reinterpret_cast<const U4*>(a.bnb_x + o);
               mbv[ii] = a.bnb_mask ? a.bnb_mask[o >> 3] : 0xffu;
@@ -614,7 +617,7 @@ __global__ void __launch_bounds__(256 * KS, KS == 2 ? 1 : ((STG == 1 && EPI != E
                 float ad[8];
                 unpack8(adv[ii], ad);
 #pragma unroll
-                for (int r = 0; r < 8; ++r) o[r] += ad[r];
+                for (int r = 0; r < 8; ++r) o[r] += ((amv[ii] >> r) & 1u) ? ad[r] : 0.f;
               }
               const U4 packed = pack8(o);
               *reinterpret_cast<U4*>(dst) = packed;
@@ -915,6 +918,11 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
   if (a.out_mode == OUT_F32_ATOMIC && a.zero_out) {
     const size_t rows = a.trans_out ? a.N : a.M;
     TFX_HIP_CHECK(hipMemsetAsync(a.Cp, 0, sizeof(float) * rows * a.ldc, s));
+  }
+  // a masked addend is applied only by the bf16 16-byte-store epilogue path
+  if (a.addend_mask && !(a.addend && a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0)) {
+    fprintf(stderr, "igemm_launch: masked addend needs a bf16 output with 8-aligned columns\n");
+    abort();
   }
   // fused-BN epilogues live in the bf16 16-byte-store path of the forward / data-gradient kernels
   if (a.stats || a.bnb_x) {

@@ -104,8 +104,18 @@ bool dgrad_classes_enabled() {
 
 // dX = dgrad(dy) (+ addend: the gradient of x's other consumer, summed in the epilogue; the
 // result is written in place into addend's storage when given)
+// addend_mask: 1-bit ReLU mask of the addend (uint8 per 8 channels): dX = dgrad + addend * mask,
+// into a fresh buffer (the addend -- a residual BN's unmasked output gradient -- stays intact)
+const uint8_t* addend_mask_ptr(const optional<Tensor>& addend, const optional<Tensor>& mask) {
+  if (!(mask.has_value() && mask->defined())) return nullptr;
+  TORCH_CHECK(addend.has_value() && addend->defined(), "addend_mask without addend");
+  TORCH_CHECK(mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() * 8 == addend->numel(),
+              "addend_mask: uint8, one byte per 8 addend elements");
+  return mask->data_ptr<uint8_t>();
+}
+
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil,
-                  optional<Tensor> addend) {
+                  optional<Tensor> addend, optional<Tensor> addend_mask) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
@@ -113,6 +123,19 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
   if (acc) {
     CHECK_BF16(*addend); CHECK_CONTIG(*addend);
     TORCH_CHECK(addend->sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "addend shape");
+  }
+  const uint8_t* amask = addend_mask_ptr(addend, addend_mask);
+  if (amask) {
+    TORCH_CHECK(stride == 1 && g.C % 8 == 0, "masked addend: stride-1 data gradients with C % 8 == 0");
+    auto dx = at::empty({g.N, g.H, g.W, g.C}, dy.options());
+    auto a = conv_args(g, stride, pad, dil);
+    a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
+    a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
+    a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+    a.out_mode = tfx::OUT_BF16;
+    a.addend = bf(*addend); a.addend_mask = amask;
+    tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
+    return dx;
   }
   if (stride == 2 && dil == 1 && dgrad_classes_enabled()) {
     // Stride-2 data gradient by output-parity class: pixel (h, w) only receives taps with
@@ -219,7 +242,8 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
 std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride,
                                          int64_t pad, int64_t dil, optional<Tensor> addend, Tensor bn_x,
                                          Tensor bn_save, optional<Tensor> bn_mask, bool relu, Tensor ws,
-                                         optional<Tensor> dgamma, optional<Tensor> dbeta) {
+                                         optional<Tensor> dgamma, optional<Tensor> dbeta,
+                                         optional<Tensor> addend_mask) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
   TORCH_CHECK(stride == 1, "conv_dgrad_bn: stride-1 convs only (stride 2 runs per parity class)");
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
@@ -232,7 +256,8 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
     CHECK_BF16(*addend); CHECK_CONTIG(*addend);
     TORCH_CHECK(addend->sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "addend shape");
   }
-  auto dx = acc ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
+  const uint8_t* amask = addend_mask_ptr(addend, addend_mask);
+  auto dx = (acc && !amask) ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
   auto red = at::empty({2 * g.C}, dy.options().dtype(at::kFloat));
   auto a = conv_args(g, stride, pad, dil);
   a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
@@ -240,6 +265,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
   a.out_mode = tfx::OUT_BF16;
   if (acc) a.addend = bf(*addend);
+  a.addend_mask = amask;
   a.bnb_x = bf(bn_x); a.bnb_save = bn_save.data_ptr<float>();
   if (bn_mask.has_value() && bn_mask->defined()) {
     TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == bn_x.numel(), "bn_mask size");
@@ -421,9 +447,11 @@ std::tuple<Tensor, Tensor> bn_fwd_eval(Tensor x, optional<Tensor> gamma, optiona
 // returns dx, dres (undefined unless res given), red = [dbeta(C) | dgamma(C)]; when dgamma/dbeta
 // are given the parameter gradients are accumulated in place by the reduce kernel.
 // residual layers: pass the forward's ``mask`` (vector path; then ``res`` may be omitted) or ``res``.
+// want_dres = false: no dres tensor is written (the residual's consumer reads g and the mask bits
+// itself: conv_dgrad(..., addend=g, addend_mask=mask))
 std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> res, Tensor save, bool relu,
                                           Tensor slots, optional<Tensor> dgamma, optional<Tensor> dbeta,
-                                          optional<Tensor> mask) {
+                                          optional<Tensor> mask, bool want_dres) {
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd grad shape");
@@ -441,8 +469,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
     CHECK_CONTIG(*res);
     r = bf(*res);
   }
-  if (r || mk) dres = at::empty_like(x);
-  TORCH_CHECK(!(relu && mk == nullptr && r == nullptr && dres.defined()), "residual bn_bwd needs res or mask");
+  if ((r || mk) && want_dres) dres = at::empty_like(x);
   tfx::bn_backward(bf(g), bf(x), r, mk, save.data_ptr<float>(), M, C, relu, slots.data_ptr<float>(),
                    red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), bfm(dx), dres.defined() ? bfm(dres) : nullptr,
                    cur_stream());
@@ -451,7 +478,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
 
 // backward apply only, with red from conv_dgrad_bn: returns (dx, dres)
 std::tuple<Tensor, Tensor> bn_bwd_apply(Tensor g, Tensor x, optional<Tensor> res, Tensor save, Tensor red,
-                                        bool relu, optional<Tensor> mask) {
+                                        bool relu, optional<Tensor> mask, bool want_dres) {
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(red);
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd_apply grad shape");
@@ -468,7 +495,7 @@ std::tuple<Tensor, Tensor> bn_bwd_apply(Tensor g, Tensor x, optional<Tensor> res
     CHECK_CONTIG(*res);
     r = bf(*res);
   }
-  if (r || mk) dres = at::empty_like(x);
+  if ((r || mk) && want_dres) dres = at::empty_like(x);
   tfx::bn_backward_apply(bf(g), bf(x), r, mk, save.data_ptr<float>(), red.data_ptr<float>(), M, C, relu, bfm(dx),
                          dres.defined() ? bfm(dres) : nullptr, cur_stream());
   return {dx, dres};
@@ -773,7 +800,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("lstm_cell_bwd", &lstm_cell_bwd);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
+        "Tensor? addend_mask=None) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("gemm", &gemm);
   m.def("gemm_into", &gemm_into);
@@ -781,11 +809,15 @@ TORCH_LIBRARY(tfx, m) {
   m.def("sgemm_into", &sgemm_into);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply_train", &bn_apply_train);
-  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
+        "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);
-  m.def("conv_dgrad_bn", &conv_dgrad_bn);
+  m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
+        "Tensor bn_x, Tensor bn_save, Tensor? bn_mask, bool relu, Tensor ws, Tensor? dgamma, Tensor? dbeta, "
+        "Tensor? addend_mask=None) -> (Tensor, Tensor)", &conv_dgrad_bn);
   m.def("bn_fwd_eval", &bn_fwd_eval);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd(Tensor g, Tensor x, Tensor? res, Tensor save, bool relu, Tensor slots, Tensor? dgamma, "
+        "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);
   m.def("softmax_xent", &softmax_xent);
   m.def("accuracy_count", &accuracy_count);
   m.def("gap_fwd", &gap_fwd);

@@ -33,6 +33,9 @@ _SINK = os.environ.get("TFX_NO_GRADSINK", "0") != "1"  # A/B switch for the fuse
 # A/B switch for the conv<->BN epilogue fusions: BN finalize in the producing conv's epilogue, BN
 # backward reduction in the consuming conv's data-gradient epilogue (igemm.hip EPI_STATS / EPI_BNB)
 _FUSE_BN = os.environ.get("TFX_FUSE_BN", "1") != "0"
+# A/B switch: identity blocks hand conv1 the residual BN's (gradient, ReLU mask) instead of the
+# masked gradient tensor (one full-size write less per block; igemm.hip masked addend)
+_MASKED_RES = os.environ.get("TFX_MASKED_RES", "1") != "0"
 
 
 class _BN:
@@ -96,6 +99,8 @@ class Bottleneck:
         # x feeds conv1 and the shortcut: the shortcut's input-gradient is folded into conv1's
         # dgrad epilogue (GradSink) instead of an autograd add kernel
         prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
+        if prod is not None and _MASKED_RES:
+            prod.accept_masked = True  # conv1 (1x1, stride 1) applies the residual ReLU mask itself
         # conv1 is x's last consumer in backward only when the GradSink carries the other branch
         o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons, fuse_input_bn_backward=cons is not None)
         o = self.b2.after_conv(self.c2, o, training, relu=True, fuse_input_bn_backward=True)
@@ -123,6 +128,8 @@ class Basic:
 
     def __call__(self, x, training):
         prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
+        if prod is not None and _MASKED_RES and self.c1.stride == 1:
+            prod.accept_masked = True
         o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons)
         if self.proj is None:
             return self.b2.after_conv(self.c2, o, training, relu=True, residual=x, residual_sink=prod)

@@ -99,13 +99,14 @@ class _Conv2d(torch.autograd.Function):
                         and x.numel() * x.element_size() <= _BNB_MAX_BYTES:
                     # dx is the complete gradient of the BN output x: the epilogue also reduces
                     # that BN's backward (sum g', sum g' xhat, dgamma, dbeta) -- see BNBackwardFusion
-                    add = sink.take() if sink is not None else None
+                    add, amask = _unpack_sink(sink.take()) if sink is not None else (None, None)
                     dx, bnb.red = torch.ops.tfx.conv_dgrad_bn(
                         gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
-                        bnb.ws, bnb.dgamma, bnb.dbeta)
+                        bnb.ws, bnb.dgamma, bnb.dbeta, amask)
                 elif sink is not None and sink.mode == "consume":
                     # last consumer of x in backward order: fold the other branch's gradient in
-                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, sink.take())
+                    add, amask = _unpack_sink(sink.take())
+                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, add, amask)
                 else:
                     dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, None)
                     if sink is not None:  # mode "produce": park it for the last consumer
@@ -136,19 +137,31 @@ def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int
     return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, ws, grad_sink if gpu else None, bnb)
 
 
+def _unpack_sink(item):
+    """A parked gradient is a tensor, or ``(g, mask)``: a residual BN's output gradient whose ReLU
+    mask the consumer applies in its epilogue (the masked copy is never written)."""
+    if isinstance(item, tuple):
+        return item
+    return item, None
+
+
 class GradSink:
     """Fuses the gradient sum of a tensor with two consumers (a ResNet block input feeds conv1 and
     the residual / projection branch).  The branch that runs FIRST in backward ("produce") parks
     its input-gradient here instead of returning it to autograd; the consumer that runs LAST
     ("consume", conv1's data-gradient) adds it in its GEMM epilogue -- no separate add kernel.
     Backward order is fixed by autograd's sequence numbers: conv1 is created first in the block,
-    so it runs last (the ``take`` assertion guards this)."""
+    so it runs last (the ``take`` assertion guards this).
+
+    ``accept_masked`` (set on the producer by a block whose consumer is a stride-1 conv): the
+    residual BN may park ``(g, relu_mask)`` instead of writing the masked gradient tensor."""
 
     def __init__(self, mode: str):
         assert mode in ("produce", "consume")
         self.mode = mode
         self.buf = None
         self.peer: Optional["GradSink"] = None
+        self.accept_masked = False
 
     @staticmethod
     def pair():
@@ -279,18 +292,24 @@ class _BatchNorm(torch.autograd.Function):
             if not training:
                 raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
             train_p = gamma is not None and gamma.trainable
+            gy = gy.contiguous()
+            # residual gradient g' = gy * relu_mask: when the sink's consumer applies the mask itself
+            # (stride-1 conv epilogue), park (gy, mask) and skip writing g' -- one full-size
+            # tensor write less per identity block
+            masked = ctx.has_res and ctx.res_sink is not None and mask is not None and \
+                getattr(ctx.res_sink, "accept_masked", False) and relu
             if ctx.bnb is not None and ctx.bnb.red is not None:
                 # the consumer conv's dgrad epilogue reduced this backward (and dgamma / dbeta)
-                dx, dres = torch.ops.tfx.bn_bwd_apply(gy.contiguous(), x, res, save, ctx.bnb.red, relu, mask)
+                dx, dres = torch.ops.tfx.bn_bwd_apply(gy, x, res, save, ctx.bnb.red, relu, mask, not masked)
                 ctx.bnb.red = None
             else:
-                dx, dres, red = torch.ops.tfx.bn_bwd(gy.contiguous(), x, res, save, relu, ctx.ws,
+                dx, dres, red = torch.ops.tfx.bn_bwd(gy, x, res, save, relu, ctx.ws,
                                                      gamma.grad if train_p else None,
-                                                     beta.grad if train_p else None, mask)
+                                                     beta.grad if train_p else None, mask, not masked)
             if train_p:
                 _grad_ready(gamma, beta)
             if ctx.has_res and ctx.res_sink is not None:
-                ctx.res_sink.put(dres)
+                ctx.res_sink.put((gy, mask) if masked else dres)
                 dres = None
             return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None, \
                 None, None, None

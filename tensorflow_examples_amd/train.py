@@ -15,6 +15,7 @@ import torch.distributed as dist
 from . import ops
 from .optim import Optimizer
 from .parallel.allreduce import GradAllReduce
+from .utils import trace
 from .variables import VariableStore
 
 
@@ -27,15 +28,20 @@ class ClassifierTrainer:
         self._static = None
 
     def _step(self, x, y):
+        # roctx ranges (TFX_ROCTX=1) label the phases on a rocprofv3 --marker-trace timeline
         self.store.zero_grad()
-        logits = self.model(x, training=True)
-        loss = ops.softmax_cross_entropy(logits, y, naive=self.naive)
-        loss.backward()
+        with trace.range("forward"):
+            logits = self.model(x, training=True)
+            loss = ops.softmax_cross_entropy(logits, y, naive=self.naive)
+        with trace.range("backward"):
+            loss.backward()
         scale = 1.0
         if self.dp is not None:
-            self.dp.finish()
+            with trace.range("allreduce_wait"):
+                self.dp.finish()
             scale = self.dp.grad_scale
-        self.opt.apply_gradients(grad_scale=scale)
+        with trace.range("optimizer"):
+            self.opt.apply_gradients(grad_scale=scale)
         return loss.detach()
 
     def step(self, x, y):

@@ -242,6 +242,53 @@ def test_conv_fwd_fused_bn_stats(gpu, shape):
     assert _rel(y1, y2) < 1e-3
 
 
+@pytest.mark.parametrize("shape", [(4, 8, 8, 64, 64, 1, 1, 0), (2, 8, 8, 64, 128, 3, 1, 1), (2, 9, 7, 256, 64, 1, 1, 0)])
+def test_conv_dgrad_masked_addend(gpu, shape):
+    """dX = dgrad(dY) + addend * relu_mask (the identity block's residual gradient consumed as
+    (gradient, mask bits) without materialising the masked tensor); the addend stays intact."""
+    N, H, W, C, Ko, R, st, pad = shape
+    torch.manual_seed(7)
+    w = _bf(torch.randn(Ko, R, R, C, device=gpu) * 0.1)
+    dy = _bf(torch.randn(N, H, W, Ko, device=gpu))
+    add = _bf(torch.randn(N, H, W, C, device=gpu))
+    keep = torch.rand(N, H, W, C, device=gpu) > 0.4
+    bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, device=gpu, dtype=torch.uint8)
+    mask = bits.sum(1, dtype=torch.int32).to(torch.uint8).contiguous()
+    add0 = add.clone()
+    ref = torch.ops.tfx.conv_dgrad(dy, w, [N, H, W, C], st, pad, 1, None).float() + add.float() * keep
+    dx = torch.ops.tfx.conv_dgrad(dy, w, [N, H, W, C], st, pad, 1, add, mask)
+    assert dx.data_ptr() != add.data_ptr() and torch.equal(add, add0)
+    assert _rel(dx, ref) < 1e-2
+    # the BN-backward-fused data gradient takes the same masked addend
+    xb = _bf(torch.randn(N, H, W, C, device=gpu))
+    gamma, beta = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
+    ws = torch.zeros(64 * 2 * C + 64, device=gpu)
+    _, save, _ = torch.ops.tfx.bn_fwd_train(xb, gamma, beta, None, None, 0.1, 1e-5, None, True, ws, False)
+    dx2, red = torch.ops.tfx.conv_dgrad_bn(dy, w, [N, H, W, C], st, pad, 1, add, xb, save, None, True, ws,
+                                           None, None, mask)
+    assert _rel(dx2, ref) < 1e-2 and torch.equal(add, add0)
+    _, _, red_ref = torch.ops.tfx.bn_bwd(dx2, xb, None, save, True, torch.zeros_like(ws), None, None, None)
+    assert _rel(red, red_ref) < 1e-3
+
+
+def test_bn_bwd_without_dres(gpu):
+    """want_dres=False: same dx / statistics, no residual-gradient tensor."""
+    torch.manual_seed(8)
+    M, C = 512, 64
+    x = _bf(torch.randn(M, C, device=gpu))
+    r = _bf(torch.randn(M, C, device=gpu))
+    g = _bf(torch.randn(M, C, device=gpu))
+    gamma, beta = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
+    ws = torch.zeros(64 * 2 * C, device=gpu)
+    y, save, mask = torch.ops.tfx.bn_fwd_train(x, gamma, beta, None, None, 0.1, 1e-5, r, True, ws, False)
+    dx1, dres1, red1 = torch.ops.tfx.bn_bwd(g, x, None, save, True, ws, None, None, mask)
+    dx2, dres2, red2 = torch.ops.tfx.bn_bwd(g, x, None, save, True, ws, None, None, mask, False)
+    assert dres1 is not None and dres2 is None
+    assert torch.equal(dx1, dx2) and torch.allclose(red1, red2, rtol=1e-5, atol=1e-5)
+    bx, bres = torch.ops.tfx.bn_bwd_apply(g, x, None, save, red1, True, mask, False)
+    assert bres is None and _rel(bx, dx1) < 1e-3
+
+
 FUSED_BN_SHAPES = [
     # N, H, W, C, Ko, R, stride, pad: 1x1 pointwise (dense loaders), 3x3 im2col, stride 2, ragged M
     (4, 8, 8, 64, 64, 1, 1, 0),
