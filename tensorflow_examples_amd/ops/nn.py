@@ -59,10 +59,11 @@ def _conv_ref(x, w, stride=1, pad=0, dil=1):
 
 
 # Largest BN input (bytes) whose backward reduction runs in the consumer conv's dgrad epilogue.
-# Above it the separate reduce kernel wins: the 128 MB block inputs of ResNet-50 stage 1 measured
-# 204 -> 229 us per dgrad + BN backward fused, while every <= 64 MB layer gains 2-8 us
-# (scripts/epi_bench.py, profiles/r01_v9).
-_BNB_MAX_BYTES = int(os.environ.get("TFX_BNB_MAX_MB", "64")) << 20
+# With the residual gradient materialised, the 128 MB block inputs of ResNet-50 stage 1 were slower
+# fused (204 -> 229 us, scripts/epi_bench.py, profiles/r01_v9) and the cap was 64 MB; since the
+# identity blocks pass (gradient, mask bits) instead, fusing them too is faster end to end
+# (9.46 -> 9.43 ms/step, TFX_BNB_MAX_MB A/B), so the default cap covers every ResNet-50 layer.
+_BNB_MAX_BYTES = int(os.environ.get("TFX_BNB_MAX_MB", "256")) << 20
 
 
 class _Conv2d(torch.autograd.Function):
