@@ -166,6 +166,11 @@ void lstm_cell_fwd(const float* gx, const float* gh, const float* bias, const fl
 void lstm_cell_bwd(const float* act, const float* c, const float* c_prev, const float* dh, const float* dc_next,
                    int B, int H, float* dgates, uint16_t* dg16, float* dc_prev, hipStream_t s);
 
+// ---------------------------------------------------------------- input pipeline
+// uint8 NHWC [npix][cin] (cin <= 4) -> bf16 NHWC [npix][cout] (cout 4 or 8): (x/255 - mean)/std, zero pad
+void image_normalize(const uint8_t* x, int64_t npix, int cin, int cout, const float* mean, const float* stdv,
+                     uint16_t* y, hipStream_t s);
+
 // ---------------------------------------------------------------- Philox4x32-10 init (dist 0 uniform [a,b),
 // 1 normal(a, b), 2 normal(a, b) truncated at 2 sigma)
 void philox_fill(float* out, int64_t n, uint64_t seed, uint64_t subseq, int dist, float a, float b, hipStream_t s);

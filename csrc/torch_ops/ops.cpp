@@ -782,9 +782,30 @@ void philox_fill(Tensor out, int64_t seed, int64_t subseq, int64_t dist, double 
                      (float)b, cur_stream());
 }
 
+// uint8 NHWC images -> normalised bf16 NHWC with cout channels (the extra ones exactly zero)
+Tensor image_normalize(Tensor x, std::vector<double> mean, std::vector<double> stdv, int64_t cout) {
+  CHECK_DEV(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.scalar_type() == at::kByte, "image_normalize: uint8 images");
+  const int64_t cin = x.size(-1);
+  TORCH_CHECK(cin >= 1 && cin <= 4 && (int64_t)mean.size() == cin && (int64_t)stdv.size() == cin,
+              "image_normalize: 1..4 channels with per-channel mean/std");
+  TORCH_CHECK(cout == 4 || cout == 8, "image_normalize: cout 4 or 8");
+  auto shape = x.sizes().vec();
+  shape.back() = cout;
+  auto y = at::empty(shape, x.options().dtype(at::kBFloat16));
+  float m[4] = {0, 0, 0, 0}, s[4] = {1, 1, 1, 1};
+  for (int64_t c = 0; c < cin; ++c) {
+    m[c] = (float)mean[c];
+    s[c] = (float)stdv[c];
+  }
+  tfx::image_normalize(x.data_ptr<uint8_t>(), x.numel() / cin, (int)cin, (int)cout, m, s, bfm(y), cur_stream());
+  return y;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tfx, m) {
+  m.def("image_normalize", &image_normalize);
   m.def("philox_fill", &philox_fill);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

@@ -18,6 +18,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from .. import ops
+from ..ops import _native
 from ..ops.nn import BNWorkspace
 from ..variables import Constant, HeNormal, VariableStore, Zeros
 
@@ -29,6 +30,8 @@ STAGES = {
     152: ("bottleneck", [3, 8, 36, 3]),
 }
 IN_CH_PAD = 8
+_MEAN = (0.4914, 0.4822, 0.4465)  # CIFAR-10 per-channel statistics
+_STD = (0.2470, 0.2435, 0.2616)
 _SINK = os.environ.get("TFX_NO_GRADSINK", "0") != "1"  # A/B switch for the fused residual-gradient sum
 # A/B switch for the conv<->BN epilogue fusions: BN finalize in the producing conv's epilogue, BN
 # backward reduction in the consuming conv's data-gradient epilogue (igemm.hip EPI_STATS / EPI_BNB)
@@ -183,12 +186,15 @@ def build_resnet_cifar(device="cuda", depth=50, num_classes=10, dtype=torch.bflo
 
 
 def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
-    """[N,32,32,3] images -> [N,32,32,8] normalised NHWC compute tensor (channels 3..7 zero)."""
+    """[N,32,32,3] images -> [N,32,32,8] normalised NHWC compute tensor (channels 3..7 zero).
+    GPU uint8 input: one fused HIP kernel (csrc/kernels/image.hip)."""
     x = images_nhwc_u8_or_f
+    if x.dtype == torch.uint8 and dtype == torch.bfloat16 and x.device.type == "cuda" and _native.use_native(x):
+        return torch.ops.tfx.image_normalize(x.contiguous(), list(_MEAN), list(_STD), IN_CH_PAD)
     if x.dtype == torch.uint8:
         x = x.float() / 255.0
-    mean = torch.tensor([0.4914, 0.4822, 0.4465], device=x.device)
-    std = torch.tensor([0.2470, 0.2435, 0.2616], device=x.device)
+    mean = torch.tensor(_MEAN, device=x.device)
+    std = torch.tensor(_STD, device=x.device)
     x = (x - mean) / std
     out = torch.zeros(*x.shape[:-1], IN_CH_PAD, device=x.device, dtype=dtype)
     out[..., :3] = x.to(dtype)

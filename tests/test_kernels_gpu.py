@@ -271,6 +271,17 @@ def test_conv_dgrad_masked_addend(gpu, shape):
     assert _rel(red, red_ref) < 1e-3
 
 
+def test_image_normalize_matches_reference(gpu):
+    """Fused input kernel == the PyTorch formulation of to_model_input (padded channels exactly 0)."""
+    from tensorflow_examples_amd.models.resnet import to_model_input
+    img = torch.randint(0, 256, (5, 32, 32, 3), dtype=torch.uint8)
+    ref = to_model_input(img)  # CPU path
+    out = to_model_input(img.to(gpu))
+    assert out.shape == (5, 32, 32, 8) and out.dtype == torch.bfloat16
+    assert torch.equal(out[..., 3:].cpu(), torch.zeros(5, 32, 32, 5, dtype=torch.bfloat16))
+    assert (out.float().cpu() - ref.float()).abs().max().item() <= 0.02
+
+
 def test_bn_bwd_without_dres(gpu):
     """want_dres=False: same dx / statistics, no residual-gradient tensor."""
     torch.manual_seed(8)
