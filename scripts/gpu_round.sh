@@ -64,6 +64,14 @@ for s in $STEPS; do
         TFX_WGRAD_TILE=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/abwg_${v}_$i.log 2>&1 || exit 1
       done; done
       tail -1 gpurun_out/conv_bench_wg*.log; grep -o '"ms_per_step": [0-9.]*' gpurun_out/abwg_*.log ;;
+    dpgraph)
+      timeout -k 10 400 python -m pytest tests/test_dp_gpu.py -x -q -p no:cacheprovider -k graph > gpurun_out/pytest_dpgraph.log 2>&1
+      rc=$?; echo "dpgraph test rc=$rc"; tail -5 gpurun_out/pytest_dpgraph.log; [ $rc -eq 0 ] || exit $rc
+      for v in 1 0; do
+        TFX_DP_FORCE_COLLECTIVE=1 TFX_DP_GRAPH=$v timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 29517 bench.py --steps 30 --warmup 5 > gpurun_out/bench_dpforce_g$v.log 2>&1
+        rc=$?; echo "dpforce graph=$v rc=$rc"; tail -2 gpurun_out/bench_dpforce_g$v.log; [ $rc -eq 0 ] || exit $rc
+      done ;;
     kerneltests)
       timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py tests/test_resnet_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_kernels.log 2>&1
       rc=$?; echo "kerneltests rc=$rc"; tail -5 gpurun_out/pytest_kernels.log

@@ -24,6 +24,7 @@ north-star RCCL path of BASELINE.json (configs 3 and 5).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -34,10 +35,15 @@ from ..variables import Variable, VariableStore
 
 class GradAllReduce:
     def __init__(self, store: VariableStore, bucket_bytes: int = 32 << 20, group=None, overlap: bool = True,
-                 compress_bf16: bool = False, tail_bytes: int = 2 << 20):
+                 compress_bf16: bool = False, tail_bytes: int = 2 << 20, force_collective: Optional[bool] = None):
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # issue the collectives even at world size 1 (TFX_DP_FORCE_COLLECTIVE=1): lets a one-GPU box
+        # exercise the RCCL launch / HIP-graph capture path of the DP step
+        if force_collective is None:
+            force_collective = os.environ.get("TFX_DP_FORCE_COLLECTIVE", "0") == "1"
+        self.force = bool(force_collective) and dist.is_initialized()
         self.overlap = overlap
         self.compress = compress_bf16
         elem = store.grad.element_size()
@@ -76,7 +82,7 @@ class GradAllReduce:
         self._pending: List[int] = []
         self._launched: List[bool] = []
         self._works = []
-        if overlap and self.world > 1:
+        if overlap and (self.world > 1 or self.force):
             store.grad_ready_hook = self._on_ready
         self.start_step()
 
@@ -108,7 +114,7 @@ class GradAllReduce:
             self._launch(b)
 
     def _launch(self, b: int) -> None:
-        if self._launched[b] or self.world == 1:
+        if self._launched[b] or (self.world == 1 and not self.force):
             self._launched[b] = True
             return
         self._launched[b] = True

@@ -32,7 +32,10 @@ def init_distributed(backend: str | None = None, device: str = "cuda", timeout_s
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    if ws > 1 and not dist.is_initialized():
+    # TFX_DP_FORCE_COLLECTIVE=1 under a launcher: a 1-rank process group, so a one-GPU box runs the
+    # real RCCL path of the DP step (GradAllReduce issues its collectives at world size 1 too)
+    force = os.environ.get("TFX_DP_FORCE_COLLECTIVE", "0") == "1" and "RANK" in os.environ
+    if (ws > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         backend = backend or ("nccl" if dev.type == "cuda" else "gloo")

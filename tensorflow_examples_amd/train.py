@@ -53,9 +53,15 @@ class ClassifierTrainer:
         return self._step(x, y)
 
     def capture(self, x, y, warmup: int = 3):
-        """Capture one training step into a HIP graph (single-process only)."""
-        if dist.is_initialized() and dist.get_world_size() > 1:
-            raise RuntimeError("graph capture of the DP step is not supported; use eager DP")
+        """Capture one training step into a HIP graph.
+
+        With a ``GradAllReduce`` the bucketed RCCL all-reduces are captured too: the grad-ready
+        hooks fire during the captured backward, so every bucket becomes a collective node on
+        RCCL's stream that forks from the compute stream where its last gradient is written and
+        joins before the optimizer -- the same overlap as eager, replayed without Python or
+        per-kernel launches.  Capture runs in thread-local mode so the process group's watchdog
+        thread (which polls events of earlier eager collectives) cannot invalidate it.  All ranks
+        must capture: the collectives are recorded, not executed, and run at replay time."""
         sx, sy = x.clone(), y.clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -64,7 +70,8 @@ class ClassifierTrainer:
                 self._step(sx, sy)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        mode = "thread_local" if self.dp is not None else "global"
+        with torch.cuda.graph(g, capture_error_mode=mode):
             loss = self._step(sx, sy)
         self.graph = g
         self._static = (sx, sy, loss)

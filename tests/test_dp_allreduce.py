@@ -70,3 +70,16 @@ def test_dp_matches_single_process_full_batch():
         ((l0 + l1) / 2).backward()
         opt.apply_gradients()
     assert torch.allclose(st.master, p0, atol=1e-5, rtol=1e-5)
+
+
+def test_force_collective_flag_without_process_group():
+    """TFX_DP_FORCE_COLLECTIVE only takes effect with an initialised process group."""
+    import torch
+    from tensorflow_examples_amd.parallel import GradAllReduce
+    from tensorflow_examples_amd.variables import VariableStore, Zeros
+    store = VariableStore(device="cpu", compute_dtype=torch.float32, seed=0)
+    store.variable([4], Zeros(), name="a")
+    store.finalize()
+    dp = GradAllReduce(store, force_collective=True)
+    assert not dp.force and dp.world == 1
+    dp.finish()  # no collectives issued, no error
