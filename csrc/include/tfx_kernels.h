@@ -171,6 +171,16 @@ void lstm_cell_bwd(const float* act, const float* c, const float* c_prev, const 
 void image_normalize(const uint8_t* x, int64_t npix, int cin, int cout, const float* mean, const float* stdv,
                      uint16_t* y, hipStream_t s);
 
+// ---------------------------------------------------------------- ps transport over xGMI peer memory
+// p -= lr*g on a (peer-mapped) arena range; if step != null, atomically bump the 64-bit global
+// step there and write the new value to step_out (worker-local).  IPC helpers return 0 / -hipError.
+void ps_peer_sgd(float* p, const float* g, int64_t n, float lr, void* step, int64_t* step_out, hipStream_t s);
+int ipc_alloc(int device, int64_t nbytes, void** ptr);
+int ipc_free(int device, void* ptr);
+int ipc_get_handle(void* ptr, uint8_t* out64);
+int ipc_open(int device, const uint8_t* handle64, void** ptr);
+int ipc_close(void* ptr);
+
 // ---------------------------------------------------------------- Philox4x32-10 init (dist 0 uniform [a,b),
 // 1 normal(a, b), 2 normal(a, b) truncated at 2 sigma)
 void philox_fill(float* out, int64_t n, uint64_t seed, uint64_t subseq, int dist, float a, float b, hipStream_t s);

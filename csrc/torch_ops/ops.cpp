@@ -592,6 +592,55 @@ void cast_f32_bf16(Tensor x, Tensor y) {
   tfx::cast_f32_bf16(x.data_ptr<float>(), x.numel(), bfm(y), cur_stream());
 }
 
+// ------------------------------------------------------------------ ps transport over xGMI peer memory
+// The arena is a raw hipMalloc allocation (IPC needs an allocation base, which the caching
+// allocator does not hand out); the returned uint8 tensor owns it and frees it on release.
+Tensor ipc_arena_alloc(int64_t nbytes, int64_t device) {
+  TORCH_CHECK(nbytes > 0 && nbytes % 256 == 0, "arena size must be a positive multiple of 256");
+  void* p = nullptr;
+  const int r = tfx::ipc_alloc((int)device, nbytes, &p);
+  TORCH_CHECK(r == 0, "hipMalloc of the ps arena failed (", r, ")");
+  const int dev = (int)device;
+  return at::from_blob(p, {nbytes}, [dev](void* q) { tfx::ipc_free(dev, q); },
+                       at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
+}
+
+Tensor ipc_handle(Tensor arena) {
+  CHECK_DEV(arena);
+  auto out = at::zeros({64}, at::TensorOptions().dtype(at::kByte));
+  const int r = tfx::ipc_get_handle(arena.data_ptr(), out.data_ptr<uint8_t>());
+  TORCH_CHECK(r > 0, "hipIpcGetMemHandle failed (", r, "): the arena must come from ipc_arena_alloc");
+  return out;
+}
+
+Tensor ipc_open(Tensor handle, int64_t nbytes, int64_t device) {
+  TORCH_CHECK(!handle.is_cuda() && handle.scalar_type() == at::kByte && handle.numel() == 64, "64-byte host handle");
+  auto h = handle.contiguous();
+  void* p = nullptr;
+  const int r = tfx::ipc_open((int)device, h.data_ptr<uint8_t>(), &p);
+  TORCH_CHECK(r == 0, "hipIpcOpenMemHandle failed (", r, ")");
+  return at::from_blob(p, {nbytes}, [](void* q) { tfx::ipc_close(q); },
+                       at::TensorOptions().dtype(at::kByte).device(at::kCUDA, (int)device));
+}
+
+// p, g: f32 ranges of equal length (p may be peer-mapped); step: int64 [1] view in the arena
+// header or None; step_out: int64 [1] worker-local, receives the new global step.
+void ps_peer_sgd(Tensor p, Tensor g, double lr, optional<Tensor> step, Tensor step_out) {
+  CHECK_DEV(p); CHECK_DEV(g); CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
+  TORCH_CHECK(p.numel() == g.numel(), "ps_peer_sgd: range sizes differ");
+  CHECK_DEV(step_out);
+  TORCH_CHECK(step_out.scalar_type() == at::kLong && step_out.numel() >= 1, "step_out must be int64");
+  void* sp = nullptr;
+  if (step.has_value() && step->defined()) {
+    CHECK_DEV(*step);
+    TORCH_CHECK(step->scalar_type() == at::kLong && reinterpret_cast<uintptr_t>(step->data_ptr()) % 8 == 0,
+                "step must be an aligned int64 view");
+    sp = step->data_ptr();
+  }
+  tfx::ps_peer_sgd(p.data_ptr<float>(), g.data_ptr<float>(), p.numel(), (float)lr, sp,
+                   step_out.data_ptr<int64_t>(), cur_stream());
+}
+
 // ------------------------------------------------------------------ pooling (NHWC bf16)
 int64_t pool_out(int64_t H, int64_t k, int64_t s, int64_t pad) { return (H + 2 * pad - k) / s + 1; }
 
@@ -846,4 +895,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("optimizer_apply", &optimizer_apply);
   m.def("sumsq", &sumsq);
   m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("ipc_arena_alloc", &ipc_arena_alloc);
+  m.def("ipc_handle", &ipc_handle);
+  m.def("ipc_open", &ipc_open);
+  m.def("ps_peer_sgd", &ps_peer_sgd);
 }
