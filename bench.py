@@ -2,17 +2,27 @@
 """Headline benchmark: ResNet-50 / CIFAR-10 bf16 training throughput (images/sec, whole job).
 
 BASELINE.json metric: "images/sec (whole node) ResNet-50/CIFAR-10 bf16 at 1/2/4/8 MI355X".
-One process per GPU (torchrun contract: RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), RCCL
-bucketed all-reduce overlapped with backward, fused momentum-SGD on the flat master
-buffer.  Weak scaling: ``--batch`` images per GPU, global batch = batch * N.
-Synthetic CIFAR-shaped data (uint8 32x32x3 images + int64 labels generated on device,
-normalised per step), random-init weights: there is no dataset or network on the box.
+One process per GPU, RCCL bucketed all-reduce overlapped with backward, fused momentum-SGD on the
+flat master buffer.  Weak scaling: ``--batch`` images per GPU, global batch = batch * N.
+Synthetic CIFAR-shaped data (uint8 32x32x3 images + int64 labels), random-init weights: there is
+no dataset or network on the box.
 
-Timing: W untimed warmup steps; barrier + synchronize; K timed steps; barrier +
-synchronize; the MAX elapsed over ranks is reported.  Rank 0 prints ONE JSON line.
+Launch modes (the process-per-task model of R/distributed/distributed.py:7-14,37-43):
+* ``python bench.py --gpus N`` with no RANK in the environment: this process is only a launcher --
+  it never touches the GPU, spawns N fresh ranks of itself (parallel/launch.py ``spawn_local``,
+  rendezvous on 127.0.0.1), relays rank 0's JSON line and exits non-zero if any rank fails;
+* under ``torch.distributed.run`` (or our launcher) every rank runs the step; each checks that the
+  process group spans exactly ``--gpus`` ranks (size + an all-reduce of ones) before timing, and
+  ``n_gpus`` in the JSON is that verified world size.
 
-``--impl torch`` runs a stock PyTorch-ROCm eager ResNet-50 (torch.nn + MIOpen,
-channels_last, bf16 autocast) for a labelled comparison; the headline is ``--impl native``.
+Timing: W untimed warmup steps; barrier + synchronize; K timed steps; barrier + synchronize; the
+MAX elapsed over ranks is reported.  Rank 0 prints ONE JSON line.
+
+``--host-input``: batches live in pinned host memory and every step copies its batch H2D through
+the framework's pinned ring (data/pipeline.py) on a side stream -- the tf.data/feed_dict path.
+``--impl torch`` runs a stock PyTorch-ROCm eager ResNet-50 (torch.nn + MIOpen, channels_last, bf16
+autocast) for a labelled comparison; the headline is ``--impl native``.
+``--device cpu`` runs the same step on the CPU reference ops over gloo (tests of the launch path).
 """
 from __future__ import annotations
 
@@ -22,15 +32,8 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
-from tensorflow_examples_amd.optim import MomentumOptimizer  # noqa: E402
-from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed  # noqa: E402
-from tensorflow_examples_amd.train import ClassifierTrainer  # noqa: E402
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 METRIC = "images/sec (whole node) ResNet-50/CIFAR-10 bf16 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no number for this metric
@@ -38,61 +41,95 @@ BASELINE_VALUE = None  # the reference publishes no number for this
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU) of the job")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="capture the whole step in a HIP graph and replay it (default on for N=1; for N>1 "
                          "TFX_DP_GRAPH=1 also captures the RCCL all-reduces -- measured on a 1-rank "
                          "RCCL group: 9.26 graph vs 9.34 ms eager, so N>1 stays eager by default)")
     ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager step launches")
+    ap.add_argument("--host-input", action="store_true",
+                    help="pinned-host batches copied H2D every step through the pinned ring")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
-    ap.add_argument("--backend", default=None, help="process-group backend (default nccl = RCCL)")
+    ap.add_argument("--backend", default=None, help="process-group backend (default nccl = RCCL, gloo on cpu)")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="launcher mode: seconds before the whole job is killed")
     return ap.parse_args(argv)
 
 
-def synthetic_batches(n, batch, device, seed):
+def synthetic_batches(n, batch, seed):
+    import torch
     g = torch.Generator(device="cpu").manual_seed(seed)
     out = []
     for _ in range(n):
         img = torch.randint(0, 256, (batch, 32, 32, 3), dtype=torch.uint8, generator=g)
         lab = torch.randint(0, 10, (batch,), dtype=torch.long, generator=g)
-        out.append((img.to(device), lab.to(device)))
+        out.append((img, lab))
     return out
 
 
-def main(argv=None):
-    a = parse(argv)
-    dev = init_distributed(backend=a.backend, device="cuda")
+def run(a):
+    import torch
+    import torch.distributed as dist
+
+    from tensorflow_examples_amd.data.pipeline import PinnedRing
+    from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
+    from tensorflow_examples_amd.optim import MomentumOptimizer
+    from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed
+    from tensorflow_examples_amd.parallel.launch import verify_world
+    from tensorflow_examples_amd.train import ClassifierTrainer
+
+    cuda = a.device == "cuda"
+    dev = init_distributed(backend=a.backend, device=a.device)
     world = dist.get_world_size() if dist.is_initialized() else 1
     forced = dist.is_initialized() and world == 1  # TFX_DP_FORCE_COLLECTIVE rehearsal of the RCCL path
+    if "RANK" in os.environ or a.gpus > 1:
+        verify_world(a.gpus if not forced else 1, dev)
     rank = dist.get_rank() if dist.is_initialized() else 0
     torch.manual_seed(1234 + rank)
-    data = synthetic_batches(a.nbatches, a.batch, dev, seed=1000 + rank)
+    host = synthetic_batches(a.nbatches, a.batch, seed=1000 + rank)
+    dtype = torch.bfloat16 if cuda else torch.float32
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    ring = None
+    if a.host_input and cuda:
+        ring = PinnedRing.for_batches(host, dev, depth=2)
+        data = None
+    else:
+        data = [(img.to(dev), lab.to(dev)) for img, lab in host]
+
+    def batch(i):
+        if ring is not None:
+            return ring.get(i % len(host))
+        return data[i % len(data)]
 
     graphed = False
     if a.impl == "native":
-        store, model = build_resnet_cifar(device=dev, depth=a.depth, dtype=torch.bfloat16, seed=0)
+        store, model = build_resnet_cifar(device=dev, depth=a.depth, dtype=dtype, seed=0)
         broadcast_variables(store)
         opt = MomentumOptimizer(store, a.lr, momentum=0.9, weight_decay=5e-4)
         dp = GradAllReduce(store, bucket_bytes=int(a.bucket_mb * (1 << 20))) if dist.is_initialized() else None
         trainer = ClassifierTrainer(store, model, opt, dp)
 
         def step(i):
-            img, lab = data[i % len(data)]
-            return trainer.step(to_model_input(img), lab)
+            img, lab = batch(i)
+            return trainer.step(to_model_input(img, dtype=dtype), lab)
 
-        graphed = False
-        if a.graph and ((world == 1 and not forced) or os.environ.get("TFX_DP_GRAPH", "0") == "1"):
+        if cuda and a.graph and ((world == 1 and not forced) or os.environ.get("TFX_DP_GRAPH", "0") == "1"):
             # the captured step is the same work (forward, backward with the bucketed RCCL
             # all-reduces, fused optimizer) replayed with one launch; the per-step input batch is
             # copied into the graph's static input
-            img, lab = data[0]
+            img, lab = batch(0)
             try:
                 trainer.capture(to_model_input(img), lab)
                 graphed = True
@@ -113,7 +150,7 @@ def main(argv=None):
         from tensorflow_examples_amd.models.torch_baseline import TorchResNet50Cifar
         net = TorchResNet50Cifar().to(dev).to(memory_format=torch.channels_last)
         if world > 1:
-            net = torch.nn.parallel.DistributedDataParallel(net, device_ids=[dev.index],
+            net = torch.nn.parallel.DistributedDataParallel(net, device_ids=[dev.index] if cuda else None,
                                                             bucket_cap_mb=a.bucket_mb)
         topt = torch.optim.SGD(net.parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-4, foreach=True)
         mean = torch.tensor([0.4914, 0.4822, 0.4465], device=dev).view(1, 3, 1, 1)
@@ -121,10 +158,10 @@ def main(argv=None):
         nparams = sum(p.numel() for p in net.parameters())
 
         def step(i):
-            img, lab = data[i % len(data)]
+            img, lab = batch(i)
             x = ((img.permute(0, 3, 1, 2).float() / 255.0 - mean) / std).contiguous(memory_format=torch.channels_last)
             topt.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast(dev.type, dtype=torch.bfloat16):
                 loss = torch.nn.functional.cross_entropy(net(x), lab)
             loss.backward()
             topt.step()
@@ -132,17 +169,17 @@ def main(argv=None):
 
     for i in range(a.warmup):
         loss = step(i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -163,8 +200,10 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
-            "dtype": "bf16",
-            "data": "synthetic (CIFAR-10-shaped uint8 32x32x3 images, random labels, random-init weights)",
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic (CIFAR-10-shaped uint8 32x32x3 images, random labels, random-init weights)"
+                    + ("; pinned-host batches copied H2D every step" if ring is not None else
+                       "; batches resident on the device"),
             "config": {
                 "model": "ResNet-%d (CIFAR-10 adaptation: 3x3 stem, bottleneck [3,4,6,3])" % a.depth,
                 "global_batch": a.batch * world,
@@ -172,18 +211,34 @@ def main(argv=None):
                 "seq_len": None,
                 "image_hw": [32, 32],
                 "parallelism": "dp%d" % world,
+                "device": a.device,
+                "backend": dist.get_backend() if dist.is_initialized() else None,
                 "impl": a.impl,
                 "optimizer": "momentum-SGD 0.9, wd 5e-4 (fused flat-buffer kernel)" if a.impl == "native" else "torch.optim.SGD foreach",
                 "allreduce_bucket_mb": a.bucket_mb,
                 "hip_graph": bool(a.impl == "native" and graphed),
+                "host_input": ring is not None,
                 "params": nparams,
                 "final_loss": round(final_loss, 4),
             },
         }
         print(json.dumps(rec), flush=True)
+    if ring is not None:
+        ring.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 
 
+def main(argv=None):
+    a = parse(argv)
+    from tensorflow_examples_amd.parallel.launch import under_launcher, spawn_local
+    if a.gpus > 1 and not under_launcher():
+        # launcher mode: this process never initialises the GPU; the ranks are fresh processes
+        args = list(sys.argv[1:] if argv is None else argv)
+        return spawn_local(a.gpus, [os.path.abspath(__file__), *args], timeout_s=a.launch_timeout)
+    run(a)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

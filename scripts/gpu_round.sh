@@ -104,6 +104,24 @@ for s in $STEPS; do
         rc=$?; echo "$spec rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_models_err.log; [ $rc -eq 1 ] || exit $rc; }
       done
       cat gpurun_out/bench_models.jsonl ;;
+    hostin)
+      for i in 1 2; do
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_dev_$i.log 2>&1 || exit 1
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 --host-input > gpurun_out/bench_hostin_$i.log 2>&1 || exit 1
+      done
+      grep -ho '"ms_per_step": [0-9.]*' gpurun_out/bench_dev_*.log gpurun_out/bench_hostin_*.log ;;
+    pmcbench)
+      # PMC passes over a short eager bench (each pass its own run; <= 8 SQ, 4 TCC, 2 GRBM counters)
+      export TMPDIR=/tmp
+      i=0
+      for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" \
+                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM TCC_HIT_sum TCC_MISS_sum" \
+                 "FETCH_SIZE" "WRITE_SIZE"; do
+        i=$((i+1))
+        timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$R/gpurun_out/pmc/p$i" -o p -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-graph > gpurun_out/pmc_p$i.log 2>&1
+        rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_p$i.log; exit $rc; }
+      done
+      python scripts/pmc_summary.py gpurun_out/pmc --steps 3 > gpurun_out/pmc_summary.txt; head -45 gpurun_out/pmc_summary.txt ;;
     prof)
       export TMPDIR=/tmp
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 2 > gpurun_out/prof.log 2>&1

@@ -1,19 +1,31 @@
-"""Host -> HBM input pipeline: pinned host staging + async copies on a side HIP stream,
-double-buffered (the tf.data ``prefetch_to_device`` of the north star).
+"""Host -> HBM input pipeline: a fixed ring of pinned host staging slots + async H2D copies on a
+side HIP stream (the north star's "pinned-host hipMemcpyAsync double-buffering"; it replaces
+TF1's per-step ``feed_dict`` conversion, R/distributed/distributed.py:146-150).
+
+    ring = PinnedRing(device, depth=2)
+    slot = ring.stage((x_np, y_np))      # host copy into a pinned slot, async H2D on the copy stream
+    x, y = ring.acquire(slot)            # compute stream waits on that copy's event only
 
     for x, y in DevicePrefetcher(batches, device, depth=2):
-        ...  # x, y are already resident in HBM; the next batch is in flight
+        ...  # x, y already resident in HBM; the next `depth` batches are in flight
 
-Each host batch (numpy or CPU tensors) is copied into a page-locked staging buffer, then a
-non-blocking copy is enqueued on a dedicated copy stream; the consumer's compute stream waits
-on that copy's event only when it takes the batch, so the DMA engine overlaps the H2D transfer
-with the previous step's kernels.  Tensors handed out are recorded on the consumer stream so the
-caching allocator never recycles them while a kernel still reads them.
+Every slot owns, for each field, one page-locked host buffer and one device buffer, allocated once
+(re-allocated only if a batch's shape changes, e.g. a ragged last batch) -- no per-batch
+``pin_memory()`` or device allocation.  Two events per slot order the reuse:
+
+* ``h2d``: recorded on the copy stream after the slot's async copy.  The compute stream waits on it
+  in :meth:`acquire`; the host waits on it (normally long since complete) before it overwrites the
+  slot's pinned buffer with a later batch.
+* ``free``: recorded on the compute stream when the consumer asks for its NEXT batch (every kernel
+  that read this slot's device tensors has been enqueued by then).  The copy stream waits on it
+  before it overwrites the slot's device buffer -- a device-side dependency, no host sync.
+
+So a tensor handed out by :meth:`acquire` stays valid until the consumer has acquired ``depth``
+more batches.  On the CPU (no GPU) the ring degenerates to plain tensors.
 """
 from __future__ import annotations
 
-import collections
-from typing import Iterable, Iterator, Sequence
+from typing import Iterable, Iterator, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -25,51 +37,151 @@ def _to_tensor(a):
     return torch.from_numpy(np.ascontiguousarray(a))
 
 
+class _Slot:
+    __slots__ = ("host", "dev", "h2d", "free", "h2d_pending", "free_pending")
+
+    def __init__(self):
+        self.host: List[torch.Tensor] = []
+        self.dev: List[torch.Tensor] = []
+        self.h2d = None
+        self.free = None
+        self.h2d_pending = False
+        self.free_pending = False
+
+
+class PinnedRing:
+    def __init__(self, device, depth: int = 2):
+        self.device = torch.device(device)
+        self.gpu = self.device.type == "cuda"
+        # depth batches in flight + the one being consumed
+        self.nslots = max(1, depth) + 1
+        self.slots = [_Slot() for _ in range(self.nslots)]
+        self.stream = torch.cuda.Stream(self.device) if self.gpu else None
+        self._next = 0
+        self._held: Optional[int] = None
+        if self.gpu:
+            for s in self.slots:
+                s.h2d = torch.cuda.Event()
+                s.free = torch.cuda.Event()
+
+    def _ensure(self, s: _Slot, items: Sequence[torch.Tensor]) -> None:
+        same = len(s.host) == len(items) and all(
+            h.shape == t.shape and h.dtype == t.dtype for h, t in zip(s.host, items))
+        if same:
+            return
+        # (re)allocate once: every earlier use of the old buffers must have finished
+        if s.h2d_pending:
+            s.h2d.synchronize()
+        if s.free_pending:
+            s.free.synchronize()
+        s.host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in items]
+        s.dev = [torch.empty(t.shape, dtype=t.dtype, device=self.device) for t in items]
+
+    def stage(self, batch) -> int:
+        """Copy one host batch (tuple of arrays/CPU tensors) into the next slot and start its async
+        H2D copy.  Returns the slot id to :meth:`acquire`."""
+        items = [_to_tensor(a) for a in (batch if isinstance(batch, (tuple, list)) else (batch,))]
+        k = self._next
+        self._next = (k + 1) % self.nslots
+        s = self.slots[k]
+        if not self.gpu:
+            s.dev = items
+            return k
+        if k == self._held:
+            raise RuntimeError("PinnedRing: staging over the slot still held by the consumer (too many in flight)")
+        self._ensure(s, items)
+        if s.h2d_pending:  # the previous copy out of this pinned buffer must have been read
+            s.h2d.synchronize()
+        for h, t in zip(s.host, items):
+            h.copy_(t)
+        with torch.cuda.stream(self.stream):
+            if s.free_pending:  # the consumer's kernels on the old device contents are enqueued first
+                self.stream.wait_event(s.free)
+            for d, h in zip(s.dev, s.host):
+                d.copy_(h, non_blocking=True)
+            s.h2d.record(self.stream)
+        s.h2d_pending = True
+        return k
+
+    def acquire(self, k: int):
+        """Device tensors of slot ``k``; the current stream waits for their copy.  The slot acquired
+        before this one is released (its ``free`` event recorded on the current stream)."""
+        s = self.slots[k]
+        if self.gpu:
+            cur = torch.cuda.current_stream(self.device)
+            if self._held is not None and self._held != k:
+                h = self.slots[self._held]
+                h.free.record(cur)
+                h.free_pending = True
+            cur.wait_event(s.h2d)
+        self._held = k
+        return tuple(s.dev)
+
+    @classmethod
+    def for_batches(cls, host_batches: Sequence, device, depth: int = 2) -> "CyclicFeeder":
+        return CyclicFeeder(host_batches, cls(device, depth), depth)
+
+    def close(self) -> None:
+        if self.gpu:
+            self.stream.synchronize()
+        self.slots = []
+
+
+class CyclicFeeder:
+    """Feeds a fixed list of host batches round-robin through a :class:`PinnedRing`, ``depth``
+    batches ahead of the consumer (bench.py ``--host-input``): ``get(i)`` returns batch
+    ``i % len(host_batches)`` on the device, its copy issued ``depth`` steps earlier."""
+
+    def __init__(self, host_batches: Sequence, ring: PinnedRing, depth: int):
+        self.host, self.ring, self.depth = list(host_batches), ring, max(1, depth)
+        self._staged: dict = {}
+        self._i = 0
+
+    def _stage_upto(self, i: int) -> None:
+        while self._i <= i:
+            self._staged[self._i] = self.ring.stage(self.host[self._i % len(self.host)])
+            self._i += 1
+
+    def get(self, i: int):
+        self._stage_upto(i)
+        k = self._staged.pop(i)
+        out = self.ring.acquire(k)
+        self._stage_upto(i + self.depth)
+        return out
+
+    def close(self) -> None:
+        self.ring.close()
+
+
 class DevicePrefetcher:
+    """Iterate host batches as device tensors, ``depth`` batches ahead (tf.data prefetch_to_device)."""
+
     def __init__(self, source: Iterable, device, depth: int = 2):
         self.source = source
-        self.device = torch.device(device)
+        self.ring = PinnedRing(device, depth)
         self.depth = max(1, depth)
-        self.gpu = self.device.type == "cuda"
-        self.stream = torch.cuda.Stream(self.device) if self.gpu else None
-
-    def _stage(self, batch):
-        items = batch if isinstance(batch, (tuple, list)) else (batch,)
-        out = []
-        for a in items:
-            t = _to_tensor(a)
-            if not self.gpu:
-                out.append(t)
-                continue
-            pinned = t.pin_memory() if not t.is_pinned() else t
-            with torch.cuda.stream(self.stream):
-                out.append(pinned.to(self.device, non_blocking=True))
-        ev = None
-        if self.gpu:
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-        return out, ev, not isinstance(batch, (tuple, list))
 
     def __iter__(self) -> Iterator:
         it = iter(self.source)
-        q = collections.deque()
+        q: List[tuple] = []
+        single = False
         for _ in range(self.depth):
             try:
-                q.append(self._stage(next(it)))
+                b = next(it)
             except StopIteration:
                 break
+            single = not isinstance(b, (tuple, list))
+            q.append(self.ring.stage(b))
         while q:
-            out, ev, single = q.popleft()
-            if ev is not None:
-                cur = torch.cuda.current_stream(self.device)
-                cur.wait_event(ev)
-                for t in out:
-                    t.record_stream(cur)
+            k = q.pop(0)
+            out = self.ring.acquire(k)
             try:
-                q.append(self._stage(next(it)))
+                b = next(it)
+                single = not isinstance(b, (tuple, list))
+                q.append(self.ring.stage(b))
             except StopIteration:
                 pass
-            yield out[0] if single else tuple(out)
+            yield out[0] if single else out
 
 
 def batches(arrays: Sequence[np.ndarray], batch_size: int, shuffle: bool = True, seed: int = 0,

@@ -35,9 +35,15 @@ from ..variables import Variable, VariableStore
 
 class GradAllReduce:
     def __init__(self, store: VariableStore, bucket_bytes: int = 32 << 20, group=None, overlap: bool = True,
-                 compress_bf16: bool = False, tail_bytes: int = 2 << 20, force_collective: Optional[bool] = None):
+                 compress_bf16: bool = False, tail_bytes: int = 2 << 20, force_collective: Optional[bool] = None,
+                 premul: Optional[float] = None):
         self.store = store
         self.group = group
+        # premul: RCCL pre-multiplied sum (each rank's bucket scaled by `premul` inside the
+        # collective).  Used by the GPU tests to make a 1-rank collective observable: a bucket whose
+        # all-reduce was dropped, or ran before its gradient was written, then shows up as a wrong
+        # (unscaled) gradient.
+        self.premul = premul
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         # issue the collectives even at world size 1 (TFX_DP_FORCE_COLLECTIVE=1): lets a one-GPU box
         # exercise the RCCL launch / HIP-graph capture path of the DP step
@@ -105,6 +111,12 @@ class GradAllReduce:
         self._launched = [False] * len(self.buckets)
         self._works = []
 
+    def reset(self) -> None:
+        """Abandon a step that failed part-way through backward (e.g. a HIP-graph capture error):
+        its queued Work objects may be captured, never-executed collectives, so they are dropped
+        without waiting, and the next step starts with every bucket pending."""
+        self.start_step()
+
     def _on_ready(self, v: Variable) -> None:
         b = self.var_bucket.get(v.index)
         if b is None:
@@ -120,12 +132,13 @@ class GradAllReduce:
         self._launched[b] = True
         lo, hi = self.buckets[b]
         view = self.store.grad[lo:hi]
+        op = dist.ReduceOp.SUM if self.premul is None else dist._make_nccl_premul_sum(float(self.premul))
         if self.compress:
             tmp = view.to(torch.bfloat16)
-            work = dist.all_reduce(tmp, group=self.group, async_op=True)
+            work = dist.all_reduce(tmp, op=op, group=self.group, async_op=True)
             self._works.append((work, view, tmp))
         else:
-            self._works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+            self._works.append((dist.all_reduce(view, op=op, group=self.group, async_op=True), None, None))
 
     def finish(self) -> None:
         """Launch buckets not yet started (in order) and make the current stream wait for all."""

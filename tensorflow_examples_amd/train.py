@@ -63,16 +63,25 @@ class ClassifierTrainer:
         thread (which polls events of earlier eager collectives) cannot invalidate it.  All ranks
         must capture: the collectives are recorded, not executed, and run at replay time."""
         sx, sy = x.clone(), y.clone()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self._step(sx, sy)
-        torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        mode = "thread_local" if self.dp is not None else "global"
-        with torch.cuda.graph(g, capture_error_mode=mode):
-            loss = self._step(sx, sy)
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    self._step(sx, sy)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            mode = "thread_local" if self.dp is not None else "global"
+            with torch.cuda.graph(g, capture_error_mode=mode):
+                loss = self._step(sx, sy)
+        except BaseException:
+            # a failure part-way through the (captured) backward leaves the bucket bookkeeping
+            # mid-step: some buckets marked launched, captured never-executed Work objects queued.
+            # Reset it so the eager fallback reduces every bucket exactly once.
+            self.graph, self._static = None, None
+            if self.dp is not None:
+                self.dp.reset()
+            raise
         self.graph = g
         self._static = (sx, sy, loss)
         return g

@@ -83,3 +83,66 @@ def test_force_collective_flag_without_process_group():
     dp = GradAllReduce(store, force_collective=True)
     assert not dp.force and dp.world == 1
     dp.finish()  # no collectives issued, no error
+
+
+def _fail_worker(rank, world, port, out):
+    """A step that dies part-way through backward (as a failed HIP-graph capture does), then a
+    reset + clean step: every bucket must be reduced exactly once and the result must equal a step
+    that never failed."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, y = _data()
+    res = {}
+    for inject in (False, True):
+        st, m = _model(seed=3)
+        dp = GradAllReduce(st, bucket_bytes=2048)
+        launches = []
+        orig = dp._launch
+
+        def counting(b, orig=orig, launches=launches):
+            launches.append(b)
+            orig(b)
+
+        dp._launch = counting
+        hook = st.grad_ready_hook
+        if inject:
+            seen = [0]
+
+            def failing(v, hook=hook, seen=seen):
+                seen[0] += 1
+                hook(v)
+                if seen[0] == 2:  # after the first bucket has been launched
+                    raise RuntimeError("injected mid-backward failure")
+
+            st.grad_ready_hook = failing
+            st.zero_grad()
+            try:
+                ops.softmax_cross_entropy(m.logits(x), y).backward()
+            except RuntimeError:
+                pass
+            dp.reset()  # what ClassifierTrainer.capture does on failure
+            st.grad_ready_hook = hook
+            launches.clear()
+        st.zero_grad()
+        ops.softmax_cross_entropy(m.logits(x), y).backward()
+        dp.finish()
+        res[inject] = (sorted(launches), st.grad.clone(), len(dp.buckets))
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_reset_after_mid_backward_failure_reduces_each_bucket_once():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_fail_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        clean, recovered = out[r][False], out[r][True]
+        nb = clean[2]
+        assert nb >= 2
+        assert clean[0] == list(range(nb)) and recovered[0] == list(range(nb))
+        assert torch.equal(clean[1], recovered[1])
