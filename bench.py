@@ -110,7 +110,7 @@ def run(a):
 
     def batch(i):
         if ring is not None:
-            return ring.get(i % len(host))
+            return ring.next()
         return data[i % len(data)]
 
     graphed = False

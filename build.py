@@ -65,7 +65,7 @@ def _run(cmd):
 
 def build_ops(jobs, force, extra_flags=()):
     inc, tlib, abi = _torch_paths()
-    headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
+    headers = glob.glob(os.path.join(CSRC, "include", "*.h")) + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     kern = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     bind = sorted(glob.glob(os.path.join(CSRC, "torch_ops", "*.cpp")))
     os.makedirs(OBJ, exist_ok=True)

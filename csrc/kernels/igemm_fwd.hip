@@ -1,0 +1,7 @@
+// Implicit-GEMM instantiations: conv forward (kernel template: igemm_impl.h).
+#include "igemm_impl.h"
+
+namespace tfx {
+void igemm_fwd_pointwise(IgemmArgs& a, hipStream_t s) { launch_epi<KM_DENSE, KM_DENSE, EPI_STATS>(a, s); }
+void igemm_fwd_im2col(IgemmArgs& a, hipStream_t s) { launch_epi<KM_FWD_X, KM_DENSE, EPI_STATS>(a, s); }
+}  // namespace tfx

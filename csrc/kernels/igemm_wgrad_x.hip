@@ -1,0 +1,7 @@
+// Implicit-GEMM instantiations: gathered weight gradient (kernel template: igemm_impl.h).
+#include "igemm_impl.h"
+
+namespace tfx {
+void igemm_wgrad_x(IgemmArgs& a, hipStream_t s) { launch_shape<MN_DENSE, MN_WGRAD_X, false>(a, s); }
+void igemm_wgrad_t_x(IgemmArgs& a, hipStream_t s) { launch_shape<MN_WGRAD_X, MN_DENSE, false>(a, s); }
+}  // namespace tfx

@@ -11,7 +11,7 @@ STEPS=${STEPS:-"tests bench torch prof"}
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_EXTRA:-} > gpurun_out/pytest_gpu.log 2>&1
       rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
       ok_or_testfail $rc || exit $rc ;;
     bench)
@@ -104,6 +104,24 @@ for s in $STEPS; do
         rc=$?; echo "$spec rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_models_err.log; [ $rc -eq 1 ] || exit $rc; }
       done
       cat gpurun_out/bench_models.jsonl ;;
+    glab)
+      for v in 3 0; do
+        TFX_GLDS=$v timeout -k 10 300 python scripts/conv_bench.py --out gpurun_out/conv_bench_gl$v.json > gpurun_out/conv_bench_gl$v.log 2>&1 || exit 1
+      done
+      for i in 1 2; do for v in 3 2 0; do
+        TFX_GLDS=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_gl${v}_$i.log 2>&1 || exit 1
+      done; done
+      grep TOTAL gpurun_out/conv_bench_gl*.log; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_gl*.log ;;
+    labn)
+      for i in 1 2; do for v in 1 0; do
+        TFX_BN_LAST_ARRIVER=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_la${v}_$i.log 2>&1 || exit 1
+      done; done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_la*.log ;;
+    diagdp)
+      for d in 50 18; do
+        timeout -k 10 300 python scripts/diag_dp.py $d > gpurun_out/diag_dp_$d.log 2>&1
+        rc=$?; echo "diagdp $d rc=$rc"; cat gpurun_out/diag_dp_$d.log | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc
+      done ;;
     hostin)
       for i in 1 2; do
         timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_dev_$i.log 2>&1 || exit 1

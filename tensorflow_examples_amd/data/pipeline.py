@@ -129,24 +129,24 @@ class PinnedRing:
 
 class CyclicFeeder:
     """Feeds a fixed list of host batches round-robin through a :class:`PinnedRing`, ``depth``
-    batches ahead of the consumer (bench.py ``--host-input``): ``get(i)`` returns batch
-    ``i % len(host_batches)`` on the device, its copy issued ``depth`` steps earlier."""
+    batches ahead of the consumer (bench.py ``--host-input``): each :meth:`next` returns the next
+    batch on the device, its H2D copy issued ``depth`` calls earlier."""
 
     def __init__(self, host_batches: Sequence, ring: PinnedRing, depth: int):
         self.host, self.ring, self.depth = list(host_batches), ring, max(1, depth)
-        self._staged: dict = {}
-        self._i = 0
+        self._q: List[int] = []
+        self._n = 0  # batches staged so far
 
-    def _stage_upto(self, i: int) -> None:
-        while self._i <= i:
-            self._staged[self._i] = self.ring.stage(self.host[self._i % len(self.host)])
-            self._i += 1
+    def _stage_one(self) -> None:
+        self._q.append(self.ring.stage(self.host[self._n % len(self.host)]))
+        self._n += 1
 
-    def get(self, i: int):
-        self._stage_upto(i)
-        k = self._staged.pop(i)
-        out = self.ring.acquire(k)
-        self._stage_upto(i + self.depth)
+    def next(self):
+        if not self._q:
+            self._stage_one()
+        out = self.ring.acquire(self._q.pop(0))
+        while len(self._q) < self.depth:
+            self._stage_one()
         return out
 
     def close(self) -> None:

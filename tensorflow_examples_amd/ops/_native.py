@@ -49,9 +49,26 @@ def fallback_allowed() -> bool:
     return os.environ.get("TFX_ALLOW_TORCH_FALLBACK", "0") == "1"
 
 
+_ref = threading.local()
+
+
+class reference_mode:
+    """Context manager: run the PyTorch reference implementation of every op even on GPU tensors.
+    Tests only -- it builds an fp32 (or bf16) PyTorch oracle of the SAME model on the GPU, for
+    shapes too large for the CPU (the batch-256 ResNet-50 gradient check)."""
+
+    def __enter__(self):
+        self._prev = getattr(_ref, "on", False)
+        _ref.on = True
+        return self
+
+    def __exit__(self, *exc):
+        _ref.on = self._prev
+
+
 def use_native(t: torch.Tensor) -> bool:
     """True when ``t`` lives on the GPU: then the HIP kernel path is mandatory."""
-    if t.device.type != "cuda":
+    if t.device.type != "cuda" or getattr(_ref, "on", False):
         return False
     if load():
         return True

@@ -24,7 +24,7 @@ from tensorflow_examples_amd.train import ClassifierTrainer
 dev = init_distributed(backend="gloo", device="cuda")
 rank, world = dist.get_rank(), dist.get_world_size()
 depth = int(os.environ["DEPTH"])
-STEPS = 2
+STEPS = int(os.environ.get('STEPS', '1'))
 
 def batch(r):
     g = torch.Generator().manual_seed(100 + r)
@@ -65,7 +65,7 @@ for lo, hi in dp.buckets:
 print(f"RANK{rank} buckets={len(dp.buckets)} diff={diff} rel={rel:.3e} worst_bucket={worst:.3e} losses={losses}",
       flush=True)
 assert diff == 0.0, diff
-assert rel < 1e-2 and worst < 5e-2, (rel, worst)
+assert rel < 2e-3 and worst < 1e-2, (rel, worst)
 dist.destroy_process_group()
 """
 
@@ -123,12 +123,18 @@ for mode in ("ref", "eager", "graphed"):
         dp = GradAllReduce(store, bucket_bytes=2 << 20, premul=2.0)
         assert dp.force and len(dp.buckets) > 2
     lr = 0.02 if mode == "ref" else 0.01
-    tr = ClassifierTrainer(store, model, MomentumOptimizer(store, lr, momentum=0.9), dp)
+    opt = MomentumOptimizer(store, lr, momentum=0.9)
+    tr = ClassifierTrainer(store, model, opt, dp)
     if mode == "graphed":
-        tr.capture(x, lab, warmup=3)  # 3 eager steps, then the captured step (recorded only)
-        losses = [tr.step(x, lab).item() for _ in range(2)]
-    else:
-        losses = [tr.step(x, lab).item() for _ in range(5)]
+        # warm-up / capture steps at lr 0 leave the weights untouched; then momentum is reset and
+        # ONE replayed step is compared (one step: no trajectory divergence to tolerate)
+        opt.set_learning_rate(0.0)
+        tr.capture(x, lab, warmup=3)
+        torch.cuda.synchronize()
+        assert torch.equal(store.master, w0)
+        opt.m.zero_()
+        opt.set_learning_rate(lr)
+    losses = [tr.step(x, lab).item()]
     torch.cuda.synchronize()
     runs[mode] = (store.master - w0, dp.buckets if dp else None)
     print(mode, losses, flush=True)
@@ -140,7 +146,7 @@ for mode in ("eager", "graphed"):
     worst = max(((d[lo:hi] - ref[lo:hi]).norm() / ref[lo:hi].norm()).item() for lo, hi in buckets
                 if ref[lo:hi].norm() > 0)
     print("REL", mode, rel, "worst_bucket", worst, "buckets", len(buckets), flush=True)
-    assert rel < 2e-2 and worst < 0.1, (mode, rel, worst)
+    assert rel < 2e-3 and worst < 1e-2, (mode, rel, worst)
 dist.destroy_process_group()
 """
 
@@ -148,7 +154,7 @@ dist.destroy_process_group()
 def test_dp_graph_capture_rccl_one_rank(gpu, tmp_path):
     """The DP step (bucketed RCCL all-reduces launched from grad-ready hooks) eager and captured in
     a HIP graph and replayed, on a 1-rank RCCL process group whose all-reduce is a pre-multiplied
-    sum by 2: both must follow the no-DP reference trajectory at twice the learning rate, bucket by
+    sum by 2: one step of each must equal one no-DP step at twice the learning rate, bucket by
     bucket (split-K atomics make the runs differ in rounding only)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -72,3 +72,43 @@ def test_resnet50_steps_reduce_loss(gpu):
     assert losses[-1] < losses[0], losses  # memorising one batch
 
 
+
+
+def test_resnet50_batch256_first_step_vs_fp32_reference(gpu):
+    """The headline step's production shapes: one batch-256 ResNet-50 forward/backward through the
+    HIP kernels vs the PyTorch reference ops of the same model in fp32 ON THE GPU
+    (_native.reference_mode), per variable, bounded by the bf16 noise floor measured the same way
+    (reference ops in bf16)."""
+    from tensorflow_examples_amd import ops
+    from tensorflow_examples_amd.ops import _native
+    g = torch.Generator().manual_seed(11)
+    img = torch.randint(0, 256, (256, 32, 32, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 10, (256,), generator=g).to(gpu)
+    res = {}
+    for mode, dt in (("native", torch.bfloat16), ("ref32", torch.float32), ("ref16", torch.bfloat16)):
+        st, m = build_resnet_cifar(device=gpu, depth=50, dtype=dt, seed=5)
+        if mode == "native":
+            w0 = st.master.bfloat16().float()
+        st.master.copy_(w0)
+        st.refresh_shadow()
+        st.zero_grad()
+        if mode == "native":
+            loss = ops.softmax_cross_entropy(m(to_model_input(img.to(gpu)), training=True), lab)
+            loss.backward()
+        else:
+            with _native.reference_mode():
+                x = to_model_input(img, dtype=dt).to(gpu)
+                loss = ops.softmax_cross_entropy(m(x, training=True), lab)
+                loss.backward()
+        torch.cuda.synchronize()
+        res[mode] = (float(loss), st)
+    (ln, sn), (l32, s32), (l16, s16) = res["native"], res["ref32"], res["ref16"]
+    assert abs(ln - l32) < 0.02 * abs(l32) + 0.02, (ln, l32)
+    bad = []
+    for v in s32.trainable():
+        gr = v.grad
+        en = ((sn.by_name[v.name].grad - gr).norm() / (gr.norm() + 1e-8)).item()
+        eb = ((s16.by_name[v.name].grad - gr).norm() / (gr.norm() + 1e-8)).item()
+        if en > 2.0 * eb + 0.02:
+            bad.append((v.name, en, eb))
+    assert not bad, bad[:5]
