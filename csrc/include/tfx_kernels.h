@@ -139,6 +139,20 @@ void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, f
 void sumsq_flat(const void* g, bool g_bf16, int64_t n, float* out, hipStream_t s);
 void cast_f32_bf16(const float* x, int64_t n, uint16_t* y, hipStream_t s);
 
+// ---------------------------------------------------------------- small fused elementwise ops (elementwise.hip)
+// y = w[c] * x + b[c] over [n/C][C]; backward dx = g * w (dx may be null), dw / db += column sums
+void affine_fwd(const float* x, const float* w, const float* b, int64_t n, int C, float* y, hipStream_t s);
+void affine_bwd(const float* g, const float* x, const float* w, int64_t n, int C, float* dx, float* dw, float* db,
+                hipStream_t s);
+// loss[0] = sum (p - y)^2 ; dp = 2 (p - y) * g[0]
+void sse_fwd(const float* p, const float* y, int64_t n, float* loss, hipStream_t s);
+void sse_bwd(const float* p, const float* y, const float* g, int64_t n, float* dp, hipStream_t s);
+// dz = g * act'(y) (act 0 none, 1 relu, 2 sigmoid, y = the activation OUTPUT); dbias += column sums
+void act_bwd_colsum(const float* g, const float* y, int act, int64_t M, int N, float* dz, float* dbias,
+                    hipStream_t s);
+// y = x * scal[0] (f32 or bf16 output)
+void scale_by_scalar(const float* x, const float* scal, int64_t n, float* y32, uint16_t* y16, hipStream_t s);
+
 // ---------------------------------------------------------------- pooling (NHWC bf16)
 void maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, uint16_t* y,
                  uint8_t* arg, hipStream_t st);
@@ -172,9 +186,12 @@ void image_normalize(const uint8_t* x, int64_t npix, int cin, int cout, const fl
                      uint16_t* y, hipStream_t s);
 
 // ---------------------------------------------------------------- ps transport over xGMI peer memory
-// p -= lr*g on a (peer-mapped) arena range; if step != null, atomically bump the 64-bit global
-// step there and write the new value to step_out (worker-local).  IPC helpers return 0 / -hipError.
-void ps_peer_sgd(float* p, const float* g, int64_t n, float lr, void* step, int64_t* step_out, hipStream_t s);
+// p -= lr*g on a (peer-mapped) arena range (g zeroed as consumed if zero_g); then, if step != null,
+// bump the 64-bit global step there (system-scope atomic, after the whole update) and write the new
+// value to step_out (worker-local).  ps_peer_copy: arena -> store.  IPC helpers return 0 / -hipError.
+void ps_peer_sgd(float* p, float* g, int64_t n, float lr, bool zero_g, void* step, int64_t* step_out,
+                 hipStream_t s);
+void ps_peer_copy(float* dst, const float* src, int64_t n, hipStream_t s);
 int ipc_alloc(int device, int64_t nbytes, void** ptr);
 int ipc_free(int device, void* ptr);
 int ipc_get_handle(void* ptr, uint8_t* out64);

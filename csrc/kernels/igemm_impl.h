@@ -1031,14 +1031,21 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
 
 // ============================================================ host launcher
 
-// LDS-DMA ring depth for the main loop (TFX_GLDS: 0 = register-staged pipeline, 2 or 3 = ring depth;
-// default 3, capped per tile shape by the LDS budget)
-int glds_stages() {
-  static const int g = [] {
-    const char* e = getenv("TFX_GLDS");
-    return e ? atoi(e) : 3;
-  }();
-  return g;
+// LDS-DMA ring depth for the main loop (0 = register-staged pipeline, 2 or 3 = ring depth, capped
+// per tile shape by the LDS budget).  Measured per mode on the ResNet-50 batch-256 layers
+// (profiles/r02_glds, scripts/conv_bench.py): the ring wins on the f32-atomic weight gradients
+// (-7 %, up to +40 % per layer) where a 3-deep ring fits next to the in-block split-K, and loses on
+// the bf16-output forward / data-gradient kernels (1 block per CU at a 3-deep ring vs 2 with the
+// register pipeline).  TFX_GLDS forces one depth everywhere; TFX_GLDS_WGRAD / TFX_GLDS_BF16 per mode.
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+int glds_stages(bool atomic_out, int g3) {
+  static const int all = env_int("TFX_GLDS", -1), wg = env_int("TFX_GLDS_WGRAD", 3), bf = env_int("TFX_GLDS_BF16", 0);
+  if (all >= 0) return all;
+  if (atomic_out) return g3 >= 3 ? wg : 0;
+  return bf;
 }
 
 int pick_splits(int tiles, int nkt, int want_blocks, int min_kps = 4) {
@@ -1078,11 +1085,11 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   if (grid == 0) return;
   // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
-  const int gls = glds_stages();
+  constexpr int STAGE_B = (BM + BN) * BKT * 2;
+  constexpr int G3 = KS * 3 * STAGE_B <= 163840 ? 3 : 2;
+  const int gls = glds_stages(a.out_mode == OUT_F32_ATOMIC, G3);
   if (gls > 0) {
     // LDS-DMA ring: single k-tile -> GLS 1; otherwise the deepest ring (<= 3) that fits the LDS
-    constexpr int STAGE = (BM + BN) * BKT * 2;
-    constexpr int G3 = KS * 3 * STAGE <= 163840 ? 3 : 2;
     const bool single = nkt == 1 && splits == 1;
 #define TFX_GL_LAUNCH(SW)                                                                              \
     if constexpr (KS == 1) {                                                                           \

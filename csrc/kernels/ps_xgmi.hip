@@ -22,11 +22,11 @@
 namespace tfx {
 
 // One pass over a contiguous parameter range: float4 body (arena and store are 16-byte
-// aligned at matching offsets for the whole-store range) + scalar tail; grid-stride.
-__global__ void __launch_bounds__(256) ps_peer_sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                          int64_t n, float lr,
-                                                          unsigned long long* __restrict__ step,
-                                                          long long* __restrict__ step_out) {
+// aligned at matching offsets) + scalar tail; grid-stride.  zero_g: the worker-local gradient is
+// cleared as it is consumed (the next step's backward accumulates into a zero buffer without a
+// separate fill launch).
+__global__ void __launch_bounds__(256) ps_peer_sgd_kernel(float* __restrict__ p, float* __restrict__ g, int64_t n,
+                                                          float lr, int zero_g) {
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
   const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g)) & 15) == 0;
@@ -38,26 +38,59 @@ __global__ void __launch_bounds__(256) ps_peer_sgd_kernel(float* __restrict__ p,
       const float4 gv = reinterpret_cast<const float4*>(g)[i];
       pv.x -= lr * gv.x; pv.y -= lr * gv.y; pv.z -= lr * gv.z; pv.w -= lr * gv.w;
       reinterpret_cast<float4*>(p)[i] = pv;
+      if (zero_g) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     done = n4 << 2;
   }
-  for (int64_t i = done + tid; i < n; i += stride) p[i] -= lr * g[i];
-  if (step && tid == 0) {
-    // AssignAdd(global_step, 1) after this worker's update was issued; device-scope atomic on
-    // the (possibly remote) arena, system scope so a peer GPU's increments are ordered too.
-    __threadfence_system();
-    const unsigned long long old = atomicAdd(step, 1ull);
-    *step_out = (long long)(old + 1);
+  for (int64_t i = done + tid; i < n; i += stride) {
+    p[i] -= lr * g[i];
+    if (zero_g) g[i] = 0.f;
   }
 }
 
-void ps_peer_sgd(float* p, const float* g, int64_t n, float lr, void* step, int64_t* step_out, hipStream_t s) {
-  if (n <= 0 && !step) return;
+// AssignAdd(global_step, 1) (R/distributed/distributed.py:108), ordered AFTER this worker's whole
+// update: it is its own single-thread launch behind the SGD kernel on the same stream, so every
+// block's writes to the (possibly peer) arena have completed first; the fence writes them back at
+// system scope before the increment becomes visible, and the increment itself is a SYSTEM-scope
+// atomic (other GPUs of the node bump the same word).
+__global__ void ps_step_inc_kernel(unsigned long long* __restrict__ step, long long* __restrict__ step_out) {
+  __threadfence_system();
+  const unsigned long long old =
+      __hip_atomic_fetch_add(step, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  *step_out = (long long)(old + 1);
+}
+
+// PULL: peer arena -> worker-local store (xGMI reads), float4 grid-stride copy
+__global__ void __launch_bounds__(256) ps_peer_copy_kernel(float* __restrict__ dst, const float* __restrict__ src,
+                                                           int64_t n) {
+  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const bool vec = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
+  int64_t done = 0;
+  if (vec) {
+    const int64_t n4 = n >> 2;
+    for (int64_t i = tid; i < n4; i += stride) reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+    done = n4 << 2;
+  }
+  for (int64_t i = done + tid; i < n; i += stride) dst[i] = src[i];
+}
+
+static int ps_blocks(int64_t n) {
   int64_t blocks = (n / 4 + 255) / 256;
-  if (blocks < 1) blocks = 1;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(ps_peer_sgd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, n, lr,
-                     reinterpret_cast<unsigned long long*>(step), reinterpret_cast<long long*>(step_out));
+  return (int)(blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks));
+}
+
+void ps_peer_sgd(float* p, float* g, int64_t n, float lr, bool zero_g, void* step, int64_t* step_out,
+                 hipStream_t s) {
+  if (n > 0)
+    hipLaunchKernelGGL(ps_peer_sgd_kernel, dim3(ps_blocks(n)), dim3(256), 0, s, p, g, n, lr, zero_g ? 1 : 0);
+  if (step)
+    hipLaunchKernelGGL(ps_step_inc_kernel, dim3(1), dim3(1), 0, s, reinterpret_cast<unsigned long long*>(step),
+                       reinterpret_cast<long long*>(step_out));
+}
+
+void ps_peer_copy(float* dst, const float* src, int64_t n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(ps_peer_copy_kernel, dim3(ps_blocks(n)), dim3(256), 0, s, dst, src, n);
 }
 
 // ---------------------------------------------------------------- IPC arena management

@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <shared_mutex>
 #include <string>
 #include <thread>
@@ -39,6 +40,10 @@
 namespace {
 
 constexpr uint32_t MAGIC = 0x53504654;  // 'TFPS'
+// Largest payload one item may carry.  The wire's u64 nbytes is untrusted: a larger value closes
+// the connection instead of resizing a buffer to it (an uncaught bad_alloc would end the ps).
+constexpr uint64_t MAX_ITEM_BYTES = 1ull << 31;
+constexpr uint32_t STATUS_SIZE_MISMATCH = 0x80000000u;  // CREATE / ASSIGN: existing var, other size
 enum Op : uint32_t {
   OP_PING = 0,
   OP_CREATE = 1,      // create + initialize if uninitialized (flags&1: force re-init = chief restart)
@@ -152,7 +157,13 @@ struct Server {
         if (!read_full(fd, &nbytes, 8)) { ok = false; break; }
         const bool carries = (op == OP_CREATE || op == OP_PUSH || op == OP_ASSIGN);
         if (carries) {
-          payload.resize(nbytes);
+          if (nbytes > MAX_ITEM_BYTES) { ok = false; break; }
+          try {
+            payload.resize(nbytes);
+          } catch (const std::bad_alloc&) {
+            ok = false;
+            break;
+          }
           if (nbytes && !read_full(fd, payload.data(), nbytes)) { ok = false; break; }
           bytes_in += nbytes;
         }
@@ -161,9 +172,14 @@ struct Server {
           Var* v = find_or_create(name, nf);
           const bool force = (op == OP_ASSIGN) || (flags & 1);
           std::lock_guard<std::mutex> g(v->mu);
-          if (v->bits.size() != nf) v->bits.assign(nf, 0u);
+          // the storage of an existing variable is never reallocated: other connection threads
+          // hold pointers into it (PULL / PUSH run lock-free); a different size is an error
+          if (v->bits.size() != nf) { status |= STATUS_SIZE_MISMATCH; continue; }
           if (!v->init.load() || force) {
-            memcpy(v->bits.data(), payload.data(), nf * 4);
+            // per-word relaxed atomic stores: concurrent pulls / Hogwild pushes on the same words
+            // (a restarted chief re-initialising while non-chiefs train) are not a data race
+            const float* src = reinterpret_cast<const float*>(payload.data());
+            for (size_t k = 0; k < nf; ++k) st(&v->bits[k], src[k]);
             std::atomic_thread_fence(std::memory_order_release);
             v->init.store(true);
             ++status;
@@ -297,7 +313,21 @@ void* tfx_ps_server_start(const char* host, int port, int use_locking) {
   sockaddr_in addr{};
   addr.sin_family = AF_INET;
   addr.sin_port = htons((uint16_t)port);
-  if (!host || !*host || inet_pton(AF_INET, host, &addr.sin_addr) != 1) addr.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (!host || !*host || strcmp(host, "0.0.0.0") == 0) {
+    addr.sin_addr.s_addr = htonl(INADDR_ANY);  // explicit wildcard only
+  } else if (inet_pton(AF_INET, host, &addr.sin_addr) != 1) {
+    // a host name: resolve it; never fall back to every interface (the service is unauthenticated)
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(host, nullptr, &hints, &res) != 0 || !res) {
+      fprintf(stderr, "tfx ps: cannot resolve bind host '%s'\n", host);
+      ::close(fd);
+      return nullptr;
+    }
+    addr.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
+    freeaddrinfo(res);
+  }
   if (::bind(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0 || ::listen(fd, 64) != 0) {
     ::close(fd);
     return nullptr;
@@ -374,13 +404,15 @@ void tfx_ps_close(void* h) {
   delete c;
 }
 
-// returns number of variables (re)initialised by this call, -1 on transport error
+// returns number of variables (re)initialised by this call, -1 on transport error, -2 if a variable
+// already exists on the ps with a different size
 int tfx_ps_create(void* h, int n, const char** names, const void* const* ptrs, const uint64_t* nbytes, int force) {
   Client* c = static_cast<Client*>(h);
   if (!send_request(c, OP_CREATE, n, names, ptrs, nbytes, 0.f, force ? 1u : 0u, true)) return -1;
   uint32_t st, k;
   double sc;
   if (!recv_header(c, &st, &k, &sc)) return -1;
+  if (st & STATUS_SIZE_MISMATCH) return -2;
   return (int)st;
 }
 

@@ -74,6 +74,18 @@ static int ps_stress(int nclient, int steps, int use_locking) {
       tfx_ps_close(c);
     });
   }
+  // a restarted chief re-initialising (force) while the workers pull and push
+  th.emplace_back([&] {
+    void* c = tfx_ps_connect("127.0.0.1", port, 5000);
+    CHECK(c != nullptr);
+    std::vector<float> W(784 * 100, 0.25f), b(100, 0.f);
+    const void* init[2] = {W.data(), b.data()};
+    for (int s = 0; s < steps / 10 + 1; ++s) CHECK(tfx_ps_create(c, 2, names + 1, init, nb + 1, 1) >= 0);
+    // a size mismatch on an existing variable is rejected, never reallocated
+    const uint64_t bad[1] = {8};
+    CHECK(tfx_ps_create(c, 1, names + 2, init + 1, bad, 1) == -2);
+    tfx_ps_close(c);
+  });
   for (auto& t : th) t.join();
   float gs = -1.f;
   CHECK(tfx_ps_server_read(srv, "global_step", &gs, 1) == 1);

@@ -558,6 +558,67 @@ Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
   return dx;
 }
 
+// ------------------------------------------------------------------ small fused elementwise ops
+Tensor affine_fwd(Tensor x, Tensor w, optional<Tensor> b) {
+  CHECK_DEV(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_F32(w); CHECK_CONTIG(w);
+  const int64_t C = w.numel();
+  TORCH_CHECK(C >= 1 && C <= 256 && x.numel() % C == 0 && (x.dim() == 0 ? C == 1 : x.size(-1) == C || C == 1),
+              "affine: w broadcasts over the last dim (<= 256 channels)");
+  if (b.has_value() && b->defined()) TORCH_CHECK(b->numel() == C && b->scalar_type() == at::kFloat, "affine bias");
+  auto y = at::empty_like(x);
+  tfx::affine_fwd(x.data_ptr<float>(), w.data_ptr<float>(), fp(b), x.numel(), (int)C, y.data_ptr<float>(),
+                  cur_stream());
+  return y;
+}
+
+// returns dx (if want_dx); dw / db accumulated in place
+Tensor affine_bwd(Tensor g, Tensor x, Tensor w, optional<Tensor> dw, optional<Tensor> db, bool want_dx) {
+  CHECK_DEV(g); CHECK_F32(g); CHECK_CONTIG(g); CHECK_F32(x); CHECK_CONTIG(x);
+  TORCH_CHECK(g.numel() == x.numel(), "affine_bwd sizes");
+  const int64_t C = w.numel();
+  Tensor dx;
+  if (want_dx) dx = at::empty_like(x);
+  tfx::affine_bwd(g.data_ptr<float>(), x.data_ptr<float>(), w.data_ptr<float>(), x.numel(), (int)C,
+                  want_dx ? dx.data_ptr<float>() : nullptr, fpm(dw), fpm(db), cur_stream());
+  return dx;
+}
+
+Tensor sse_fwd(Tensor p, Tensor y) {
+  CHECK_DEV(p); CHECK_F32(p); CHECK_CONTIG(p); CHECK_F32(y); CHECK_CONTIG(y);
+  TORCH_CHECK(p.numel() == y.numel(), "sse sizes");
+  auto loss = at::empty({}, p.options());
+  tfx::sse_fwd(p.data_ptr<float>(), y.data_ptr<float>(), p.numel(), loss.data_ptr<float>(), cur_stream());
+  return loss;
+}
+
+Tensor sse_bwd(Tensor p, Tensor y, Tensor g) {
+  CHECK_DEV(p); CHECK_F32(p); CHECK_CONTIG(p); CHECK_F32(y); CHECK_CONTIG(y); CHECK_F32(g);
+  TORCH_CHECK(g.numel() == 1, "sse_bwd: scalar upstream gradient");
+  auto dp = at::empty_like(p);
+  tfx::sse_bwd(p.data_ptr<float>(), y.data_ptr<float>(), g.data_ptr<float>(), p.numel(), dp.data_ptr<float>(),
+               cur_stream());
+  return dp;
+}
+
+Tensor act_bwd_colsum(Tensor g, Tensor y, int64_t act, optional<Tensor> dbias) {
+  CHECK_DEV(g); CHECK_F32(g); CHECK_CONTIG(g); CHECK_F32(y); CHECK_CONTIG(y);
+  TORCH_CHECK(g.dim() == 2 && g.sizes() == y.sizes(), "act_bwd_colsum: [M, N] gradient and activation");
+  if (dbias.has_value() && dbias->defined()) TORCH_CHECK(dbias->numel() == g.size(1), "dbias size");
+  auto dz = at::empty_like(g);
+  tfx::act_bwd_colsum(g.data_ptr<float>(), y.data_ptr<float>(), (int)act, g.size(0), (int)g.size(1),
+                      dz.data_ptr<float>(), fpm(dbias), cur_stream());
+  return dz;
+}
+
+Tensor scale_by_scalar(Tensor x, Tensor scal, bool out_bf16) {
+  CHECK_DEV(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_F32(scal);
+  TORCH_CHECK(scal.numel() == 1, "scale_by_scalar: scalar");
+  auto y = at::empty_like(x, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  tfx::scale_by_scalar(x.data_ptr<float>(), scal.data_ptr<float>(), x.numel(),
+                       out_bf16 ? nullptr : y.data_ptr<float>(), out_bf16 ? bfm(y) : nullptr, cur_stream());
+  return y;
+}
+
 // ------------------------------------------------------------------ optimizers
 void optimizer_apply(int64_t kind, Tensor p, Tensor g, optional<Tensor> m, optional<Tensor> v, Tensor lr,
                      double gscale, double wd, double b1, double b2, double eps, optional<Tensor> step,
@@ -625,7 +686,7 @@ Tensor ipc_open(Tensor handle, int64_t nbytes, int64_t device) {
 
 // p, g: f32 ranges of equal length (p may be peer-mapped); step: int64 [1] view in the arena
 // header or None; step_out: int64 [1] worker-local, receives the new global step.
-void ps_peer_sgd(Tensor p, Tensor g, double lr, optional<Tensor> step, Tensor step_out) {
+void ps_peer_sgd(Tensor p, Tensor g, double lr, optional<Tensor> step, Tensor step_out, bool zero_g) {
   CHECK_DEV(p); CHECK_DEV(g); CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
   TORCH_CHECK(p.numel() == g.numel(), "ps_peer_sgd: range sizes differ");
   CHECK_DEV(step_out);
@@ -637,8 +698,15 @@ void ps_peer_sgd(Tensor p, Tensor g, double lr, optional<Tensor> step, Tensor st
                 "step must be an aligned int64 view");
     sp = step->data_ptr();
   }
-  tfx::ps_peer_sgd(p.data_ptr<float>(), g.data_ptr<float>(), p.numel(), (float)lr, sp,
+  tfx::ps_peer_sgd(p.data_ptr<float>(), g.data_ptr<float>(), p.numel(), (float)lr, zero_g, sp,
                    step_out.data_ptr<int64_t>(), cur_stream());
+}
+
+// dst (worker-local store range) <- src (peer arena range)
+void ps_peer_copy(Tensor dst, Tensor src) {
+  CHECK_DEV(dst); CHECK_DEV(src); CHECK_F32(dst); CHECK_F32(src); CHECK_CONTIG(dst); CHECK_CONTIG(src);
+  TORCH_CHECK(dst.numel() == src.numel(), "ps_peer_copy: range sizes differ");
+  tfx::ps_peer_copy(dst.data_ptr<float>(), src.data_ptr<float>(), dst.numel(), cur_stream());
 }
 
 // ------------------------------------------------------------------ pooling (NHWC bf16)
@@ -893,10 +961,17 @@ TORCH_LIBRARY(tfx, m) {
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("optimizer_apply", &optimizer_apply);
+  m.def("affine_fwd", &affine_fwd);
+  m.def("affine_bwd", &affine_bwd);
+  m.def("sse_fwd", &sse_fwd);
+  m.def("sse_bwd", &sse_bwd);
+  m.def("act_bwd_colsum", &act_bwd_colsum);
+  m.def("scale_by_scalar", &scale_by_scalar);
   m.def("sumsq", &sumsq);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("ipc_arena_alloc", &ipc_arena_alloc);
   m.def("ipc_handle", &ipc_handle);
   m.def("ipc_open", &ipc_open);
   m.def("ps_peer_sgd", &ps_peer_sgd);
+  m.def("ps_peer_copy", &ps_peer_copy);
 }

@@ -47,6 +47,10 @@ flags.DEFINE_boolean("ps_exit_after_workers", False, "ps exits once every worker
 flags.DEFINE_boolean("sync_replicas", False, "aggregate all workers' gradients per global step "
                      "(SyncReplicasOptimizer semantics, R/distributed/distributed.py:109-112)")
 flags.DEFINE_integer("sync_port_offset", 1000, "worker-group rendezvous port = worker 0 port + offset")
+flags.DEFINE_string("transport", "tcp", "ps data path: tcp (portable) | xgmi (same-node GPUs: the ps arena "
+                    "is mapped into every worker over xGMI peer memory, SURVEY.md §5.8)")
+flags.DEFINE_integer("xgmi_arena_mb", 64, "size of each ps task's xGMI arena")
+flags.DEFINE_integer("ps_device", -1, "GPU of the ps arena with --transport=xgmi (-1: task_index % n_gpus)")
 flags.DEFINE_integer("save_checkpoint_steps", 0, "chief saves a checkpoint into --logdir every N local steps "
                      "(0 = only at the end; TF1 Supervisor saves on a timer when logdir is set)")
 FLAGS = app.flags.FLAGS
@@ -72,6 +76,13 @@ logs_path = FLAGS.logs_path
 DONE = "__workers_done__"
 
 if FLAGS.job_name == "ps":
+    if FLAGS.transport == "xgmi":
+        # the ps owns its variables in one GPU arena that every worker maps over xGMI
+        import torch
+        from tensorflow_examples_amd.cluster.xgmi import XgmiArena
+        ps_dev = FLAGS.ps_device if FLAGS.ps_device >= 0 else FLAGS.task_index % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(ps_dev)
+        arena = XgmiArena(server, FLAGS.xgmi_arena_mb << 20, ps_dev)
     if FLAGS.ps_exit_after_workers:
         n_workers = cluster.num_tasks("worker")
         while True:
@@ -109,7 +120,11 @@ elif FLAGS.job_name == "worker":
     store = VariableStore(device=device, compute_dtype=torch.float32, seed=2)  # tf.set_random_seed(2)
     model = MnistMLP(store)
     store.finalize()
-    client = PSClient(cluster, store)
+    if FLAGS.transport == "xgmi":
+        from tensorflow_examples_amd.cluster.xgmi import XgmiPSClient
+        client = XgmiPSClient(cluster, store)
+    else:
+        client = PSClient(cluster, store)
     # done-counter for --ps_exit_after_workers lives on ps task 0
     if FLAGS.sync_replicas:
         group = init_worker_group(FLAGS.worker_hosts.split(","), FLAGS.task_index, FLAGS.sync_port_offset)

@@ -112,6 +112,22 @@ for s in $STEPS; do
         TFX_GLDS=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_gl${v}_$i.log 2>&1 || exit 1
       done; done
       grep TOTAL gpurun_out/conv_bench_gl*.log; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_gl*.log ;;
+    glmode)
+      for i in 1 2; do for v in def 0; do
+        if [ $v = def ]; then timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_glm${v}_$i.log 2>&1 || exit 1
+        else TFX_GLDS=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_glm${v}_$i.log 2>&1 || exit 1; fi
+      done; done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_glm*.log ;;
+    mlp)
+      # SURVEY §7.2 minimum slice: 1 ps + 1 worker on the GPU, full 50 x 550, tcp vs xgmi transport
+      for tr in xgmi tcp; do
+        P=$((29700 + RANDOM % 200)); W=$((P + 1))
+        A="--ps_hosts=127.0.0.1:$P --worker_hosts=127.0.0.1:$W --device=cuda --logs_path=$R/gpurun_out/mnist_$tr --ps_exit_after_workers --transport=$tr"
+        timeout -k 10 400 python distributed/distributed.py $A --job_name=ps --task_index=0 > gpurun_out/mlp_ps_$tr.log 2>&1 &
+        PSPID=$!
+        timeout -k 10 400 python distributed/distributed.py $A --job_name=worker --task_index=0 > gpurun_out/mlp_worker_$tr.log 2>&1
+        rc=$?; wait $PSPID; echo "mlp $tr rc=$rc"; tail -4 gpurun_out/mlp_worker_$tr.log; [ $rc -eq 0 ] || exit $rc
+      done ;;
     labn)
       for i in 1 2; do for v in 1 0; do
         TFX_BN_LAST_ARRIVER=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_la${v}_$i.log 2>&1 || exit 1

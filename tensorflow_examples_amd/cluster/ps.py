@@ -92,6 +92,8 @@ class PSClient:
         done = 0
         for sh in self.pull_shards:
             r = runtime.lib().tfx_ps_create(sh.h, sh.n, sh.c_names, sh.c_ptrs, sh.c_sizes, int(force))
+            if r == -2:
+                raise PSError("a variable already exists on the ps with a different shape (model mismatch)")
             if r < 0:
                 raise PSError("ps connection lost during initialisation")
             done += r

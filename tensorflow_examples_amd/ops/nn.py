@@ -541,7 +541,9 @@ class _SoftmaxXent(torch.autograd.Function):
     def backward(ctx, g):
         if ctx.native:
             (dz,) = ctx.saved_tensors
-            return (dz * g).to(ctx.dtype), None, None
+            # upstream scale (1.0 for loss.backward()) + cast in one HIP launch
+            gs = g.reshape(1).float().contiguous()
+            return torch.ops.tfx.scale_by_scalar(dz, gs, ctx.dtype == torch.bfloat16), None, None
         logits, labels = ctx.saved_tensors
         with torch.enable_grad():
             z = logits.detach().requires_grad_(True)
@@ -612,11 +614,18 @@ class _DenseF32(torch.autograd.Function):
     def backward(ctx, gy):
         x, y = ctx.saved_tensors
         w, b, act = ctx.w, ctx.b, ctx.act
-        g = gy
-        if act == 1:
-            g = g * (y > 0)
-        elif act == 2:
-            g = g * y * (1 - y)  # TF1 SigmoidGrad: dy * y * (1 - y)
+        bias_done = False
+        if ctx.native:
+            # SigmoidGrad / ReluGrad x upstream and the bias column sum in ONE HIP launch
+            db = b.grad if (b is not None and b.trainable) else None
+            g = torch.ops.tfx.act_bwd_colsum(gy.float().contiguous(), y, act, db)
+            bias_done = True
+        else:
+            g = gy
+            if act == 1:
+                g = g * (y > 0)
+            elif act == 2:
+                g = g * y * (1 - y)  # TF1 SigmoidGrad: dy * y * (1 - y)
         g = g.contiguous()
         dx = None
         if ctx.native:
@@ -629,7 +638,7 @@ class _DenseF32(torch.autograd.Function):
                 dx = g @ w.master.t()
             if w.trainable:
                 w.grad.add_(x.t() @ g)
-        if b is not None and b.trainable:
+        if b is not None and b.trainable and not bias_done:
             b.grad.add_(g.sum(0))
         _grad_ready(w, b)
         return dx, None, None, None, None
@@ -638,3 +647,68 @@ class _DenseF32(torch.autograd.Function):
 def dense(x, w: Variable, b: Optional[Variable] = None, activation=None):
     """f32 fully-connected layer: ``activation(x @ W + b)``, W is [in, out]."""
     return _DenseF32.apply(x, w.store.anchor, w, b, _ACT[activation])
+
+
+# ====================================================================== scalar / per-channel affine + SSE
+class _Affine(torch.autograd.Function):
+    """y = W * x + b with W, b per-channel (broadcast over the last dim; shape [1] for the scalar
+    linear model of R/simple/simple.py:16).  GPU: elementwise.hip affine_fwd / affine_bwd."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, w: Variable, b: Optional[Variable]):
+        ctx.w, ctx.b = w, b
+        ctx.native = _native.use_native(x)
+        ctx.save_for_backward(x)
+        if ctx.native:
+            return torch.ops.tfx.affine_fwd(x.contiguous().float(), w.master, b.master if b is not None else None)
+        y = w.master * x
+        return y + b.master if b is not None else y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        w, b = ctx.w, ctx.b
+        need_dx = ctx.needs_input_grad[0]
+        dw = w.grad if w.trainable else None
+        db = b.grad if (b is not None and b.trainable) else None
+        if ctx.native:
+            dx = torch.ops.tfx.affine_bwd(g.contiguous().float(), x.contiguous().float(), w.master, dw, db, need_dx)
+        else:
+            # TF1 Mul/Add gradients reduced back to the parameter shape: dW = sum g*x, db = sum g
+            C = w.numel
+            gx = (g * x).reshape(-1, C)
+            if dw is not None:
+                dw.add_(torch.sum(gx, 0) if C > 1 else torch.sum(g * x).reshape(1))
+            if db is not None:
+                db.add_(torch.sum(g.reshape(-1, C), 0) if C > 1 else torch.sum(g).reshape(1))
+            dx = g * w.master if need_dx else None
+        _grad_ready(w, b)
+        return dx, None, None, None
+
+
+def scale_shift(x: torch.Tensor, w: Variable, b: Optional[Variable] = None) -> torch.Tensor:
+    """``W * x + b`` (R/simple/simple.py:16: ``linear_model = W * x + b``)."""
+    return _Affine.apply(x, w.store.anchor, w, b)
+
+
+class _SSE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, y):
+        ctx.native = _native.use_native(pred)
+        ctx.save_for_backward(pred, y)
+        if ctx.native:
+            return torch.ops.tfx.sse_fwd(pred.contiguous().float(), y.contiguous().float())
+        return ((pred - y) ** 2).sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, y = ctx.saved_tensors
+        if ctx.native:
+            return torch.ops.tfx.sse_bwd(pred.contiguous().float(), y.contiguous().float(),
+                                         g.reshape(1).float().contiguous()), None
+        return 2.0 * (pred - y) * g, None
+
+
+def sum_squared_error(pred: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """``reduce_sum(square(pred - y))`` (R/simple/simple.py:20), a scalar."""
+    return _SSE.apply(pred, y)

@@ -16,6 +16,7 @@ import torch
 
 from .. import ops
 from ..cluster.ps import PSClient
+from ..data.pipeline import PinnedRing
 
 
 class AsyncPSWorker:
@@ -23,6 +24,17 @@ class AsyncPSWorker:
         self.model, self.client, self.lr, self.naive = model, client, float(learning_rate), naive_xent
         self.store = client.store
         self.device = self.store.device
+        # the feed (feed_dict of R/distributed/distributed.py:150) goes through a fixed pinned ring:
+        # host batch -> pinned slot -> async H2D on the copy stream, no per-batch pinning
+        self.ring = PinnedRing(self.device, depth=2) if self.device.type == "cuda" else None
+        # an xGMI push clears the local gradient in its SGD kernel: no separate zero pass
+        self._grad_clean = False
+
+    def _feed(self, *arrays):
+        hs = [np.ascontiguousarray(a, dtype=np.float32) for a in arrays]
+        if self.ring is None:
+            return tuple(torch.from_numpy(h) for h in hs)
+        return self.ring.acquire(self.ring.stage(tuple(hs)))
 
     def _to_dev(self, a) -> torch.Tensor:
         t = torch.as_tensor(np.asarray(a, dtype=np.float32))
@@ -30,16 +42,24 @@ class AsyncPSWorker:
             t = t.pin_memory().to(self.device, non_blocking=True)
         return t
 
+    def _push(self) -> int:
+        if getattr(self.client, "push_zeroes_grad", False):
+            step = self.client.push(self.lr, zero_grad=True)
+            self._grad_clean = True
+            return step
+        return self.client.push(self.lr)
+
     def step(self, batch_x, batch_y) -> Tuple[float, float, int]:
         """Returns (cost, accuracy, global_step before this update)."""
-        x, y = self._to_dev(batch_x), self._to_dev(batch_y)
+        x, y = self._feed(batch_x, batch_y)
         self.client.pull()
-        self.store.zero_grad()
+        if not self._grad_clean:
+            self.store.zero_grad()
         logits = self.model.logits(x)
         loss = ops.softmax_cross_entropy(logits, y, naive=self.naive)
         acc = ops.accuracy(logits.detach(), y)
         loss.backward()
-        new_step = self.client.push(self.lr)
+        new_step = self._push()
         return float(loss.item()), float(acc.item()), new_step - 1
 
     @torch.no_grad()
@@ -75,7 +95,7 @@ class SyncReplicasPSWorker(AsyncPSWorker):
         self._step_t = torch.zeros(1, dtype=torch.float64)
 
     def step(self, batch_x, batch_y):
-        x, y = self._to_dev(batch_x), self._to_dev(batch_y)
+        x, y = self._feed(batch_x, batch_y)
         self.client.pull()
         self.store.zero_grad()
         logits = self.model.logits(x)
