@@ -375,7 +375,9 @@ __device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n
   float s = 0.f, q = 0.f;
   if (c < a.N) {
     // 8 slot rows in flight per step (bounded registers: this runs in every fused-BN kernel)
-    constexpr int CH = NSLOT / NPH < 8 ? NSLOT / NPH : 8;
+    // every slot row in flight at once: the reducer runs on the kernel's critical tail, and the slots
+    // (written by memory-side atomics) are an HBM / MALL round trip away -- one round trip, not four
+    constexpr int CH = NSLOT / NPH;
     for (int k0 = 0; k0 < NSLOT / NPH; k0 += CH) {
       float vs[CH], vq[CH];
 #pragma unroll

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Diagnostic: gradients of one step without DP vs through GradAllReduce on a 1-rank RCCL group
+(plain sum = identity, and pre-multiplied sum by 2), per bucket.  Run with RANK=0 WORLD_SIZE=1
+TFX_DP_FORCE_COLLECTIVE=1 (MASTER_ADDR/PORT set)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tensorflow_examples_amd import ops  # noqa: E402
+from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
+from tensorflow_examples_amd.parallel import GradAllReduce, init_distributed  # noqa: E402
+
+depth = int(sys.argv[1]) if len(sys.argv) > 1 else 18
+dev = init_distributed(device="cuda")
+g = torch.Generator().manual_seed(0)
+img = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, generator=g).to(dev)
+lab = torch.randint(0, 10, (16,), generator=g).to(dev)
+x = to_model_input(img)
+res = {}
+for mode in ("none", "none2", "sum", "premul", "sum_nooverlap"):
+    st, m = build_resnet_cifar(device=dev, depth=depth, dtype=torch.bfloat16, seed=0)
+    dp = None
+    if mode == "sum":
+        dp = GradAllReduce(st, bucket_bytes=2 << 20)
+    elif mode == "premul":
+        dp = GradAllReduce(st, bucket_bytes=2 << 20, premul=2.0)
+    elif mode == "sum_nooverlap":
+        dp = GradAllReduce(st, bucket_bytes=2 << 20, overlap=False)
+    st.zero_grad()
+    ops.softmax_cross_entropy(m(x, training=True), lab).backward()
+    if dp is not None:
+        dp.finish()
+    torch.cuda.synchronize()
+    res[mode] = (st.grad.clone() / (2.0 if mode == "premul" else 1.0), dp)
+ref = res["none"][0]
+buckets = res["sum"][1].buckets
+for mode in ("none2", "sum", "premul", "sum_nooverlap"):
+    gm = res[mode][0]
+    rel = ((gm - ref).norm() / ref.norm()).item()
+    per = [((gm[lo:hi] - ref[lo:hi]).norm() / (ref[lo:hi].norm() + 1e-30)).item() for lo, hi in buckets]
+    print("%-14s rel %.3e  per-bucket %s" % (mode, rel, " ".join("%.1e" % p for p in per)), flush=True)

@@ -113,7 +113,7 @@ for s in $STEPS; do
       done; done
       grep TOTAL gpurun_out/conv_bench_gl*.log; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_gl*.log ;;
     glmode)
-      for i in 1 2; do for v in def 0; do
+      for i in 1 2 3; do for v in def 0; do
         if [ $v = def ]; then timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_glm${v}_$i.log 2>&1 || exit 1
         else TFX_GLDS=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_glm${v}_$i.log 2>&1 || exit 1; fi
       done; done
@@ -128,8 +128,14 @@ for s in $STEPS; do
         timeout -k 10 400 python distributed/distributed.py $A --job_name=worker --task_index=0 > gpurun_out/mlp_worker_$tr.log 2>&1
         rc=$?; wait $PSPID; echo "mlp $tr rc=$rc"; tail -4 gpurun_out/mlp_worker_$tr.log; [ $rc -eq 0 ] || exit $rc
       done ;;
+    diagrccl)
+      for d in 18 50; do
+        RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29531 TFX_DP_FORCE_COLLECTIVE=1 \
+          timeout -k 10 300 python scripts/diag_dp_rccl.py $d > gpurun_out/diag_rccl_$d.log 2>&1
+        rc=$?; echo "diagrccl $d rc=$rc"; grep -v amdgpu.ids gpurun_out/diag_rccl_$d.log | tail -6; [ $rc -eq 0 ] || exit $rc
+      done ;;
     labn)
-      for i in 1 2; do for v in 1 0; do
+      for i in 1 2 3; do for v in 1 0; do
         TFX_BN_LAST_ARRIVER=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_la${v}_$i.log 2>&1 || exit 1
       done; done
       grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_la*.log ;;

@@ -87,6 +87,17 @@ def graph_def(nodes: Sequence[Dict]) -> bytes:
     return bytes(out)
 
 
+def meta_graph_def(graph: bytes, tags: Sequence[str] = ()) -> bytes:
+    """Minimal MetaGraphDef: meta_info_def { meta_graph_version, tags*, tensorflow_version,
+    tensorflow_git_version } + graph_def (what TF1's FileWriter(graph=...) writes after the GraphDef
+    event, R/distributed/distributed.py:138)."""
+    info = _bytes_field(1, b"v1")
+    for t in tags:
+        info += _bytes_field(4, t.encode())
+    info += _bytes_field(5, b"tensorflow_examples_amd") + _bytes_field(6, b"mi355x-native")
+    return _bytes_field(1, info) + _bytes_field(2, bytes(graph))
+
+
 # ---------------------------------------------------------------- writer
 class FileWriter:
     def __init__(self, logdir: str, graph: Optional[Union[bytes, Sequence[Dict]]] = None, filename_suffix: str = ""):
@@ -102,10 +113,17 @@ class FileWriter:
             raise OSError(f"cannot open event file {path}")
         if graph is not None:
             self.add_graph(graph)
+            self.add_meta_graph(graph)
 
     def add_graph(self, graph: Union[bytes, Sequence[Dict]], step: int = 0) -> None:
         data = graph if isinstance(graph, (bytes, bytearray)) else graph_def(graph)
         runtime.lib().tfx_events_add_bytes(self._h, int(step), time.time(), 4, bytes(data), len(data))
+
+    def add_meta_graph(self, graph: Union[bytes, Sequence[Dict]], step: int = 0) -> None:
+        """Event.meta_graph_def (field 9), as TF1's FileWriter writes it next to the GraphDef."""
+        g = graph if isinstance(graph, (bytes, bytearray)) else graph_def(graph)
+        data = meta_graph_def(g)
+        runtime.lib().tfx_events_add_bytes(self._h, int(step), time.time(), 9, bytes(data), len(data))
 
     def add_summary(self, summary: Union[Summary, bytes], global_step: Optional[int] = None) -> None:
         step = int(global_step or 0)
@@ -198,6 +216,8 @@ def summary_iterator(path: str) -> Iterator[Dict]:
             ev["file_version"] = f[3][0].decode()
         if 4 in f:
             ev["graph_def"] = f[4][0]
+        if 9 in f:
+            ev["meta_graph_def"] = f[9][0]
         if 5 in f:
             vals = []
             for vb in _parse(f[5][0]).get(1, []):
@@ -208,4 +228,4 @@ def summary_iterator(path: str) -> Iterator[Dict]:
 
 
 __all__ = ["Summary", "scalar", "merge_all", "FileWriter", "summary_iterator", "read_records", "graph_def",
-           "reset_registry"]
+           "meta_graph_def", "reset_registry"]

@@ -24,7 +24,7 @@ from tensorflow_examples_amd.train import ClassifierTrainer
 dev = init_distributed(backend="gloo", device="cuda")
 rank, world = dist.get_rank(), dist.get_world_size()
 depth = int(os.environ["DEPTH"])
-STEPS = int(os.environ.get('STEPS', '1'))
+STEPS = int(os.environ.get('DP_TEST_STEPS', '1'))
 
 def batch(r):
     g = torch.Generator().manual_seed(100 + r)

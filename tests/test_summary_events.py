@@ -33,6 +33,10 @@ def test_event_file_roundtrip(tmp_path):
     evs = list(summary.summary_iterator(files[0]))
     assert evs[0]["file_version"] == "brain.Event:2"
     assert b"Placeholder" in evs[1]["graph_def"]
+    # TF1 FileWriter(graph=...) also writes the MetaGraphDef (Event field 9) wrapping the same GraphDef
+    meta = summary._parse(evs[2]["meta_graph_def"])
+    assert meta[2][0] == evs[1]["graph_def"]
+    assert summary._parse(meta[1][0])[1][0] == b"v1"
     scal = [e for e in evs if "summary" in e]
     assert [e["step"] for e in scal] == list(range(5))
     assert scal[3]["summary"] == [("cost", -0.5), ("accuracy", 0.25)]
