@@ -1035,16 +1035,19 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
 
 // LDS-DMA ring depth for the main loop (0 = register-staged pipeline, 2 or 3 = ring depth, capped
 // per tile shape by the LDS budget).  Measured per mode on the ResNet-50 batch-256 layers
-// (profiles/r02_glds, scripts/conv_bench.py): the ring wins on the f32-atomic weight gradients
-// (-7 %, up to +40 % per layer) where a 3-deep ring fits next to the in-block split-K, and loses on
-// the bf16-output forward / data-gradient kernels (1 block per CU at a 3-deep ring vs 2 with the
-// register pipeline).  TFX_GLDS forces one depth everywhere; TFX_GLDS_WGRAD / TFX_GLDS_BF16 per mode.
+// (profiles/r02_glds, scripts/conv_bench.py): in isolation the ring wins on the f32-atomic weight
+// gradients (-7 %, up to +40 % per layer) where a 3-deep ring fits next to the in-block split-K, and
+// loses on the bf16-output forward / data-gradient kernels (1 block per CU at a 3-deep ring vs 2
+// with the register pipeline).  Inside the full training step the wgrad win does not survive
+// (bench.py 9.334 vs 9.266 ms/step, 3 runs each, profiles/r02_glds/step_ab.txt: the ring's
+// 1-block-per-CU occupancy leaves no room for the overlapping kernels), so every mode defaults to
+// the register pipeline.  TFX_GLDS forces one depth everywhere; TFX_GLDS_WGRAD / TFX_GLDS_BF16 per mode.
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
 int glds_stages(bool atomic_out, int g3) {
-  static const int all = env_int("TFX_GLDS", -1), wg = env_int("TFX_GLDS_WGRAD", 3), bf = env_int("TFX_GLDS_BF16", 0);
+  static const int all = env_int("TFX_GLDS", -1), wg = env_int("TFX_GLDS_WGRAD", 0), bf = env_int("TFX_GLDS_BF16", 0);
   if (all >= 0) return all;
   if (atomic_out) return g3 >= 3 ? wg : 0;
   return bf;

@@ -19,7 +19,7 @@ img = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, generator=g).to(
 lab = torch.randint(0, 10, (16,), generator=g).to(dev)
 x = to_model_input(img)
 res = {}
-for mode in ("none", "none2", "sum", "premul", "sum_nooverlap"):
+for mode in ("none", "none2", "sum", "premul", "sum_nooverlap", "premul_nooverlap", "premul_synced"):
     st, m = build_resnet_cifar(device=dev, depth=depth, dtype=torch.bfloat16, seed=0)
     dp = None
     if mode == "sum":
@@ -28,16 +28,34 @@ for mode in ("none", "none2", "sum", "premul", "sum_nooverlap"):
         dp = GradAllReduce(st, bucket_bytes=2 << 20, premul=2.0)
     elif mode == "sum_nooverlap":
         dp = GradAllReduce(st, bucket_bytes=2 << 20, overlap=False)
+    elif mode == "premul_nooverlap":
+        dp = GradAllReduce(st, bucket_bytes=2 << 20, overlap=False, premul=2.0)
+    elif mode == "premul_synced":
+        # every bucket launched from a fully drained device: isolates late gradient writes from
+        # RCCL's own premul-sum behaviour
+        dp = GradAllReduce(st, bucket_bytes=2 << 20, premul=2.0)
+        orig = dp._launch
+        dp._launch = lambda b, o=orig: (torch.cuda.synchronize(), o(b))
     st.zero_grad()
     ops.softmax_cross_entropy(m(x, training=True), lab).backward()
     if dp is not None:
         dp.finish()
     torch.cuda.synchronize()
-    res[mode] = (st.grad.clone() / (2.0 if mode == "premul" else 1.0), dp)
+    res[mode] = (st.grad.clone() / (2.0 if mode.startswith("premul") else 1.0), dp, st)
 ref = res["none"][0]
 buckets = res["sum"][1].buckets
-for mode in ("none2", "sum", "premul", "sum_nooverlap"):
+for mode in ("none2", "sum", "premul", "sum_nooverlap", "premul_nooverlap", "premul_synced"):
     gm = res[mode][0]
     rel = ((gm - ref).norm() / ref.norm()).item()
     per = [((gm[lo:hi] - ref[lo:hi]).norm() / (ref[lo:hi].norm() + 1e-30)).item() for lo, hi in buckets]
     print("%-14s rel %.3e  per-bucket %s" % (mode, rel, " ".join("%.1e" % p for p in per)), flush=True)
+    if mode.startswith("premul"):
+        st = res[mode][2]
+        for v in st.trainable():
+            a, r = gm[v.offset:v.offset + v.numel], ref[v.offset:v.offset + v.numel]
+            e = ((a - r).norm() / (r.norm() + 1e-30)).item()
+            if e > 1e-4:
+                bad = (a - r).abs() > 1e-3 * r.abs().max()
+                ratio = (a[bad] / r[bad]).median().item() if bad.any() else float("nan")
+                print("   %-40s bucket %d rel %.2e bad %d/%d median ratio %.3f" % (
+                    v.name, res["sum"][1].var_bucket.get(v.index, -1), e, int(bad.sum()), v.numel, ratio), flush=True)

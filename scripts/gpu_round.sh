@@ -132,7 +132,7 @@ for s in $STEPS; do
       for d in 18 50; do
         RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29531 TFX_DP_FORCE_COLLECTIVE=1 \
           timeout -k 10 300 python scripts/diag_dp_rccl.py $d > gpurun_out/diag_rccl_$d.log 2>&1
-        rc=$?; echo "diagrccl $d rc=$rc"; grep -v amdgpu.ids gpurun_out/diag_rccl_$d.log | tail -6; [ $rc -eq 0 ] || exit $rc
+        rc=$?; echo "diagrccl $d rc=$rc"; grep -v amdgpu.ids gpurun_out/diag_rccl_$d.log | tail -40; [ $rc -eq 0 ] || exit $rc
       done ;;
     labn)
       for i in 1 2 3; do for v in 1 0; do

@@ -30,7 +30,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
-from ..variables import Variable, VariableStore
+from ..variables import ALIGN, Variable, VariableStore
 
 
 class GradAllReduce:
@@ -94,7 +94,11 @@ class GradAllReduce:
 
     def _close(self, vs: List[Variable]) -> None:
         lo = min(v.offset for v in vs)
-        hi = max(v.offset + v.numel for v in vs)
+        # every bucket spans whole ALIGN-element (256-B) granules: the store pads each variable to
+        # ALIGN, so the padding is zeros owned by nobody.  RCCL's pre-multiplied sum left the tail
+        # of a bucket ending mid-granule unscaled (ResNet fc/bias, 10 floats: profiles/r02_dp/
+        # diag_rccl_18.log) -- keep every collective on a 256-B multiple.
+        hi = min(self.store.total, -(-max(v.offset + v.numel for v in vs) // ALIGN) * ALIGN)
         b = len(self.buckets)
         self.buckets.append([lo, hi])
         self.members.append(list(vs))
