@@ -179,6 +179,13 @@ void lstm_cell_fwd(const float* gx, const float* gh, const float* bias, const fl
                    float* act, float* c, float* h, uint16_t* h16, hipStream_t s);
 void lstm_cell_bwd(const float* act, const float* c, const float* c_prev, const float* dh, const float* dc_next,
                    int B, int H, float* dgates, uint16_t* dg16, float* dc_prev, hipStream_t s);
+// persistent whole-sequence recurrence (lstm_seq.hip): one launch per layer and direction
+int lstm_seq_sync_words(int B);
+bool lstm_seq_supported(int B, int H, int num_cus);
+void lstm_seq_fwd(const float* gx, const uint16_t* whh, int T, int B, int H, uint16_t* hbuf, float* cbuf, float* act,
+                  float* hT, unsigned* sync, hipStream_t s);
+void lstm_seq_bwd(const float* act, const float* cbuf, const float* dH, const float* dc_in, const uint16_t* whh, int T,
+                  int B, int H, uint16_t* dg, float* dc_out, unsigned* sync, hipStream_t s);
 
 // ---------------------------------------------------------------- input pipeline
 // uint8 NHWC [npix][cin] (cin <= 4) -> bf16 NHWC [npix][cout] (cout 4 or 8): (x/255 - mean)/std, zero pad

@@ -891,6 +891,57 @@ void lstm_cell_bwd(Tensor act, Tensor c, optional<Tensor> c_prev, optional<Tenso
                      fpm(dgates), d16, fpm(dc_prev), cur_stream());
 }
 
+// Whole-sequence persistent LSTM (lstm_seq.hip).  gx [T,B,4H] f32 (input projection + bias),
+// whh [4H,H] bf16; hbuf [T+1,B,H] bf16 and cbuf [T+1,B,H] f32 with h0 / c0 in slot 0; act [T,B,4H]
+// f32 and hT [B,H] f32 are written.  Returns the launch's status word (int32 [1]; nonzero = a
+// hand-off wait exceeded its bound and the results are invalid).
+bool lstm_seq_supported(int64_t B, int64_t H) {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return tfx::lstm_seq_supported((int)B, (int)H, cus);
+}
+
+Tensor lstm_seq_fwd(Tensor gx, Tensor whh, Tensor hbuf, Tensor cbuf, Tensor act, Tensor hT) {
+  CHECK_DEV(gx); CHECK_F32(gx); CHECK_CONTIG(gx); CHECK_BF16(whh); CHECK_CONTIG(whh);
+  CHECK_BF16(hbuf); CHECK_CONTIG(hbuf); CHECK_F32(cbuf); CHECK_CONTIG(cbuf); CHECK_F32(act); CHECK_CONTIG(act);
+  CHECK_F32(hT); CHECK_CONTIG(hT);
+  TORCH_CHECK(hbuf.dim() == 3, "hbuf must be [T+1,B,H]");
+  const int64_t T = hbuf.size(0) - 1, B = hbuf.size(1), H = hbuf.size(2);
+  TORCH_CHECK(T >= 1 && lstm_seq_supported(B, H), "lstm_seq: unsupported shape (B%16, H in 128..1024, grid <= CUs)");
+  TORCH_CHECK(gx.numel() == T * B * 4 * H && act.numel() == T * B * 4 * H && cbuf.numel() == (T + 1) * B * H &&
+                  whh.numel() == 4 * H * H && hT.numel() == B * H, "lstm_seq_fwd shapes");
+  TORCH_CHECK(T * B * 4 * H * 4 < (int64_t(1) << 31), "lstm_seq: tensors must be < 2 GiB");
+  for (const Tensor* t : {&gx, &whh, &hbuf}) check_aligned16(*t, "lstm_seq operand");
+  Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B)}, gx.options().dtype(at::kInt));
+  tfx::lstm_seq_fwd(gx.data_ptr<float>(), bf(whh), (int)T, (int)B, (int)H, bfm(hbuf), cbuf.data_ptr<float>(),
+                    act.data_ptr<float>(), hT.data_ptr<float>(), reinterpret_cast<unsigned*>(sync.data_ptr()),
+                    cur_stream());
+  return sync.narrow(0, sync.numel() - 32, 1);
+}
+
+// act, cbuf from the forward; dH [T,B,H] f32 = gradient of every h_t from outside the recurrence
+// (h_T's own gradient folded into dH[T-1]); dc_in = gradient of c_T (optional).  Writes dg [T,B,4H]
+// bf16 (gate pre-activation gradients) and optionally dc_out [B,H] (gradient of c_0).
+Tensor lstm_seq_bwd(Tensor act, Tensor cbuf, Tensor dH, optional<Tensor> dc_in, Tensor whh, Tensor dg,
+                    optional<Tensor> dc_out) {
+  CHECK_DEV(act); CHECK_F32(act); CHECK_CONTIG(act); CHECK_F32(cbuf); CHECK_CONTIG(cbuf);
+  CHECK_F32(dH); CHECK_CONTIG(dH); CHECK_BF16(whh); CHECK_CONTIG(whh); CHECK_BF16(dg); CHECK_CONTIG(dg);
+  TORCH_CHECK(cbuf.dim() == 3, "cbuf must be [T+1,B,H]");
+  const int64_t T = cbuf.size(0) - 1, B = cbuf.size(1), H = cbuf.size(2);
+  TORCH_CHECK(T >= 1 && lstm_seq_supported(B, H), "lstm_seq: unsupported shape");
+  TORCH_CHECK(act.numel() == T * B * 4 * H && dg.numel() == T * B * 4 * H && dH.numel() == T * B * H &&
+                  whh.numel() == 4 * H * H, "lstm_seq_bwd shapes");
+  for (const auto* t : {&dc_in, &dc_out})
+    if (fp(*t)) TORCH_CHECK((*t)->numel() == B * H && (*t)->is_contiguous() && (*t)->scalar_type() == at::kFloat,
+                            "lstm_seq_bwd state shape");
+  check_aligned16(dg, "dg");
+  Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B)}, act.options().dtype(at::kInt));
+  tfx::lstm_seq_bwd(act.data_ptr<float>(), cbuf.data_ptr<float>(), dH.data_ptr<float>(), fp(dc_in), bf(whh), (int)T,
+                    (int)B, (int)H, bfm(dg), fpm(dc_out), reinterpret_cast<unsigned*>(sync.data_ptr()), cur_stream());
+  return sync.narrow(0, sync.numel() - 32, 1);
+}
+
 void philox_fill(Tensor out, int64_t seed, int64_t subseq, int64_t dist, double a, double b) {
   CHECK_DEV(out); CHECK_F32(out); CHECK_CONTIG(out);
   TORCH_CHECK(dist >= 0 && dist <= 2, "philox dist");
@@ -936,6 +987,9 @@ TORCH_LIBRARY(tfx, m) {
   m.def("skipgram_batch", &skipgram_batch);
   m.def("lstm_cell_fwd", &lstm_cell_fwd);
   m.def("lstm_cell_bwd", &lstm_cell_bwd);
+  m.def("lstm_seq_supported", &lstm_seq_supported);
+  m.def("lstm_seq_fwd", &lstm_seq_fwd);
+  m.def("lstm_seq_bwd", &lstm_seq_bwd);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("conv_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "

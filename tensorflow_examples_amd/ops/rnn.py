@@ -15,12 +15,19 @@ backward:
     dW_hh += dG^T @ H_prev,  dW_ih += dG^T @ X,  dX = dG @ W_ih     three GEMMs over ALL steps
 so only the inherently sequential part (one small GEMM + one pointwise kernel per step and
 direction) runs T times; the weight gradients are batched over time into large GEMMs.
+
+Persistent recurrence (default where it fits: B % 16 == 0, H in {128, 256, 512, 1024},
+(B/16)*(H/16) <= CUs): the whole time loop of each direction is ONE kernel
+(csrc/kernels/lstm_seq.hip) -- W_hh stays in VGPRs, h_t / dg_t move between workgroups through
+write-through stores and per-row-block counters -- so the 2T dependent launches per direction
+become one.  ``TFX_LSTM_PERSISTENT=0`` selects the per-step kernels above.
 Gate order: i, f, g, o (f gets ``forget_bias`` added in the pointwise kernel through ``b``).
 The whole step is HIP-graph capturable (no host syncs), which removes the per-step launch cost.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+import os
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -46,7 +53,23 @@ def _lstm_ref(x, w_ih, w_hh, b, h0, c0):
     return torch.stack(outs), h, c
 
 
+_SEQ_OK: Dict[Tuple[int, int, int], bool] = {}
+
+
+def _persistent(B: int, H: int, dev: torch.device) -> bool:
+    if os.environ.get("TFX_LSTM_PERSISTENT", "1") == "0":
+        return False
+    key = (B, H, dev.index or 0)
+    if key not in _SEQ_OK:
+        _SEQ_OK[key] = bool(torch.ops.tfx.lstm_seq_supported(B, H))
+    return _SEQ_OK[key]
+
+
 class _LSTMLayer(torch.autograd.Function):
+    # status words of the last persistent launches (nonzero = a hand-off wait hit its bound);
+    # read by the GPU tests, never synchronised on in the training step
+    last_status: Dict[str, torch.Tensor] = {}
+
     @staticmethod
     def forward(ctx, x, anchor, w_ih: Variable, w_hh: Variable, b: Variable, h0, c0):
         T, B, In = x.shape
@@ -68,9 +91,13 @@ class _LSTMLayer(torch.autograd.Function):
         act = torch.empty(T, B, 4 * H, dtype=torch.float32, device=dev)
         hT = torch.empty(B, H, dtype=torch.float32, device=dev)
         gx = gx.view(T, B, 4 * H)
-        for t in range(T):
-            torch.ops.tfx.gemm_into(hbuf[t], w_hh.value, False, True, gx[t], True)
-            torch.ops.tfx.lstm_cell_fwd(gx[t], None, None, cbuf[t], act[t], cbuf[t + 1], hT, hbuf[t + 1])
+        ctx.persistent = _persistent(B, H, dev)
+        if ctx.persistent:
+            _LSTMLayer.last_status["fwd"] = torch.ops.tfx.lstm_seq_fwd(gx, w_hh.value, hbuf, cbuf, act, hT)
+        else:
+            for t in range(T):
+                torch.ops.tfx.gemm_into(hbuf[t], w_hh.value, False, True, gx[t], True)
+                torch.ops.tfx.lstm_cell_fwd(gx[t], None, None, cbuf[t], act[t], cbuf[t + 1], hT, hbuf[t + 1])
         ctx.save_for_backward(xf, hbuf, cbuf, act)
         return hbuf[1:], hT, cbuf[T].clone()
 
@@ -103,13 +130,17 @@ class _LSTMLayer(torch.autograd.Function):
             torch.zeros(T, B, H, dtype=torch.float32, device=xf.device)
         if g_hT is not None:
             dH[T - 1].add_(g_hT)
-        dc = g_cT.float().contiguous().clone() if g_cT is not None else \
-            torch.zeros(B, H, dtype=torch.float32, device=xf.device)
         dg = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=xf.device)
-        for t in range(T - 1, -1, -1):
-            torch.ops.tfx.lstm_cell_bwd(act[t], cbuf[t + 1], cbuf[t], dH[t], dc, None, dg[t], dc)
-            if t > 0:
-                torch.ops.tfx.gemm_into(dg[t], w_hh.value, False, False, dH[t - 1], True)
+        if ctx.persistent:
+            dc_in = g_cT.float().contiguous() if g_cT is not None else None
+            _LSTMLayer.last_status["bwd"] = torch.ops.tfx.lstm_seq_bwd(act, cbuf, dH, dc_in, w_hh.value, dg, None)
+        else:
+            dc = g_cT.float().contiguous().clone() if g_cT is not None else \
+                torch.zeros(B, H, dtype=torch.float32, device=xf.device)
+            for t in range(T - 1, -1, -1):
+                torch.ops.tfx.lstm_cell_bwd(act[t], cbuf[t + 1], cbuf[t], dH[t], dc, None, dg[t], dc)
+                if t > 0:
+                    torch.ops.tfx.gemm_into(dg[t], w_hh.value, False, False, dH[t - 1], True)
         dgf = dg.view(T * B, 4 * H)
         if w_hh.trainable:
             torch.ops.tfx.gemm_into(dgf, hbuf[:T].reshape(T * B, H), True, False, w_hh.grad, True)

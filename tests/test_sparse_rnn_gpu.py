@@ -159,9 +159,13 @@ def test_lstm_cell_kernels(gpu):
     assert _rel(dg, gz) < 1e-5 and _rel(dcp, gc) < 1e-5 and _rel(dg16, gz) < 5e-3
 
 
-def test_lstm_layer_vs_reference(gpu):
+@pytest.mark.parametrize("persistent", ["1", "0"])
+@pytest.mark.parametrize("T,B,In,H", [(12, 16, 64, 128), (100, 64, 128, 512), (7, 32, 256, 256)])
+def test_lstm_layer_vs_reference(gpu, monkeypatch, persistent, T, B, In, H):
+    """Whole layer (persistent whole-sequence kernel, or the per-step kernels) vs the fp32 PyTorch
+    reference with the same bf16-rounded weights; every output and gradient, incl. h_T / c_T grads."""
+    monkeypatch.setenv("TFX_LSTM_PERSISTENT", persistent)
     torch.manual_seed(0)
-    T, B, In, H = 12, 16, 64, 128
     store = VariableStore(device=gpu, compute_dtype=torch.bfloat16, seed=1)
     w_ih = store.variable([4 * H, In], Uniform(-0.1, 0.1), name="w_ih")
     w_hh = store.variable([4 * H, H], Uniform(-0.1, 0.1), name="w_hh")
@@ -170,18 +174,49 @@ def test_lstm_layer_vs_reference(gpu):
     x = torch.randn(T, B, In, device=gpu).to(torch.bfloat16).requires_grad_(True)
     h0, c0 = torch.randn(B, H, device=gpu) * 0.5, torch.randn(B, H, device=gpu) * 0.5
     store.zero_grad()
-    out, (hT, cT) = ops.lstm_layer(x, w_ih, w_hh, b, (h0, c0))
+    rnn_ops._LSTMLayer.last_status.clear()
+    out, hT, cT = rnn_ops._LSTMLayer.apply(x, w_ih.store.anchor, w_ih, w_hh, b, h0, c0)
     gout = torch.randn(T, B, H, device=gpu)
-    out.backward(gout.to(out.dtype))
-    # fp32 reference with the same bf16-rounded weights
+    ghT, gcT = torch.randn(B, H, device=gpu), torch.randn(B, H, device=gpu)
+    torch.autograd.backward([out, hT, cT], [gout.to(out.dtype), ghT, gcT])
+    if persistent == "1":
+        assert set(rnn_ops._LSTMLayer.last_status) == {"fwd", "bwd"}
+        assert all(int(v.item()) == 0 for v in rnn_ops._LSTMLayer.last_status.values())
+    else:
+        assert not rnn_ops._LSTMLayer.last_status
     ps = [v.value.float().clone().requires_grad_(True) for v in (w_ih, w_hh)] + [b.master.clone().requires_grad_(True)]
     xr = x.detach().float().requires_grad_(True)
     outr, hr, cr = rnn_ops._lstm_ref(xr, *ps, h0, c0)
-    gr = torch.autograd.grad(outr, [xr] + ps, gout.to(torch.bfloat16).float())
+    gr = torch.autograd.grad([outr, hr, cr], [xr] + ps, [gout.to(torch.bfloat16).float(), ghT, gcT])
     assert _rel(out, outr) < 1e-2 and _rel(hT, hr) < 1e-2 and _rel(cT, cr) < 1e-2
     assert _rel(x.grad, gr[0]) < 3e-2
     for v, g in zip((w_ih, w_hh, b), gr[1:]):
         assert _rel(v.grad, g) < 3e-2, v.name
+
+
+def test_lstm_persistent_matches_per_step(gpu, monkeypatch):
+    """The persistent kernel and the per-step kernels compute the same recurrence: outputs agree to
+    bf16 rounding of h_t, repeated launches (graph-replay style reuse of the counters) included."""
+    T, B, In, H = 50, 64, 128, 512
+    torch.manual_seed(3)
+    store = VariableStore(device=gpu, compute_dtype=torch.bfloat16, seed=4)
+    w_ih = store.variable([4 * H, In], Uniform(-0.1, 0.1), name="w_ih")
+    w_hh = store.variable([4 * H, H], Uniform(-0.1, 0.1), name="w_hh")
+    b = store.variable([4 * H], Uniform(-0.1, 0.1), name="b")
+    store.finalize()
+    x = torch.randn(T, B, In, device=gpu).to(torch.bfloat16)
+    res = {}
+    for mode in ("0", "1", "1"):
+        monkeypatch.setenv("TFX_LSTM_PERSISTENT", mode)
+        store.zero_grad()
+        out, (hT, cT) = ops.lstm_layer(x.clone().requires_grad_(True), w_ih, w_hh, b)
+        out.float().sum().backward()
+        res.setdefault(mode, []).append((out.float(), hT, cT, store.grad.clone()))
+    ref = res["0"][0]
+    for got in res["1"]:
+        for a, r in zip(got, ref):
+            assert _rel(a, r) < 2e-2
+    assert torch.equal(res["1"][0][0], res["1"][1][0])  # deterministic
 
 
 # ---------------------------------------------------------------- models
