@@ -150,6 +150,8 @@ void sse_bwd(const float* p, const float* y, const float* g, int64_t n, float* d
 // dz = g * act'(y) (act 0 none, 1 relu, 2 sigmoid, y = the activation OUTPUT); dbias += column sums
 void act_bwd_colsum(const float* g, const float* y, int act, int64_t M, int N, float* dz, float* dbias,
                     hipStream_t s);
+void act_bwd_colsum_bf16(const uint16_t* g, const uint16_t* y, int act, int64_t M, int N, uint16_t* dz,
+                         float* dbias, hipStream_t s);
 // y = x * scal[0] (f32 or bf16 output)
 void scale_by_scalar(const float* x, const float* scal, int64_t n, float* y32, uint16_t* y16, hipStream_t s);
 
@@ -184,8 +186,9 @@ int lstm_seq_sync_words(int B);
 bool lstm_seq_supported(int B, int H, int num_cus);
 void lstm_seq_fwd(const float* gx, const uint16_t* whh, int T, int B, int H, uint16_t* hbuf, float* cbuf, float* act,
                   float* hT, unsigned* sync, hipStream_t s);
-void lstm_seq_bwd(const float* act, const float* cbuf, const float* dH, const float* dc_in, const uint16_t* whh, int T,
-                  int B, int H, uint16_t* dg, float* dc_out, unsigned* sync, hipStream_t s);
+void lstm_seq_bwd(const float* act, const float* cbuf, const uint16_t* dH, const float* dhT, const float* dc_in,
+                  const uint16_t* whh, int T, int B, int H, uint16_t* dg, float* dc_out, float* dbias, unsigned* sync,
+                  hipStream_t s);
 
 // ---------------------------------------------------------------- input pipeline
 // uint8 NHWC [npix][cin] (cin <= 4) -> bf16 NHWC [npix][cout] (cout 4 or 8): (x/255 - mean)/std, zero pad

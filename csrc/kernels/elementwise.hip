@@ -94,10 +94,17 @@ __global__ void __launch_bounds__(256) sse_bwd_kernel(const float* __restrict__ 
     dp[i] = 2.f * (p[i] - y[i]) * gg;
 }
 
-// dz = g * act'(y); dbias[c] += sum_rows dz.  Block = 64 columns x 4 row lanes.
-template <int ACT>
-__global__ void __launch_bounds__(256) act_bwd_colsum_kernel(const float* __restrict__ g, const float* __restrict__ y,
-                                                             int64_t M, int N, float* __restrict__ dz,
+// dz = g * act'(y); dbias[c] += sum_rows dz.  Block = 64 columns x 4 row lanes.  T = float, or
+// uint16_t for bf16 g / y / dz (the bf16 dense layers: ReLU mask + bias column-sum in one pass;
+// dz == nullptr when the caller needs only the column sums).
+__device__ __forceinline__ float ld_as_f32(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float ld_as_f32(const uint16_t* p, int64_t i) { return bf16_to_f32(p[i]); }
+__device__ __forceinline__ void st_from_f32(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void st_from_f32(uint16_t* p, int64_t i, float v) { p[i] = f32_to_bf16(v); }
+
+template <int ACT, typename T>
+__global__ void __launch_bounds__(256) act_bwd_colsum_kernel(const T* __restrict__ g, const T* __restrict__ y,
+                                                             int64_t M, int N, T* __restrict__ dz,
                                                              float* __restrict__ dbias) {
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
@@ -105,10 +112,13 @@ __global__ void __launch_bounds__(256) act_bwd_colsum_kernel(const float* __rest
   if (c < N) {
     for (int64_t r = (int64_t)blockIdx.y * 4 + ty; r < M; r += (int64_t)gridDim.y * 4) {
       const int64_t i = r * N + c;
-      float d = g[i];
-      if (ACT == 1) d = y[i] > 0.f ? d : 0.f;
-      if (ACT == 2) d = d * y[i] * (1.f - y[i]);  // TF1 SigmoidGrad: dy * y * (1 - y)
-      dz[i] = d;
+      float d = ld_as_f32(g, i);
+      if (ACT == 1) d = ld_as_f32(y, i) > 0.f ? d : 0.f;
+      if (ACT == 2) {
+        const float yv = ld_as_f32(y, i);
+        d = d * yv * (1.f - yv);  // TF1 SigmoidGrad: dy * y * (1 - y)
+      }
+      if (dz) st_from_f32(dz, i, d);
       s += d;
     }
   }
@@ -163,12 +173,22 @@ void sse_bwd(const float* p, const float* y, const float* g, int64_t n, float* d
   sse_bwd_kernel<<<egrid(n), 256, 0, s>>>(p, y, g, n, dp);
 }
 
+template <typename T>
+void act_bwd_colsum_t(const T* g, const T* y, int act, int64_t M, int N, T* dz, float* dbias, hipStream_t s) {
+  dim3 grid((N + 63) / 64, (unsigned)std::max<int64_t>(1, std::min<int64_t>((M + 63) / 64, 256)));
+  if (act == 1) act_bwd_colsum_kernel<1, T><<<grid, 256, 0, s>>>(g, y, M, N, dz, dbias);
+  else if (act == 2) act_bwd_colsum_kernel<2, T><<<grid, 256, 0, s>>>(g, y, M, N, dz, dbias);
+  else act_bwd_colsum_kernel<0, T><<<grid, 256, 0, s>>>(g, y, M, N, dz, dbias);
+}
+
 void act_bwd_colsum(const float* g, const float* y, int act, int64_t M, int N, float* dz, float* dbias,
                     hipStream_t s) {
-  dim3 grid((N + 63) / 64, (unsigned)std::max<int64_t>(1, std::min<int64_t>((M + 63) / 64, 256)));
-  if (act == 1) act_bwd_colsum_kernel<1><<<grid, 256, 0, s>>>(g, y, M, N, dz, dbias);
-  else if (act == 2) act_bwd_colsum_kernel<2><<<grid, 256, 0, s>>>(g, y, M, N, dz, dbias);
-  else act_bwd_colsum_kernel<0><<<grid, 256, 0, s>>>(g, y, M, N, dz, dbias);
+  act_bwd_colsum_t<float>(g, y, act, M, N, dz, dbias, s);
+}
+
+void act_bwd_colsum_bf16(const uint16_t* g, const uint16_t* y, int act, int64_t M, int N, uint16_t* dz,
+                         float* dbias, hipStream_t s) {
+  act_bwd_colsum_t<uint16_t>(g, y, act, M, N, dz, dbias, s);
 }
 
 void scale_by_scalar(const float* x, const float* scal, int64_t n, float* y32, uint16_t* y16, hipStream_t s) {

@@ -8,8 +8,84 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 namespace tfx {
+
+// ------------------------------------------------------------------ measured launch configurations
+// Written at import (tensorflow_examples_amd/ops/tuning.py loads the committed table) or by the
+// tuner; read on every launch.  A mutex keeps the rare writes and the reads apart (autograd's device
+// thread launches the backward kernels).
+namespace {
+struct TuneEntry {
+  int fam, M, N, K;
+  TuneCfg c;
+};
+std::mutex g_tune_mu;
+std::vector<TuneEntry> g_tune;
+TuneCfg g_force[FAM_COUNT];
+bool g_forced[FAM_COUNT] = {};
+bool g_tracing = false;
+std::vector<int> g_trace;
+}  // namespace
+
+bool igemm_tune_lookup(int fam, int M, int N, int K, TuneCfg* out) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  if (g_tracing) g_trace.insert(g_trace.end(), {fam, M, N, K});
+  if (fam < 0 || fam >= FAM_COUNT) return false;
+  if (g_forced[fam]) {
+    *out = g_force[fam];
+    return true;
+  }
+  for (const auto& e : g_tune)
+    if (e.fam == fam && e.M == M && e.N == N && e.K == K) {
+      *out = e.c;
+      return true;
+    }
+  return false;
+}
+
+void igemm_tune_set(int fam, int M, int N, int K, TuneCfg c) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  for (auto& e : g_tune)
+    if (e.fam == fam && e.M == M && e.N == N && e.K == K) {
+      e.c = c;
+      return;
+    }
+  g_tune.push_back({fam, M, N, K, c});
+}
+
+void igemm_tune_clear() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tune.clear();
+}
+
+void igemm_tune_force(int fam, TuneCfg c) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  if (fam < 0) {
+    for (int i = 0; i < FAM_COUNT; ++i) g_forced[i] = false;
+    return;
+  }
+  if (fam < FAM_COUNT) {
+    g_force[fam] = c;
+    g_forced[fam] = true;
+  }
+}
+
+void igemm_tune_trace(bool on) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  if (on) g_trace.clear();
+  g_tracing = on;
+}
+
+int igemm_tune_traced(int* out, int cap) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  const int n = (int)g_trace.size() / 4;
+  for (int i = 0; i < n && 4 * i + 3 < cap; ++i)
+    for (int j = 0; j < 4; ++j) out[4 * i + j] = g_trace[4 * i + j];
+  return n;
+}
 
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
   if (a.out_mode == OUT_F32_ATOMIC && a.zero_out) {

@@ -1053,6 +1053,9 @@ int glds_stages(bool atomic_out, int g3) {
   return bf;
 }
 
+// launch configuration of the current launch_shape call (igemm_tune_lookup), read by launch_t
+thread_local TuneCfg g_tc;
+
 int pick_splits(int tiles, int nkt, int want_blocks, int min_kps = 4) {
   if (tiles >= want_blocks) return 1;
   // floor: never more blocks than the target (1 or 2 per CU) -- a few CUs holding an extra block
@@ -1074,13 +1077,15 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
     const char* e = getenv("TFX_SPLITK_BLOCKS");
     return e ? atoi(e) : 256;  // one block per CU: measured best (fewer f32 atomic partials)
   }();
-  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, want * want_mult, min_kps);
+  const int want_blocks = g_tc.want > 0 ? g_tc.want : want * want_mult;
+  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, want_blocks, min_kps);
   a.kps = (nkt + splits - 1) / splits;
   if constexpr (KS == 2) {
     // each 4-wave group takes kps/2 k-tiles: a multiple of 4 keeps both halves even (no zero step).
     // An 8-wave block holds its CU's LDS alone, so more blocks than CUs would run a second wave
     // (e.g. 144 tiles x 2 splits): the 4-wave form fits those at two blocks per CU.
-    if (a.kps < 4 || tiles * splits > want) return launch_t<AK, BK, BM, BN, EPI, 1>(a, s, want_mult, min_kps);
+    if (a.kps < 4 || tiles * splits > (g_tc.want > 0 ? g_tc.want : want))
+      return launch_t<AK, BK, BM, BN, EPI, 1>(a, s, want_mult, min_kps);
     a.kps = (a.kps + 3) & ~3;
   } else if (splits > 1) {
     a.kps += a.kps & 1;  // even k-tiles per split: no zero step in the loop
@@ -1092,7 +1097,7 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
   constexpr int STAGE_B = (BM + BN) * BKT * 2;
   constexpr int G3 = KS * 3 * STAGE_B <= 163840 ? 3 : 2;
-  const int gls = glds_stages(a.out_mode == OUT_F32_ATOMIC, G3);
+  const int gls = g_tc.gls >= 0 ? g_tc.gls : glds_stages(a.out_mode == OUT_F32_ATOMIC, G3);
   if (gls > 0) {
     // LDS-DMA ring: single k-tile -> GLS 1; otherwise the deepest ring (<= 3) that fits the LDS
     const bool single = nkt == 1 && splits == 1;
@@ -1169,10 +1174,28 @@ int skinny_min_kps() {
 }
 
 template <int AK, int BK, bool ALLOW256 = true, int EPI = EPI_PLAIN>
-void launch_shape(IgemmArgs& a, hipStream_t s) {
+void launch_shape(IgemmArgs& a, hipStream_t s, int fam = -1) {
+  TuneCfg tc;
+  const bool tuned = igemm_tune_lookup(fam, a.M, a.N, a.K, &tc);
+  g_tc = tuned ? tc : TuneCfg{};
+  if (tuned && tc.tile > 0) {
+    if constexpr (!ALLOW256) {
+      if (tc.ks == 2 || (tc.ks == 0 && wgrad_ks() == 2)) {
+        if (tc.tile == 2) return launch_t<AK, BK, 128, 64, EPI, 2>(a, s);
+        return launch_t<AK, BK, 128, 128, EPI, 2>(a, s);
+      }
+      if (tc.tile == 2) return launch_t<AK, BK, 128, 64, EPI>(a, s, 2);
+      return launch_t<AK, BK, 128, 128, EPI>(a, s);
+    } else {
+      if (tc.tile == 3) return launch_t<AK, BK, 256, 64, EPI>(a, s);
+      if (tc.tile == 2) return launch_t<AK, BK, 128, 64, EPI>(a, s);
+      return launch_t<AK, BK, 128, 128, EPI>(a, s);
+    }
+  }
   if constexpr (!ALLOW256) {
     const bool dense_pair = (AK == MN_DENSE && BK == MN_DENSE) || (a.R == 1 && a.S == 1);  // 1x1 (any stride)
-    if (wgrad_ks() == 2) {
+    const bool ks2 = tuned && tc.ks > 0 ? tc.ks == 2 : wgrad_ks() == 2;
+    if (ks2) {
       // 8-wave blocks, one per CU: 128x64 tiles for the dense pair (half the atomic bytes of the
       // 2-blocks-per-CU 128x64 form), 128x128 for the im2col-gathered ones
       if (a.N <= 64 || (dense_pair && wgrad_tile() != 128) || wgrad_tile() == 64)
@@ -1197,9 +1220,9 @@ void launch_shape(IgemmArgs& a, hipStream_t s) {
 
 
 template <int AK, int BK, int EPI_ON>
-void launch_epi(IgemmArgs& a, hipStream_t s) {
-  if (a.stats || a.bnb_x) launch_shape<AK, BK, true, EPI_ON>(a, s);
-  else launch_shape<AK, BK, true, EPI_PLAIN>(a, s);
+void launch_epi(IgemmArgs& a, hipStream_t s, int fam) {
+  if (a.stats || a.bnb_x) launch_shape<AK, BK, true, EPI_ON>(a, s, fam);
+  else launch_shape<AK, BK, true, EPI_PLAIN>(a, s, fam);
 }
 
 }  // namespace

@@ -2,5 +2,5 @@
 #include "igemm_impl.h"
 
 namespace tfx {
-void igemm_wgrad_dense(IgemmArgs& a, hipStream_t s) { launch_shape<MN_DENSE, MN_DENSE, false>(a, s); }
+void igemm_wgrad_dense(IgemmArgs& a, hipStream_t s) { launch_shape<MN_DENSE, MN_DENSE, false>(a, s, FAM_WGRAD_DENSE); }
 }  // namespace tfx

@@ -21,16 +21,25 @@
 //                          a register and writes dg_t (bf16) for the recurrence AND for the
 //                          batched weight-gradient GEMMs that follow the launch.
 //
-// Inter-workgroup hand-off (cdna_hip_programming.md §6 Guideline 16, recipe R1 with sc1 loads,
-// MI355X_MICROARCH.md "Valid forms" table row 1): h_t / dg_t tiles are published with 16-byte
-// write-through (sc1) buffer stores by the row block's workgroups, every storing wave drains
-// vmcnt, a workgroup barrier, then ONE lane adds 1 to the row block's counter (agent-scope
-// atomic).  A consumer polls that counter relaxed (one lane, s_sleep between polls, bounded),
-// then a workgroup barrier, then reads the handed-off bytes ONLY with sc1 buffer loads (no
-// acquire fence needed; TFX_LSTM_ACQUIRE=1 adds one anyway).  A row block depends only on its own
-// 16 rows, so only H/16 workgroups meet on each counter.  Counters are zeroed by a memset node
-// before every launch; a spin that exceeds its bound sets the status word and the whole grid
-// drains (no hang).
+// Inter-workgroup hand-off of h_t / dg_t: every handed-off byte is written ONCE per launch (hbuf
+// and dg keep one slot per time step) with 16-byte write-through (sc1) buffer stores and read
+// ONLY with sc1 buffer loads (cdna_hip_programming.md §6 Guideline 16).  Two protocols:
+//
+//   PROTO_DATA (TFX_LSTM_PROTO=1): the data is its own flag.  A memset node fills the slots with 0xFFFF
+//     (a bf16 NaN bit pattern the producers never store: a computed NaN is canonicalised to
+//     0x7FC0) before the launch; a consumer wave re-loads the fragments it still lacks until none
+//     holds the sentinel -- no drain, no counter, no barrier between producer and consumer
+//     (MI355X_MICROARCH.md price list: handoff-1to1 ~0.8-1.0 us vs handoff-flag 1.7-1.9x that).
+//     Measured SLOWER here (char-LSTM 2x512: 2.13 vs 1.79 ms/step, profiles/r02_lstm): each
+//     consumer must re-read 16-64 KB of fragments per attempt, and the sentinel memsets add
+//     ~65 MB of writes per step.
+//   PROTO_COUNTER (default): every storing wave drains vmcnt, a workgroup barrier, ONE
+//     lane adds 1 to the row block's counter (agent-scope atomic); a consumer lane polls the
+//     counter relaxed, a workgroup barrier, then the sc1 loads (Valid forms table row 1;
+//     TFX_LSTM_ACQUIRE=1 adds an agent acquire anyway).
+//
+// A row block depends only on its own 16 rows.  Every spin is bounded: on expiry the status word
+// is set and the whole grid drains (no hang); the caller can read the status.
 #include <cstdlib>
 
 #include "tfx_common.h"
@@ -41,10 +50,14 @@ namespace {
 
 constexpr int LS_LDS = 96 * 1024;      // > 80 KB: one workgroup per CU (160 KB LDS)
 constexpr int LS_STRIDE = 32;          // u32 words per counter (own 128-B line)
-constexpr unsigned LS_SPIN_LIMIT = 1u << 22;
+constexpr unsigned LS_SPIN_LIMIT = 1u << 20;
+enum { PROTO_COUNTER = 0, PROTO_DATA = 1 };
+constexpr uint16_t LS_SENTINEL = 0xFFFF;
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+template <int NK>
+constexpr int H_of() { return NK * 32; }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ls_rsrc(const void* p, int64_t bytes) {
   const int n = bytes > 0x7fffffff ? 0x7fffffff : (int)bytes;
@@ -59,6 +72,43 @@ __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int off, u32x4v
 }
 
 __device__ __forceinline__ float ls_sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// bf16 for a handed-off slot: never the sentinel pattern (NaN -> canonical quiet NaN)
+__device__ __forceinline__ uint16_t ls_bf16(float f) {
+  const uint16_t b = f32_to_bf16(f);
+  return b == LS_SENTINEL ? (uint16_t)0x7FC0 : b;
+}
+
+__device__ __forceinline__ bool ls_ready(bf16x8_t v) {
+  const u32x4v w = __builtin_bit_cast(u32x4v, v);
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ok = ok && (w[i] & 0xFFFFu) != 0xFFFFu && (w[i] >> 16) != 0xFFFFu;
+  return ok;
+}
+
+// PROTO_DATA consumer, one wave: load N fragments (byte offsets off0 + 64 kk) and re-load the ones
+// still holding the sentinel until the whole wave has real data.  false = bound hit (status set).
+template <int N>
+__device__ __forceinline__ bool ls_poll_load(__amdgpu_buffer_rsrc_t r, int off0, bf16x8_t (&a)[N], gu32* status) {
+  static_assert(N <= 32, "pending mask");
+  unsigned pend = N == 32 ? 0xFFFFFFFFu : ((1u << N) - 1u);
+  for (unsigned spins = 0;; ++spins) {
+#pragma unroll
+    for (int kk = 0; kk < N; ++kk)
+      if (pend & (1u << kk)) a[kk] = ld_sc1(r, off0 + kk * 64);
+#pragma unroll
+    for (int kk = 0; kk < N; ++kk)
+      if ((pend & (1u << kk)) && ls_ready(a[kk])) pend &= ~(1u << kk);
+    if (__all(pend == 0)) return true;
+    if (spins >= LS_SPIN_LIMIT) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");  // the re-loads are real loads
+  }
+}
 
 // One lane: wait until *ctr >= target.  false = gave up (status word set).
 __device__ __forceinline__ bool ls_wait(gu32* ctr, unsigned target, gu32* status) {
@@ -96,7 +146,7 @@ __device__ __forceinline__ void ls_publish(gu32* ctr) {
 }
 
 // ------------------------------------------------------------------ forward
-template <int NK, bool ACQ>
+template <int NK, int PROTO, bool ACQ>
 __global__ void __launch_bounds__(256, 1)
     lstm_seq_fwd_kernel(const float* __restrict__ gx, const uint16_t* __restrict__ whh, int T, int B,
                         uint16_t* hbuf, float* __restrict__ cbuf, float* __restrict__ act, float* __restrict__ hT,
@@ -105,11 +155,12 @@ __global__ void __launch_bounds__(256, 1)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);                    // [wave][gate][lane][4]  16 KB
   uint16_t* hs = reinterpret_cast<uint16_t*>(smem + 16384);      // [row][unit] bf16       512 B
-  int* flag = reinterpret_cast<int*>(smem + 16384 + 512);
+  int* flag = reinterpret_cast<int*>(smem + 16384 + 512);         // [0] wait result, [1] abort
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int nub = gridDim.x, u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
   gu32* ctr = (gu32*)(sync + blockIdx.y * LS_STRIDE);
   gu32* status = (gu32*)(sync + gridDim.y * LS_STRIDE);
+  if (tid == 0) flag[1] = 0;
 
   // W_hh rows (gate q, unit u0 + lane%16), this wave's K quarter: B operand, resident all sequence
   bf16x8_t w[4][NKW];
@@ -125,16 +176,21 @@ __global__ void __launch_bounds__(256, 1)
   float c = cbuf[cidx];
   const int aoff = ((lane & 15) * H + wave * KQ + (lane >> 4) * 8) * 2;  // byte offset in a row tile
   const int rl = (cr >> 2) * 16 + cu, ri = cr & 3;                      // (lane, reg) holding (cr, cu)
+  __syncthreads();
 
   for (int t = 0; t < T; ++t) {
     const float* g = gx + (int64_t)t * 4 * BH + (int64_t)(r0 + cr) * 4 * H + u0 + cu;
     const float z0 = g[0], z1 = g[H], z2 = g[2 * H], z3 = g[3 * H];  // hoisted projection, pre-launch data
-    if (t > 0 && !ls_block_wait<ACQ>(ctr, (unsigned)(t * nub), status, flag)) return;
     const __amdgpu_buffer_rsrc_t hr = ls_rsrc(hbuf + t * BH + (int64_t)r0 * H, 16 * H * 2);
     bf16x8_t a[NKW];
+    if constexpr (PROTO == PROTO_DATA) {
+      if (!ls_poll_load<NKW>(hr, aoff, a, status)) flag[1] = 1;
+    } else {
+      if (t > 0 && !ls_block_wait<ACQ>(ctr, (unsigned)(t * nub), status, flag)) return;
 #pragma unroll
-    for (int kk = 0; kk < NKW; ++kk) a[kk] = ld_sc1(hr, aoff + kk * 64);
-    __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
+      for (int kk = 0; kk < NKW; ++kk) a[kk] = ld_sc1(hr, aoff + kk * 64);
+      __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
+    }
     f32x4_t acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -146,6 +202,7 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4_t*>(red + ((wave * 4 + q) * 64 + lane) * 4) = acc[q];
     __syncthreads();
+    if (PROTO == PROTO_DATA && flag[1]) return;  // a wave's wait expired: the whole grid drains
     float z[4] = {z0, z1, z2, z3};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -161,7 +218,7 @@ __global__ void __launch_bounds__(256, 1)
     ap[3 * H] = og;
     cbuf[(t + 1) * BH + cidx] = c;
     if (t == T - 1) hT[cidx] = h;
-    hs[cr * 16 + cu] = f32_to_bf16(h);
+    hs[cr * 16 + cu] = ls_bf16(h);
     __syncthreads();
     if (tid < 32) {
       const int row = tid >> 1, half = tid & 1;
@@ -169,16 +226,19 @@ __global__ void __launch_bounds__(256, 1)
       const __amdgpu_buffer_rsrc_t hw = ls_rsrc(hbuf + (t + 1) * BH + (int64_t)r0 * H, 16 * H * 2);
       st_sc1(hw, (row * H + u0 + half * 8) * 2, v);
     }
-    ls_publish(ctr);
+    if constexpr (PROTO == PROTO_COUNTER) ls_publish(ctr);
   }
 }
 
 // ------------------------------------------------------------------ backward
-template <int NK, bool ACQ>
+// dH (bf16, optional): gradient of every h_t from outside the recurrence; dhT / dc_in (f32,
+// optional): gradients of h_T / c_T; dbias (optional): += sum over t and rows of dgates (f32).
+template <int NK, int PROTO, bool ACQ>
 __global__ void __launch_bounds__(256, 1)
-    lstm_seq_bwd_kernel(const float* __restrict__ act, const float* __restrict__ cbuf, const float* __restrict__ dH,
+    lstm_seq_bwd_kernel(const float* __restrict__ act, const float* __restrict__ cbuf,
+                        const uint16_t* __restrict__ dH, const float* __restrict__ dhT,
                         const float* __restrict__ dc_in, const uint16_t* __restrict__ whh, int T, int B, uint16_t* dg,
-                        float* __restrict__ dc_out, unsigned* sync) {
+                        float* __restrict__ dc_out, float* __restrict__ dbias, unsigned* sync) {
   constexpr int H = NK * 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);                    // [wave][lane][4]  4 KB
@@ -188,6 +248,7 @@ __global__ void __launch_bounds__(256, 1)
   const int nub = gridDim.x, u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
   gu32* ctr = (gu32*)(sync + blockIdx.y * LS_STRIDE);
   gu32* status = (gu32*)(sync + gridDim.y * LS_STRIDE);
+  if (tid == 0) flag[1] = 0;
 
   // W_hh^T slice: B operand k = gate column q*H + kk*32 + (lane/16)*8 + e, n = unit u0 + lane%16
   bf16x8_t w[NK];
@@ -203,22 +264,29 @@ __global__ void __launch_bounds__(256, 1)
   const int64_t BH = (int64_t)B * H;
   float dc = dc_in ? dc_in[cidx] : 0.f;
   float cn = cbuf[T * BH + cidx];
+  float db0 = 0.f, db1 = 0.f, db2 = 0.f, db3 = 0.f;
   const int aoff = ((lane & 15) * 4 * H + wave * H + (lane >> 4) * 8) * 2;
   const int rl = (cr >> 2) * 16 + cu, ri = cr & 3;
+  __syncthreads();
 
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
     const float* ap = act + (int64_t)t * 4 * BH + (int64_t)(r0 + cr) * 4 * H + u0 + cu;
     const float ig = ap[0], fg = ap[H], gg = ap[2 * H], og = ap[3 * H];
     const float cp = cbuf[t * BH + cidx];
-    float dhv = dH[t * BH + cidx];
+    float dhv = dH ? bf16_to_f32(dH[t * BH + cidx]) : 0.f;
+    if (s == 0 && dhT) dhv += dhT[cidx];
     if (s > 0) {
-      if (!ls_block_wait<ACQ>(ctr, (unsigned)(s * nub), status, flag)) return;
       const __amdgpu_buffer_rsrc_t gr = ls_rsrc(dg + (t + 1) * 4 * BH + (int64_t)r0 * 4 * H, 16 * 4 * H * 2);
       bf16x8_t a[NK];
+      if constexpr (PROTO == PROTO_DATA) {
+        if (!ls_poll_load<NK>(gr, aoff, a, status)) flag[1] = 1;
+      } else {
+        if (!ls_block_wait<ACQ>(ctr, (unsigned)(s * nub), status, flag)) return;
 #pragma unroll
-      for (int kk = 0; kk < NK; ++kk) a[kk] = ld_sc1(gr, aoff + kk * 64);
-      __builtin_amdgcn_sched_barrier(0);
+        for (int kk = 0; kk < NK; ++kk) a[kk] = ld_sc1(gr, aoff + kk * 64);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NK; kk += 2) {
@@ -227,6 +295,7 @@ __global__ void __launch_bounds__(256, 1)
       }
       *reinterpret_cast<f32x4_t*>(red + (wave * 64 + lane) * 4) = acc0 + acc1;
       __syncthreads();
+      if (PROTO == PROTO_DATA && flag[1]) return;
 #pragma unroll
       for (int w2 = 0; w2 < 4; ++w2) dhv += red[(w2 * 64 + rl) * 4 + ri];
     }
@@ -234,13 +303,17 @@ __global__ void __launch_bounds__(256, 1)
     dc = fmaf(dhv * og, 1.f - tc * tc, dc);
     const float d0 = dc * gg * ig * (1.f - ig), d1 = dc * cp * fg * (1.f - fg);
     const float d2 = dc * ig * (1.f - gg * gg), d3 = dhv * tc * og * (1.f - og);
+    db0 += d0;
+    db1 += d1;
+    db2 += d2;
+    db3 += d3;
     dc *= fg;
     cn = cp;
     uint16_t* dp = ds + cr * 64 + cu;
-    dp[0] = f32_to_bf16(d0);
-    dp[16] = f32_to_bf16(d1);
-    dp[32] = f32_to_bf16(d2);
-    dp[48] = f32_to_bf16(d3);
+    dp[0] = ls_bf16(d0);
+    dp[16] = ls_bf16(d1);
+    dp[32] = ls_bf16(d2);
+    dp[48] = ls_bf16(d3);
     __syncthreads();
     if (tid < 128) {
       const int row = tid >> 3, q = (tid >> 1) & 3, half = tid & 1;
@@ -248,41 +321,75 @@ __global__ void __launch_bounds__(256, 1)
       const __amdgpu_buffer_rsrc_t gw = ls_rsrc(dg + t * 4 * BH + (int64_t)r0 * 4 * H, 16 * 4 * H * 2);
       st_sc1(gw, (row * 4 * H + q * H + u0 + half * 8) * 2, v);
     }
-    ls_publish(ctr);
+    if constexpr (PROTO == PROTO_COUNTER) ls_publish(ctr);
   }
   if (dc_out) dc_out[cidx] = dc;
+  if (dbias) {
+    // bias gradient: this tile's sum over its 16 rows, one f32 atomic per (gate, unit)
+    __syncthreads();
+    float* bsum = red;  // [gate][row][unit]
+    bsum[(0 * 16 + cr) * 16 + cu] = db0;
+    bsum[(1 * 16 + cr) * 16 + cu] = db1;
+    bsum[(2 * 16 + cr) * 16 + cu] = db2;
+    bsum[(3 * 16 + cr) * 16 + cu] = db3;
+    __syncthreads();
+    if (tid < 64) {
+      const int q = tid >> 4, u = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v += bsum[(q * 16 + r) * 16 + u];
+      atomicAdd(dbias + q * H + u0 + u, v);
+    }
+  }
 }
 
+template <typename K>
+void ls_prepare(K k) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LS_LDS);
+}
+
+int ls_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// kernel selection: protocol (TFX_LSTM_PROTO, default counter) x acquire (TFX_LSTM_ACQUIRE)
 template <int NK>
-void fwd_launch(bool acq, dim3 grid, const float* gx, const uint16_t* whh, int T, int B, uint16_t* hbuf, float* cbuf,
+void fwd_launch(dim3 grid, const float* gx, const uint16_t* whh, int T, int B, uint16_t* hbuf, float* cbuf,
                 float* act, float* hT, unsigned* sync, hipStream_t s) {
-  auto k = acq ? lstm_seq_fwd_kernel<NK, true> : lstm_seq_fwd_kernel<NK, false>;
-  static bool attr[2] = {false, false};
-  if (!attr[acq]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LS_LDS);
-    attr[acq] = true;
-  }
+  static const int proto = ls_env("TFX_LSTM_PROTO", PROTO_COUNTER) == PROTO_DATA ? PROTO_DATA : PROTO_COUNTER;
+  static const bool acq = ls_env("TFX_LSTM_ACQUIRE", 0) != 0;
+  auto k = proto == PROTO_DATA ? lstm_seq_fwd_kernel<NK, PROTO_DATA, false>
+                               : (acq ? lstm_seq_fwd_kernel<NK, PROTO_COUNTER, true>
+                                      : lstm_seq_fwd_kernel<NK, PROTO_COUNTER, false>);
+  static bool once = (ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_DATA, false>),
+                      ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_COUNTER, true>),
+                      ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_COUNTER, false>), true);
+  (void)once;
+  const int64_t BH = (int64_t)B * H_of<NK>();
+  (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B) * 4, s);
+  if (proto == PROTO_DATA) (void)hipMemsetAsync(hbuf + BH, 0xFF, (size_t)T * BH * 2, s);
   k<<<grid, 256, LS_LDS, s>>>(gx, whh, T, B, hbuf, cbuf, act, hT, sync);
 }
 
 template <int NK>
-void bwd_launch(bool acq, dim3 grid, const float* act, const float* cbuf, const float* dH, const float* dc_in,
-                const uint16_t* whh, int T, int B, uint16_t* dg, float* dc_out, unsigned* sync, hipStream_t s) {
-  auto k = acq ? lstm_seq_bwd_kernel<NK, true> : lstm_seq_bwd_kernel<NK, false>;
-  static bool attr[2] = {false, false};
-  if (!attr[acq]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LS_LDS);
-    attr[acq] = true;
-  }
-  k<<<grid, 256, LS_LDS, s>>>(act, cbuf, dH, dc_in, whh, T, B, dg, dc_out, sync);
-}
-
-bool ls_acquire() {
-  static const bool on = [] {
-    const char* e = getenv("TFX_LSTM_ACQUIRE");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  return on;
+void bwd_launch(dim3 grid, const float* act, const float* cbuf, const uint16_t* dH, const float* dhT,
+                const float* dc_in, const uint16_t* whh, int T, int B, uint16_t* dg, float* dc_out, float* dbias,
+                unsigned* sync, hipStream_t s) {
+  static const int proto = ls_env("TFX_LSTM_PROTO", PROTO_COUNTER) == PROTO_DATA ? PROTO_DATA : PROTO_COUNTER;
+  static const bool acq = ls_env("TFX_LSTM_ACQUIRE", 0) != 0;
+  auto k = proto == PROTO_DATA ? lstm_seq_bwd_kernel<NK, PROTO_DATA, false>
+                               : (acq ? lstm_seq_bwd_kernel<NK, PROTO_COUNTER, true>
+                                      : lstm_seq_bwd_kernel<NK, PROTO_COUNTER, false>);
+  static bool once = (ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_DATA, false>),
+                      ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_COUNTER, true>),
+                      ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_COUNTER, false>), true);
+  (void)once;
+  const int64_t BH = (int64_t)B * H_of<NK>();
+  (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B) * 4, s);
+  // slot t = 0..T-2 are consumed in-launch (slot T-1 is produced first and read at step 1)
+  if (proto == PROTO_DATA) (void)hipMemsetAsync(dg, 0xFF, (size_t)T * 4 * BH * 2, s);
+  k<<<grid, 256, LS_LDS, s>>>(act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync);
 }
 
 }  // namespace
@@ -297,27 +404,24 @@ bool lstm_seq_supported(int B, int H, int num_cus) {
 
 void lstm_seq_fwd(const float* gx, const uint16_t* whh, int T, int B, int H, uint16_t* hbuf, float* cbuf, float* act,
                   float* hT, unsigned* sync, hipStream_t s) {
-  (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B) * 4, s);
   const dim3 grid(H / 16, B / 16);
-  const bool acq = ls_acquire();
   switch (H) {
-    case 128: fwd_launch<4>(acq, grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
-    case 256: fwd_launch<8>(acq, grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
-    case 512: fwd_launch<16>(acq, grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
-    default: fwd_launch<32>(acq, grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
+    case 128: fwd_launch<4>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
+    case 256: fwd_launch<8>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
+    case 512: fwd_launch<16>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
+    default: fwd_launch<32>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
   }
 }
 
-void lstm_seq_bwd(const float* act, const float* cbuf, const float* dH, const float* dc_in, const uint16_t* whh, int T,
-                  int B, int H, uint16_t* dg, float* dc_out, unsigned* sync, hipStream_t s) {
-  (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B) * 4, s);
+void lstm_seq_bwd(const float* act, const float* cbuf, const uint16_t* dH, const float* dhT, const float* dc_in,
+                  const uint16_t* whh, int T, int B, int H, uint16_t* dg, float* dc_out, float* dbias, unsigned* sync,
+                  hipStream_t s) {
   const dim3 grid(H / 16, B / 16);
-  const bool acq = ls_acquire();
   switch (H) {
-    case 128: bwd_launch<4>(acq, grid, act, cbuf, dH, dc_in, whh, T, B, dg, dc_out, sync, s); break;
-    case 256: bwd_launch<8>(acq, grid, act, cbuf, dH, dc_in, whh, T, B, dg, dc_out, sync, s); break;
-    case 512: bwd_launch<16>(acq, grid, act, cbuf, dH, dc_in, whh, T, B, dg, dc_out, sync, s); break;
-    default: bwd_launch<32>(acq, grid, act, cbuf, dH, dc_in, whh, T, B, dg, dc_out, sync, s); break;
+    case 128: bwd_launch<4>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, s); break;
+    case 256: bwd_launch<8>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, s); break;
+    case 512: bwd_launch<16>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, s); break;
+    default: bwd_launch<32>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, s); break;
   }
 }
 

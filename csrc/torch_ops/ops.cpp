@@ -7,11 +7,13 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <tuple>
 #include <vector>
 
 #include "tfx_kernels.h"
+#include "../kernels/igemm_entry.h"
 
 using at::Tensor;
 using c10::optional;
@@ -600,10 +602,23 @@ Tensor sse_bwd(Tensor p, Tensor y, Tensor g) {
   return dp;
 }
 
+// f32: returns dz = g * act'(y).  bf16 (g, y bf16): returns dz for act != 0, or an empty tensor when
+// act == 0 (only the bias column sums are wanted: g itself is the GEMM operand).
 Tensor act_bwd_colsum(Tensor g, Tensor y, int64_t act, optional<Tensor> dbias) {
-  CHECK_DEV(g); CHECK_F32(g); CHECK_CONTIG(g); CHECK_F32(y); CHECK_CONTIG(y);
-  TORCH_CHECK(g.dim() == 2 && g.sizes() == y.sizes(), "act_bwd_colsum: [M, N] gradient and activation");
-  if (dbias.has_value() && dbias->defined()) TORCH_CHECK(dbias->numel() == g.size(1), "dbias size");
+  CHECK_DEV(g); CHECK_CONTIG(g); CHECK_CONTIG(y);
+  TORCH_CHECK(g.dim() == 2 && g.sizes() == y.sizes() && g.scalar_type() == y.scalar_type(),
+              "act_bwd_colsum: [M, N] gradient and activation of one dtype");
+  if (dbias.has_value() && dbias->defined()) {
+    CHECK_F32(*dbias);
+    TORCH_CHECK(dbias->numel() == g.size(1) && dbias->is_contiguous(), "dbias size");
+  }
+  if (g.scalar_type() == at::kBFloat16) {
+    Tensor dz = act != 0 ? at::empty_like(g) : at::Tensor();
+    tfx::act_bwd_colsum_bf16(bf(g), bf(y), (int)act, g.size(0), (int)g.size(1), act != 0 ? bfm(dz) : nullptr,
+                             fpm(dbias), cur_stream());
+    return dz;
+  }
+  CHECK_F32(g); CHECK_F32(y);
   auto dz = at::empty_like(g);
   tfx::act_bwd_colsum(g.data_ptr<float>(), y.data_ptr<float>(), (int)act, g.size(0), (int)g.size(1),
                       dz.data_ptr<float>(), fpm(dbias), cur_stream());
@@ -920,26 +935,55 @@ Tensor lstm_seq_fwd(Tensor gx, Tensor whh, Tensor hbuf, Tensor cbuf, Tensor act,
   return sync.narrow(0, sync.numel() - 32, 1);
 }
 
-// act, cbuf from the forward; dH [T,B,H] f32 = gradient of every h_t from outside the recurrence
-// (h_T's own gradient folded into dH[T-1]); dc_in = gradient of c_T (optional).  Writes dg [T,B,4H]
-// bf16 (gate pre-activation gradients) and optionally dc_out [B,H] (gradient of c_0).
-Tensor lstm_seq_bwd(Tensor act, Tensor cbuf, Tensor dH, optional<Tensor> dc_in, Tensor whh, Tensor dg,
-                    optional<Tensor> dc_out) {
+// act, cbuf from the forward; dH [T,B,H] bf16 (optional) = gradient of every h_t from outside the
+// recurrence; dhT / dc_in [B,H] f32 (optional) = gradients of h_T / c_T.  Writes dg [T,B,4H] bf16
+// (gate pre-activation gradients), optionally dc_out [B,H] (gradient of c_0) and accumulates the
+// bias gradient into dbias [4H] f32 (optional).
+Tensor lstm_seq_bwd(Tensor act, Tensor cbuf, optional<Tensor> dH, optional<Tensor> dhT, optional<Tensor> dc_in,
+                    Tensor whh, Tensor dg, optional<Tensor> dc_out, optional<Tensor> dbias) {
   CHECK_DEV(act); CHECK_F32(act); CHECK_CONTIG(act); CHECK_F32(cbuf); CHECK_CONTIG(cbuf);
-  CHECK_F32(dH); CHECK_CONTIG(dH); CHECK_BF16(whh); CHECK_CONTIG(whh); CHECK_BF16(dg); CHECK_CONTIG(dg);
+  CHECK_BF16(whh); CHECK_CONTIG(whh); CHECK_BF16(dg); CHECK_CONTIG(dg);
   TORCH_CHECK(cbuf.dim() == 3, "cbuf must be [T+1,B,H]");
   const int64_t T = cbuf.size(0) - 1, B = cbuf.size(1), H = cbuf.size(2);
   TORCH_CHECK(T >= 1 && lstm_seq_supported(B, H), "lstm_seq: unsupported shape");
-  TORCH_CHECK(act.numel() == T * B * 4 * H && dg.numel() == T * B * 4 * H && dH.numel() == T * B * H &&
-                  whh.numel() == 4 * H * H, "lstm_seq_bwd shapes");
-  for (const auto* t : {&dc_in, &dc_out})
+  TORCH_CHECK(act.numel() == T * B * 4 * H && dg.numel() == T * B * 4 * H && whh.numel() == 4 * H * H,
+              "lstm_seq_bwd shapes");
+  const uint16_t* dh16 = nullptr;
+  if (dH.has_value() && dH->defined()) {
+    CHECK_BF16(*dH); CHECK_CONTIG(*dH);
+    TORCH_CHECK(dH->numel() == T * B * H, "dH shape");
+    dh16 = bf(*dH);
+  }
+  for (const auto* t : {&dhT, &dc_in, &dc_out})
     if (fp(*t)) TORCH_CHECK((*t)->numel() == B * H && (*t)->is_contiguous() && (*t)->scalar_type() == at::kFloat,
                             "lstm_seq_bwd state shape");
+  if (fp(dbias)) TORCH_CHECK(dbias->numel() == 4 * H && dbias->is_contiguous() && dbias->scalar_type() == at::kFloat,
+                             "dbias shape");
   check_aligned16(dg, "dg");
   Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B)}, act.options().dtype(at::kInt));
-  tfx::lstm_seq_bwd(act.data_ptr<float>(), cbuf.data_ptr<float>(), dH.data_ptr<float>(), fp(dc_in), bf(whh), (int)T,
-                    (int)B, (int)H, bfm(dg), fpm(dc_out), reinterpret_cast<unsigned*>(sync.data_ptr()), cur_stream());
+  tfx::lstm_seq_bwd(act.data_ptr<float>(), cbuf.data_ptr<float>(), dh16, fp(dhT), fp(dc_in), bf(whh), (int)T,
+                    (int)B, (int)H, bfm(dg), fpm(dc_out), fpm(dbias), reinterpret_cast<unsigned*>(sync.data_ptr()),
+                    cur_stream());
   return sync.narrow(0, sync.numel() - 32, 1);
+}
+
+// ------------------------------------------------------------------ measured igemm launch configurations
+void igemm_tune_set(int64_t fam, int64_t M, int64_t N, int64_t K, int64_t tile, int64_t ks, int64_t gls,
+                    int64_t want) {
+  TORCH_CHECK(fam >= 0 && fam < tfx::FAM_COUNT, "igemm_tune_set: family");
+  tfx::igemm_tune_set((int)fam, (int)M, (int)N, (int)K, tfx::TuneCfg{(int)tile, (int)ks, (int)gls, (int)want});
+}
+void igemm_tune_clear() { tfx::igemm_tune_clear(); }
+void igemm_tune_force(int64_t fam, int64_t tile, int64_t ks, int64_t gls, int64_t want) {
+  tfx::igemm_tune_force((int)fam, tfx::TuneCfg{(int)tile, (int)ks, (int)gls, (int)want});
+}
+void igemm_tune_trace(bool on) { tfx::igemm_tune_trace(on); }
+Tensor igemm_tune_traced() {
+  std::vector<int> buf(4 * 4096);
+  const int n = std::min(tfx::igemm_tune_traced(buf.data(), (int)buf.size()), 4096);
+  auto out = at::empty({n, 4}, at::TensorOptions().dtype(at::kInt));
+  std::copy(buf.begin(), buf.begin() + 4 * n, out.data_ptr<int>());
+  return out;
 }
 
 void philox_fill(Tensor out, int64_t seed, int64_t subseq, int64_t dist, double a, double b) {
@@ -988,6 +1032,11 @@ TORCH_LIBRARY(tfx, m) {
   m.def("lstm_cell_fwd", &lstm_cell_fwd);
   m.def("lstm_cell_bwd", &lstm_cell_bwd);
   m.def("lstm_seq_supported", &lstm_seq_supported);
+  m.def("igemm_tune_set", &igemm_tune_set);
+  m.def("igemm_tune_clear", &igemm_tune_clear);
+  m.def("igemm_tune_force", &igemm_tune_force);
+  m.def("igemm_tune_trace", &igemm_tune_trace);
+  m.def("igemm_tune_traced", &igemm_tune_traced);
   m.def("lstm_seq_fwd", &lstm_seq_fwd);
   m.def("lstm_seq_bwd", &lstm_seq_bwd);
   m.def("conv_fwd", &conv_fwd);

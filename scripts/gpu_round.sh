@@ -96,10 +96,12 @@ for s in $STEPS; do
       timeout -k 10 300 python -u -m pytest tests/test_sparse_rnn_gpu.py -k lstm -v -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_lstm.log 2>&1
       rc=$?; echo "lstm tests rc=$rc"; tail -15 gpurun_out/pytest_lstm.log; [ $rc -eq 0 ] || exit $rc
       : > gpurun_out/bench_lstm.jsonl
-      for p in 1 0; do for g in "" "--graph"; do
-        TFX_LSTM_PERSISTENT=$p timeout -k 10 300 python scripts/bench_models.py --model char_lstm --impl native $g >> gpurun_out/bench_lstm.jsonl 2> gpurun_out/bench_lstm_err.log || { tail -20 gpurun_out/bench_lstm_err.log; exit 1; }
-        echo "persistent=$p $g: $(tail -1 gpurun_out/bench_lstm.jsonl)"
+      for v in "1 0" "1 1"; do set -- $v; for g in "" "--graph"; do
+        TFX_LSTM_PERSISTENT=$1 TFX_LSTM_PROTO=$2 timeout -k 10 300 python scripts/bench_models.py --model char_lstm --impl native $g >> gpurun_out/bench_lstm.jsonl 2> gpurun_out/bench_lstm_err.log || { tail -20 gpurun_out/bench_lstm_err.log; exit 1; }
+        echo "persistent=$1 proto=$2 $g: $(tail -1 gpurun_out/bench_lstm.jsonl | cut -c1-200)"
       done; done
+      TFX_LSTM_PROTO=1 timeout -k 10 300 python -u -m pytest tests/test_sparse_rnn_gpu.py -k "lstm and persistent" -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_lstm_proto1.log 2>&1
+      rc=$?; echo "lstm proto1 tests rc=$rc"; tail -3 gpurun_out/pytest_lstm_proto1.log; [ $rc -eq 0 ] || exit $rc
       cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_lstm" -o lstm -- python3 "$R/scripts/bench_models.py" --model char_lstm --impl native --graph --steps 20 --warmup 5 > "$R/gpurun_out/prof_lstm.log" 2>&1
       rc=$?; cd "$R"; echo "prof lstm rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     models)

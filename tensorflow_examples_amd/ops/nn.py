@@ -406,10 +406,14 @@ class _Linear(torch.autograd.Function):
         w, b, relu = ctx.w, ctx.b, ctx.relu
         need_dx = ctx.needs_input_grad[0]
         if ctx.native:
-            g = gy.to(torch.bfloat16)
-            if relu:
-                g = torch.where(y > 0, g, torch.zeros_like(g))
-            g = g.contiguous()
+            g = gy.to(torch.bfloat16).contiguous()
+            bias_grad = b.grad if (b is not None and b.trainable) else None
+            if relu or bias_grad is not None:
+                # one pass: ReLU mask (g' = g * [y > 0]) and the bias column sums
+                yy = y.to(torch.bfloat16).contiguous() if relu else g
+                gm = torch.ops.tfx.act_bwd_colsum(g, yy, 1 if relu else 0, bias_grad)
+                if relu:
+                    g = gm
             out_f, in_f = w.shape
             gp = _pad_to(g, 1, 8)
             dx = None
@@ -426,9 +430,7 @@ class _Linear(torch.autograd.Function):
                     tmp = torch.zeros(gp.shape[1], xp.shape[1], device=x.device, dtype=torch.float32)
                     torch.ops.tfx.gemm_into(gp, xp, True, False, tmp, True)
                     w.grad.add_(tmp[:out_f, :in_f])
-                if b is not None:
-                    b.grad.add_(g.float().sum(0))
-                _grad_ready(w, b)
+            _grad_ready(w if w.trainable else None, b if bias_grad is not None else None)
             return dx, None, None, None, None
         params = [w] + ([b] if b is not None else [])
         fn = (lambda xx, ww, bb: _linear_ref(xx, ww, bb, relu)) if b is not None else \

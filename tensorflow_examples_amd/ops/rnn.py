@@ -126,15 +126,22 @@ class _LSTMLayer(torch.autograd.Function):
         xf, hbuf, cbuf, act = ctx.saved_tensors
         T = act.shape[0]
         B, H = cbuf.shape[1], cbuf.shape[2]
-        dH = gout.float().contiguous().clone() if gout is not None else \
-            torch.zeros(T, B, H, dtype=torch.float32, device=xf.device)
-        if g_hT is not None:
-            dH[T - 1].add_(g_hT)
         dg = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=xf.device)
+        bias_done = False
         if ctx.persistent:
+            # the kernel reads the bf16 output gradient as is, folds in dh_T / dc_T, and accumulates
+            # the bias gradient (sum over t and rows of the f32 gate gradients)
+            dH16 = gout.to(torch.bfloat16).contiguous() if gout is not None else None
+            dhT = g_hT.float().contiguous() if g_hT is not None else None
             dc_in = g_cT.float().contiguous() if g_cT is not None else None
-            _LSTMLayer.last_status["bwd"] = torch.ops.tfx.lstm_seq_bwd(act, cbuf, dH, dc_in, w_hh.value, dg, None)
+            _LSTMLayer.last_status["bwd"] = torch.ops.tfx.lstm_seq_bwd(
+                act, cbuf, dH16, dhT, dc_in, w_hh.value, dg, None, b.grad if b.trainable else None)
+            bias_done = True
         else:
+            dH = gout.float().contiguous().clone() if gout is not None else \
+                torch.zeros(T, B, H, dtype=torch.float32, device=xf.device)
+            if g_hT is not None:
+                dH[T - 1].add_(g_hT)
             dc = g_cT.float().contiguous().clone() if g_cT is not None else \
                 torch.zeros(B, H, dtype=torch.float32, device=xf.device)
             for t in range(T - 1, -1, -1):
@@ -146,7 +153,7 @@ class _LSTMLayer(torch.autograd.Function):
             torch.ops.tfx.gemm_into(dgf, hbuf[:T].reshape(T * B, H), True, False, w_hh.grad, True)
         if w_ih.trainable:
             torch.ops.tfx.gemm_into(dgf, xf, True, False, w_ih.grad, True)
-        if b.trainable:
+        if b.trainable and not bias_done:
             b.grad.add_(dgf.float().sum(0))
         _grad_ready(w_ih, w_hh, b)
         dx = None

@@ -113,6 +113,16 @@ def test_elementwise_kernels(gpu):
         ref = gy if act == 0 else (gy * (ya > 0) if act == 1 else gy * ya * (1 - ya))
         assert torch.allclose(dz, ref, atol=1e-6)
         assert torch.allclose(dbias - 1, ref.sum(0), atol=1e-4, rtol=1e-5)
+    # bf16 dense-layer backward: ReLU mask + bias column sums in one pass (M large: atomic partials)
+    for act in (0, 1):
+        gy = torch.randn(6400, 65, device=gpu).to(torch.bfloat16)
+        ya = torch.relu(torch.randn(6400, 65, device=gpu)).to(torch.bfloat16) if act else gy
+        dbias = torch.zeros(65, device=gpu)
+        dz = torch.ops.tfx.act_bwd_colsum(gy, ya, act, dbias)
+        ref = gy.float() * (ya.float() > 0) if act else gy.float()
+        if act:
+            assert dz.dtype == torch.bfloat16 and torch.equal(dz.float(), ref)
+        assert torch.allclose(dbias, ref.sum(0), atol=1e-2, rtol=1e-4)
     z = torch.randn(64, 10, device=gpu)
     s16 = torch.ops.tfx.scale_by_scalar(z, torch.tensor([2.0], device=gpu), True)
     assert s16.dtype == torch.bfloat16 and torch.allclose(s16.float(), 2 * z, rtol=1e-2)
