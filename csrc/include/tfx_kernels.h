@@ -182,7 +182,7 @@ void lstm_cell_fwd(const float* gx, const float* gh, const float* bias, const fl
 void lstm_cell_bwd(const float* act, const float* c, const float* c_prev, const float* dh, const float* dc_next,
                    int B, int H, float* dgates, uint16_t* dg16, float* dc_prev, hipStream_t s);
 // persistent whole-sequence recurrence (lstm_seq.hip): one launch per layer and direction
-int lstm_seq_sync_words(int B);
+int lstm_seq_sync_words(int B, int H);
 bool lstm_seq_supported(int B, int H, int num_cus);
 void lstm_seq_fwd(const float* gx, const uint16_t* whh, int T, int B, int H, uint16_t* hbuf, float* cbuf, float* act,
                   float* hT, unsigned* sync, hipStream_t s);

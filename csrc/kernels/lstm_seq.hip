@@ -51,7 +51,7 @@ namespace {
 constexpr int LS_LDS = 96 * 1024;      // > 80 KB: one workgroup per CU (160 KB LDS)
 constexpr int LS_STRIDE = 32;          // u32 words per counter (own 128-B line)
 constexpr unsigned LS_SPIN_LIMIT = 1u << 20;
-enum { PROTO_COUNTER = 0, PROTO_DATA = 1 };
+enum { PROTO_COUNTER = 0, PROTO_DATA = 1, PROTO_FLAGS = 2 };
 constexpr uint16_t LS_SENTINEL = 0xFFFF;
 
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -138,6 +138,44 @@ __device__ __forceinline__ bool ls_block_wait(gu32* ctr, unsigned target, gu32* 
   return *flag != 0;
 }
 
+// PROTO_FLAGS: one flag word per producing workgroup (own 128-B line), holding the last step it
+// published.  Wave 0 of the consumer polls all of its row block's flags at once (lane l <-> flag
+// l), so no two producers ever meet on one atomic.
+template <bool ACQ>
+__device__ __forceinline__ bool ls_block_wait_flags(gu32* rbase, int nub, unsigned target, gu32* status,
+                                                    int* flag) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    bool ok = true;
+    for (unsigned spins = 0;; ++spins) {
+      const unsigned v =
+          lane < nub ? __hip_atomic_load(rbase + lane * LS_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
+      if (__all(v >= target)) break;
+      if (spins >= LS_SPIN_LIMIT) {
+        if (lane == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) {
+      if constexpr (ACQ) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = ok ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+__device__ __forceinline__ void ls_publish_flag(gu32* mine, unsigned v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(mine, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Publish: every storing wave drains, barrier, one lane bumps the counter.
 __device__ __forceinline__ void ls_publish(gu32* ctr) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -158,8 +196,8 @@ __global__ void __launch_bounds__(256, 1)
   int* flag = reinterpret_cast<int*>(smem + 16384 + 512);         // [0] wait result, [1] abort
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int nub = gridDim.x, u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
-  gu32* ctr = (gu32*)(sync + blockIdx.y * LS_STRIDE);
-  gu32* status = (gu32*)(sync + gridDim.y * LS_STRIDE);
+  gu32* ctr = (gu32*)(sync + blockIdx.y * nub * LS_STRIDE);  // row block's counter / flag lines
+  gu32* status = (gu32*)(sync + gridDim.y * nub * LS_STRIDE);
   if (tid == 0) flag[1] = 0;
 
   // W_hh rows (gate q, unit u0 + lane%16), this wave's K quarter: B operand, resident all sequence
@@ -186,7 +224,11 @@ __global__ void __launch_bounds__(256, 1)
     if constexpr (PROTO == PROTO_DATA) {
       if (!ls_poll_load<NKW>(hr, aoff, a, status)) flag[1] = 1;
     } else {
-      if (t > 0 && !ls_block_wait<ACQ>(ctr, (unsigned)(t * nub), status, flag)) return;
+      if constexpr (PROTO == PROTO_FLAGS) {
+        if (t > 0 && !ls_block_wait_flags<ACQ>(ctr, nub, (unsigned)t, status, flag)) return;
+      } else {
+        if (t > 0 && !ls_block_wait<ACQ>(ctr, (unsigned)(t * nub), status, flag)) return;
+      }
 #pragma unroll
       for (int kk = 0; kk < NKW; ++kk) a[kk] = ld_sc1(hr, aoff + kk * 64);
       __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
@@ -227,6 +269,7 @@ __global__ void __launch_bounds__(256, 1)
       st_sc1(hw, (row * H + u0 + half * 8) * 2, v);
     }
     if constexpr (PROTO == PROTO_COUNTER) ls_publish(ctr);
+    if constexpr (PROTO == PROTO_FLAGS) ls_publish_flag(ctr + blockIdx.x * LS_STRIDE, (unsigned)(t + 1));
   }
 }
 
@@ -246,8 +289,8 @@ __global__ void __launch_bounds__(256, 1)
   int* flag = reinterpret_cast<int*>(smem + 4096 + 2048);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int nub = gridDim.x, u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
-  gu32* ctr = (gu32*)(sync + blockIdx.y * LS_STRIDE);
-  gu32* status = (gu32*)(sync + gridDim.y * LS_STRIDE);
+  gu32* ctr = (gu32*)(sync + blockIdx.y * nub * LS_STRIDE);
+  gu32* status = (gu32*)(sync + gridDim.y * nub * LS_STRIDE);
   if (tid == 0) flag[1] = 0;
 
   // W_hh^T slice: B operand k = gate column q*H + kk*32 + (lane/16)*8 + e, n = unit u0 + lane%16
@@ -282,7 +325,11 @@ __global__ void __launch_bounds__(256, 1)
       if constexpr (PROTO == PROTO_DATA) {
         if (!ls_poll_load<NK>(gr, aoff, a, status)) flag[1] = 1;
       } else {
-        if (!ls_block_wait<ACQ>(ctr, (unsigned)(s * nub), status, flag)) return;
+        if constexpr (PROTO == PROTO_FLAGS) {
+          if (!ls_block_wait_flags<ACQ>(ctr, nub, (unsigned)s, status, flag)) return;
+        } else {
+          if (!ls_block_wait<ACQ>(ctr, (unsigned)(s * nub), status, flag)) return;
+        }
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) a[kk] = ld_sc1(gr, aoff + kk * 64);
         __builtin_amdgcn_sched_barrier(0);
@@ -322,6 +369,7 @@ __global__ void __launch_bounds__(256, 1)
       st_sc1(gw, (row * 4 * H + q * H + u0 + half * 8) * 2, v);
     }
     if constexpr (PROTO == PROTO_COUNTER) ls_publish(ctr);
+    if constexpr (PROTO == PROTO_FLAGS) ls_publish_flag(ctr + blockIdx.x * LS_STRIDE, (unsigned)(s + 1));
   }
   if (dc_out) dc_out[cidx] = dc;
   if (dbias) {
@@ -353,21 +401,31 @@ int ls_env(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-// kernel selection: protocol (TFX_LSTM_PROTO, default counter) x acquire (TFX_LSTM_ACQUIRE)
+// kernel selection: protocol (TFX_LSTM_PROTO: 0 counter (default), 1 data-as-flag, 2 per-producer
+// flags) x acquire (TFX_LSTM_ACQUIRE)
+int ls_proto() {
+  const int p = ls_env("TFX_LSTM_PROTO", PROTO_COUNTER);
+  return (p == PROTO_DATA || p == PROTO_FLAGS) ? p : PROTO_COUNTER;
+}
+
 template <int NK>
 void fwd_launch(dim3 grid, const float* gx, const uint16_t* whh, int T, int B, uint16_t* hbuf, float* cbuf,
                 float* act, float* hT, unsigned* sync, hipStream_t s) {
-  static const int proto = ls_env("TFX_LSTM_PROTO", PROTO_COUNTER) == PROTO_DATA ? PROTO_DATA : PROTO_COUNTER;
+  static const int proto = ls_proto();
   static const bool acq = ls_env("TFX_LSTM_ACQUIRE", 0) != 0;
   auto k = proto == PROTO_DATA ? lstm_seq_fwd_kernel<NK, PROTO_DATA, false>
-                               : (acq ? lstm_seq_fwd_kernel<NK, PROTO_COUNTER, true>
-                                      : lstm_seq_fwd_kernel<NK, PROTO_COUNTER, false>);
+         : proto == PROTO_FLAGS ? (acq ? lstm_seq_fwd_kernel<NK, PROTO_FLAGS, true>
+                                       : lstm_seq_fwd_kernel<NK, PROTO_FLAGS, false>)
+                                : (acq ? lstm_seq_fwd_kernel<NK, PROTO_COUNTER, true>
+                                       : lstm_seq_fwd_kernel<NK, PROTO_COUNTER, false>);
   static bool once = (ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_DATA, false>),
+                      ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_FLAGS, true>),
+                      ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_FLAGS, false>),
                       ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_COUNTER, true>),
                       ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_COUNTER, false>), true);
   (void)once;
   const int64_t BH = (int64_t)B * H_of<NK>();
-  (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B) * 4, s);
+  (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B, H_of<NK>()) * 4, s);
   if (proto == PROTO_DATA) (void)hipMemsetAsync(hbuf + BH, 0xFF, (size_t)T * BH * 2, s);
   k<<<grid, 256, LS_LDS, s>>>(gx, whh, T, B, hbuf, cbuf, act, hT, sync);
 }
@@ -376,17 +434,21 @@ template <int NK>
 void bwd_launch(dim3 grid, const float* act, const float* cbuf, const uint16_t* dH, const float* dhT,
                 const float* dc_in, const uint16_t* whh, int T, int B, uint16_t* dg, float* dc_out, float* dbias,
                 unsigned* sync, hipStream_t s) {
-  static const int proto = ls_env("TFX_LSTM_PROTO", PROTO_COUNTER) == PROTO_DATA ? PROTO_DATA : PROTO_COUNTER;
+  static const int proto = ls_proto();
   static const bool acq = ls_env("TFX_LSTM_ACQUIRE", 0) != 0;
   auto k = proto == PROTO_DATA ? lstm_seq_bwd_kernel<NK, PROTO_DATA, false>
-                               : (acq ? lstm_seq_bwd_kernel<NK, PROTO_COUNTER, true>
-                                      : lstm_seq_bwd_kernel<NK, PROTO_COUNTER, false>);
+         : proto == PROTO_FLAGS ? (acq ? lstm_seq_bwd_kernel<NK, PROTO_FLAGS, true>
+                                       : lstm_seq_bwd_kernel<NK, PROTO_FLAGS, false>)
+                                : (acq ? lstm_seq_bwd_kernel<NK, PROTO_COUNTER, true>
+                                       : lstm_seq_bwd_kernel<NK, PROTO_COUNTER, false>);
   static bool once = (ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_DATA, false>),
+                      ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_FLAGS, true>),
+                      ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_FLAGS, false>),
                       ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_COUNTER, true>),
                       ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_COUNTER, false>), true);
   (void)once;
   const int64_t BH = (int64_t)B * H_of<NK>();
-  (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B) * 4, s);
+  (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B, H_of<NK>()) * 4, s);
   // slot t = 0..T-2 are consumed in-launch (slot T-1 is produced first and read at step 1)
   if (proto == PROTO_DATA) (void)hipMemsetAsync(dg, 0xFF, (size_t)T * 4 * BH * 2, s);
   k<<<grid, 256, LS_LDS, s>>>(act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync);
@@ -394,7 +456,7 @@ void bwd_launch(dim3 grid, const float* act, const float* cbuf, const uint16_t* 
 
 }  // namespace
 
-int lstm_seq_sync_words(int B) { return (B / 16 + 1) * LS_STRIDE; }
+int lstm_seq_sync_words(int B, int H) { return ((B / 16) * (H / 16) + 1) * LS_STRIDE; }
 
 bool lstm_seq_supported(int B, int H, int num_cus) {
   if (B <= 0 || B % 16 != 0) return false;

@@ -928,7 +928,7 @@ Tensor lstm_seq_fwd(Tensor gx, Tensor whh, Tensor hbuf, Tensor cbuf, Tensor act,
                   whh.numel() == 4 * H * H && hT.numel() == B * H, "lstm_seq_fwd shapes");
   TORCH_CHECK(T * B * 4 * H * 4 < (int64_t(1) << 31), "lstm_seq: tensors must be < 2 GiB");
   for (const Tensor* t : {&gx, &whh, &hbuf}) check_aligned16(*t, "lstm_seq operand");
-  Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B)}, gx.options().dtype(at::kInt));
+  Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B, (int)H)}, gx.options().dtype(at::kInt));
   tfx::lstm_seq_fwd(gx.data_ptr<float>(), bf(whh), (int)T, (int)B, (int)H, bfm(hbuf), cbuf.data_ptr<float>(),
                     act.data_ptr<float>(), hT.data_ptr<float>(), reinterpret_cast<unsigned*>(sync.data_ptr()),
                     cur_stream());
@@ -960,7 +960,7 @@ Tensor lstm_seq_bwd(Tensor act, Tensor cbuf, optional<Tensor> dH, optional<Tenso
   if (fp(dbias)) TORCH_CHECK(dbias->numel() == 4 * H && dbias->is_contiguous() && dbias->scalar_type() == at::kFloat,
                              "dbias shape");
   check_aligned16(dg, "dg");
-  Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B)}, act.options().dtype(at::kInt));
+  Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B, (int)H)}, act.options().dtype(at::kInt));
   tfx::lstm_seq_bwd(act.data_ptr<float>(), cbuf.data_ptr<float>(), dh16, fp(dhT), fp(dc_in), bf(whh), (int)T,
                     (int)B, (int)H, bfm(dg), fpm(dc_out), fpm(dbias), reinterpret_cast<unsigned*>(sync.data_ptr()),
                     cur_stream());

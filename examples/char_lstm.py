@@ -24,6 +24,7 @@ import torch.distributed as dist  # noqa: E402
 from tensorflow_examples_amd import app  # noqa: E402
 from tensorflow_examples_amd.ckpt import Saver  # noqa: E402
 from tensorflow_examples_amd.data.text import CharCorpus, ptb_batches, synthetic_char_ids  # noqa: E402
+from tensorflow_examples_amd.data.pipeline import DevicePrefetcher  # noqa: E402
 from tensorflow_examples_amd.models.char_lstm import LMTrainer, build_char_lstm  # noqa: E402
 from tensorflow_examples_amd.optim import GradientDescentOptimizer  # noqa: E402
 from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed  # noqa: E402
@@ -74,10 +75,11 @@ def main(_):
     for ep in range(FLAGS.max_max_epoch):
         opt.set_learning_rate(FLAGS.learning_rate * FLAGS.lr_decay ** max(ep + 1 - FLAGS.max_epoch, 0))
         state, costs, iters = None, 0.0, 0
-        # global batch = B * world rows; rank r trains rows [r*B, (r+1)*B)
-        for x, y in ptb_batches(train, B * world, T):
-            xs = torch.as_tensor(x[:, rank * B:(rank + 1) * B].copy(), device=dev)
-            ys = torch.as_tensor(y[:, rank * B:(rank + 1) * B].copy(), device=dev)
+        # global batch = B * world rows; rank r trains rows [r*B, (r+1)*B).  Windows reach the GPU
+        # through the pinned ring (async H2D on a copy stream, two windows ahead of the step)
+        shard = ((x[:, rank * B:(rank + 1) * B], y[:, rank * B:(rank + 1) * B])
+                 for x, y in ptb_batches(train, B * world, T))
+        for xs, ys in DevicePrefetcher(shard, dev, depth=2):
             loss, state = trainer.step(xs, ys, state)
             step += 1
             tokens += B * T * world

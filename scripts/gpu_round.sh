@@ -96,14 +96,34 @@ for s in $STEPS; do
       timeout -k 10 300 python -u -m pytest tests/test_sparse_rnn_gpu.py -k lstm -v -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_lstm.log 2>&1
       rc=$?; echo "lstm tests rc=$rc"; tail -15 gpurun_out/pytest_lstm.log; [ $rc -eq 0 ] || exit $rc
       : > gpurun_out/bench_lstm.jsonl
-      for v in "1 0" "1 1"; do set -- $v; for g in "" "--graph"; do
+      for v in "1 0" "1 2"; do set -- $v; for g in "" "--graph"; do
         TFX_LSTM_PERSISTENT=$1 TFX_LSTM_PROTO=$2 timeout -k 10 300 python scripts/bench_models.py --model char_lstm --impl native $g >> gpurun_out/bench_lstm.jsonl 2> gpurun_out/bench_lstm_err.log || { tail -20 gpurun_out/bench_lstm_err.log; exit 1; }
         echo "persistent=$1 proto=$2 $g: $(tail -1 gpurun_out/bench_lstm.jsonl | cut -c1-200)"
       done; done
-      TFX_LSTM_PROTO=1 timeout -k 10 300 python -u -m pytest tests/test_sparse_rnn_gpu.py -k "lstm and persistent" -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_lstm_proto1.log 2>&1
-      rc=$?; echo "lstm proto1 tests rc=$rc"; tail -3 gpurun_out/pytest_lstm_proto1.log; [ $rc -eq 0 ] || exit $rc
-      cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_lstm" -o lstm -- python3 "$R/scripts/bench_models.py" --model char_lstm --impl native --graph --steps 20 --warmup 5 > "$R/gpurun_out/prof_lstm.log" 2>&1
+      TFX_LSTM_PROTO=2 timeout -k 10 300 python -u -m pytest tests/test_sparse_rnn_gpu.py -k "lstm and (persistent or reference)" -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_lstm_proto2.log 2>&1
+      rc=$?; echo "lstm proto2 tests rc=$rc"; tail -3 gpurun_out/pytest_lstm_proto2.log; [ $rc -eq 0 ] || exit $rc
+      cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lstm" -o lstm -- python3 "$R/scripts/bench_models.py" --model char_lstm --impl native --graph --steps 20 --warmup 5 > "$R/gpurun_out/prof_lstm.log" 2>&1
       rc=$?; cd "$R"; echo "prof lstm rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    tune)
+      timeout -k 10 900 python scripts/tune_convs.py --out gpurun_out/igemm_gfx950.json > gpurun_out/tune.log 2>&1
+      rc=$?; echo "tune rc=$rc"; tail -3 gpurun_out/tune.log; [ $rc -eq 0 ] || exit $rc
+      for i in 1 2 3; do
+        TFX_TUNE=0 timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_tune0_$i.log 2>&1 || exit 1
+        TFX_TUNE_FILE=gpurun_out/igemm_gfx950.json timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_tune1_$i.log 2>&1 || exit 1
+      done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_tune*.log
+      TFX_TUNE_FILE=gpurun_out/igemm_gfx950.json timeout -k 10 600 python -u -m pytest tests/test_conv_production_gpu.py tests/test_resnet_gpu.py -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_tuned.log 2>&1
+      rc=$?; echo "tuned tests rc=$rc"; tail -3 gpurun_out/pytest_tuned.log; [ $rc -eq 0 ] || exit $rc ;;
+    w2v)
+      for g in "" "--graph"; do
+        timeout -k 10 300 python scripts/bench_models.py --model word2vec --impl native $g >> gpurun_out/bench_w2v.jsonl 2> gpurun_out/bench_w2v_err.log || { tail -20 gpurun_out/bench_w2v_err.log; exit 1; }
+      done
+      timeout -k 10 300 python scripts/bench_models.py --model word2vec --impl torch >> gpurun_out/bench_w2v.jsonl 2>> gpurun_out/bench_w2v_err.log || exit 1
+      cut -c1-200 gpurun_out/bench_w2v.jsonl
+      cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_w2v" -o w2v -- python3 "$R/scripts/bench_models.py" --model word2vec --impl native --graph --steps 50 --warmup 10 > "$R/gpurun_out/prof_w2v.log" 2>&1
+      rc=$?; cd "$R"; echo "prof w2v rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_w2v_torch" -o w2vt -- python3 "$R/scripts/bench_models.py" --model word2vec --impl torch --steps 50 --warmup 10 > "$R/gpurun_out/prof_w2v_torch.log" 2>&1
+      rc=$?; cd "$R"; echo "prof w2v torch rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     models)
       : > gpurun_out/bench_models.jsonl
       for spec in "lenet5 native" "lenet5 native --graph" "lenet5 torch" "lenet5 torch --graph" \

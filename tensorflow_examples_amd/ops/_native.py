@@ -35,6 +35,8 @@ def load() -> bool:
             if not os.path.exists(OPS_LIB):
                 raise FileNotFoundError(f"{OPS_LIB} not built (run `python build.py`)")
             torch.ops.load_library(OPS_LIB)
+            from . import tuning
+            tuning.load()
             _loaded = True
         except Exception as e:  # pragma: no cover - depends on build state
             _load_error = e
