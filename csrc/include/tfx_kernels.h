@@ -120,6 +120,21 @@ void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t
 void bn_backward_apply(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask,
                        const float* save, const float* red, int64_t M, int C, bool relu, uint16_t* dx,
                        uint16_t* dres, hipStream_t s);
+// slot-consuming passes (batchnorm.hip "slot-consuming passes"): the forward apply reduces the
+// forward statistics slots S_f itself (row group 0 writes save / running stats and zeroes
+// slots_zero = the layer's backward slots S_b); the backward apply reduces S_b itself (row group 0
+// accumulates dgamma / dbeta and zeroes slots_zero = S_f).  bn_slots_ok(C): C in {64,128,256} or a
+// multiple of 256.
+bool bn_slots_ok(int C);
+void bn_apply_slots(const uint16_t* x, const uint16_t* res, const float* slots_f, float* slots_zero, int64_t M, int C,
+                    const float* gamma, const float* beta, float eps, float momentum, float* run_mean, float* run_var,
+                    float* save, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s);
+void bn_bwd_apply_slots(const uint16_t* g, const uint16_t* x, const uint8_t* mask, bool has_res, const float* save,
+                        const float* slots_b, float* slots_zero, int64_t M, int C, bool relu, float* dgamma,
+                        float* dbeta, uint16_t* dx, uint16_t* dres, hipStream_t s);
+// backward partials (sum g', sum g' xhat) of the vector path into slots (no slot reduce)
+void bn_bwd_reduce(const uint16_t* g, const uint16_t* x, const uint8_t* mask, bool has_res, const float* save,
+                   int64_t M, int C, bool relu, float* slots, hipStream_t s);
 void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask, const float* save,
                  int64_t M, int C, bool relu, float* slots, float* red, float* dgamma, float* dbeta, uint16_t* dx,
                  uint16_t* dres, hipStream_t s);

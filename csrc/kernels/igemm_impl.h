@@ -475,8 +475,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   constexpr int A_BYTES = BM * BKT * 2, STAGE = (BM + BN) * BKT * 2;
   constexpr bool GL = GLS > 0;
   constexpr int NSTG = GL ? GLS : STG;  // LDS stages per 4-wave group
-  static_assert(KS == 1 || (KS == 2 && EPI == EPI_PLAIN && (STG == 2 || GLS >= 2)),
-                "in-block split-K: plain pipelined kernels");
+  static_assert(KS == 1 || (KS == 2 && (STG == 2 || GLS >= 2)), "in-block split-K: pipelined kernels");
   static_assert(KS == 1 || TM * TN * 4096 <= NSTG * STAGE, "accumulator hand-off must fit its LDS region");
   static_assert(!GL || (A_BYTES % 4096 == 0 && (STAGE - A_BYTES) % 4096 == 0), "hand-off pairs tile the arrays");
   static_assert(KS * NSTG * STAGE <= 163840, "LDS budget");
@@ -589,6 +588,48 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   };
   auto compute = [&](int st) { compute_ab(smem, st * STAGE, smem, st * STAGE + A_BYTES); };
 
+  // ---- epilogue-operand prefetch (fused BN-backward data gradients).  The epilogue reads, per
+  // output element, the BN input x, its ReLU mask bits and the residual-branch addend: as much as
+  // the GEMM itself moves on the memory-bound 1x1 layers.  Issued in the epilogue they cost one
+  // exposed memory round trip per block after the last MFMA (measured: conv_dgrad_bn 92 us vs
+  // conv_dgrad 30 us at M 262144, N 256, K 64 -- scripts/operand_major_bench.py).  They do not
+  // depend on the GEMM, so PF issues them while the last k-tile(s) compute: in place of the final
+  // (zero-tile) refill of the LDS-DMA ring or of the register pipeline, or with the single tile.  Kept to tiles whose per-lane set fits (<= 4 rows x 8 columns, 40 VGPRs;
+  // 8 on the single-tile path).
+  constexpr int NPF = SWAP ? (TN / 2) * TM : 1;
+  constexpr bool PF = EPI == EPI_BNB && SWAP && (NPF <= 4 || (STG == 1 && !GL && NPF <= 8));
+  U4 pf_ad[PF ? NPF : 1], pf_x[PF ? NPF : 1];
+  uint32_t pf_am[PF ? NPF : 1], pf_m[PF ? NPF : 1];
+  auto epi_prefetch = [&]() {
+    if constexpr (PF) {
+      if (KS == 2 && grp != 0) return;  // group 1 only hands its accumulators over
+      const int mb0 = m0 + wm * WM, nb0 = n0 + wn * WN;
+      const bool odd = (lane >> 4) & 1;
+#pragma unroll
+      for (int j = 0; j < TN; j += 2) {
+        const int n = nb0 + (j + (odd ? 1 : 0)) * 16 + ((lane >> 5) << 3);
+        const int nl = min(n, a.N - 8);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = min(mb0 + i * 16 + (lane & 15), a.M - 1);
+          int row = m;
+          if (a.cls) {
+            const int nn = a.fd_cHW.div(m), yx = m - nn * a.H * a.W, y = a.fd_cW.div(yx), x = yx - y * a.W;
+            row = (nn * a.out_H + 2 * y + a.cph) * a.out_W + 2 * x + a.cpw;
+          }
+          const int64_t o = (int64_t)row * a.ldc + nl;
+          const int e = (j / 2) * TM + i;
+          if (a.addend) {
+            pf_ad[e] = *reinterpret_cast<const U4*>(a.addend + o);
+            pf_am[e] = a.addend_mask ? a.addend_mask[o >> 3] : 0xffu;
+          }
+          pf_x[e] = *reinterpret_cast<const U4*>(a.bnb_x + o);
+          pf_m[e] = a.bnb_mask ? a.bnb_mask[o >> 3] : 0xffu;
+        }
+      }
+    }
+  };
+
   if constexpr (GL) {
     constexpr int NPT = LA::NP + LB::NP;  // LDS-DMA pieces per thread per k-tile
     const int wv = t >> 6;
@@ -627,6 +668,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
     auto ring = [&](auto G) {
       if constexpr (GLS == 1) {  // host guarantees a single k-tile
         issue_gl(kt0, G, IC<0>{});
+        epi_prefetch();
         wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         compute_ab(img_a(G, IC<0>{}), 0, img_b(G, IC<0>{}), 0);
@@ -642,18 +684,58 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
           compute_ab(img_a(G, IC<st>{}), 0, img_b(G, IC<st>{}), 0);
           __builtin_amdgcn_sched_barrier(0);
         };
+        // PF: the last step's ring refill would be a zero tile -- the epilogue operands go out
+        // instead (nothing after that step waits on a count, only the final drain).  Peeled so the
+        // operand registers are live only from there on.
+        auto last = [&](auto S) {
+          constexpr int st = decltype(S)::value;
+          wait_vmcnt<NPT * (GLS - 2)>();
+          __builtin_amdgcn_s_barrier();
+          epi_prefetch();
+          __builtin_amdgcn_sched_barrier(0);
+          compute_ab(img_a(G, IC<st>{}), 0, img_b(G, IC<st>{}), 0);
+          __builtin_amdgcn_sched_barrier(0);
+        };
         issue_gl(kt0, G, IC<0>{});
         if constexpr (GLS >= 3) issue_gl(kt0 + 1, G, IC<1>{});
         int it = 0;
-        for (; it + GLS <= kh; it += GLS) {
-          body(IC<0>{}, it);
-          body(IC<1>{}, it + 1);
-          if constexpr (GLS >= 3) body(IC<2>{}, it + 2);
-        }
-        const int rem = kh - it;  // < GLS
-        if (rem > 0) body(IC<0>{}, it);
-        if constexpr (GLS >= 3) {
-          if (rem > 1) body(IC<1>{}, it + 1);
+        if constexpr (PF) {
+          for (; it + GLS < kh; it += GLS) {
+            body(IC<0>{}, it);
+            body(IC<1>{}, it + 1);
+            if constexpr (GLS >= 3) body(IC<2>{}, it + 2);
+          }
+          const int rem = kh - it;  // 1 .. GLS steps left, the final one peeled
+          if constexpr (GLS >= 3) {
+            if (rem == 3) {
+              body(IC<0>{}, it);
+              body(IC<1>{}, it + 1);
+              last(IC<2>{});
+            } else if (rem == 2) {
+              body(IC<0>{}, it);
+              last(IC<1>{});
+            } else {
+              last(IC<0>{});
+            }
+          } else {
+            if (rem == 2) {
+              body(IC<0>{}, it);
+              last(IC<1>{});
+            } else {
+              last(IC<0>{});
+            }
+          }
+        } else {
+          for (; it + GLS <= kh; it += GLS) {
+            body(IC<0>{}, it);
+            body(IC<1>{}, it + 1);
+            if constexpr (GLS >= 3) body(IC<2>{}, it + 2);
+          }
+          const int rem = kh - it;  // < GLS
+          if (rem > 0) body(IC<0>{}, it);
+          if constexpr (GLS >= 3) {
+            if (rem > 1) body(IC<1>{}, it + 1);
+          }
         }
       }
     };
@@ -670,6 +752,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
     __builtin_amdgcn_s_barrier();
   } else if constexpr (STG == 1) {  // host guarantees a single k-tile
     issue(kt0, sa0, sb0);
+    epi_prefetch();
     stage_store(0, sa0, sb0);
     __syncthreads();
     compute(0);
@@ -680,7 +763,34 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   stage_store(0, sa0, sb0);
   __syncthreads();
   if (kh == 1) {
+    epi_prefetch();
     compute(0);
+  } else if constexpr (PF) {
+    // as below, with the final pair peeled: its two tiles are already staged / in flight, so the
+    // epilogue operands go out in place of the (zero-filled) prefetches past the end
+    const int ktend = kt0 + kh;
+    int kt = kt0;
+    for (; kt + 2 < ktend; kt += 2) {
+      issue(kt + 2, sa0, sb0);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0);
+      __builtin_amdgcn_sched_barrier(0);
+      stage_store(1, sa1, sb1);
+      __syncthreads();
+      issue(kt + 3, sa1, sb1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1);
+      __builtin_amdgcn_sched_barrier(0);
+      stage_store(0, sa0, sb0);
+      __syncthreads();
+    }
+    epi_prefetch();
+    __builtin_amdgcn_sched_barrier(0);
+    compute(0);
+    __builtin_amdgcn_sched_barrier(0);
+    stage_store(1, sa1, sb1);  // tile kt + 1 (zero-filled when kh is odd)
+    __syncthreads();
+    compute(1);
   } else {
     // single exit at the bottom: every path into the loop header has set 1 in flight and set 0
     // free, so the vmcnt bookkeeping is identical on both edges (no conservative vmcnt(0)).
@@ -737,6 +847,9 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] += x[r * 256 + t];
     });
+    // the fused-BN epilogues reuse this LDS for their partials: every group-0 wave must be past its
+    // hand-off reads first (group 1 has exited; s_barrier waits only on the surviving waves)
+    if constexpr (EPI != EPI_PLAIN) __syncthreads();
   }
 
   // Element (m, n) of lane's acc[i][j][r]:
@@ -827,6 +940,14 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
           uint32_t mbv[IC], amv[IC];
 #pragma unroll
           for (int ii = 0; ii < IC; ++ii) {
+            if constexpr (PF) {  // issued during the last k-tile(s): see epi_prefetch
+              const int e = (j / 2) * TM + i0 + ii;
+              adv[ii] = pf_ad[e];
+              amv[ii] = pf_am[e];
+              xvv[ii] = pf_x[e];
+              mbv[ii] = pf_m[e];
+              continue;
+            }
             const int64_t o = rowoff[i0 + ii] + nl;
             if (a.addend) {
               adv[ii] = *reinterpret_cast<const U4*>(a.addend + o);
@@ -1116,8 +1237,12 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
     return;
   }
   if constexpr (KS == 2) {
-    if (swap) igemm_kernel<AK, BK, BM, BN, true, 2, EPI_PLAIN, 2><<<grid, 2 * NT, 0, s>>>(a);
-    else igemm_kernel<AK, BK, BM, BN, false, 2, EPI_PLAIN, 2><<<grid, 2 * NT, 0, s>>>(a);
+    if constexpr (EPI != EPI_PLAIN) {
+      igemm_kernel<AK, BK, BM, BN, true, 2, EPI, 2><<<grid, 2 * NT, 0, s>>>(a);
+    } else {
+      if (swap) igemm_kernel<AK, BK, BM, BN, true, 2, EPI_PLAIN, 2><<<grid, 2 * NT, 0, s>>>(a);
+      else igemm_kernel<AK, BK, BM, BN, false, 2, EPI_PLAIN, 2><<<grid, 2 * NT, 0, s>>>(a);
+    }
     return;
   }
   if constexpr (EPI != EPI_PLAIN) {  // fused-BN epilogues: bf16 outputs only (SWAP orientation)
@@ -1187,6 +1312,12 @@ void launch_shape(IgemmArgs& a, hipStream_t s, int fam = -1) {
       if (tc.tile == 2) return launch_t<AK, BK, 128, 64, EPI>(a, s, 2);
       return launch_t<AK, BK, 128, 128, EPI>(a, s);
     } else {
+      // ks 2 on a bf16-output family: 8-wave blocks, two 4-wave groups splitting the tile's K (twice the
+      // loads in flight per CU for the under-filled late-stage layers); group 0 runs the epilogue
+      if (tc.ks == 2 && tc.tile != 3) {
+        if (tc.tile == 2) return launch_t<AK, BK, 128, 64, EPI, 2>(a, s);
+        return launch_t<AK, BK, 128, 128, EPI, 2>(a, s);
+      }
       if (tc.tile == 3) return launch_t<AK, BK, 256, 64, EPI>(a, s);
       if (tc.tile == 2) return launch_t<AK, BK, 128, 64, EPI>(a, s);
       return launch_t<AK, BK, 128, 128, EPI>(a, s);

@@ -245,7 +245,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
                                          int64_t pad, int64_t dil, optional<Tensor> addend, Tensor bn_x,
                                          Tensor bn_save, optional<Tensor> bn_mask, bool relu, Tensor ws,
                                          optional<Tensor> dgamma, optional<Tensor> dbeta,
-                                         optional<Tensor> addend_mask) {
+                                         optional<Tensor> addend_mask, bool reduce) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
   TORCH_CHECK(stride == 1, "conv_dgrad_bn: stride-1 convs only (stride 2 runs per parity class)");
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
@@ -260,7 +260,8 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   }
   const uint8_t* amask = addend_mask_ptr(addend, addend_mask);
   auto dx = (acc && !amask) ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
-  auto red = at::empty({2 * g.C}, dy.options().dtype(at::kFloat));
+  // reduce = false: the partials stay in the slots for bn_bwd_slots (no red, no slot reduce)
+  auto red = reduce ? at::empty({2 * g.C}, dy.options().dtype(at::kFloat)) : Tensor();
   auto a = conv_args(g, stride, pad, dil);
   a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
   a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
@@ -276,10 +277,12 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   a.bnb_relu = relu ? 1 : 0;
   a.bnb_slots = ws.data_ptr<float>();
   a.bn_cnt = bn_counters(ws, g.C);
-  a.bn_final = bn_final_ok(ws, g.C);
-  a.bnb_red = red.data_ptr<float>(); a.bnb_dgamma = fpm(dgamma); a.bnb_dbeta = fpm(dbeta);
+  a.bn_final = reduce ? bn_final_ok(ws, g.C) : 0;
+  a.bnb_red = reduce ? red.data_ptr<float>() : nullptr;
+  a.bnb_dgamma = reduce ? fpm(dgamma) : nullptr;
+  a.bnb_dbeta = reduce ? fpm(dbeta) : nullptr;
   tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
-  if (!a.bn_final) tfx::bn_slot_reduce(a.bnb_slots, g.C, a.bnb_red, a.bnb_dgamma, a.bnb_dbeta, cur_stream());
+  if (reduce && !a.bn_final) tfx::bn_slot_reduce(a.bnb_slots, g.C, a.bnb_red, a.bnb_dgamma, a.bnb_dbeta, cur_stream());
   return {dx, red};
 }
 
@@ -502,6 +505,72 @@ std::tuple<Tensor, Tensor> bn_bwd_apply(Tensor g, Tensor x, optional<Tensor> res
                          dres.defined() ? bfm(dres) : nullptr, cur_stream());
   return {dx, dres};
 }
+
+// ---- two-slot-set BN (batchnorm.hip "slot-consuming passes"): slots_f = the layer's forward
+// statistics slots S_f, slots_b = its backward slots S_b, each [NSLOT][2][C] f32.  The forward
+// apply reduces S_f itself and zeroes S_b; the backward apply reduces S_b itself and zeroes S_f.
+// have_stats = false: a standalone statistics pass fills S_f first.
+std::tuple<Tensor, Tensor, Tensor> bn_fwd_slots(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
+                                                optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
+                                                double eps, optional<Tensor> res, bool relu, Tensor slots_f,
+                                                Tensor slots_b, bool have_stats) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(slots_f); CHECK_F32(slots_b);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(slots_f.numel() >= tfx::NSLOT * 2 * C && slots_b.numel() >= tfx::NSLOT * 2 * C, "stat slots");
+  TORCH_CHECK(tfx::bn_slots_ok((int)C), "bn_fwd_slots: C must be 64, 128, 256 or a multiple of 256");
+  auto save = at::empty({4 * C}, x.options().dtype(at::kFloat));
+  auto y = at::empty_like(x);
+  const uint16_t* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    CHECK_BF16(*res); CHECK_CONTIG(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+    r = bf(*res);
+  }
+  auto s = cur_stream();
+  if (!have_stats) tfx::bn_stats(bf(x), M, C, slots_f.data_ptr<float>(), s);
+  Tensor mask;
+  if (r && relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  tfx::bn_apply_slots(bf(x), r, slots_f.data_ptr<float>(), slots_b.data_ptr<float>(), M, C, fp(gamma), fp(beta),
+                      (float)eps, (float)momentum, fpm(run_mean), fpm(run_var), save.data_ptr<float>(), relu, bfm(y),
+                      mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, s);
+  return {y, save, mask};
+}
+
+// have_partials = true: a conv dgrad epilogue (conv_dgrad_bn, reduce=false) already accumulated
+// [sum g' | sum g' xhat] into S_b; else the vector reduce pass does.  Residual + ReLU layers need
+// the forward's mask.  Returns (dx, dres) as bn_bwd_apply.
+std::tuple<Tensor, Tensor> bn_bwd_slots(Tensor g, Tensor x, bool has_res, Tensor save, bool relu, optional<Tensor> mask,
+                                        Tensor slots_b, Tensor slots_f, optional<Tensor> dgamma,
+                                        optional<Tensor> dbeta, bool have_partials, bool want_dres) {
+  CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(save);
+  CHECK_F32(slots_b); CHECK_F32(slots_f);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd_slots grad shape");
+  TORCH_CHECK(save.numel() == 4 * C, "save size");
+  TORCH_CHECK(slots_f.numel() >= tfx::NSLOT * 2 * C && slots_b.numel() >= tfx::NSLOT * 2 * C, "stat slots");
+  TORCH_CHECK(tfx::bn_slots_ok((int)C), "bn_bwd_slots: C must be 64, 128, 256 or a multiple of 256");
+  const uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() * 8 == x.numel(), "relu mask size");
+    mk = mask->data_ptr<uint8_t>();
+  }
+  TORCH_CHECK(!(has_res && relu) || mk, "bn_bwd_slots: residual + ReLU needs the forward mask");
+  auto dx = at::empty_like(x);
+  Tensor dres;
+  if (has_res && want_dres) dres = at::empty_like(x);
+  auto s = cur_stream();
+  if (!have_partials) {
+    TORCH_CHECK(C <= 2048, "bn_bwd_slots: standalone reduce needs C <= 2048");
+    tfx::bn_bwd_reduce(bf(g), bf(x), mk, has_res, save.data_ptr<float>(), M, C, relu, slots_b.data_ptr<float>(), s);
+  }
+  tfx::bn_bwd_apply_slots(bf(g), bf(x), mk, has_res, save.data_ptr<float>(), slots_b.data_ptr<float>(),
+                          slots_f.data_ptr<float>(), M, C, relu, fpm(dgamma), fpm(dbeta), bfm(dx),
+                          dres.defined() ? bfm(dres) : nullptr, s);
+  return {dx, dres};
+}
+
+bool bn_slots_supported(int64_t C) { return tfx::bn_slots_ok((int)C); }
+int64_t bn_nslot() { return tfx::NSLOT; }
 
 // ------------------------------------------------------------------ loss / metrics / pooling
 std::tuple<Tensor, Tensor> softmax_xent(Tensor z, optional<Tensor> lab_idx, optional<Tensor> lab_dense, bool naive,
@@ -1055,7 +1124,11 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
         "Tensor bn_x, Tensor bn_save, Tensor? bn_mask, bool relu, Tensor ws, Tensor? dgamma, Tensor? dbeta, "
-        "Tensor? addend_mask=None) -> (Tensor, Tensor)", &conv_dgrad_bn);
+        "Tensor? addend_mask=None, bool reduce=True) -> (Tensor, Tensor)", &conv_dgrad_bn);
+  m.def("bn_fwd_slots", &bn_fwd_slots);
+  m.def("bn_bwd_slots", &bn_bwd_slots);
+  m.def("bn_slots_supported", &bn_slots_supported);
+  m.def("bn_nslot", &bn_nslot);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd(Tensor g, Tensor x, Tensor? res, Tensor save, bool relu, Tensor slots, Tensor? dgamma, "
         "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);

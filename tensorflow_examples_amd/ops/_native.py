@@ -79,6 +79,17 @@ def use_native(t: torch.Tensor) -> bool:
     raise RuntimeError(f"tensorflow_examples_amd: HIP kernel library unavailable on a GPU run: {_load_error}")
 
 
+def use_native_device(device: torch.device) -> bool:
+    """use_native for a device instead of a tensor."""
+    if device.type != "cuda" or getattr(_ref, "on", False):
+        return False
+    if load():
+        return True
+    if fallback_allowed():
+        return False
+    raise RuntimeError(f"tensorflow_examples_amd: HIP kernel library unavailable on a GPU run: {_load_error}")
+
+
 def ops():
     if not load():
         raise RuntimeError(f"HIP kernel library unavailable: {_load_error}")

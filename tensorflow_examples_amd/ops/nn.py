@@ -74,8 +74,18 @@ class _Conv2d(torch.autograd.Function):
         ctx.save_for_backward(x)
         if ctx.native:
             if isinstance(stats_into, BNWorkspace):
-                # epilogue statistics + last-arriver finalize: the BN only applies
                 ws = stats_into
+                if ws.two_phase(x.device):
+                    # epilogue statistics into the layer's forward slots S_f; the BN's apply pass
+                    # reduces them itself (bn_fwd_slots): no finalize launch
+                    sf = ws.fwd(x.device)
+                    if ws.fwd_dirty:  # an earlier training forward's backward never ran
+                        sf.zero_()
+                        ws.fwd_dirty = False
+                    y = torch.ops.tfx.conv_fwd_stats(x.contiguous(), w.value, stride, pad, dil, sf)
+                    ws.stats_ready = True
+                    return y
+                # epilogue statistics + last-arriver finalize: the BN only applies
                 y, ws.pending_save = torch.ops.tfx.conv_fwd_bn(x.contiguous(), w.value, stride, pad, dil,
                                                                ws.get(x.device), *ws.finalize_args)
                 return y
@@ -101,9 +111,21 @@ class _Conv2d(torch.autograd.Function):
                     # dx is the complete gradient of the BN output x: the epilogue also reduces
                     # that BN's backward (sum g', sum g' xhat, dgamma, dbeta) -- see BNBackwardFusion
                     add, amask = _unpack_sink(sink.take()) if sink is not None else (None, None)
-                    dx, bnb.red = torch.ops.tfx.conv_dgrad_bn(
-                        gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
-                        bnb.ws, bnb.dgamma, bnb.dbeta, amask)
+                    if bnb.wsobj is not None:
+                        # partials stay in the layer's backward slots S_b: the BN's backward apply
+                        # reduces them itself (bn_bwd_slots), no slot-reduce launch
+                        sb = bnb.wsobj.bwd(x.device)
+                        if bnb.wsobj.bwd_dirty:
+                            sb.zero_()
+                            bnb.wsobj.bwd_dirty = False
+                        dx, _ = torch.ops.tfx.conv_dgrad_bn(
+                            gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
+                            sb, None, None, amask, False)
+                        bnb.red = BNBackwardFusion.IN_SLOTS
+                    else:
+                        dx, bnb.red = torch.ops.tfx.conv_dgrad_bn(
+                            gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
+                            bnb.ws, bnb.dgamma, bnb.dbeta, amask)
                 elif sink is not None and sink.mode == "consume":
                     # last consumer of x in backward order: fold the other branch's gradient in
                     add, amask = _unpack_sink(sink.take())
@@ -183,14 +205,19 @@ class GradSink:
 
 
 class BNWorkspace:
-    """Per-BN-layer persistent f32 workspace: [NSLOT][2][C] statistics slots followed by BN_CNT
-    column-tile arrival counters (always zero between uses: whoever consumes the slots re-zeroes
-    them and resets the counters), so no per-step memsets.
+    """Per-BN-layer persistent f32 workspace.  Two slot sets, each [NSLOT][2][C] statistics slots
+    followed by BN_CNT column-tile arrival counters: S_f (forward statistics, filled by the producing
+    conv's epilogue) and S_b (backward partials, filled by the consuming conv's data-gradient
+    epilogue).  With channel counts the slab kernels take (``two_phase``), the BN's own passes
+    reduce the slots (bn_fwd_slots / bn_bwd_slots: no finalize or slot-reduce launch) and each
+    direction zeroes the OTHER direction's slots, so they are zero again before their next producer
+    runs (csrc/kernels/batchnorm.hip "slot-consuming passes").  ``fwd_dirty`` / ``bwd_dirty`` track
+    a direction whose slots were consumed but not yet zeroed -- a training forward with no backward,
+    or two backwards -- and the next producer then clears them explicitly.
 
-    ``finalize_args`` (gamma, beta, running mean, running var, momentum, eps) are set by the model
-    when the producing conv may finalize the BN in its epilogue; the conv then leaves the
-    [mean | invstd | scale | shift] vector in ``pending_save`` for the BN forward to consume."""
-    NSLOT = 64
+    Otherwise (``finalize_args`` set, older single-slot path) the producing conv may finalize the BN
+    in its epilogue and leave [mean | invstd | scale | shift] in ``pending_save``."""
+    NSLOT = 64  # = tfx::NSLOT (csrc/include/tfx_kernels.h), checked on first GPU use
     BN_CNT = 64
 
     def __init__(self, channels: int):
@@ -198,23 +225,57 @@ class BNWorkspace:
         self.buf = None
         self.finalize_args = None
         self.pending_save = None
+        self.stats_ready = False
+        self.fwd_dirty = False
+        self.bwd_dirty = False
+
+    def _half(self) -> int:
+        return self.NSLOT * 2 * self.c + self.BN_CNT
 
     def get(self, device) -> torch.Tensor:
         if self.buf is None or self.buf.device != device:
-            self.buf = torch.zeros(self.NSLOT * 2 * self.c + self.BN_CNT, dtype=torch.float32, device=device)
+            if device.type == "cuda" and _native.use_native_device(device):
+                assert int(torch.ops.tfx.bn_nslot()) == self.NSLOT, "BNWorkspace.NSLOT != tfx::NSLOT"
+            self.buf = torch.zeros(2 * self._half(), dtype=torch.float32, device=device)
+            self.fwd_dirty = self.bwd_dirty = False
         return self.buf
+
+    def fwd(self, device) -> torch.Tensor:
+        return self.get(device)[: self._half()]
+
+    def bwd(self, device) -> torch.Tensor:
+        return self.get(device)[self._half():]
+
+    def two_phase(self, device) -> bool:
+        return device.type == "cuda" and _native.use_native_device(device) and _slots_ok(self.c)
+
+
+_SLOTS_OK = {}
+
+
+def _slots_ok(c: int) -> bool:
+    if c not in _SLOTS_OK:
+        # opt-in (TFX_BN_SLOTS=1): inside the HIP-graph-replayed step the slot-reducing passes ran
+        # slower than finalize / slot-reduce kernel + lean apply (8.73 vs 8.60 ms/step; a graph
+        # replays the tiny kernels back to back, while every slab block pays the slot prologue):
+        # profiles/r02_bnslots
+        _SLOTS_OK[c] = bool(torch.ops.tfx.bn_slots_supported(c)) and os.environ.get("TFX_BN_SLOTS", "0") == "1"
+    return _SLOTS_OK[c]
 
 
 class BNBackwardFusion:
     """What a consumer conv's data-gradient epilogue needs to reduce a BN's backward (attached to
     the BN output as ``_tfx_bnb``): the BN input, its [mean|invstd|scale|shift], the residual
     layer's ReLU mask bits, the slot workspace and the parameter-gradient views.  The conv fills
-    ``red`` ([sum g' | sum g' xhat]); the BN backward then runs only its apply pass."""
-    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red")
+    ``red`` ([sum g' | sum g' xhat]), or -- two-slot-set workspaces (``wsobj``) -- leaves the
+    partials in the layer's backward slots and sets ``red = IN_SLOTS``; the BN backward then runs
+    only its apply pass."""
+    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "wsobj")
+    IN_SLOTS = "slots"
 
-    def __init__(self, x, save, mask, relu, ws, dgamma, dbeta):
+    def __init__(self, x, save, mask, relu, ws, dgamma, dbeta, wsobj=None):
         self.x, self.save, self.mask, self.relu, self.ws = x, save, mask, relu, ws
-        self.dgamma, self.dbeta, self.red = dgamma, dbeta, None
+        self.dgamma, self.dbeta, self.red, self.wsobj = dgamma, dbeta, None, wsobj
 
 
 # ====================================================================== batch norm (+res, +relu)
@@ -259,8 +320,20 @@ class _BatchNorm(torch.autograd.Function):
                                  device=x.device)
                 stats_ready = False
             ctx.ws = ws
+            ctx.wsobj = None
             mask = None
-            if training and wsobj is not None and wsobj.pending_save is not None:
+            if training and wsobj is not None and wsobj.two_phase(x.device):
+                sf, sb = wsobj.fwd(x.device), wsobj.bwd(x.device)
+                have = bool(stats_ready) and wsobj.stats_ready
+                if not have and wsobj.fwd_dirty:
+                    sf.zero_()
+                wsobj.stats_ready = False
+                y, save, mask = torch.ops.tfx.bn_fwd_slots(x, g_t, b_t, rm, rv, momentum, eps, res, relu, sf, sb,
+                                                           have)
+                # S_f consumed (zeroed by this layer's backward apply); S_b zeroed by this pass
+                wsobj.fwd_dirty, wsobj.bwd_dirty = True, False
+                ctx.wsobj = wsobj
+            elif training and wsobj is not None and wsobj.pending_save is not None:
                 # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
                 save, wsobj.pending_save = wsobj.pending_save, None
                 y, mask = torch.ops.tfx.bn_apply_train(x, res, save, relu)
@@ -277,7 +350,7 @@ class _BatchNorm(torch.autograd.Function):
                     and x.shape[-1] % 8 == 0:
                 train_p = gamma is not None and gamma.trainable
                 ctx.bnb = BNBackwardFusion(x, save, mask, relu, ws, gamma.grad if train_p else None,
-                                           beta.grad if train_p else None)
+                                           beta.grad if train_p else None, ctx.wsobj)
                 bnb_out.append(ctx.bnb)
             return y
         ctx.save_for_backward(x, res)
@@ -299,7 +372,20 @@ class _BatchNorm(torch.autograd.Function):
             # tensor write less per identity block
             masked = ctx.has_res and ctx.res_sink is not None and mask is not None and \
                 getattr(ctx.res_sink, "accept_masked", False) and relu
-            if ctx.bnb is not None and ctx.bnb.red is not None:
+            if ctx.wsobj is not None:
+                wsobj = ctx.wsobj
+                sf, sb = wsobj.fwd(x.device), wsobj.bwd(x.device)
+                have = ctx.bnb is not None and ctx.bnb.red is BNBackwardFusion.IN_SLOTS
+                if ctx.bnb is not None:
+                    ctx.bnb.red = None
+                if not have and wsobj.bwd_dirty:
+                    sb.zero_()
+                dx, dres = torch.ops.tfx.bn_bwd_slots(gy, x, ctx.has_res, save, relu, mask, sb, sf,
+                                                      gamma.grad if train_p else None,
+                                                      beta.grad if train_p else None, have, not masked)
+                # S_b consumed (zeroed by the next forward); S_f zeroed by this pass
+                wsobj.fwd_dirty, wsobj.bwd_dirty = False, True
+            elif ctx.bnb is not None and ctx.bnb.red is not None:
                 # the consumer conv's dgrad epilogue reduced this backward (and dgamma / dbeta)
                 dx, dres = torch.ops.tfx.bn_bwd_apply(gy, x, res, save, ctx.bnb.red, relu, mask, not masked)
                 ctx.bnb.red = None
