@@ -48,6 +48,11 @@ struct IgemmArgs {
   // optional ReLU-mask bits of the addend (1 bit per element, one byte per 8 channels): C = acc +
   // addend * mask -- a residual BN's masked output gradient consumed without materialising it
   const uint8_t* addend_mask = nullptr;
+  // addend_s2: the addend holds only the even-(y, x) pixels of the output grid, compact
+  // [Nb][s2_P][s2_Q][ldc] (the data gradient of a 1x1 stride-2 projection shortcut): odd pixels add
+  // nothing.  Output rows decode as pixel (n, y, x) of an H x W grid (fd_s2HW / fd_s2W).
+  int addend_s2 = 0, s2_P = 0, s2_Q = 0;
+  FastDiv fd_s2HW, fd_s2W;
   void* Cp = nullptr;
   const float* bias = nullptr;
   int M = 0, N = 0, K = 0;

@@ -97,6 +97,12 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
     fprintf(stderr, "igemm_launch: masked addend needs a bf16 output with 8-aligned columns\n");
     abort();
   }
+  // a stride-2 compact addend likewise (and never with mask bits or a parity-class output)
+  if (a.addend_s2 && !(a.addend && !a.addend_mask && !a.cls && a.out_mode == OUT_BF16 && !a.trans_out &&
+                       (a.ldc & 7) == 0 && (a.N & 7) == 0)) {
+    fprintf(stderr, "igemm_launch: stride-2 compact addend needs a bf16 16-byte-store output\n");
+    abort();
+  }
   // fused-BN epilogues live in the bf16 16-byte-store path of the forward / data-gradient kernels
   if (a.stats || a.bnb_x) {
     if (!(a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0 &&

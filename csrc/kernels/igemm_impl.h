@@ -97,6 +97,22 @@ __device__ __forceinline__ bf16x8_t lds_read_mn(const char* img, int img_off, in
 // all of a thread's rows, with 24-bit multiplies (v_mul_u32_u24, full rate; the host guarantees
 // pixel counts < 2^24) instead of quarter-rate 32-bit ones: the K loop's VALU issue competes with
 // the MFMAs for the SIMD (MI355X_MICROARCH.md 'vector-instruction ISSUE cost').
+// zero the bf16 halves of an 8 x bf16 vector whose bit in `bits` (element k = bit k) is clear:
+// each 32-bit word gets a mask from two sign-extended 1-bit fields (v_bfe_i32), no selects
+__device__ __forceinline__ U4 mask_bf16x8(const U4& v, uint32_t bits) {
+  auto wmask = [&](int s) -> uint32_t {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)bits, s, 1) & 0xffffu;
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)bits, s + 1, 1) << 16;
+    return lo | hi;
+  };
+  U4 r;
+  r.x = v.x & wmask(0);
+  r.y = v.y & wmask(2);
+  r.z = v.z & wmask(4);
+  r.w = v.w & wmask(6);
+  return r;
+}
+
 __device__ __forceinline__ int mul24(int a, int b) { return (int)__umul24((unsigned)a, (unsigned)b); }
 
 // s_waitcnt vmcnt(N) only (expcnt / lgkmcnt fields left at their maxima): the counted wait of the
@@ -596,6 +612,39 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   // depend on the GEMM, so PF issues them while the last k-tile(s) compute: in place of the final
   // (zero-tile) refill of the LDS-DMA ring or of the register pipeline, or with the single tile.  Kept to tiles whose per-lane set fits (<= 4 rows x 8 columns, 40 VGPRs;
   // 8 on the single-tile path).
+  // Epilogue operands are read through buffer resources with 32-bit offsets (no 64-bit address
+  // math per row).  A null operand gets a zero-extent resource: its loads return 0 without a memory
+  // access, so every load is unconditional -- a load under a runtime flag makes hipcc branch around
+  // it and drain vmcnt(0) at the join (cdna_hip_programming.md "Projection GEMM" item 4(c)).
+  struct EpiRes {
+    __amdgpu_buffer_rsrc_t ad, am, x, m;
+  };
+  auto epi_res = [&]() {
+    EpiRes r;
+    r.ad = make_rsrc(a.addend, a.addend ? 0x7fffffff : 0);
+    r.am = make_rsrc(a.addend_mask, a.addend_mask ? 0x7fffffff : 0);
+    r.x = make_rsrc(a.bnb_x, a.bnb_x ? 0x7fffffff : 0);
+    r.m = make_rsrc(a.bnb_mask, a.bnb_mask ? 0x7fffffff : 0);
+    return r;
+  };
+  // element offset o (bf16 elements) of the output / addend / BN-input tensors
+  // addend element offset of output pixel `row`, column nl (BAD bytes -> zeros: an odd pixel of a
+  // stride-2 compact addend)
+  auto addend_off = [&](int row, int nl) -> uint32_t {
+    if (!a.addend_s2) return ((uint32_t)row * (uint32_t)a.ldc + (uint32_t)nl) * 2u;
+    const int HW = a.H * a.W;
+    const int nn = a.fd_s2HW.div(row), yx = row - nn * HW, y = a.fd_s2W.div(yx), x = yx - y * a.W;
+    const uint32_t o = ((uint32_t)((nn * a.s2_P + (y >> 1)) * a.s2_Q + (x >> 1)) * (uint32_t)a.ldc + nl) * 2u;
+    return ((y | x) & 1) ? BAD : o;
+  };
+  auto epi_load = [&](const EpiRes& r, uint32_t o, uint32_t oa, U4& ad, uint32_t& am, U4& xv, uint32_t& mb) {
+    ad = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(r.ad, oa, 0, 0));
+    am = a.addend_mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r.am, o >> 3, 0, 0) : 0xffu;
+    if constexpr (EPI == EPI_BNB) {
+      xv = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(r.x, o * 2u, 0, 0));
+      mb = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r.m, o >> 3, 0, 0);
+    }
+  };
   constexpr int NPF = SWAP ? (TN / 2) * TM : 1;
   constexpr bool PF = EPI == EPI_BNB && SWAP && (NPF <= 4 || (STG == 1 && !GL && NPF <= 8));
   U4 pf_ad[PF ? NPF : 1], pf_x[PF ? NPF : 1];
@@ -603,6 +652,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   auto epi_prefetch = [&]() {
     if constexpr (PF) {
       if (KS == 2 && grp != 0) return;  // group 1 only hands its accumulators over
+      const EpiRes er = epi_res();
       const int mb0 = m0 + wm * WM, nb0 = n0 + wn * WN;
       const bool odd = (lane >> 4) & 1;
 #pragma unroll
@@ -617,14 +667,9 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
             const int nn = a.fd_cHW.div(m), yx = m - nn * a.H * a.W, y = a.fd_cW.div(yx), x = yx - y * a.W;
             row = (nn * a.out_H + 2 * y + a.cph) * a.out_W + 2 * x + a.cpw;
           }
-          const int64_t o = (int64_t)row * a.ldc + nl;
+          const uint32_t o = (uint32_t)row * (uint32_t)a.ldc + (uint32_t)nl;
           const int e = (j / 2) * TM + i;
-          if (a.addend) {
-            pf_ad[e] = *reinterpret_cast<const U4*>(a.addend + o);
-            pf_am[e] = a.addend_mask ? a.addend_mask[o >> 3] : 0xffu;
-          }
-          pf_x[e] = *reinterpret_cast<const U4*>(a.bnb_x + o);
-          pf_m[e] = a.bnb_mask ? a.bnb_mask[o >> 3] : 0xffu;
+          epi_load(er, o, addend_off(row, nl), pf_ad[e], pf_am[e], pf_x[e], pf_m[e]);
         }
       }
     }
@@ -884,6 +929,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
     const bool relu = a.relu != 0;
     // element offset of output row m (MODE_DGRAD_CLS: class sub-grid pixel -> full-grid pixel)
     int64_t rowoff[TM];
+    int rowpix[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = min(mb + i * 16 + (lane & 15), a.M - 1);
@@ -893,6 +939,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
         row = (n * a.out_H + 2 * y + a.cph) * a.out_W + 2 * x + a.cpw;
       }
       rowoff[i] = (int64_t)row * a.ldc;
+      rowpix[i] = row;
     }
     // fused-BN variants only ever take the 16-byte path (igemm_launch checks): compile only that one
     if (EPI != EPI_PLAIN ||
@@ -905,6 +952,11 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
       constexpr bool bnb = EPI == EPI_BNB;    // fused BN-backward partials of this output
       constexpr bool sts = EPI == EPI_STATS;  // fused BN statistics of this (bf16-rounded) output
       float* red = reinterpret_cast<float*>(smem);  // [2 wm][BN cols][2] partials (LDS free after the loop)
+      // BN-backward ReLU mask source, decided once: 2 = the residual layer's bits, 1 = recomputed
+      // from x*scale+shift, 0 = none
+      const int bnb_mode = !a.bnb_relu ? 0 : (a.bnb_mask ? 2 : 1);
+      const EpiRes er = epi_res();
+      const __amdgpu_buffer_rsrc_t r_out = make_rsrc(a.Cp, 0x7fffffff);
 #pragma unroll
       for (int j = 0; j < TN; j += 2) {
         const int n = nb + (j + (odd ? 1 : 0)) * 16 + ((lane >> 5) << 3);
@@ -917,15 +969,22 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
             bq[k] = 0.f;
           }
         }
+        float nmi[8];  // -mean * invstd
         if constexpr (bnb) {
           const int nc = min(n, a.N - 8);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            mu[k] = a.bnb_save[nc + k];
-            is[k] = a.bnb_save[a.N + nc + k];
-            sc[k] = a.bnb_save[2 * a.N + nc + k];
-            sh[k] = a.bnb_save[3 * a.N + nc + k];
+          for (int q = 0; q < 2; ++q) {  // nc and N are multiples of 8: 16-byte loads
+            const float4 m4 = *reinterpret_cast<const float4*>(a.bnb_save + nc + 4 * q);
+            const float4 i4 = *reinterpret_cast<const float4*>(a.bnb_save + a.N + nc + 4 * q);
+            const float4 c4 = *reinterpret_cast<const float4*>(a.bnb_save + 2 * a.N + nc + 4 * q);
+            const float4 h4 = *reinterpret_cast<const float4*>(a.bnb_save + 3 * a.N + nc + 4 * q);
+            mu[4 * q] = m4.x; mu[4 * q + 1] = m4.y; mu[4 * q + 2] = m4.z; mu[4 * q + 3] = m4.w;
+            is[4 * q] = i4.x; is[4 * q + 1] = i4.y; is[4 * q + 2] = i4.z; is[4 * q + 3] = i4.w;
+            sc[4 * q] = c4.x; sc[4 * q + 1] = c4.y; sc[4 * q + 2] = c4.z; sc[4 * q + 3] = c4.w;
+            sh[4 * q] = h4.x; sh[4 * q + 1] = h4.y; sh[4 * q + 2] = h4.z; sh[4 * q + 3] = h4.w;
           }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) nmi[k] = -mu[k] * is[k];
         }
         // The epilogue's global reads (addend, BN input, ReLU mask bits) of IC rows are issued
         // together BEFORE the rows' stores: the compiler cannot hoist a load over a store it may
@@ -948,15 +1007,11 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
               mbv[ii] = pf_m[e];
               continue;
             }
-            const int64_t o = rowoff[i0 + ii] + nl;
-            if (a.addend) {
-              adv[ii] = *reinterpret_cast<const U4*>(a.addend + o);
-              amv[ii] = a.addend_mask ? a.addend_mask[o >> 3] : 0xffu;
-            }
-            if constexpr (bnb) {
-              xvv[ii] = *reinterpret_cast<const U4*>(a.bnb_x + o);
-              mbv[ii] = a.bnb_mask ? a.bnb_mask[o >> 3] : 0xffu;
-            }
+            // BN-backward kernels load unconditionally (null operands read zeros); the others only
+            // ever read an addend, under its (uniform) flag
+            if (bnb || a.addend)
+              epi_load(er, (uint32_t)rowoff[i0 + ii] + (uint32_t)nl, addend_off(rowpix[i0 + ii], nl), adv[ii],
+                       amv[ii], xvv[ii], mbv[ii]);
           }
 #pragma unroll
           for (int ii = 0; ii < IC; ++ii) {
@@ -983,15 +1038,17 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
               o[4 + r] = __uint_as_float(sw[1]);
             }
             if (m < a.M && n < a.N) {
-              uint16_t* dst = Cb + rowoff[i] + n;
               if (a.addend) {  // fused residual-branch gradient sum (dX = dgrad + other branch)
+                // the addend's ReLU mask bits (0xff when unmasked) zero its bf16 halves before the
+                // unpack: straight-line bit ops, no per-element select on a runtime flag
                 float ad[8];
-                unpack8(adv[ii], ad);
+                unpack8(mask_bf16x8(adv[ii], amv[ii]), ad);
 #pragma unroll
-                for (int r = 0; r < 8; ++r) o[r] += ((amv[ii] >> r) & 1u) ? ad[r] : 0.f;
+                for (int r = 0; r < 8; ++r) o[r] += ad[r];
               }
               const U4 packed = pack8(o);
-              *reinterpret_cast<U4*>(dst) = packed;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, packed), r_out,
+                                                     ((uint32_t)rowoff[i] + (uint32_t)n) * 2u, 0, 0);
               if constexpr (sts) {
                 // per-column sum / sum of squares of exactly the bf16 values the BN will read
                 float g[8];
@@ -1003,18 +1060,26 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
                 }
               }
               if constexpr (bnb) {
-                // g' = bf16(out) * relu mask; xhat from the BN input x (same NHWC position)
-                float g[8], xv[8];
-                unpack8(packed, g);
+                // g' = bf16(out) * relu mask; xhat = x * invstd - mean * invstd from the BN input x
+                // (same NHWC position).  The mask comes from the residual layer's bits or from
+                // x*scale+shift > 0, chosen once per kernel (bnb_mode), and is applied to the bf16
+                // words before the unpack.
+                float xv[8];
                 unpack8(xvv[ii], xv);
-                const uint32_t mbits = mbv[ii];
+                uint32_t on8 = 0xffu;
+                if (bnb_mode == 2) {
+                  on8 = mbv[ii];
+                } else if (bnb_mode == 1) {
+                  on8 = 0;
+#pragma unroll
+                  for (int k = 0; k < 8; ++k) on8 |= (fmaf(xv[k], sc[k], sh[k]) > 0.f ? 1u : 0u) << k;
+                }
+                float g[8];
+                unpack8(mask_bf16x8(packed, on8), g);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                  bool on = true;
-                  if (a.bnb_relu) on = a.bnb_mask ? ((mbits >> k) & 1u) != 0 : fmaf(xv[k], sc[k], sh[k]) > 0.f;
-                  const float gg = on ? g[k] : 0.f;
-                  bs[k] += gg;
-                  bq[k] = fmaf(gg, (xv[k] - mu[k]) * is[k], bq[k]);
+                  bs[k] += g[k];
+                  bq[k] = fmaf(g[k], fmaf(xv[k], is[k], nmi[k]), bq[k]);
                 }
               }
             }

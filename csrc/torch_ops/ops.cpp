@@ -116,12 +116,37 @@ const uint8_t* addend_mask_ptr(const optional<Tensor>& addend, const optional<Te
   return mask->data_ptr<uint8_t>();
 }
 
+// addend_s2: the addend is the compact even-pixel gradient [N][ceil(H/2)][ceil(W/2)][C] of a 1x1
+// stride-2 branch (its data gradient computed on the strided grid only); the epilogue adds it at the
+// even (y, x) pixels and nothing elsewhere -- no zero-filled full-size tensor is ever written
+void set_addend_s2(tfx::IgemmArgs& a, const Tensor& addend, int64_t N, int64_t H, int64_t W, int64_t C) {
+  const int64_t P2 = (H + 1) / 2, Q2 = (W + 1) / 2;
+  CHECK_BF16(addend); CHECK_CONTIG(addend);
+  TORCH_CHECK(addend.sizes() == at::IntArrayRef({N, P2, Q2, C}), "stride-2 compact addend shape");
+  a.addend = bf(addend);
+  a.addend_s2 = 1; a.s2_P = (int)P2; a.s2_Q = (int)Q2;
+  a.fd_s2HW = tfx::FastDiv((uint32_t)(H * W)); a.fd_s2W = tfx::FastDiv((uint32_t)W);
+}
+
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil,
-                  optional<Tensor> addend, optional<Tensor> addend_mask) {
+                  optional<Tensor> addend, optional<Tensor> addend_mask, bool addend_s2) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
   const bool acc = addend.has_value() && addend->defined();
+  if (addend_s2) {
+    TORCH_CHECK(acc && stride == 1 && !(addend_mask.has_value() && addend_mask->defined()),
+                "stride-2 compact addend: stride-1 data gradients, no mask");
+    auto dx = at::empty({g.N, g.H, g.W, g.C}, dy.options());
+    auto a = conv_args(g, stride, pad, dil);
+    a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
+    a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
+    a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+    a.out_mode = tfx::OUT_BF16;
+    set_addend_s2(a, *addend, g.N, g.H, g.W, g.C);
+    tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
+    return dx;
+  }
   if (acc) {
     CHECK_BF16(*addend); CHECK_CONTIG(*addend);
     TORCH_CHECK(addend->sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "addend shape");
@@ -245,7 +270,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
                                          int64_t pad, int64_t dil, optional<Tensor> addend, Tensor bn_x,
                                          Tensor bn_save, optional<Tensor> bn_mask, bool relu, Tensor ws,
                                          optional<Tensor> dgamma, optional<Tensor> dbeta,
-                                         optional<Tensor> addend_mask, bool reduce) {
+                                         optional<Tensor> addend_mask, bool reduce, bool addend_s2) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
   TORCH_CHECK(stride == 1, "conv_dgrad_bn: stride-1 convs only (stride 2 runs per parity class)");
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
@@ -254,12 +279,14 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   TORCH_CHECK(bn_x.sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "bn_x shape");
   TORCH_CHECK(bn_save.numel() == 4 * g.C, "bn_save size");
   const bool acc = addend.has_value() && addend->defined();
-  if (acc) {
+  if (acc && !addend_s2) {
     CHECK_BF16(*addend); CHECK_CONTIG(*addend);
     TORCH_CHECK(addend->sizes() == at::IntArrayRef({g.N, g.H, g.W, g.C}), "addend shape");
   }
-  const uint8_t* amask = addend_mask_ptr(addend, addend_mask);
-  auto dx = (acc && !amask) ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
+  TORCH_CHECK(!addend_s2 || (acc && !(addend_mask.has_value() && addend_mask->defined())),
+              "stride-2 compact addend: no mask");
+  const uint8_t* amask = addend_s2 ? nullptr : addend_mask_ptr(addend, addend_mask);
+  auto dx = (acc && !amask && !addend_s2) ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
   // reduce = false: the partials stay in the slots for bn_bwd_slots (no red, no slot reduce)
   auto red = reduce ? at::empty({2 * g.C}, dy.options().dtype(at::kFloat)) : Tensor();
   auto a = conv_args(g, stride, pad, dil);
@@ -268,6 +295,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
   a.out_mode = tfx::OUT_BF16;
   if (acc) a.addend = bf(*addend);
+  if (addend_s2) set_addend_s2(a, *addend, g.N, g.H, g.W, g.C);
   a.addend_mask = amask;
   a.bnb_x = bf(bn_x); a.bnb_save = bn_save.data_ptr<float>();
   if (bn_mask.has_value() && bn_mask->defined()) {
@@ -1111,7 +1139,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("conv_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
-        "Tensor? addend_mask=None) -> Tensor", &conv_dgrad);
+        "Tensor? addend_mask=None, bool addend_s2=False) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("gemm", &gemm);
   m.def("gemm_into", &gemm_into);
@@ -1124,7 +1152,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
         "Tensor bn_x, Tensor bn_save, Tensor? bn_mask, bool relu, Tensor ws, Tensor? dgamma, Tensor? dbeta, "
-        "Tensor? addend_mask=None, bool reduce=True) -> (Tensor, Tensor)", &conv_dgrad_bn);
+        "Tensor? addend_mask=None, bool reduce=True, bool addend_s2=False) -> (Tensor, Tensor)", &conv_dgrad_bn);
   m.def("bn_fwd_slots", &bn_fwd_slots);
   m.def("bn_bwd_slots", &bn_bwd_slots);
   m.def("bn_slots_supported", &bn_slots_supported);

@@ -62,5 +62,27 @@ def main():
               f"  conv_fwd_stats(same dims) {t_fw:6.1f}", flush=True)
 
 
+def bench_3x3():
+    """Stride-1 3x3 data gradient as the forward conv of dY with the flipped, transposed filter
+    (Wf[c][r][s][ko] = W[ko][R-1-r][S-1-s][c]) vs the gathered data-gradient kernel."""
+    for (B, H, W, C) in [(256, 32, 32, 64), (256, 16, 16, 128), (256, 8, 8, 256), (256, 4, 4, 512)]:
+        Ko = C
+        dy = torch.randn(B, H, W, Ko, device="cuda").bfloat16()
+        w = (torch.randn(Ko, 3, 3, C, device="cuda") * 0.05).bfloat16()
+        wf = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+        t_dg = graph_us(lambda: torch.ops.tfx.conv_dgrad(dy, w, [B, H, W, C], 1, 1, 1, None, None))
+        t_fw = graph_us(lambda: torch.ops.tfx.conv_fwd(dy, wf, 1, 1, 1))
+        t_tr = graph_us(lambda: w.flip(1, 2).permute(3, 1, 2, 0).contiguous())
+        a = torch.ops.tfx.conv_dgrad(dy, w, [B, H, W, C], 1, 1, 1, None, None)
+        b = torch.ops.tfx.conv_fwd(dy, wf, 1, 1, 1)
+        err = ((a.float() - b.float()).norm() / a.float().norm()).item()
+        print(f"3x3 {B}x{H}x{W}x{C}: conv_dgrad {t_dg:6.1f} us | conv_fwd(dY, Wf) {t_fw:6.1f} us  "
+              f"(torch flip-transpose {t_tr:5.1f} us, rel diff {err:.2e})", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "3x3":
+        assert _native.load()
+        bench_3x3()
+        sys.exit(0)
     main()

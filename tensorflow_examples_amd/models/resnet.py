@@ -39,6 +39,9 @@ _FUSE_BN = os.environ.get("TFX_FUSE_BN", "1") != "0"
 # A/B switch: identity blocks hand conv1 the residual BN's (gradient, ReLU mask) instead of the
 # masked gradient tensor (one full-size write less per block; igemm.hip masked addend)
 _MASKED_RES = os.environ.get("TFX_MASKED_RES", "1") != "0"
+# A/B switch: a 1x1 stride-2 projection parks its input gradient compact (even pixels only) and
+# conv1's data-gradient epilogue adds it there -- no zero-filled full-size gradient (ops/nn.py)
+_S2_ADDEND = os.environ.get("TFX_S2_ADDEND", "1") != "0"
 
 
 class _BN:
@@ -104,6 +107,8 @@ class Bottleneck:
         prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
         if prod is not None and _MASKED_RES:
             prod.accept_masked = True  # conv1 (1x1, stride 1) applies the residual ReLU mask itself
+        if prod is not None and _S2_ADDEND:
+            prod.accept_s2 = True  # ... and a 1x1 stride-2 projection's compact gradient
         # conv1 is x's last consumer in backward only when the GradSink carries the other branch
         o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons, fuse_input_bn_backward=cons is not None)
         o = self.b2.after_conv(self.c2, o, training, relu=True, fuse_input_bn_backward=True)

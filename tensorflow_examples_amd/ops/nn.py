@@ -110,7 +110,7 @@ class _Conv2d(torch.autograd.Function):
                         and x.numel() * x.element_size() <= _BNB_MAX_BYTES:
                     # dx is the complete gradient of the BN output x: the epilogue also reduces
                     # that BN's backward (sum g', sum g' xhat, dgamma, dbeta) -- see BNBackwardFusion
-                    add, amask = _unpack_sink(sink.take()) if sink is not None else (None, None)
+                    add, amask, s2 = _unpack_sink(sink.take()) if sink is not None else (None, None, False)
                     if bnb.wsobj is not None:
                         # partials stay in the layer's backward slots S_b: the BN's backward apply
                         # reduces them itself (bn_bwd_slots), no slot-reduce launch
@@ -120,16 +120,24 @@ class _Conv2d(torch.autograd.Function):
                             bnb.wsobj.bwd_dirty = False
                         dx, _ = torch.ops.tfx.conv_dgrad_bn(
                             gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
-                            sb, None, None, amask, False)
+                            sb, None, None, amask, False, s2)
                         bnb.red = BNBackwardFusion.IN_SLOTS
                     else:
                         dx, bnb.red = torch.ops.tfx.conv_dgrad_bn(
                             gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
-                            bnb.ws, bnb.dgamma, bnb.dbeta, amask)
+                            bnb.ws, bnb.dgamma, bnb.dbeta, amask, True, s2)
                 elif sink is not None and sink.mode == "consume":
                     # last consumer of x in backward order: fold the other branch's gradient in
-                    add, amask = _unpack_sink(sink.take())
-                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, add, amask)
+                    add, amask, s2 = _unpack_sink(sink.take())
+                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, add, amask, s2)
+                elif sink is not None and sink.accept_s2 and stride == 2 and pad == 0 and w.shape[1] == 1 \
+                        and w.shape[2] == 1 and x.shape[-1] % 8 == 0:
+                    # 1x1 stride-2 branch: its input gradient is nonzero only at the even pixels --
+                    # compute it on the strided grid (a 1x1 stride-1 data gradient) and park it compact
+                    n, h, wd, c = x.shape
+                    dxc = torch.ops.tfx.conv_dgrad(gy, w.value, [n, gy.shape[1], gy.shape[2], c], 1, 0, dil, None)
+                    sink.put(("s2", dxc))
+                    dx = None
                 else:
                     dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, None)
                     if sink is not None:  # mode "produce": park it for the last consumer
@@ -161,11 +169,17 @@ def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int
 
 
 def _unpack_sink(item):
-    """A parked gradient is a tensor, or ``(g, mask)``: a residual BN's output gradient whose ReLU
-    mask the consumer applies in its epilogue (the masked copy is never written)."""
+    """A parked gradient is a tensor, ``(g, mask)``: a residual BN's output gradient whose ReLU
+    mask the consumer applies in its epilogue (the masked copy is never written), or
+    ``("s2", g)``: a 1x1 stride-2 branch's gradient at the even pixels only (compact grid; the
+    consumer adds it there and nothing elsewhere -- no zero-filled full-size tensor).
+    Returns (addend, mask, compact_stride2)."""
     if isinstance(item, tuple):
-        return item
-    return item, None
+        if isinstance(item[0], str):
+            assert item[0] == "s2"
+            return item[1], None, True
+        return item[0], item[1], False
+    return item, None, False
 
 
 class GradSink:
@@ -177,7 +191,9 @@ class GradSink:
     so it runs last (the ``take`` assertion guards this).
 
     ``accept_masked`` (set on the producer by a block whose consumer is a stride-1 conv): the
-    residual BN may park ``(g, relu_mask)`` instead of writing the masked gradient tensor."""
+    residual BN may park ``(g, relu_mask)`` instead of writing the masked gradient tensor.
+    ``accept_s2`` (same condition): a 1x1 stride-2 projection may park its gradient compact on the
+    strided grid, ``("s2", g)``."""
 
     def __init__(self, mode: str):
         assert mode in ("produce", "consume")
@@ -185,6 +201,7 @@ class GradSink:
         self.buf = None
         self.peer: Optional["GradSink"] = None
         self.accept_masked = False
+        self.accept_s2 = False
 
     @staticmethod
     def pair():
