@@ -106,8 +106,10 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s);
 
 // ---------------------------------------------------------------- f32 GEMM (MFMA f32, exact)
 // C[M][N] = act(alpha * op(A) op(B) + bias) (+ C if accumulate); op = transpose flags
+// allow_split: split K over blocks with f32-atomic partials when the output has few tiles (act 0)
 void sgemm_launch(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int lda,
-                  int ldb, int ldc, bool transA, bool transB, int act, bool accumulate, hipStream_t s);
+                  int ldb, int ldc, bool transA, bool transB, int act, bool accumulate, hipStream_t s,
+                  bool allow_split = false);
 
 // ---------------------------------------------------------------- batch norm (NHWC)
 // slots: persistent per-layer workspace [NSLOT][2][C] f32, zero between uses (consumers re-zero it)

@@ -389,7 +389,7 @@ void gemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor out, bool accumulate
 }
 
 // ------------------------------------------------------------------ f32 GEMM (MFMA f32)
-Tensor sgemm(Tensor a, Tensor b, bool ta, bool tb, optional<Tensor> bias, int64_t act) {
+Tensor sgemm(Tensor a, Tensor b, bool ta, bool tb, optional<Tensor> bias, int64_t act, bool split) {
   CHECK_DEV(a); CHECK_F32(a); CHECK_F32(b);
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "sgemm operands");
   const int64_t M = ta ? a.size(1) : a.size(0), K = ta ? a.size(0) : a.size(1);
@@ -397,17 +397,17 @@ Tensor sgemm(Tensor a, Tensor b, bool ta, bool tb, optional<Tensor> bias, int64_
   TORCH_CHECK((tb ? b.size(1) : b.size(0)) == K, "sgemm inner dims");
   auto out = at::empty({M, N}, a.options());
   tfx::sgemm_launch(a.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(), fp(bias), M, N, K,
-                    a.stride(0), b.stride(0), N, ta, tb, act, false, cur_stream());
+                    a.stride(0), b.stride(0), N, ta, tb, act, false, cur_stream(), split);
   return out;
 }
 
-void sgemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor out, bool accumulate) {
+void sgemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor out, bool accumulate, bool split) {
   CHECK_DEV(a); CHECK_F32(a); CHECK_F32(b); CHECK_F32(out);
   const int64_t M = ta ? a.size(1) : a.size(0), K = ta ? a.size(0) : a.size(1);
   const int64_t N = tb ? b.size(0) : b.size(1);
   TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.stride(1) == 1, "sgemm_into out shape");
   tfx::sgemm_launch(a.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(), nullptr, M, N, K,
-                    a.stride(0), b.stride(0), out.stride(0), ta, tb, 0, accumulate, cur_stream());
+                    a.stride(0), b.stride(0), out.stride(0), ta, tb, 0, accumulate, cur_stream(), split);
 }
 
 // ------------------------------------------------------------------ batch norm
@@ -1143,8 +1143,9 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("gemm", &gemm);
   m.def("gemm_into", &gemm_into);
-  m.def("sgemm", &sgemm);
-  m.def("sgemm_into", &sgemm_into);
+  m.def("sgemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, int act, bool split=False) -> Tensor", &sgemm);
+  m.def("sgemm_into(Tensor a, Tensor b, bool ta, bool tb, Tensor(a!) out, bool accumulate, bool split=False) -> ()",
+        &sgemm_into);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply_train", &bn_apply_train);
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "

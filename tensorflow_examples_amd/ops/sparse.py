@@ -124,11 +124,12 @@ def sampled_loss_grads(E: torch.Tensor, Wt: torch.Tensor, bt: Optional[torch.Ten
     (remove_accidental_hits=True). Returns (loss_rows [B], dE [B,D], dWt [B,D], dbt [B], dWs [S,D],
     dbs [S]); gradients are of ``gscale * sum(loss_rows)``."""
     if _native.use_native(E):
-        neg = torch.ops.tfx.sgemm(E, Ws, False, True, bs, 0)
+        neg = torch.ops.tfx.sgemm(E, Ws, False, True, bs, 0, True)
         loss, dn, dE, dWt, dbt = torch.ops.tfx.sampled_loss(E, Wt, bt, neg, logq_t, logq_s, true_ids, sampled_ids,
                                                              gscale, softmax)
         torch.ops.tfx.sgemm_into(dn, Ws, False, False, dE, True)
-        dWs = torch.ops.tfx.sgemm(dn, E, True, False, None, 0)
+        # dWs = dn^T E reduces over the whole batch into 64 x D: split-K over blocks (f32 atomics)
+        dWs = torch.ops.tfx.sgemm(dn, E, True, False, None, 0, True)
         dbs = dn.sum(0)
         return loss, dE, dWt, dbt, dWs, dbs
     return _sampled_ref(E, Wt, bt, Ws, bs, logq_t, logq_s, true_ids, sampled_ids, softmax, gscale)

@@ -99,6 +99,27 @@ def test_gemm_bias_relu_bf16(gpu):
     assert out.dtype == torch.bfloat16 and _rel(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("M,N,K,split", [(64, 128, 4096, True), (4096, 64, 128, True), (4096, 128, 64, False),
+                                         (100, 784, 100, False), (37, 61, 1029, True)])
+def test_sgemm_shapes(gpu, ta, tb, M, N, K, split):
+    """The word2vec sampled-loss GEMMs (neg = E Ws^T, dE += dn Ws, dWs = dn^T E with split-K f32
+    atomics) and ragged shapes that take the scalar (non-16-byte) staging path."""
+    torch.manual_seed(5)
+    A = torch.randn(M, K, device=gpu)
+    B = torch.randn(K, N, device=gpu)
+    a = A.t().contiguous() if ta else A
+    b = B.t().contiguous() if tb else B
+    out = torch.ops.tfx.sgemm(a, b, ta, tb, None, 0, split)
+    ref = (A.double() @ B.double()).float()
+    tol = 1e-4 * max(1.0, K / 100) ** 0.5
+    assert (out - ref).abs().max().item() < 10 * tol
+    acc = torch.randn(M, N, device=gpu)
+    acc0 = acc.clone()
+    torch.ops.tfx.sgemm_into(a, b, ta, tb, acc, True, split)
+    assert (acc - (acc0 + ref)).abs().max().item() < 10 * tol
+
+
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True)])
 def test_sgemm_exact_f32(gpu, ta, tb):
     torch.manual_seed(2)
