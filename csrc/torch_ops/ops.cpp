@@ -701,6 +701,22 @@ Tensor sse_bwd(Tensor p, Tensor y, Tensor g) {
 
 // f32: returns dz = g * act'(y).  bf16 (g, y bf16): returns dz for act != 0, or an empty tensor when
 // act == 0 (only the bias column sums are wanted: g itself is the GEMM operand).
+// backward of y = x W^T + b with few outputs: returns dx (undefined unless want_dx); dW / db
+// (f32, [O][I] / [O]) are accumulated in place when given
+Tensor linear_small_bwd(Tensor g, Tensor x, Tensor w, bool want_dx, optional<Tensor> dw, optional<Tensor> db) {
+  CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
+  const int64_t B = g.size(0), O = g.size(1), I = x.size(1);
+  TORCH_CHECK(x.size(0) == B && w.size(0) == O && w.size(1) == I, "linear_small_bwd shapes");
+  TORCH_CHECK(O <= 64 && B * O <= 16384, "linear_small_bwd: O <= 64 and B*O <= 16384");
+  Tensor dx;
+  if (want_dx) dx = at::empty({B, I}, x.options());
+  if (dw.has_value() && dw->defined()) { CHECK_F32(*dw); TORCH_CHECK(dw->numel() == O * I && dw->is_contiguous(), "dw"); }
+  if (db.has_value() && db->defined()) { CHECK_F32(*db); TORCH_CHECK(db->numel() == O, "db"); }
+  tfx::linear_small_bwd(bf(g), bf(x), bf(w), (int)B, (int)I, (int)O, want_dx ? bfm(dx) : nullptr, fpm(dw), fpm(db),
+                        cur_stream());
+  return dx;
+}
+
 Tensor act_bwd_colsum(Tensor g, Tensor y, int64_t act, optional<Tensor> dbias) {
   CHECK_DEV(g); CHECK_CONTIG(g); CHECK_CONTIG(y);
   TORCH_CHECK(g.dim() == 2 && g.sizes() == y.sizes() && g.scalar_type() == y.scalar_type(),
@@ -1171,6 +1187,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("sse_fwd", &sse_fwd);
   m.def("sse_bwd", &sse_bwd);
   m.def("act_bwd_colsum", &act_bwd_colsum);
+  m.def("linear_small_bwd", &linear_small_bwd);
   m.def("scale_by_scalar", &scale_by_scalar);
   m.def("sumsq", &sumsq);
   m.def("cast_f32_bf16", &cast_f32_bf16);

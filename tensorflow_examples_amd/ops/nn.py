@@ -489,10 +489,10 @@ class _Linear(torch.autograd.Function):
         if ctx.native:
             out_f = w.shape[0]
             xp = _pad_to(x.contiguous(), 1, 8)
-            wp = _pad_to(_pad_to(w.value, 1, 8), 0, 8)
+            # W is the K-major B operand: rows past out_f are zero-filled by the loader's bounds, so
+            # only its K (input) dim needs the 8-multiple -- no padded copy of W or the bias
+            wp = _pad_to(w.value, 1, 8)
             bias = b.master if b is not None else None
-            if bias is not None and wp.shape[0] != out_f:
-                bias = _pad_to(bias, 0, 8)
             y = torch.ops.tfx.gemm(xp, wp, False, True, bias, relu, False)
             if y.shape[1] != out_f:
                 y = y[:, :out_f].contiguous()
@@ -508,6 +508,15 @@ class _Linear(torch.autograd.Function):
         x, y = ctx.saved_tensors
         w, b, relu = ctx.w, ctx.b, ctx.relu
         need_dx = ctx.needs_input_grad[0]
+        if ctx.native and not relu and w.shape[0] <= 64 and gy.shape[0] * w.shape[0] <= 16384 \
+                and x.dim() == 2 and w.value.is_contiguous():
+            # few outputs (classifier head): dx, dW, db in one launch (elementwise.hip linear_small_bwd)
+            g = gy.to(torch.bfloat16).contiguous()
+            bias_grad = b.grad if (b is not None and b.trainable) else None
+            dx = torch.ops.tfx.linear_small_bwd(g, x.contiguous(), w.value, need_dx,
+                                                w.grad if w.trainable else None, bias_grad)
+            _grad_ready(w if w.trainable else None, b if bias_grad is not None else None)
+            return (dx if need_dx else None), None, None, None, None
         if ctx.native:
             g = gy.to(torch.bfloat16).contiguous()
             bias_grad = b.grad if (b is not None and b.trainable) else None

@@ -406,3 +406,18 @@ def test_conv_dgrad_bn_reduce(gpu, shape, variant):
     assert _rel(bx, ref_bx) < 1e-2
     if mask is not None:
         assert _rel(dres, ref_dres) < 1e-2
+
+
+@pytest.mark.parametrize("B,I,O", [(256, 2048, 10), (100, 84, 10), (64, 520, 64)])
+def test_linear_small_bwd(gpu, B, I, O):
+    """Classifier-head backward in one launch: dx = g W, dW += g^T x, db += colsum(g)."""
+    torch.manual_seed(41)
+    g = _bf(torch.randn(B, O, device=gpu))
+    x = _bf(torch.randn(B, I, device=gpu))
+    w = _bf(torch.randn(O, I, device=gpu) * 0.1)
+    dw = torch.ones(O, I, device=gpu)
+    db = torch.ones(O, device=gpu)
+    dx = torch.ops.tfx.linear_small_bwd(g, x, w, True, dw, db)
+    assert _rel(dx, g.float() @ w.float()) < 1e-2
+    assert _rel(dw - 1, g.float().t() @ x.float()) < 1e-3
+    assert _rel(db - 1, g.float().sum(0)) < 1e-3
