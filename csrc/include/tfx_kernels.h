@@ -175,7 +175,7 @@ void act_bwd_colsum(const float* g, const float* y, int act, int64_t M, int N, f
 void act_bwd_colsum_bf16(const uint16_t* g, const uint16_t* y, int act, int64_t M, int N, uint16_t* dz,
                          float* dbias, hipStream_t s);
 // linear layer with O <= 64 outputs (classifier head), bf16 g [B][O], x [B][I], W [O][I]:
-// dx = g W (bf16, skipped when null), dW += g^T x, db += colsum(g) (f32, skipped when null); B*O <= 16384
+// dx = g W (bf16, skipped when null), dW += g^T x, db += colsum(g) (f32 atomics, skipped when null)
 void linear_small_bwd(const uint16_t* g, const uint16_t* x, const uint16_t* w, int B, int I, int O, uint16_t* dx,
                       float* dw, float* db, hipStream_t s);
 // y = x * scal[0] (f32 or bf16 output)

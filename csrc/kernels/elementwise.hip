@@ -193,18 +193,22 @@ void act_bwd_colsum_bf16(const uint16_t* g, const uint16_t* y, int act, int64_t 
 
 // ---- backward of a linear layer with few outputs (a classifier head: O <= 64, e.g. ResNet's
 // 2048 -> 10 FC): dx = g W, dW += g^T x, db += colsum(g) in ONE launch instead of padded bf16 GEMMs
-// plus pad / copy / zero-fill kernels.  Block = 64 input columns x all B rows: g ([B][O], bf16) is
-// staged in LDS as f32; each thread owns one column and sweeps the rows for dx (O FMAs per element)
-// and keeps the O partial sums of dW for its column in registers.  Block 0 also writes db.
+// plus pad / copy / zero-fill kernels.  Block = 64 input columns x LRB rows (grid.y over the batch):
+// the rows' g ([LRB][O], bf16) is staged in LDS as f32; a thread owns one column and LRB/4 rows (dx:
+// O FMAs per element) and keeps its column's O partial dW sums in registers; the block's dW / db
+// partials go out as f32 atomics (dW, db are accumulated gradients).
+constexpr int LRB = 32;
 template <int OMAX>
 __global__ void __launch_bounds__(256) linear_small_bwd_kernel(const uint16_t* __restrict__ g,
                                                                const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ w, int B, int I, int O,
                                                                uint16_t* __restrict__ dx, float* __restrict__ dw,
                                                                float* __restrict__ db) {
-  extern __shared__ float gs[];  // [B][O]
-  const int t = threadIdx.x;
-  for (int i = t; i < B * O; i += 256) gs[i] = bf16_to_f32(g[i]);
+  __shared__ float gs[LRB * OMAX];
+  __shared__ float part[4][64][OMAX + 1];
+  const int t = threadIdx.x, b0 = blockIdx.y * LRB;
+  const int nb = min(LRB, B - b0);
+  for (int i = t; i < nb * O; i += 256) gs[i] = bf16_to_f32(g[(int64_t)b0 * O + i]);
   __syncthreads();
   const int c = blockIdx.x * 64 + (t & 63), rq = t >> 6;  // 4 row phases x 64 columns
   float wcol[OMAX], acc[OMAX];
@@ -214,44 +218,50 @@ __global__ void __launch_bounds__(256) linear_small_bwd_kernel(const uint16_t* _
     acc[o] = 0.f;
   }
   if (c < I) {
-    for (int b = rq; b < B; b += 4) {
-      const float* gr = gs + b * O;
-      const float xv = bf16_to_f32(x[(int64_t)b * I + c]);
-      float s = 0.f;
+    float xv[LRB / 4];
 #pragma unroll
-      for (int o = 0; o < OMAX; ++o) {
-        if (o < O) {
-          s = fmaf(gr[o], wcol[o], s);
-          acc[o] = fmaf(gr[o], xv, acc[o]);
+    for (int k = 0; k < LRB / 4; ++k) {
+      const int r = rq + 4 * k;
+      xv[k] = r < nb ? bf16_to_f32(x[(int64_t)(b0 + r) * I + c]) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < LRB / 4; ++k) {
+      const int r = rq + 4 * k;
+      if (r < nb) {
+        const float* gr = gs + r * O;
+        float s = 0.f;
+#pragma unroll
+        for (int o = 0; o < OMAX; ++o) {
+          if (o < O) {
+            s = fmaf(gr[o], wcol[o], s);
+            acc[o] = fmaf(gr[o], xv[k], acc[o]);
+          }
         }
+        if (dx) dx[(int64_t)(b0 + r) * I + c] = f32_to_bf16(s);
       }
-      if (dx) dx[(int64_t)b * I + c] = f32_to_bf16(s);
     }
   }
-  // reduce the 4 row phases of dW through LDS
-  __shared__ float part[4][64][OMAX + 1];
 #pragma unroll
   for (int o = 0; o < OMAX; ++o) part[rq][t & 63][o] = acc[o];
   __syncthreads();
   if (rq == 0 && c < I && dw) {
 #pragma unroll
     for (int o = 0; o < OMAX; ++o) {
-      if (o < O) dw[(int64_t)o * I + c] += part[0][t][o] + part[1][t][o] + part[2][t][o] + part[3][t][o];
+      if (o < O) atomicAdd(dw + (int64_t)o * I + c, part[0][t][o] + part[1][t][o] + part[2][t][o] + part[3][t][o]);
     }
   }
   if (blockIdx.x == 0 && db && t < O) {
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += gs[b * O + t];
-    db[t] += s;
+    for (int r = 0; r < nb; ++r) s += gs[r * O + t];
+    atomicAdd(db + t, s);
   }
 }
 
 void linear_small_bwd(const uint16_t* g, const uint16_t* x, const uint16_t* w, int B, int I, int O, uint16_t* dx,
                       float* dw, float* db, hipStream_t s) {
-  const size_t lds = sizeof(float) * (size_t)B * O;
-  const dim3 grid((I + 63) / 64);
-  if (O <= 16) linear_small_bwd_kernel<16><<<grid, 256, lds, s>>>(g, x, w, B, I, O, dx, dw, db);
-  else linear_small_bwd_kernel<64><<<grid, 256, lds, s>>>(g, x, w, B, I, O, dx, dw, db);
+  const dim3 grid((I + 63) / 64, (B + LRB - 1) / LRB);
+  if (O <= 16) linear_small_bwd_kernel<16><<<grid, 256, 0, s>>>(g, x, w, B, I, O, dx, dw, db);
+  else linear_small_bwd_kernel<64><<<grid, 256, 0, s>>>(g, x, w, B, I, O, dx, dw, db);
 }
 
 void scale_by_scalar(const float* x, const float* scal, int64_t n, float* y32, uint16_t* y16, hipStream_t s) {

@@ -508,8 +508,7 @@ class _Linear(torch.autograd.Function):
         x, y = ctx.saved_tensors
         w, b, relu = ctx.w, ctx.b, ctx.relu
         need_dx = ctx.needs_input_grad[0]
-        if ctx.native and not relu and w.shape[0] <= 64 and gy.shape[0] * w.shape[0] <= 16384 \
-                and x.dim() == 2 and w.value.is_contiguous():
+        if ctx.native and not relu and w.shape[0] <= 64 and x.dim() == 2 and w.value.is_contiguous():
             # few outputs (classifier head): dx, dW, db in one launch (elementwise.hip linear_small_bwd)
             g = gy.to(torch.bfloat16).contiguous()
             bias_grad = b.grad if (b is not None and b.trainable) else None
