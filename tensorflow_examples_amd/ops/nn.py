@@ -24,6 +24,56 @@ from . import _native
 from ..variables import Variable
 
 
+# ---------------------------------------------------------------- side-stream weight gradients
+# A conv's weight gradient is off the backward critical path: nothing but the optimizer (and the
+# DP all-reduce of its bucket) reads it.  Running it on a second stream lets it overlap the data-
+# gradient / BN-backward chain of the next layers -- most of those kernels leave CUs idle (small
+# grids, memory latency).  The end of the backward pass (an autograd engine callback, so every
+# caller of .backward() gets it) makes the current stream wait for the side stream; the DP
+# all-reduce orders each bucket after both streams (parallel/allreduce.py).  Opt-in
+# (TFX_WGRAD_STREAM=1): the kernels do overlap (rocprofv3 traces: ~4.5 ms of overlapped kernel time
+# per step), but a replayed HIP graph with the branches ran 8.72-8.77 vs 8.37-8.39 ms/step, and
+# eager launches with it 8.26-8.86 ms (host-noise bound) -- profiles/r02_side.
+_WGRAD_STREAM = os.environ.get("TFX_WGRAD_STREAM", "0") == "1"
+_side = {}
+_side_pending = {"active": False}
+
+
+def wgrad_side_stream(device) -> Optional[torch.cuda.Stream]:
+    """The persistent side stream of `device` when side-stream weight gradients are on, else None."""
+    if not _WGRAD_STREAM or device.type != "cuda":
+        return None
+    s = _side.get(device.index)
+    if s is None:
+        s = _side[device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
+def _join_side_streams() -> None:
+    _side_pending["active"] = False
+    for s in _side.values():
+        torch.cuda.current_stream(s.device).wait_stream(s)
+
+
+def compute_stream_of_backward(device) -> Optional[torch.cuda.Stream]:
+    """The stream the current backward pass runs its main chain on (recorded at the first side-
+    stream launch; None when no side-stream work is pending)."""
+    return _side_pending.get("main") if _side_pending["active"] else None
+
+
+def _enter_side(device) -> Optional[torch.cuda.Stream]:
+    ss = wgrad_side_stream(device)
+    if ss is None:
+        return None
+    cur = torch.cuda.current_stream(device)
+    ss.wait_stream(cur)
+    _side_pending["main"] = cur
+    if not _side_pending["active"]:
+        _side_pending["active"] = True
+        torch.autograd.Variable._execution_engine.queue_callback(_join_side_streams)
+    return ss
+
+
 def _grad_ready(*vs: Optional[Variable]) -> None:
     for v in vs:
         if v is not None and v.store is not None and getattr(v.store, "grad_ready_hook", None) is not None:
@@ -144,8 +194,17 @@ class _Conv2d(torch.autograd.Function):
                         sink.put(dx)
                         dx = None
             if w.trainable:
-                torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
-                _grad_ready(w)
+                ss = _enter_side(gy.device)
+                if ss is not None:
+                    with torch.cuda.stream(ss):
+                        torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
+                        # the bucket hook (DP) runs with the side stream current: see allreduce.py
+                        _grad_ready(w)
+                    gy.record_stream(ss)
+                    x.record_stream(ss)
+                else:
+                    torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
+                    _grad_ready(w)
             return dx, None, None, None, None, None, None, None, None
         dx = _ref_param_grads(lambda xx, ww: _conv_ref(xx, ww, stride, pad, dil), x, [w], gy, need_dx)
         return dx, None, None, None, None, None, None, None, None
