@@ -124,6 +124,10 @@ void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
               uint16_t* y, uint8_t* mask, hipStream_t s);
 // residual + ReLU: pass the forward's mask (vector path) or res (generic path) for the ReLU mask
+bool bn_backward_apply_sec_ok(int C);
+void bn_backward_apply_sec(const uint16_t* g, const uint16_t* x, const uint8_t* mask, const float* save,
+                           const float* red, int64_t M, int C, bool relu, uint16_t* dx, uint16_t* dres,
+                           const uint16_t* x2, const float* save2, float* slots2, hipStream_t s);
 void bn_backward_apply(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask,
                        const float* save, const float* red, int64_t M, int C, bool relu, uint16_t* dx,
                        uint16_t* dres, hipStream_t s);

@@ -381,19 +381,27 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_gen_kernel(const uint16_t* 
 
 // ------------------------------------------------------------------ backward apply (fixed channel)
 // dx = scale*(g' - sum_g/M - (x-mu)*is*sum_gx/M) = A*g' + B*x + D
-template <bool RES, bool RELU>
+// SEC (RES only): the residual input is itself a BN output used nowhere else (the projection
+// shortcut's BN of a ResNet block), so its incoming gradient is exactly dres = g'.  While g' is in
+// registers, also accumulate that BN's backward partials [sum g' | sum g' xhat2] (xhat2 from its
+// input x2 and save2) into its slots2: its separate reduce pass (re-reading dres and x2) goes away.
+template <bool RES, bool RELU, bool SEC = false>
 __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* __restrict__ g,
                                                                const uint16_t* __restrict__ x,
                                                                const uint8_t* __restrict__ mask,
                                                                const float* __restrict__ save,
                                                                const float* __restrict__ red, int64_t nvec, int64_t M,
                                                                int C, uint16_t* __restrict__ dx,
-                                                               uint16_t* __restrict__ dres) {
+                                                               uint16_t* __restrict__ dres,
+                                                               const uint16_t* __restrict__ x2 = nullptr,
+                                                               const float* __restrict__ save2 = nullptr,
+                                                               float* __restrict__ slots2 = nullptr) {
   const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int c0 = (int)(i0 % (C >> 3)) * 8;
   const float inv_m = 1.f / (float)M;
   float A[8], B[8], D[8], sc[8], sh[8];
+  float mu2[8], is2[8], s2[8], q2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int c = c0 + k;
@@ -404,11 +412,18 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* _
     A[k] = sc[k];
     B[k] = -sc[k] * kx;
     D[k] = sc[k] * (kx * mu - kg);
+    if (SEC) {
+      mu2[k] = save2[c];
+      is2[k] = save2[C + c];
+      s2[k] = 0.f;
+      q2[k] = 0.f;
+    }
   }
   for (int64_t i = i0; i < nvec; i += stride) {
-    float gf[8], xf[8], o[8];
+    float gf[8], xf[8], o[8], x2f[8];
     unpack8(reinterpret_cast<const U4*>(g)[i], gf);
     unpack8(reinterpret_cast<const U4*>(x)[i], xf);
+    if (SEC) unpack8(reinterpret_cast<const U4*>(x2)[i], x2f);
     const uint32_t mb = (RES && RELU) ? mask[i] : 0u;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -420,10 +435,35 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* _
       }
       gf[k] = gg;
       o[k] = fmaf(A[k], gg, fmaf(B[k], xf[k], D[k]));
+      if (SEC) {
+        s2[k] += gg;
+        q2[k] = fmaf(gg, (x2f[k] - mu2[k]) * is2[k], q2[k]);
+      }
     }
     reinterpret_cast<U4*>(dx)[i] = pack8(o);
     // dres == nullptr: the consumer reads g and the mask bits itself (masked conv addend)
     if (RES && dres) reinterpret_cast<U4*>(dres)[i] = pack8(gf);
+  }
+  if constexpr (SEC) {
+    // threads t and t + k*tpr share channel vector t % tpr (256 % tpr == 0, vec_ok): tree over rows
+    const int t = threadIdx.x, tpr = C >> 3, rpb = 256 / tpr, r0 = t / tpr;
+    __shared__ float lds[256 * 8];
+    for (int pass = 0; pass < 2; ++pass) {
+      const float* v = pass ? q2 : s2;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) lds[k * 256 + t] = v[k];
+      __syncthreads();
+      for (int h = rpb >> 1; h > 0; h >>= 1) {
+        if (r0 < h) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) lds[k * 256 + t] += lds[k * 256 + t + h * tpr];
+        }
+        __syncthreads();
+      }
+      float* slot = slots2 + (size_t)(blockIdx.x % NSLOT) * 2 * C + pass * C;
+      for (int c = t; c < C; c += 256) atomicAdd(slot + c, lds[(c & 7) * 256 + (c >> 3)]);
+      __syncthreads();
+    }
   }
 }
 
@@ -848,6 +888,27 @@ void bn_bwd_reduce(const uint16_t* g, const uint16_t* x, const uint8_t* mask, bo
   const int gr = grid_for(M, rpb * 8);
   TFX_DISPATCH_RR(has_res, relu,
                   (bn_bwd_reduce_vec_kernel<R_, L_, 1><<<gr, 256, 0, s>>>(g, x, mask, save, M, C, slots)));
+}
+
+// bn_backward_apply (vector path, residual input, dres written) that also reduces the residual's
+// own BN backward into slots2 (bn_bwd_apply_vec_kernel SEC); the caller finishes it with
+// bn_slot_reduce(slots2, ...).  Fewer, fatter blocks than the plain apply: each ends in 2C atomics.
+bool bn_backward_apply_sec_ok(int C) { return vec_ok(C); }
+
+void bn_backward_apply_sec(const uint16_t* g, const uint16_t* x, const uint8_t* mask, const float* save,
+                           const float* red, int64_t M, int C, bool relu, uint16_t* dx, uint16_t* dres,
+                           const uint16_t* x2, const float* save2, float* slots2, hipStream_t s) {
+  const int64_t nvec = M * C / 8;
+  const int cv = C / 8;
+  const int mult = cv / gcd(cv, 256);
+  int ga = grid_for(nvec, 256 * 4, 1024);
+  ga = (ga + mult - 1) / mult * mult;
+  if (relu)
+    bn_bwd_apply_vec_kernel<true, true, true><<<ga, 256, 0, s>>>(g, x, mask, save, red, nvec, M, C, dx, dres, x2,
+                                                                 save2, slots2);
+  else
+    bn_bwd_apply_vec_kernel<true, false, true><<<ga, 256, 0, s>>>(g, x, mask, save, red, nvec, M, C, dx, dres,
+                                                                  x2, save2, slots2);
 }
 
 // the apply half of bn_backward, for a red[] produced elsewhere (a conv dgrad epilogue)

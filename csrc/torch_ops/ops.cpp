@@ -509,6 +509,37 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
   return {dx, dres, red};
 }
 
+// bn_bwd_apply for a residual layer whose residual is another BN's output used only here (ResNet
+// projection shortcut): dres is written as usual AND that BN's backward is reduced in the same pass
+// (x2 = its input, save2 = its [mean|invstd|scale|shift], slots2 = its zeroed slot workspace).
+// Returns (dx, dres, red2); dgamma2 / dbeta2 (optional) accumulate its parameter gradients.
+std::tuple<Tensor, Tensor, Tensor> bn_bwd_apply_sec(Tensor g, Tensor x, Tensor save, Tensor red, bool relu,
+                                                    optional<Tensor> mask, Tensor x2, Tensor save2, Tensor slots2,
+                                                    optional<Tensor> dgamma2, optional<Tensor> dbeta2) {
+  CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(red);
+  CHECK_BF16(x2); CHECK_CONTIG(x2); CHECK_F32(save2); CHECK_F32(slots2);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(g.sizes() == x.sizes() && x2.sizes() == x.sizes(), "bn_bwd_apply_sec shapes");
+  TORCH_CHECK(tfx::bn_backward_apply_sec_ok((int)C), "bn_bwd_apply_sec: channel count needs the vector path");
+  TORCH_CHECK(red.numel() == 2 * C && save.numel() == 4 * C && save2.numel() == 4 * C, "red / save size");
+  TORCH_CHECK(slots2.numel() >= tfx::NSLOT * 2 * C, "stat slots");
+  const uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() * 8 == x.numel(), "relu mask size");
+    mk = mask->data_ptr<uint8_t>();
+  }
+  TORCH_CHECK(!relu || mk, "bn_bwd_apply_sec: a residual ReLU needs the forward mask bits");
+  auto dx = at::empty_like(x);
+  auto dres = at::empty_like(x);
+  auto red2 = at::empty({2 * C}, x.options().dtype(at::kFloat));
+  tfx::bn_backward_apply_sec(bf(g), bf(x), mk, save.data_ptr<float>(), red.data_ptr<float>(), M, (int)C, relu,
+                             bfm(dx), bfm(dres), bf(x2), save2.data_ptr<float>(), slots2.data_ptr<float>(),
+                             cur_stream());
+  tfx::bn_slot_reduce(slots2.data_ptr<float>(), (int)C, red2.data_ptr<float>(), fpm(dgamma2), fpm(dbeta2),
+                      cur_stream());
+  return {dx, dres, red2};
+}
+
 // backward apply only, with red from conv_dgrad_bn: returns (dx, dres)
 std::tuple<Tensor, Tensor> bn_bwd_apply(Tensor g, Tensor x, optional<Tensor> res, Tensor save, Tensor red,
                                         bool relu, optional<Tensor> mask, bool want_dres) {
@@ -1164,6 +1195,9 @@ TORCH_LIBRARY(tfx, m) {
         &sgemm_into);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply_train", &bn_apply_train);
+  m.def("bn_bwd_apply_sec(Tensor g, Tensor x, Tensor save, Tensor red, bool relu, Tensor? mask, Tensor x2, "
+        "Tensor save2, Tensor slots2, Tensor? dgamma2=None, Tensor? dbeta2=None) -> (Tensor, Tensor, Tensor)",
+        &bn_bwd_apply_sec);
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);

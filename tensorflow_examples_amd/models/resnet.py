@@ -53,14 +53,15 @@ class _BN:
             self.var = store.add_state("moving_variance", torch.ones(c))
         self.ws = BNWorkspace(c)
 
-    def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None, ws_obj=False):
+    def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None, ws_obj=False,
+                 residual_is_bn=False):
         ws = (self.ws if ws_obj else self.ws.get(x.device)) if x.device.type == "cuda" else None
         return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
                               eps=1e-5, residual=residual, relu=relu, workspace=ws, stats_ready=stats_ready,
-                              residual_grad_sink=residual_sink)
+                              residual_grad_sink=residual_sink, fuse_residual_bn_backward=residual_is_bn)
 
     def after_conv(self, conv, x, training, relu=False, residual=None, sink=None, residual_sink=None,
-                   fuse_input_bn_backward=False):
+                   fuse_input_bn_backward=False, residual_is_bn=False):
         """conv -> BN with the BN statistics produced (and, with _FUSE_BN, finalized) by the conv's
         epilogue (GPU, training).  ``fuse_input_bn_backward``: the conv's data gradient is the
         complete gradient of ``x`` -- reduce x's producing BN's backward in its epilogue."""
@@ -69,9 +70,10 @@ class _BN:
             self.ws.finalize_args = (self.gamma.master, self.beta.master, self.mean, self.var, 0.1, 1e-5)
             y = conv(x, self.ws, sink, fuse_input_bn_backward and _FUSE_BN)
             return self(y, training, relu=relu, residual=residual, stats_ready=True, residual_sink=residual_sink,
-                        ws_obj=True)
+                        ws_obj=True, residual_is_bn=residual_is_bn)
         y = conv(x, self.ws.get(x.device) if fused else None, sink)
-        return self(y, training, relu=relu, residual=residual, stats_ready=fused, residual_sink=residual_sink)
+        return self(y, training, relu=relu, residual=residual, stats_ready=fused, residual_sink=residual_sink,
+                    residual_is_bn=residual_is_bn)
 
 
 class _Conv:
@@ -117,7 +119,9 @@ class Bottleneck:
             return self.b3.after_conv(self.c3, o, training, relu=True, residual=x, residual_sink=prod,
                                       fuse_input_bn_backward=o3_fuse)
         sc = self.bp.after_conv(self.proj, x, training, sink=prod)
-        return self.b3.after_conv(self.c3, o, training, relu=True, residual=sc, fuse_input_bn_backward=o3_fuse)
+        # sc (the shortcut BN's output) is used only as this residual: its BN backward rides along
+        return self.b3.after_conv(self.c3, o, training, relu=True, residual=sc, fuse_input_bn_backward=o3_fuse,
+                                  residual_is_bn=True)
 
 
 class Basic:
@@ -142,7 +146,7 @@ class Basic:
         if self.proj is None:
             return self.b2.after_conv(self.c2, o, training, relu=True, residual=x, residual_sink=prod)
         sc = self.bp.after_conv(self.proj, x, training, sink=prod)
-        return self.b2.after_conv(self.c2, o, training, relu=True, residual=sc)
+        return self.b2.after_conv(self.c2, o, training, relu=True, residual=sc, residual_is_bn=True)
 
 
 class ResNetCifar:

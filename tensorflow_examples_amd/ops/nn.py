@@ -378,12 +378,30 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
     return y.to(x.dtype)
 
 
+# A/B switch for batch_norm(fuse_residual_bn_backward=True)
+_FUSE_RES_BN = os.environ.get("TFX_FUSE_RES_BN", "1") != "0"
+
+
+def _res_bn_sec_ok(ctx, gy, mask, relu, masked):
+    """Can this residual BN's backward apply also reduce its residual's BN (bn_bwd_apply_sec)?"""
+    rb = ctx.res_bnb
+    if rb is None or not ctx.has_res or masked or ctx.res_sink is not None or rb.red is not None:
+        return False
+    if rb.relu or rb.mask is not None or rb.ws is None or rb.wsobj is not None:
+        return False
+    if relu and mask is None:
+        return False
+    C = gy.shape[-1]
+    return rb.x.shape == gy.shape and rb.x.is_contiguous() and C % 8 == 0 and C // 8 <= 256 and 256 % (C // 8) == 0
+
+
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
-                training, ws, stats_ready, res_sink, wsobj, bnb_out):
+                training, ws, stats_ready, res_sink, wsobj, bnb_out, res_bnb):
         ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
         ctx.res_sink = res_sink
+        ctx.res_bnb = res_bnb
         ctx.native = _native.use_native(x)
         ctx.has_res = res is not None
         ctx.bnb = None
@@ -461,6 +479,14 @@ class _BatchNorm(torch.autograd.Function):
                                                       beta.grad if train_p else None, have, not masked)
                 # S_b consumed (zeroed by the next forward); S_f zeroed by this pass
                 wsobj.fwd_dirty, wsobj.bwd_dirty = False, True
+            elif ctx.bnb is not None and ctx.bnb.red is not None and _res_bn_sec_ok(ctx, gy, mask, relu, masked):
+                # ... and the residual's own BN backward is reduced in the same pass
+                rb = ctx.res_bnb
+                p_t = rb.dgamma is not None
+                dx, dres, rb.red = torch.ops.tfx.bn_bwd_apply_sec(gy, x, save, ctx.bnb.red, relu, mask, rb.x, rb.save,
+                                                                   rb.ws, rb.dgamma if p_t else None,
+                                                                   rb.dbeta if p_t else None)
+                ctx.bnb.red = None
             elif ctx.bnb is not None and ctx.bnb.red is not None:
                 # the consumer conv's dgrad epilogue reduced this backward (and dgamma / dbeta)
                 dx, dres = torch.ops.tfx.bn_bwd_apply(gy, x, res, save, ctx.bnb.red, relu, mask, not masked)
@@ -475,7 +501,7 @@ class _BatchNorm(torch.autograd.Function):
                 ctx.res_sink.put((gy, mask) if masked else dres)
                 dres = None
             return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None, \
-                None, None, None
+                None, None, None, None
         x, res = ctx.saved_tensors
         with torch.enable_grad():
             xs = x.detach().requires_grad_(True)
@@ -490,20 +516,24 @@ class _BatchNorm(torch.autograd.Function):
             gamma.grad.add_(grads[0])
             beta.grad.add_(grads[1])
             _grad_ready(gamma, beta)
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
                momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False,
                workspace=None, stats_ready: bool = False,
-               residual_grad_sink: Optional[GradSink] = None):
+               residual_grad_sink: Optional[GradSink] = None, fuse_residual_bn_backward: bool = False):
     """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
     ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass).
 
     ``workspace``: the layer's slot tensor or :class:`BNWorkspace` (then a statistics finalize
     done by the producing conv is picked up).  On the GPU in training mode the output carries a
     :class:`BNBackwardFusion` (``_tfx_bnb``) for a consumer conv that opts into reducing this
-    BN's backward in its data-gradient epilogue."""
+    BN's backward in its data-gradient epilogue.
+
+    ``fuse_residual_bn_backward``: ``residual`` is another BN's output used ONLY here (a ResNet
+    projection shortcut), so its gradient is exactly this layer's residual gradient -- reduce that
+    BN's backward inside this layer's backward apply (one full pass over two tensors less)."""
     anchor = gamma.store.anchor if gamma is not None else None
     wsobj = workspace if isinstance(workspace, BNWorkspace) else None
     if wsobj is not None:
@@ -512,8 +542,9 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
         workspace = None
     sink = residual_grad_sink if (x.device.type == "cuda" and residual is not None) else None
     bnb_out = [] if (x.device.type == "cuda" and training) else None
+    res_bnb = getattr(residual, "_tfx_bnb", None) if (fuse_residual_bn_backward and _FUSE_RES_BN) else None
     y = _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
-                         workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out)
+                         workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out, res_bnb)
     if bnb_out:
         y._tfx_bnb = bnb_out[0]
     return y
