@@ -513,9 +513,12 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
 // projection shortcut): dres is written as usual AND that BN's backward is reduced in the same pass
 // (x2 = its input, save2 = its [mean|invstd|scale|shift], slots2 = its zeroed slot workspace).
 // Returns (dx, dres, red2); dgamma2 / dbeta2 (optional) accumulate its parameter gradients.
+// want_dres = false: dres is not written -- that BN's apply then reads g and the mask bits itself
+// (bn_bwd_apply(g, x2, None, save2, red2, relu=True, mask): g' = g * mask is exactly its gradient).
 std::tuple<Tensor, Tensor, Tensor> bn_bwd_apply_sec(Tensor g, Tensor x, Tensor save, Tensor red, bool relu,
                                                     optional<Tensor> mask, Tensor x2, Tensor save2, Tensor slots2,
-                                                    optional<Tensor> dgamma2, optional<Tensor> dbeta2) {
+                                                    optional<Tensor> dgamma2, optional<Tensor> dbeta2,
+                                                    bool want_dres) {
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(red);
   CHECK_BF16(x2); CHECK_CONTIG(x2); CHECK_F32(save2); CHECK_F32(slots2);
   const int64_t C = x.size(-1), M = x.numel() / C;
@@ -530,10 +533,11 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd_apply_sec(Tensor g, Tensor x, Tensor s
   }
   TORCH_CHECK(!relu || mk, "bn_bwd_apply_sec: a residual ReLU needs the forward mask bits");
   auto dx = at::empty_like(x);
-  auto dres = at::empty_like(x);
+  Tensor dres;
+  if (want_dres) dres = at::empty_like(x);
   auto red2 = at::empty({2 * C}, x.options().dtype(at::kFloat));
   tfx::bn_backward_apply_sec(bf(g), bf(x), mk, save.data_ptr<float>(), red.data_ptr<float>(), M, (int)C, relu,
-                             bfm(dx), bfm(dres), bf(x2), save2.data_ptr<float>(), slots2.data_ptr<float>(),
+                             bfm(dx), want_dres ? bfm(dres) : nullptr, bf(x2), save2.data_ptr<float>(), slots2.data_ptr<float>(),
                              cur_stream());
   tfx::bn_slot_reduce(slots2.data_ptr<float>(), (int)C, red2.data_ptr<float>(), fpm(dgamma2), fpm(dbeta2),
                       cur_stream());
@@ -1196,7 +1200,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply_train", &bn_apply_train);
   m.def("bn_bwd_apply_sec(Tensor g, Tensor x, Tensor save, Tensor red, bool relu, Tensor? mask, Tensor x2, "
-        "Tensor save2, Tensor slots2, Tensor? dgamma2=None, Tensor? dbeta2=None) -> (Tensor, Tensor, Tensor)",
+        "Tensor save2, Tensor slots2, Tensor? dgamma2=None, Tensor? dbeta2=None, bool want_dres=True) -> "
+        "(Tensor, Tensor, Tensor)",
         &bn_bwd_apply_sec);
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);

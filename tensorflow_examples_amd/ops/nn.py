@@ -346,12 +346,15 @@ class BNBackwardFusion:
     ``red`` ([sum g' | sum g' xhat]), or -- two-slot-set workspaces (``wsobj``) -- leaves the
     partials in the layer's backward slots and sets ``red = IN_SLOTS``; the BN backward then runs
     only its apply pass."""
-    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "wsobj")
+    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "wsobj", "in_mask")
     IN_SLOTS = "slots"
 
     def __init__(self, x, save, mask, relu, ws, dgamma, dbeta, wsobj=None):
         self.x, self.save, self.mask, self.relu, self.ws = x, save, mask, relu, ws
         self.dgamma, self.dbeta, self.red, self.wsobj = dgamma, dbeta, None, wsobj
+        # set by a residual consumer (bn_bwd_apply_sec): the incoming gradient arrives unmasked,
+        # the true gradient is g * in_mask (the consumer's ReLU mask bits)
+        self.in_mask = None
 
 
 # ====================================================================== batch norm (+res, +relu)
@@ -380,6 +383,8 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
 
 # A/B switch for batch_norm(fuse_residual_bn_backward=True)
 _FUSE_RES_BN = os.environ.get("TFX_FUSE_RES_BN", "1") != "0"
+# ... and with the tail's ReLU, pass gy + mask bits instead of writing gy * mask
+_FUSE_RES_BN_MASK = os.environ.get("TFX_FUSE_RES_BN_MASK", "1") != "0"
 
 
 def _res_bn_sec_ok(ctx, gy, mask, relu, masked):
@@ -483,10 +488,20 @@ class _BatchNorm(torch.autograd.Function):
                 # ... and the residual's own BN backward is reduced in the same pass
                 rb = ctx.res_bnb
                 p_t = rb.dgamma is not None
+                # with a ReLU the residual gradient is gy * mask: hand the residual BN gy itself and
+                # the mask bits instead of writing the masked copy
+                pass_mask = relu and _FUSE_RES_BN_MASK
                 dx, dres, rb.red = torch.ops.tfx.bn_bwd_apply_sec(gy, x, save, ctx.bnb.red, relu, mask, rb.x, rb.save,
                                                                    rb.ws, rb.dgamma if p_t else None,
-                                                                   rb.dbeta if p_t else None)
+                                                                   rb.dbeta if p_t else None, not pass_mask)
+                if pass_mask:
+                    rb.in_mask, dres = mask, gy
                 ctx.bnb.red = None
+            elif ctx.bnb is not None and ctx.bnb.red is not None and ctx.bnb.in_mask is not None:
+                # gy arrived unmasked from a residual consumer: the apply's ReLU-mask path is g * mask
+                assert not relu and not ctx.has_res
+                dx, dres = torch.ops.tfx.bn_bwd_apply(gy, x, None, save, ctx.bnb.red, True, ctx.bnb.in_mask, False)
+                ctx.bnb.red = ctx.bnb.in_mask = None
             elif ctx.bnb is not None and ctx.bnb.red is not None:
                 # the consumer conv's dgrad epilogue reduced this backward (and dgamma / dbeta)
                 dx, dres = torch.ops.tfx.bn_bwd_apply(gy, x, res, save, ctx.bnb.red, relu, mask, not masked)

@@ -54,4 +54,14 @@ def test_bn_bwd_apply_sec_matches_separate_passes(gpu, shape, relu):
     assert _rel(dg1, dg0) < 1e-4 and _rel(db1, db0) < 1e-4
     assert _rel(dx21, dx20) < 1e-2
     assert ws1.abs().max().item() == 0  # slots handed back zeroed
+    if relu:
+        # no dres written: the residual BN's apply reads gy and the mask bits (g' = gy * mask)
+        ws2 = torch.zeros_like(ws0)
+        dx2, dres2, red22 = torch.ops.tfx.bn_bwd_apply_sec(gy, x, save, red, True, mask, x2, save2, ws2, None, None,
+                                                           False)
+        dx22, none = torch.ops.tfx.bn_bwd_apply(gy, x2, None, save2, red22, True, mask, False)
+        torch.cuda.synchronize()
+        assert dres2 is None and none is None
+        assert torch.equal(dx2, dx0) and _rel(red22, red20) < 1e-4
+        assert _rel(dx22, dx20) < 1e-2
 
