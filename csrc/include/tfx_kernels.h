@@ -124,6 +124,9 @@ void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
               uint16_t* y, uint8_t* mask, hipStream_t s);
 // residual + ReLU: pass the forward's mask (vector path) or res (generic path) for the ReLU mask
+// y = act(bn(x) + bn'(res_x)): the residual BN (res_save) applied on the fly (vector path, vec_ok(C))
+void bn_apply_res_bn(const uint16_t* x, const uint16_t* res_x, const float* save, const float* res_save, int64_t M,
+                     int C, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s);
 bool bn_backward_apply_sec_ok(int C);
 void bn_backward_apply_sec(const uint16_t* g, const uint16_t* x, const uint8_t* mask, const float* save,
                            const float* red, int64_t M, int C, bool relu, uint16_t* dx, uint16_t* dres,

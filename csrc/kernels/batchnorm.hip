@@ -213,19 +213,26 @@ __global__ void bn_eval_prep_kernel(int C, const float* __restrict__ gamma, cons
 // With RES && RELU the ReLU mask of the output is also stored, one bit per element (one byte per
 // 8-channel vector): the backward then reads 1/16 of the residual tensor's bytes instead of the
 // residual itself (twice: reduce and apply).
-template <bool RES, bool RELU>
+// RBN: the residual is another BN's INPUT, normalized here on the fly with its rsave -- that BN
+// (a ResNet projection shortcut's, used only as this residual) never writes its output.
+template <bool RES, bool RELU, bool RBN = false>
 __global__ void __launch_bounds__(256) bn_apply_vec_kernel(const uint16_t* __restrict__ x,
                                                            const uint16_t* __restrict__ res,
                                                            const float* __restrict__ save, int64_t nvec, int C,
-                                                           uint16_t* __restrict__ y, uint8_t* __restrict__ mask) {
+                                                           uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                                                           const float* __restrict__ rsave = nullptr) {
   const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int c0 = (int)(i0 % (C >> 3)) * 8;
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     sc[k] = save[2 * C + c0 + k];
     sh[k] = save[3 * C + c0 + k];
+    if (RBN) {
+      rsc[k] = rsave[2 * C + c0 + k];
+      rsh[k] = rsave[3 * C + c0 + k];
+    }
   }
   auto one = [&](int64_t i) {
     float f[8], r[8];
@@ -235,7 +242,8 @@ __global__ void __launch_bounds__(256) bn_apply_vec_kernel(const uint16_t* __res
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float z = fmaf(f[k], sc[k], sh[k]);
-      if (RES) z += r[k];
+      if (RBN) z += fmaf(r[k], rsc[k], rsh[k]);
+      else if (RES) z += r[k];
       bits |= (z > 0.f ? 1u : 0u) << k;
       f[k] = RELU ? fmaxf(z, 0.f) : z;
     }
@@ -825,6 +833,16 @@ void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t
     const int g = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_apply_gen_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, n, C, y)));
   }
+}
+
+void bn_apply_res_bn(const uint16_t* x, const uint16_t* res_x, const float* save, const float* res_save, int64_t M,
+                     int C, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s) {
+  const int64_t nvec = M * C / 8;
+  const int g = fixed_channel_grid(nvec, C);
+  if (relu)
+    bn_apply_vec_kernel<true, true, true><<<g, 256, 0, s>>>(x, res_x, save, nvec, C, y, mask, res_save);
+  else
+    bn_apply_vec_kernel<true, false, true><<<g, 256, 0, s>>>(x, res_x, save, nvec, C, y, mask, res_save);
 }
 
 void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask, const float* save,

@@ -463,6 +463,23 @@ std::tuple<Tensor, Tensor> bn_apply_train(Tensor x, optional<Tensor> res, Tensor
   return {y, mask};
 }
 
+// bn_apply_train whose residual is a BN that was never applied: y = act(bn(x) + bn'(res_x)), with
+// res_save = that BN's [mean|invstd|scale|shift] (ResNet projection shortcut, ops/nn.py defer).
+std::tuple<Tensor, Tensor> bn_apply_res_bn(Tensor x, Tensor res_x, Tensor save, Tensor res_save, bool relu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(save); CHECK_BF16(res_x); CHECK_CONTIG(res_x);
+  CHECK_F32(res_save);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(save.numel() == 4 * C && res_save.numel() == 4 * C, "save size");
+  TORCH_CHECK(res_x.sizes() == x.sizes(), "residual shape");
+  TORCH_CHECK(tfx::bn_backward_apply_sec_ok((int)C), "bn_apply_res_bn: channel count needs the vector path");
+  auto y = at::empty_like(x);
+  Tensor mask;
+  if (relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  tfx::bn_apply_res_bn(bf(x), bf(res_x), save.data_ptr<float>(), res_save.data_ptr<float>(), M, (int)C, relu,
+                       bfm(y), relu ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return {y, mask};
+}
+
 std::tuple<Tensor, Tensor> bn_fwd_eval(Tensor x, optional<Tensor> gamma, optional<Tensor> beta, Tensor run_mean,
                                        Tensor run_var, double eps, optional<Tensor> res, bool relu) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x);
@@ -1199,6 +1216,8 @@ TORCH_LIBRARY(tfx, m) {
         &sgemm_into);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply_train", &bn_apply_train);
+  m.def("bn_apply_res_bn(Tensor x, Tensor res_x, Tensor save, Tensor res_save, bool relu) -> (Tensor, Tensor)",
+        &bn_apply_res_bn);
   m.def("bn_bwd_apply_sec(Tensor g, Tensor x, Tensor save, Tensor red, bool relu, Tensor? mask, Tensor x2, "
         "Tensor save2, Tensor slots2, Tensor? dgamma2=None, Tensor? dbeta2=None, bool want_dres=True) -> "
         "(Tensor, Tensor, Tensor)",

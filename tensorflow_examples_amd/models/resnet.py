@@ -54,14 +54,15 @@ class _BN:
         self.ws = BNWorkspace(c)
 
     def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None, ws_obj=False,
-                 residual_is_bn=False):
+                 residual_is_bn=False, defer_output=False):
         ws = (self.ws if ws_obj else self.ws.get(x.device)) if x.device.type == "cuda" else None
         return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
                               eps=1e-5, residual=residual, relu=relu, workspace=ws, stats_ready=stats_ready,
-                              residual_grad_sink=residual_sink, fuse_residual_bn_backward=residual_is_bn)
+                              residual_grad_sink=residual_sink, fuse_residual_bn_backward=residual_is_bn,
+                              defer_output=defer_output)
 
     def after_conv(self, conv, x, training, relu=False, residual=None, sink=None, residual_sink=None,
-                   fuse_input_bn_backward=False, residual_is_bn=False):
+                   fuse_input_bn_backward=False, residual_is_bn=False, defer_output=False):
         """conv -> BN with the BN statistics produced (and, with _FUSE_BN, finalized) by the conv's
         epilogue (GPU, training).  ``fuse_input_bn_backward``: the conv's data gradient is the
         complete gradient of ``x`` -- reduce x's producing BN's backward in its epilogue."""
@@ -70,7 +71,7 @@ class _BN:
             self.ws.finalize_args = (self.gamma.master, self.beta.master, self.mean, self.var, 0.1, 1e-5)
             y = conv(x, self.ws, sink, fuse_input_bn_backward and _FUSE_BN)
             return self(y, training, relu=relu, residual=residual, stats_ready=True, residual_sink=residual_sink,
-                        ws_obj=True, residual_is_bn=residual_is_bn)
+                        ws_obj=True, residual_is_bn=residual_is_bn, defer_output=defer_output)
         y = conv(x, self.ws.get(x.device) if fused else None, sink)
         return self(y, training, relu=relu, residual=residual, stats_ready=fused, residual_sink=residual_sink,
                     residual_is_bn=residual_is_bn)
@@ -118,8 +119,9 @@ class Bottleneck:
         if self.proj is None:
             return self.b3.after_conv(self.c3, o, training, relu=True, residual=x, residual_sink=prod,
                                       fuse_input_bn_backward=o3_fuse)
-        sc = self.bp.after_conv(self.proj, x, training, sink=prod)
-        # sc (the shortcut BN's output) is used only as this residual: its BN backward rides along
+        # sc (the shortcut BN's output) is used only as the tail's residual: never written (the tail
+        # normalizes the shortcut conv's output on the fly), and its BN backward rides along
+        sc = self.bp.after_conv(self.proj, x, training, sink=prod, defer_output=True)
         return self.b3.after_conv(self.c3, o, training, relu=True, residual=sc, fuse_input_bn_backward=o3_fuse,
                                   residual_is_bn=True)
 
@@ -145,7 +147,7 @@ class Basic:
         o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons)
         if self.proj is None:
             return self.b2.after_conv(self.c2, o, training, relu=True, residual=x, residual_sink=prod)
-        sc = self.bp.after_conv(self.proj, x, training, sink=prod)
+        sc = self.bp.after_conv(self.proj, x, training, sink=prod, defer_output=True)
         return self.b2.after_conv(self.c2, o, training, relu=True, residual=sc, residual_is_bn=True)
 
 

@@ -346,7 +346,7 @@ class BNBackwardFusion:
     ``red`` ([sum g' | sum g' xhat]), or -- two-slot-set workspaces (``wsobj``) -- leaves the
     partials in the layer's backward slots and sets ``red = IN_SLOTS``; the BN backward then runs
     only its apply pass."""
-    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "wsobj", "in_mask")
+    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "wsobj", "in_mask", "deferred")
     IN_SLOTS = "slots"
 
     def __init__(self, x, save, mask, relu, ws, dgamma, dbeta, wsobj=None):
@@ -355,6 +355,9 @@ class BNBackwardFusion:
         # set by a residual consumer (bn_bwd_apply_sec): the incoming gradient arrives unmasked,
         # the true gradient is g * in_mask (the consumer's ReLU mask bits)
         self.in_mask = None
+        # the BN's output was never written (batch_norm(defer_output=True)): its only consumer, a
+        # residual BN, normalizes ``x`` with ``save`` on the fly
+        self.deferred = False
 
 
 # ====================================================================== batch norm (+res, +relu)
@@ -383,8 +386,14 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
 
 # A/B switch for batch_norm(fuse_residual_bn_backward=True)
 _FUSE_RES_BN = os.environ.get("TFX_FUSE_RES_BN", "1") != "0"
+# ... and the shortcut BN's output is never written (the tail normalizes its input on the fly)
+_DEFER_RES_BN = os.environ.get("TFX_DEFER_RES_BN", "1") != "0"
 # ... and with the tail's ReLU, pass gy + mask bits instead of writing gy * mask
 _FUSE_RES_BN_MASK = os.environ.get("TFX_FUSE_RES_BN_MASK", "1") != "0"
+
+
+def _vec_ok(C):
+    return C % 8 == 0 and C // 8 <= 256 and 256 % (C // 8) == 0
 
 
 def _res_bn_sec_ok(ctx, gy, mask, relu, masked):
@@ -396,17 +405,17 @@ def _res_bn_sec_ok(ctx, gy, mask, relu, masked):
         return False
     if relu and mask is None:
         return False
-    C = gy.shape[-1]
-    return rb.x.shape == gy.shape and rb.x.is_contiguous() and C % 8 == 0 and C // 8 <= 256 and 256 % (C // 8) == 0
+    return rb.x.shape == gy.shape and rb.x.is_contiguous() and _vec_ok(gy.shape[-1])
 
 
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
-                training, ws, stats_ready, res_sink, wsobj, bnb_out, res_bnb):
+                training, ws, stats_ready, res_sink, wsobj, bnb_out, res_bnb, defer):
         ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
         ctx.res_sink = res_sink
-        ctx.res_bnb = res_bnb
+        res_bnb, res_sec = res_bnb if res_bnb is not None else (None, False)
+        ctx.res_bnb = res_bnb if res_sec else None
         ctx.native = _native.use_native(x)
         ctx.has_res = res is not None
         ctx.bnb = None
@@ -421,7 +430,17 @@ class _BatchNorm(torch.autograd.Function):
             ctx.ws = ws
             ctx.wsobj = None
             mask = None
-            if training and wsobj is not None and wsobj.two_phase(x.device):
+            two_phase = training and wsobj is not None and wsobj.two_phase(x.device)
+            pending = training and wsobj is not None and not two_phase and wsobj.pending_save is not None
+            # residual = a BN output that was never written: normalize its input on the fly here
+            # (bn_apply_res_bn), or materialize it for the other paths (autograd still routes its
+            # gradient to that BN: the lazy tensor stays this Function's input)
+            res_lazy = res is not None and res_bnb is not None and res_bnb.deferred
+            fuse_res = res_lazy and pending and relu
+            if res_lazy and not fuse_res:
+                res = torch.ops.tfx.bn_apply_train(res_bnb.x, None, res_bnb.save, False)[0]
+            defer_out = defer and pending and res is None and bnb_out is not None and _vec_ok(x.shape[-1])
+            if two_phase:
                 sf, sb = wsobj.fwd(x.device), wsobj.bwd(x.device)
                 have = bool(stats_ready) and wsobj.stats_ready
                 if not have and wsobj.fwd_dirty:
@@ -432,10 +451,15 @@ class _BatchNorm(torch.autograd.Function):
                 # S_f consumed (zeroed by this layer's backward apply); S_b zeroed by this pass
                 wsobj.fwd_dirty, wsobj.bwd_dirty = True, False
                 ctx.wsobj = wsobj
-            elif training and wsobj is not None and wsobj.pending_save is not None:
+            elif pending:
                 # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
                 save, wsobj.pending_save = wsobj.pending_save, None
-                y, mask = torch.ops.tfx.bn_apply_train(x, res, save, relu)
+                if fuse_res:
+                    y, mask = torch.ops.tfx.bn_apply_res_bn(x, res_bnb.x, save, res_bnb.save, relu)
+                elif defer_out:
+                    y = torch.zeros((), dtype=x.dtype, device=x.device).expand(x.shape)
+                else:
+                    y, mask = torch.ops.tfx.bn_apply_train(x, res, save, relu)
             elif training:
                 y, save, mask = torch.ops.tfx.bn_fwd_train(x, g_t, b_t, rm, rv, momentum, eps, res, relu, ws,
                                                            bool(stats_ready))
@@ -444,12 +468,14 @@ class _BatchNorm(torch.autograd.Function):
             if mask is not None and mask.numel() == 0:
                 mask = None
             # residual + ReLU: the backward needs only the 1-bit ReLU mask, not the residual tensor
+            assert not fuse_res or mask is not None
             ctx.save_for_backward(x, None if mask is not None else res, save, mask)
             if training and bnb_out is not None and (res is None or not relu or mask is not None) \
                     and x.shape[-1] % 8 == 0:
                 train_p = gamma is not None and gamma.trainable
                 ctx.bnb = BNBackwardFusion(x, save, mask, relu, ws, gamma.grad if train_p else None,
                                            beta.grad if train_p else None, ctx.wsobj)
+                ctx.bnb.deferred = defer_out
                 bnb_out.append(ctx.bnb)
             return y
         ctx.save_for_backward(x, res)
@@ -516,7 +542,7 @@ class _BatchNorm(torch.autograd.Function):
                 ctx.res_sink.put((gy, mask) if masked else dres)
                 dres = None
             return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None, \
-                None, None, None, None
+                None, None, None, None, None
         x, res = ctx.saved_tensors
         with torch.enable_grad():
             xs = x.detach().requires_grad_(True)
@@ -531,13 +557,14 @@ class _BatchNorm(torch.autograd.Function):
             gamma.grad.add_(grads[0])
             beta.grad.add_(grads[1])
             _grad_ready(gamma, beta)
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
                momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False,
                workspace=None, stats_ready: bool = False,
-               residual_grad_sink: Optional[GradSink] = None, fuse_residual_bn_backward: bool = False):
+               residual_grad_sink: Optional[GradSink] = None, fuse_residual_bn_backward: bool = False,
+               defer_output: bool = False):
     """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
     ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass).
 
@@ -548,7 +575,12 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
 
     ``fuse_residual_bn_backward``: ``residual`` is another BN's output used ONLY here (a ResNet
     projection shortcut), so its gradient is exactly this layer's residual gradient -- reduce that
-    BN's backward inside this layer's backward apply (one full pass over two tensors less)."""
+    BN's backward inside this layer's backward apply (one full pass over two tensors less).
+
+    ``defer_output``: the caller promises the output is used ONLY as the ``residual`` of one
+    later batch_norm (with ``fuse_residual_bn_backward``).  On the fused GPU path the output is then
+    never written (a zero-stride placeholder that keeps the autograd edge); the consumer
+    normalizes this BN's input on the fly."""
     anchor = gamma.store.anchor if gamma is not None else None
     wsobj = workspace if isinstance(workspace, BNWorkspace) else None
     if wsobj is not None:
@@ -557,9 +589,13 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
         workspace = None
     sink = residual_grad_sink if (x.device.type == "cuda" and residual is not None) else None
     bnb_out = [] if (x.device.type == "cuda" and training) else None
-    res_bnb = getattr(residual, "_tfx_bnb", None) if (fuse_residual_bn_backward and _FUSE_RES_BN) else None
+    rb = getattr(residual, "_tfx_bnb", None) if residual is not None else None
+    res_bnb = None
+    if rb is not None and (rb.deferred or fuse_residual_bn_backward):
+        res_bnb = (rb, bool(fuse_residual_bn_backward and _FUSE_RES_BN))
     y = _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
-                         workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out, res_bnb)
+                         workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out, res_bnb,
+                         bool(defer_output and _DEFER_RES_BN))
     if bnb_out:
         y._tfx_bnb = bnb_out[0]
     return y

@@ -65,3 +65,29 @@ def test_bn_bwd_apply_sec_matches_separate_passes(gpu, shape, relu):
         assert torch.equal(dx2, dx0) and _rel(red22, red20) < 1e-4
         assert _rel(dx22, dx20) < 1e-2
 
+
+
+@pytest.mark.parametrize("shape", [(256, 16, 16, 512), (5, 3, 7, 64)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_bn_apply_res_bn_matches_materialized_residual(gpu, shape, relu):
+    """Forward: the shortcut BN is never applied; the tail normalizes its input on the fly."""
+    torch.manual_seed(43)
+    C = shape[-1]
+    x = torch.randn(*shape, device=gpu).bfloat16()
+    rx = (torch.randn(*shape, device=gpu) * 2 - 0.3).bfloat16()
+    save, rsave = _save(C, gpu, 3), _save(C, gpu, 4)
+    y, mask = torch.ops.tfx.bn_apply_res_bn(x, rx, save, rsave, relu)
+    # fp32 reference of the same op
+    ref = x.float() * save[2 * C:3 * C] + save[3 * C:] + rx.float() * rsave[2 * C:3 * C] + rsave[3 * C:]
+    if relu:
+        ref = ref.clamp_min(0)
+    assert _rel(y, ref) < 1e-2
+    # against the two-pass path (the residual rounded to bf16 in between)
+    res = torch.ops.tfx.bn_apply_train(rx, None, rsave, False)[0]
+    y0, mask0 = torch.ops.tfx.bn_apply_train(x, res, save, relu)
+    torch.cuda.synchronize()
+    assert _rel(y, y0) < 1e-2
+    if relu:
+        assert (mask != mask0).float().mean().item() < 1e-2
+    else:
+        assert mask is None

@@ -34,7 +34,11 @@ def test_resnet_gpu_matches_cpu_reference_first_step(gpu, depth):
         loss = ops.softmax_cross_entropy(m(xin.to(dev).to(dt), training=True), lab.to(dev))
         loss.backward()
         st._loss = loss.item()
-    assert abs(sg._loss - sc._loss) < 0.02 * abs(sc._loss) + 0.02
+    # the bf16 forward itself drifts from fp32 block by block (ResNet-50 at init: ~0.3% after the
+    # stem, ~40% relative at the last block, scripts/diag_defer.py), so the loss bound is the same
+    # bf16 noise floor as the gradients: the CPU bf16 run's own distance from fp32
+    assert abs(sg._loss - sc._loss) < max(0.02 * abs(sc._loss) + 0.02, 2.0 * abs(sb._loss - sc._loss) + 0.02), \
+        (sg._loss, sc._loss, sb._loss)
     bad = []
     for v in sc.trainable():
         gc = v.grad
