@@ -36,7 +36,10 @@ struct FastDiv {
 };
 
 // ---------------------------------------------------------------- implicit GEMM
-enum { MODE_GEMM = 0, MODE_FWD = 1, MODE_DGRAD = 2, MODE_WGRAD = 3, MODE_WGRAD_T = 4, MODE_DGRAD_CLS = 5 };
+// MODE_DGRAD_FLIP: a 3x3 stride-1 data gradient posed as the forward conv of dY with the flipped,
+// transposed filter (args built as that forward: A = dY, B = Wf [C][3][3][Ko]; igemm_dgrad_flip.hip)
+enum { MODE_GEMM = 0, MODE_FWD = 1, MODE_DGRAD = 2, MODE_WGRAD = 3, MODE_WGRAD_T = 4, MODE_DGRAD_CLS = 5,
+       MODE_DGRAD_FLIP = 6 };
 enum { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ADD = 2, OUT_F32_ATOMIC = 3 };
 
 struct IgemmArgs {
@@ -127,6 +130,9 @@ void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t
 // y = act(bn(x) + bn'(res_x)): the residual BN (res_save) applied on the fly (vector path, vec_ok(C))
 void bn_apply_res_bn(const uint16_t* x, const uint16_t* res_x, const float* save, const float* res_save, int64_t M,
                      int C, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s);
+// every 3x3 filter W[Ko][3][3][C] of a flat bf16 buffer -> Wf[C][3][3][Ko] flipped (wflip.hip);
+// desc: nlayers x {src_off, dst_off, Ko, C, first_tile} int64 on the device, Ko % 64 == C % 64 == 0
+void wflip3x3(const uint16_t* src, uint16_t* dst, const int64_t* desc, int nlayers, int ntiles, hipStream_t s);
 bool bn_backward_apply_sec_ok(int C);
 void bn_backward_apply_sec(const uint16_t* g, const uint16_t* x, const uint8_t* mask, const float* save,
                            const float* red, int64_t M, int C, bool relu, uint16_t* dx, uint16_t* dres,

@@ -106,7 +106,8 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
   // fused-BN epilogues live in the bf16 16-byte-store path of the forward / data-gradient kernels
   if (a.stats || a.bnb_x) {
     if (!(a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0 &&
-          (mode == MODE_FWD || (a.bnb_x && mode == MODE_DGRAD)) && (a.stats == nullptr || a.bnb_x == nullptr))) {
+          (mode == MODE_FWD || (a.bnb_x && (mode == MODE_DGRAD || mode == MODE_DGRAD_FLIP))) &&
+          (a.stats == nullptr || a.bnb_x == nullptr))) {
       fprintf(stderr, "igemm_launch: unsupported fused-BN epilogue configuration\n");
       abort();
     }
@@ -150,6 +151,7 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
   switch (mode) {
     case MODE_FWD: igemm_fwd_im2col(a, s); break;
     case MODE_DGRAD: igemm_dgrad_general(a, s); break;
+    case MODE_DGRAD_FLIP: igemm_dgrad_flip(a, s); break;
     case MODE_DGRAD_CLS: igemm_dgrad_cls(a, s); break;
     case MODE_WGRAD: igemm_wgrad_x(a, s); break;
     case MODE_WGRAD_T: igemm_wgrad_t_x(a, s); break;

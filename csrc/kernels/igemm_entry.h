@@ -9,6 +9,7 @@ void igemm_fwd_pointwise(IgemmArgs& a, hipStream_t s);   // X[M][C] . W[Ko][C]^T
 void igemm_fwd_im2col(IgemmArgs& a, hipStream_t s);      // im2col(X) . W^T (+ fused BN stats)
 void igemm_dgrad_pointwise(IgemmArgs& a, hipStream_t s); // dY[M][Ko] . W[Ko][C] (+ fused BN backward)
 void igemm_dgrad_general(IgemmArgs& a, hipStream_t s);   // gathered dY . W (+ fused BN backward)
+void igemm_dgrad_flip(IgemmArgs& a, hipStream_t s);      // 3x3 s1: im2col(dY) . Wf^T (+ fused BN backward)
 void igemm_dgrad_cls_dense(IgemmArgs& a, hipStream_t s); // single-tap stride-2 parity class
 void igemm_dgrad_cls(IgemmArgs& a, hipStream_t s);       // stride-2 parity class, gathered
 void igemm_wgrad_dense(IgemmArgs& a, hipStream_t s);     // dY^T . X (1x1) -- f32 atomics, split-K
@@ -23,7 +24,7 @@ void igemm_gemm(IgemmArgs& a, hipStream_t s);            // plain GEMMs (FC laye
 // want = split-K block target.  0 / -1 = keep the heuristic's choice.
 enum {
   FAM_FWD_PW = 0, FAM_FWD_X, FAM_DGRAD_PW, FAM_DGRAD_X, FAM_DGRAD_CLS_DENSE, FAM_DGRAD_CLS, FAM_WGRAD_DENSE,
-  FAM_WGRAD_X, FAM_WGRAD_T_X, FAM_COUNT
+  FAM_WGRAD_X, FAM_WGRAD_T_X, FAM_DGRAD_FLIP, FAM_COUNT
 };
 struct TuneCfg {
   int tile = 0, ks = 0, gls = -1, want = 0;

@@ -128,8 +128,31 @@ void set_addend_s2(tfx::IgemmArgs& a, const Tensor& addend, int64_t N, int64_t H
   a.fd_s2HW = tfx::FastDiv((uint32_t)(H * W)); a.fd_s2W = tfx::FastDiv((uint32_t)W);
 }
 
+// Data-gradient GEMM setup.  With ``wflip`` (= W flipped and channel-transposed, [C][3][3][Ko]) a
+// 3x3 stride-1 pad-1 data gradient is posed as the forward conv of dY with it (MODE_DGRAD_FLIP:
+// K-major operands, igemm_dgrad_flip.hip); otherwise the gathered data-gradient GEMM (MODE_DGRAD).
+int dgrad_setup(tfx::IgemmArgs& a, const ConvGeom& g, const Tensor& dy, const Tensor& w,
+                const optional<Tensor>& wflip, int64_t stride, int64_t pad, int64_t dil) {
+  if (wflip.has_value() && wflip->defined() && g.R == 3 && g.S == 3 && stride == 1 && pad == 1 && dil == 1) {
+    CHECK_BF16(*wflip); CHECK_CONTIG(*wflip);
+    TORCH_CHECK(wflip->sizes() == at::IntArrayRef({g.C, 3, 3, g.Ko}), "wflip shape");
+    auto gf = geom({g.N, g.P, g.Q, g.Ko}, {g.C, 3, 3, g.Ko}, 1, 1, 1);
+    a = conv_args(gf, 1, 1, 1);
+    a.A = bf(dy); a.B = bf(*wflip);
+    a.a_bytes = dy.nbytes(); a.b_bytes = wflip->nbytes();
+    a.M = g.N * g.H * g.W; a.N = g.C; a.K = 9 * g.Ko; a.ldb = a.K; a.ldc = g.C;
+    return tfx::MODE_DGRAD_FLIP;
+  }
+  a = conv_args(g, stride, pad, dil);
+  a.A = bf(dy); a.B = bf(w);
+  a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
+  a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+  return tfx::MODE_DGRAD;
+}
+
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil,
-                  optional<Tensor> addend, optional<Tensor> addend_mask, bool addend_s2) {
+                  optional<Tensor> addend, optional<Tensor> addend_mask, bool addend_s2,
+                  optional<Tensor> wflip) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
@@ -138,13 +161,12 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
     TORCH_CHECK(acc && stride == 1 && !(addend_mask.has_value() && addend_mask->defined()),
                 "stride-2 compact addend: stride-1 data gradients, no mask");
     auto dx = at::empty({g.N, g.H, g.W, g.C}, dy.options());
-    auto a = conv_args(g, stride, pad, dil);
-    a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
-    a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
-    a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+    tfx::IgemmArgs a;
+    const int mode = dgrad_setup(a, g, dy, w, wflip, stride, pad, dil);
+    a.Cp = dx.data_ptr();
     a.out_mode = tfx::OUT_BF16;
     set_addend_s2(a, *addend, g.N, g.H, g.W, g.C);
-    tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
+    tfx::igemm_launch(a, mode, cur_stream());
     return dx;
   }
   if (acc) {
@@ -155,13 +177,12 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
   if (amask) {
     TORCH_CHECK(stride == 1 && g.C % 8 == 0, "masked addend: stride-1 data gradients with C % 8 == 0");
     auto dx = at::empty({g.N, g.H, g.W, g.C}, dy.options());
-    auto a = conv_args(g, stride, pad, dil);
-    a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
-    a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
-    a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+    tfx::IgemmArgs a;
+    const int mode = dgrad_setup(a, g, dy, w, wflip, stride, pad, dil);
+    a.Cp = dx.data_ptr();
     a.out_mode = tfx::OUT_BF16;
     a.addend = bf(*addend); a.addend_mask = amask;
-    tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
+    tfx::igemm_launch(a, mode, cur_stream());
     return dx;
   }
   if (stride == 2 && dil == 1 && dgrad_classes_enabled()) {
@@ -200,13 +221,12 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
     return dx;
   }
   auto dx = acc ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
-  auto a = conv_args(g, stride, pad, dil);
-  a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
-  a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
-  a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+  tfx::IgemmArgs a;
+  const int mode = dgrad_setup(a, g, dy, w, wflip, stride, pad, dil);
+  a.Cp = dx.data_ptr();
   a.out_mode = tfx::OUT_BF16;
   if (acc) a.addend = bf(*addend);
-  tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
+  tfx::igemm_launch(a, mode, cur_stream());
   return dx;
 }
 
@@ -270,7 +290,8 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
                                          int64_t pad, int64_t dil, optional<Tensor> addend, Tensor bn_x,
                                          Tensor bn_save, optional<Tensor> bn_mask, bool relu, Tensor ws,
                                          optional<Tensor> dgamma, optional<Tensor> dbeta,
-                                         optional<Tensor> addend_mask, bool reduce, bool addend_s2) {
+                                         optional<Tensor> addend_mask, bool reduce, bool addend_s2,
+                                         optional<Tensor> wflip) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
   TORCH_CHECK(stride == 1, "conv_dgrad_bn: stride-1 convs only (stride 2 runs per parity class)");
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
@@ -289,10 +310,9 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   auto dx = (acc && !amask && !addend_s2) ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
   // reduce = false: the partials stay in the slots for bn_bwd_slots (no red, no slot reduce)
   auto red = reduce ? at::empty({2 * g.C}, dy.options().dtype(at::kFloat)) : Tensor();
-  auto a = conv_args(g, stride, pad, dil);
-  a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
-  a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
-  a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.Ko; a.ldc = g.C;
+  tfx::IgemmArgs a;
+  const int mode = dgrad_setup(a, g, dy, w, wflip, stride, pad, dil);
+  a.Cp = dx.data_ptr();
   a.out_mode = tfx::OUT_BF16;
   if (acc) a.addend = bf(*addend);
   if (addend_s2) set_addend_s2(a, *addend, g.N, g.H, g.W, g.C);
@@ -309,7 +329,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   a.bnb_red = reduce ? red.data_ptr<float>() : nullptr;
   a.bnb_dgamma = reduce ? fpm(dgamma) : nullptr;
   a.bnb_dbeta = reduce ? fpm(dbeta) : nullptr;
-  tfx::igemm_launch(a, tfx::MODE_DGRAD, cur_stream());
+  tfx::igemm_launch(a, mode, cur_stream());
   if (reduce && !a.bn_final) tfx::bn_slot_reduce(a.bnb_slots, g.C, a.bnb_red, a.bnb_dgamma, a.bnb_dbeta, cur_stream());
   return {dx, red};
 }
@@ -461,6 +481,17 @@ std::tuple<Tensor, Tensor> bn_apply_train(Tensor x, optional<Tensor> res, Tensor
   tfx::bn_apply(bf(x), r, save.data_ptr<float>(), M, C, relu, bfm(y),
                 mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
   return {y, mask};
+}
+
+// flipped 3x3 filter copies for the flipped-weight data gradient (wflip.hip): src / dst = flat bf16
+// buffers, desc = [nlayers][5] int64 {src_off, dst_off, Ko, C, first_tile}, ntiles = total tiles
+void wflip3x3(Tensor src, Tensor dst, Tensor desc, int64_t ntiles) {
+  CHECK_DEV(src); CHECK_BF16(src); CHECK_BF16(dst); CHECK_CONTIG(src); CHECK_CONTIG(dst); CHECK_DEV(desc);
+  TORCH_CHECK(desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 5 && desc.is_contiguous(),
+              "wflip3x3 desc");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(dst.data_ptr()) & 15) == 0, "wflip3x3: 16-byte aligned buffers");
+  tfx::wflip3x3(bf(src), bfm(dst), desc.data_ptr<int64_t>(), (int)desc.size(0), (int)ntiles, cur_stream());
 }
 
 // bn_apply_train whose residual is a BN that was never applied: y = act(bn(x) + bn'(res_x)), with
@@ -1207,7 +1238,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("conv_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
-        "Tensor? addend_mask=None, bool addend_s2=False) -> Tensor", &conv_dgrad);
+        "Tensor? addend_mask=None, bool addend_s2=False, Tensor? wflip=None) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("gemm", &gemm);
   m.def("gemm_into", &gemm_into);
@@ -1216,6 +1247,7 @@ TORCH_LIBRARY(tfx, m) {
         &sgemm_into);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply_train", &bn_apply_train);
+  m.def("wflip3x3(Tensor src, Tensor(a!) dst, Tensor desc, int ntiles) -> ()", &wflip3x3);
   m.def("bn_apply_res_bn(Tensor x, Tensor res_x, Tensor save, Tensor res_save, bool relu) -> (Tensor, Tensor)",
         &bn_apply_res_bn);
   m.def("bn_bwd_apply_sec(Tensor g, Tensor x, Tensor save, Tensor red, bool relu, Tensor? mask, Tensor x2, "
@@ -1227,7 +1259,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
         "Tensor bn_x, Tensor bn_save, Tensor? bn_mask, bool relu, Tensor ws, Tensor? dgamma, Tensor? dbeta, "
-        "Tensor? addend_mask=None, bool reduce=True, bool addend_s2=False) -> (Tensor, Tensor)", &conv_dgrad_bn);
+        "Tensor? addend_mask=None, bool reduce=True, bool addend_s2=False, Tensor? wflip=None) -> (Tensor, Tensor)",
+        &conv_dgrad_bn);
   m.def("bn_fwd_slots", &bn_fwd_slots);
   m.def("bn_bwd_slots", &bn_bwd_slots);
   m.def("bn_slots_supported", &bn_slots_supported);

@@ -116,6 +116,25 @@ def _conv_ref(x, w, stride=1, pad=0, dil=1):
 _BNB_MAX_BYTES = int(os.environ.get("TFX_BNB_MAX_MB", "256")) << 20
 
 
+# A/B switch: stride-1 3x3 data gradients as the forward conv of dY with flipped, transposed
+# filters (igemm_dgrad_flip.hip), all layers' copies refreshed by one launch per step
+_DGRAD_FLIP = os.environ.get("TFX_DGRAD_FLIP", "1") != "0"
+
+
+def _flip_ok(w, stride, pad, dil):
+    sh = w.shape
+    return _DGRAD_FLIP and stride == 1 and pad == 1 and dil == 1 and len(sh) == 4 and sh[1] == 3 and sh[2] == 3 \
+        and getattr(w.store, "shadow", None) is not None and w.store.flip_index(w) is not None
+
+
+def _wflip(w, stride, pad, dil):
+    """The flipped copy of a 3x3 filter (refreshing every layer's copy first if the weights may
+    have changed since the last refresh), or None where the data gradient stays gathered."""
+    if not _flip_ok(w, stride, pad, dil):
+        return None
+    return w.store.flipped3x3(w)
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into, sink, bnb):
@@ -123,6 +142,8 @@ class _Conv2d(torch.autograd.Function):
         ctx.native = _native.use_native(x)
         ctx.save_for_backward(x)
         if ctx.native:
+            if _flip_ok(w, stride, pad, dil):
+                w.store.flip_stale = True  # the weights may have changed since the last refresh
             if isinstance(stats_into, BNWorkspace):
                 ws = stats_into
                 if ws.two_phase(x.device):
@@ -170,16 +191,17 @@ class _Conv2d(torch.autograd.Function):
                             bnb.wsobj.bwd_dirty = False
                         dx, _ = torch.ops.tfx.conv_dgrad_bn(
                             gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
-                            sb, None, None, amask, False, s2)
+                            sb, None, None, amask, False, s2, _wflip(w, stride, pad, dil))
                         bnb.red = BNBackwardFusion.IN_SLOTS
                     else:
                         dx, bnb.red = torch.ops.tfx.conv_dgrad_bn(
                             gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
-                            bnb.ws, bnb.dgamma, bnb.dbeta, amask, True, s2)
+                            bnb.ws, bnb.dgamma, bnb.dbeta, amask, True, s2, _wflip(w, stride, pad, dil))
                 elif sink is not None and sink.mode == "consume":
                     # last consumer of x in backward order: fold the other branch's gradient in
                     add, amask, s2 = _unpack_sink(sink.take())
-                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, add, amask, s2)
+                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, add, amask, s2,
+                                                  _wflip(w, stride, pad, dil))
                 elif sink is not None and sink.accept_s2 and stride == 2 and pad == 0 and w.shape[1] == 1 \
                         and w.shape[2] == 1 and x.shape[-1] % 8 == 0:
                     # 1x1 stride-2 branch: its input gradient is nonzero only at the even pixels --
@@ -189,7 +211,8 @@ class _Conv2d(torch.autograd.Function):
                     sink.put(("s2", dxc))
                     dx = None
                 else:
-                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, None)
+                    dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, None, None, False,
+                                                  _wflip(w, stride, pad, dil))
                     if sink is not None:  # mode "produce": park it for the last consumer
                         sink.put(dx)
                         dx = None

@@ -19,7 +19,7 @@ import torch
 TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tune", "igemm_gfx950.json")
 
 FAMILIES = ["fwd_pointwise", "fwd_im2col", "dgrad_pointwise", "dgrad_general", "dgrad_cls_dense", "dgrad_cls",
-            "wgrad_dense", "wgrad_x", "wgrad_t_x"]
+            "wgrad_dense", "wgrad_x", "wgrad_t_x", "dgrad_flip"]
 ATOMIC_FAMILIES = {6, 7, 8}
 
 

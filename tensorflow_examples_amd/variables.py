@@ -265,6 +265,8 @@ class VariableStore:
         self.master: Optional[torch.Tensor] = None
         self.grad: Optional[torch.Tensor] = None
         self.shadow: Optional[torch.Tensor] = None
+        self._flip = None          # flipped 3x3 filter copies (flip_index / flipped3x3)
+        self.flip_stale = True
         self.total = 0
         # autograd anchor: a leaf that requires grad, passed to every parameterised op so the
         # graph is recorded even when no input activation requires grad (params are not
@@ -377,6 +379,40 @@ class VariableStore:
     def refresh_shadow(self) -> None:
         if self.shadow is not None:
             self.shadow.copy_(self.master)
+        self.flip_stale = True
+
+    # -- flipped 3x3 filters (the stride-1 3x3 data gradient runs as a forward conv with them)
+    def flip_index(self, v: "Variable"):
+        """Slot of ``v`` in the flipped-filter buffer, or None (not a [Ko, 3, 3, C] filter with
+        Ko, C multiples of 64 in a bf16 GPU store)."""
+        if self._flip is None:
+            self._build_flip()
+        return self._flip["slot"].get(v.name)
+
+    def _build_flip(self) -> None:
+        slot, rows, doff, tiles = {}, [], 0, 0
+        if self.shadow is not None and self.shadow.is_cuda:
+            for v in self.vars:
+                sh = v.shape
+                if len(sh) == 4 and sh[1] == 3 and sh[2] == 3 and sh[0] % 64 == 0 and sh[3] % 64 == 0:
+                    slot[v.name] = (doff, tuple(int(d) for d in (sh[3], 3, 3, sh[0])))
+                    rows.append([v.offset, doff, sh[0], sh[3], tiles])
+                    doff += _round_up(v.numel, ALIGN)
+                    tiles += 9 * (sh[0] // 64) * (sh[3] // 64)
+        self._flip = {"slot": slot, "tiles": tiles, "buf": None, "desc": None}
+        if rows:
+            self._flip["buf"] = torch.zeros(doff, dtype=self.shadow.dtype, device=self.device)
+            self._flip["desc"] = torch.tensor(rows, dtype=torch.int64).to(self.device)
+
+    def flipped3x3(self, v: "Variable") -> torch.Tensor:
+        """Wf[c][r][s][ko] = W[ko][2-r][2-s][c] of ``v`` (bf16), every layer's copy refreshed from
+        the shadow in one launch when ``flip_stale`` (set by each forward conv that will want it)."""
+        off, shape = self._flip["slot"][v.name]
+        f = self._flip
+        if self.flip_stale:
+            torch.ops.tfx.wflip3x3(self.shadow, f["buf"], f["desc"], f["tiles"])
+            self.flip_stale = False
+        return f["buf"][off:off + v.numel].view(shape)
 
     def zero_grad(self) -> None:
         self.grad.zero_()
