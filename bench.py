@@ -18,8 +18,10 @@ Launch modes (the process-per-task model of R/distributed/distributed.py:7-14,37
 Timing: W untimed warmup steps; barrier + synchronize; K timed steps; barrier + synchronize; the
 MAX elapsed over ranks is reported.  Rank 0 prints ONE JSON line.
 
-``--host-input``: batches live in pinned host memory and every step copies its batch H2D through
-the framework's pinned ring (data/pipeline.py) on a side stream -- the tf.data/feed_dict path.
+``--host-input [zerocopy|copy]``: batches live in pinned host memory (the tf.data/feed_dict path)
+and go through the framework's pinned ring (data/pipeline.py): ``zerocopy`` -- the fused input
+kernel reads the pinned slot over the host link; ``copy`` -- an async H2D copy per step on a side
+stream into device slots.
 ``--impl torch`` runs a stock PyTorch-ROCm eager ResNet-50 (torch.nn + MIOpen, channels_last, bf16
 autocast) for a labelled comparison; the headline is ``--impl native``.
 ``--device cpu`` runs the same step on the CPU reference ops over gloo (tests of the launch path).
@@ -54,8 +56,10 @@ def parse(argv=None):
                          "TFX_DP_GRAPH=1 also captures the RCCL all-reduces -- measured on a 1-rank "
                          "RCCL group: 9.26 graph vs 9.34 ms eager, so N>1 stays eager by default)")
     ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager step launches")
-    ap.add_argument("--host-input", action="store_true",
-                    help="pinned-host batches copied H2D every step through the pinned ring")
+    ap.add_argument("--host-input", nargs="?", const="zerocopy", default=None, choices=["copy", "zerocopy"],
+                    help="batches live in pinned host memory: 'zerocopy' (default when given) = the input kernel "
+                         "reads the pinned slot over the host link; 'copy' = async H2D into device slots on a "
+                         "side stream (data/pipeline.py PinnedRing)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--backend", default=None, help="process-group backend (default nccl = RCCL, gloo on cpu)")
@@ -103,7 +107,7 @@ def run(a):
 
     ring = None
     if a.host_input and cuda:
-        ring = PinnedRing.for_batches(host, dev, depth=2)
+        ring = PinnedRing.for_batches(host, dev, depth=2, zero_copy=a.host_input == "zerocopy")
         data = None
     else:
         data = [(img.to(dev), lab.to(dev)) for img, lab in host]
@@ -123,6 +127,8 @@ def run(a):
 
         def step(i):
             img, lab = batch(i)
+            if img.device.type == "cpu" and cuda:  # zero-copy ring: pinned host tensors
+                return trainer.step(to_model_input(img, dtype=dtype, device=dev), lab.to(dev, non_blocking=True))
             return trainer.step(to_model_input(img, dtype=dtype), lab)
 
         if cuda and a.graph and ((world == 1 and not forced) or os.environ.get("TFX_DP_GRAPH", "0") == "1"):
@@ -131,7 +137,7 @@ def run(a):
             # copied into the graph's static input
             img, lab = batch(0)
             try:
-                trainer.capture(to_model_input(img), lab)
+                trainer.capture(to_model_input(img, device=dev), lab.to(dev))
                 graphed = True
             except Exception as e:  # pragma: no cover - capture is best effort, eager is the fallback
                 print("rank %d: hip graph capture failed (%s)" % (rank, e), file=sys.stderr)
@@ -159,6 +165,8 @@ def run(a):
 
         def step(i):
             img, lab = batch(i)
+            if img.device != dev:  # zero-copy ring: stock torch has no zero-copy kernel, copy H2D
+                img, lab = img.to(dev, non_blocking=True), lab.to(dev, non_blocking=True)
             x = ((img.permute(0, 3, 1, 2).float() / 255.0 - mean) / std).contiguous(memory_format=torch.channels_last)
             topt.zero_grad(set_to_none=True)
             with torch.autocast(dev.type, dtype=torch.bfloat16):
@@ -202,8 +210,9 @@ def run(a):
             "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
             "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
             "data": "synthetic (CIFAR-10-shaped uint8 32x32x3 images, random labels, random-init weights)"
-                    + ("; pinned-host batches copied H2D every step" if ring is not None else
-                       "; batches resident on the device"),
+                    + ({"copy": "; pinned-host batches copied H2D every step",
+                        "zerocopy": "; pinned-host batches read by the input kernel every step (zero-copy)"}
+                       [a.host_input] if ring is not None else "; batches resident on the device"),
             "config": {
                 "model": "ResNet-%d (CIFAR-10 adaptation: 3x3 stem, bottleneck [3,4,6,3])" % a.depth,
                 "global_batch": a.batch * world,
@@ -217,7 +226,7 @@ def run(a):
                 "optimizer": "momentum-SGD 0.9, wd 5e-4 (fused flat-buffer kernel)" if a.impl == "native" else "torch.optim.SGD foreach",
                 "allreduce_bucket_mb": a.bucket_mb,
                 "hip_graph": bool(a.impl == "native" and graphed),
-                "host_input": ring is not None,
+                "host_input": a.host_input if ring is not None else False,
                 "params": nparams,
                 "final_loss": round(final_loss, 4),
             },

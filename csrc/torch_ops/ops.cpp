@@ -1210,10 +1210,41 @@ Tensor image_normalize(Tensor x, std::vector<double> mean, std::vector<double> s
   return y;
 }
 
+// Same kernel, written into a caller-owned device tensor.  `x` may be a GPU tensor or a PINNED host
+// tensor: page-locked memory is mapped into the GPU's address space, so the kernel reads the batch
+// straight over the host link (zero-copy input: no H2D staging copy, no copy stream, no device
+// staging buffer).  The caller keeps the pinned buffer unmodified until the kernel has run
+// (data/pipeline.py PinnedRing(zero_copy=True) orders that with an event per slot).
+void image_normalize_into(Tensor x, std::vector<double> mean, std::vector<double> stdv, Tensor out) {
+  CHECK_CONTIG(x); CHECK_DEV(out); CHECK_CONTIG(out); CHECK_BF16(out);
+  TORCH_CHECK(x.scalar_type() == at::kByte, "image_normalize_into: uint8 images");
+  const int64_t cin = x.size(-1), cout = out.size(-1);
+  TORCH_CHECK(cin >= 1 && cin <= 4 && (int64_t)mean.size() == cin && (int64_t)stdv.size() == cin,
+              "image_normalize_into: 1..4 channels with per-channel mean/std");
+  TORCH_CHECK(cout == 4 || cout == 8, "image_normalize_into: cout 4 or 8");
+  TORCH_CHECK(x.numel() / cin == out.numel() / cout && x.dim() == out.dim(),
+              "image_normalize_into: pixel counts of x and out differ");
+  const uint8_t* src = x.data_ptr<uint8_t>();
+  if (!x.is_cuda()) {
+    TORCH_CHECK(x.is_pinned(), "image_normalize_into: a host input must be pinned (page-locked)");
+    void* dp = nullptr;
+    TORCH_CHECK(hipHostGetDevicePointer(&dp, const_cast<uint8_t*>(src), 0) == hipSuccess && dp,
+                "image_normalize_into: pinned host buffer is not mapped into the GPU's address space");
+    src = static_cast<const uint8_t*>(dp);
+  }
+  float m[4] = {0, 0, 0, 0}, s[4] = {1, 1, 1, 1};
+  for (int64_t c = 0; c < cin; ++c) {
+    m[c] = (float)mean[c];
+    s[c] = (float)stdv[c];
+  }
+  tfx::image_normalize(src, x.numel() / cin, (int)cin, (int)cout, m, s, bfm(out), cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tfx, m) {
   m.def("image_normalize", &image_normalize);
+  m.def("image_normalize_into", &image_normalize_into);
   m.def("philox_fill", &philox_fill);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

@@ -182,6 +182,20 @@ for s in $STEPS; do
         timeout -k 10 400 python bench.py --steps 30 --warmup 5 --host-input > gpurun_out/bench_hostin_$i.log 2>&1 || exit 1
       done
       grep -ho '"ms_per_step": [0-9.]*' gpurun_out/bench_dev_*.log gpurun_out/bench_hostin_*.log ;;
+    hostin2)
+      timeout -k 10 300 python -u -m pytest tests/test_pipeline_gpu.py -v -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_pipeline.log 2>&1
+      rc=$?; echo "pipeline tests rc=$rc"; tail -12 gpurun_out/pytest_pipeline.log; [ $rc -eq 0 ] || exit $rc
+      for i in 1 2; do
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_dev_$i.log 2>&1 || exit 1
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 --host-input zerocopy > gpurun_out/bench_hostzc_$i.log 2>&1 || exit 1
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 --host-input copy > gpurun_out/bench_hostcp_$i.log 2>&1 || exit 1
+      done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_dev_*.log gpurun_out/bench_hostzc_*.log gpurun_out/bench_hostcp_*.log
+      export TMPDIR=/tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$R/gpurun_out/prof_hostcp" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --host-input copy > gpurun_out/prof_hostcp.log 2>&1
+      rc=$?; echo "prof hostcp rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_hostzc" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --host-input zerocopy > gpurun_out/prof_hostzc.log 2>&1
+      rc=$?; echo "prof hostzc rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmcbench)
       # PMC passes over a short eager bench (each pass its own run; <= 8 SQ, 4 TCC, 2 GRBM counters)
       export TMPDIR=/tmp

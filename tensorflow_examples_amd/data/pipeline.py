@@ -50,13 +50,21 @@ class _Slot:
 
 
 class PinnedRing:
-    def __init__(self, device, depth: int = 2):
+    """``zero_copy=True``: no device staging buffers and no copy stream -- :meth:`acquire` hands out
+    the pinned host tensors themselves and the consumer's first kernel reads them over the host
+    link (``torch.ops.tfx.image_normalize_into`` maps page-locked memory into the GPU's address
+    space).  The host then waits on a slot's ``free`` event (the consumer's kernels that read it have
+    run) before overwriting it; ``nslots`` = ``depth`` + 1 slots let the host run ``depth`` steps
+    ahead of the GPU."""
+
+    def __init__(self, device, depth: int = 2, zero_copy: bool = False):
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
+        self.zero_copy = bool(zero_copy) and self.gpu
         # depth batches in flight + the one being consumed
         self.nslots = max(1, depth) + 1
         self.slots = [_Slot() for _ in range(self.nslots)]
-        self.stream = torch.cuda.Stream(self.device) if self.gpu else None
+        self.stream = torch.cuda.Stream(self.device) if self.gpu and not self.zero_copy else None
         self._next = 0
         self._held: Optional[int] = None
         if self.gpu:
@@ -75,7 +83,7 @@ class PinnedRing:
         if s.free_pending:
             s.free.synchronize()
         s.host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in items]
-        s.dev = [torch.empty(t.shape, dtype=t.dtype, device=self.device) for t in items]
+        s.dev = s.host if self.zero_copy else [torch.empty(t.shape, dtype=t.dtype, device=self.device) for t in items]
 
     def stage(self, batch) -> int:
         """Copy one host batch (tuple of arrays/CPU tensors) into the next slot and start its async
@@ -90,6 +98,14 @@ class PinnedRing:
         if k == self._held:
             raise RuntimeError("PinnedRing: staging over the slot still held by the consumer (too many in flight)")
         self._ensure(s, items)
+        if self.zero_copy:
+            # the consumer's kernels read this pinned buffer directly: they must have run
+            if s.free_pending:
+                s.free.synchronize()
+                s.free_pending = False
+            for h, t in zip(s.host, items):
+                h.copy_(t)
+            return k
         if s.h2d_pending:  # the previous copy out of this pinned buffer must have been read
             s.h2d.synchronize()
         for h, t in zip(s.host, items):
@@ -113,17 +129,20 @@ class PinnedRing:
                 h = self.slots[self._held]
                 h.free.record(cur)
                 h.free_pending = True
-            cur.wait_event(s.h2d)
+            if not self.zero_copy:
+                cur.wait_event(s.h2d)
         self._held = k
         return tuple(s.dev)
 
     @classmethod
-    def for_batches(cls, host_batches: Sequence, device, depth: int = 2) -> "CyclicFeeder":
-        return CyclicFeeder(host_batches, cls(device, depth), depth)
+    def for_batches(cls, host_batches: Sequence, device, depth: int = 2, zero_copy: bool = False) -> "CyclicFeeder":
+        return CyclicFeeder(host_batches, cls(device, depth, zero_copy=zero_copy), depth)
 
     def close(self) -> None:
-        if self.gpu:
+        if self.stream is not None:
             self.stream.synchronize()
+        elif self.zero_copy:
+            torch.cuda.synchronize(self.device)  # no kernel may still read a pinned slot
         self.slots = []
 
 
@@ -142,6 +161,11 @@ class CyclicFeeder:
         self._n += 1
 
     def next(self):
+        if self.ring.zero_copy:
+            # nothing to prefetch (no copy): stage on demand into the slot used nslots batches ago,
+            # whose free event is nslots - 1 steps old -- the host stays that far ahead of the GPU
+            self._stage_one()
+            return self.ring.acquire(self._q.pop(0))
         if not self._q:
             self._stage_one()
         out = self.ring.acquire(self._q.pop(0))

@@ -196,12 +196,19 @@ def build_resnet_cifar(device="cuda", depth=50, num_classes=10, dtype=torch.bflo
     return store, model
 
 
-def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16, device=None) -> torch.Tensor:
     """[N,32,32,3] images -> [N,32,32,8] normalised NHWC compute tensor (channels 3..7 zero).
-    GPU uint8 input: one fused HIP kernel (csrc/kernels/image.hip)."""
+    GPU uint8 input: one fused HIP kernel (csrc/kernels/image.hip).  A pinned host uint8 batch with
+    ``device`` = a GPU: the same kernel reads it over the host link (zero-copy input)."""
     x = images_nhwc_u8_or_f
     if x.dtype == torch.uint8 and dtype == torch.bfloat16 and x.device.type == "cuda" and _native.use_native(x):
         return torch.ops.tfx.image_normalize(x.contiguous(), list(_MEAN), list(_STD), IN_CH_PAD)
+    if device is not None and torch.device(device).type == "cuda" and x.device.type == "cpu" and \
+            x.dtype == torch.uint8 and dtype == torch.bfloat16 and x.is_pinned():
+        # zero-copy input: the kernel reads the pinned host batch directly (no H2D staging copy)
+        out = torch.empty((*x.shape[:-1], IN_CH_PAD), dtype=dtype, device=device)
+        torch.ops.tfx.image_normalize_into(x.contiguous(), list(_MEAN), list(_STD), out)
+        return out
     if x.dtype == torch.uint8:
         x = x.float() / 255.0
     mean = torch.tensor(_MEAN, device=x.device)

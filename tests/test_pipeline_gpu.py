@@ -56,4 +56,56 @@ def test_bench_host_input_runs(gpu):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
     assert p.returncode == 0, p.stderr[-3000:]
     rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
-    assert rec["config"]["host_input"] is True and rec["value"] > 0
+    assert rec["config"]["host_input"] == "zerocopy" and rec["value"] > 0
+
+
+def test_image_normalize_into_zero_copy_matches_reference(gpu):
+    from tensorflow_examples_amd.models.resnet import _MEAN, _STD, to_model_input
+    g = torch.Generator().manual_seed(3)
+    img = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, generator=g)
+    ref = to_model_input(img, dtype=torch.float32)  # CPU fp32 reference path
+    dev_out = to_model_input(img.to(gpu))  # device-resident input
+    pin_out = to_model_input(img.pin_memory(), device=gpu)  # zero-copy from pinned host memory
+    torch.cuda.synchronize()
+    assert pin_out.device.type == "cuda" and pin_out.shape == (16, 32, 32, 8)
+    assert torch.equal(pin_out, dev_out)
+    assert (pin_out.float().cpu() - ref).abs().max().item() < 2e-2
+    assert float(pin_out[..., 3:].abs().max()) == 0.0
+    with pytest.raises(RuntimeError):  # pageable host memory is refused, not silently copied
+        torch.ops.tfx.image_normalize_into(img, list(_MEAN), list(_STD), torch.empty_like(dev_out))
+
+
+def test_zero_copy_ring_never_overwrites_a_queued_batch(gpu):
+    """The host restages a slot only after the kernels that read it (queued behind slow work) ran."""
+    from tensorflow_examples_amd.models.resnet import to_model_input
+    host = [(torch.full((8, 32, 32, 3), 10 * i, dtype=torch.uint8), torch.full((8,), i, dtype=torch.long))
+            for i in range(7)]
+    feeder = PinnedRing.for_batches(host, gpu, depth=2, zero_copy=True)
+    big = torch.randn(2048, 2048, device=gpu)
+    outs = []
+    for i in range(20):
+        for _ in range(3):  # keep the stream busy so the host runs ahead of the GPU
+            big = big @ big * 1e-3
+        img, lab = feeder.next()
+        assert img.device.type == "cpu" and img.is_pinned()
+        outs.append((to_model_input(img, device=gpu), lab.to(gpu, non_blocking=True)))
+    torch.cuda.synchronize()
+    ref = [to_model_input(h[0].to(gpu)) for h in host]
+    for i, (x, y) in enumerate(outs):
+        assert torch.equal(x, ref[i % 7]), i
+        assert int(y[0]) == i % 7
+    feeder.close()
+
+
+def test_bench_host_input_copy_mode_runs(gpu):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--depth", "18", "--batch", "32", "--steps", "4",
+           "--warmup", "2", "--host-input", "copy"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["config"]["host_input"] == "copy" and rec["value"] > 0
