@@ -196,6 +196,19 @@ for s in $STEPS; do
       rc=$?; echo "prof hostcp rc=$rc"; [ $rc -eq 0 ] || exit $rc
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_hostzc" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --host-input zerocopy > gpurun_out/prof_hostzc.log 2>&1
       rc=$?; echo "prof hostzc rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    eager)
+      for i in 1 2; do
+        timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-graph > gpurun_out/bench_eager_$i.log 2>&1 || exit 1
+      done
+      for v in 0 1; do
+        TFX_DP_FORCE_COLLECTIVE=1 TFX_DP_GRAPH=$v timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 29517 bench.py --steps 30 --warmup 5 > gpurun_out/bench_dpforce_g$v.log 2>&1
+        rc=$?; echo "dpforce graph=$v rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_dpforce_g$v.log; exit $rc; }
+      done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_eager_*.log gpurun_out/bench_dpforce_g*.log
+      export TMPDIR=/tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_eager" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-graph > gpurun_out/prof_eager.log 2>&1
+      rc=$?; echo "prof eager rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmcbench)
       # PMC passes over a short eager bench (each pass its own run; <= 8 SQ, 4 TCC, 2 GRBM counters)
       export TMPDIR=/tmp
