@@ -52,9 +52,9 @@ def parse(argv=None):
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
-                    help="capture the whole step in a HIP graph and replay it (default on for N=1; for N>1 "
-                         "TFX_DP_GRAPH=1 also captures the RCCL all-reduces -- measured on a 1-rank "
-                         "RCCL group: 9.26 graph vs 9.34 ms eager, so N>1 stays eager by default)")
+                    help="capture the whole step in a HIP graph and replay it (default on; for N>1 the bucketed "
+                         "RCCL all-reduces are captured too -- measured on a 1-rank RCCL group: 8.16 ms graph vs "
+                         "9.03 ms eager, profiles/r02_final/dp_graph_ab.txt; TFX_DP_GRAPH=0 keeps N>1 eager)")
     ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager step launches")
     ap.add_argument("--host-input", nargs="?", const="zerocopy", default=None, choices=["copy", "zerocopy"],
                     help="batches live in pinned host memory: 'zerocopy' (default when given) = the input kernel "
@@ -131,7 +131,7 @@ def run(a):
                 return trainer.step(to_model_input(img, dtype=dtype, device=dev), lab.to(dev, non_blocking=True))
             return trainer.step(to_model_input(img, dtype=dtype), lab)
 
-        if cuda and a.graph and ((world == 1 and not forced) or os.environ.get("TFX_DP_GRAPH", "0") == "1"):
+        if cuda and a.graph and ((world == 1 and not forced) or os.environ.get("TFX_DP_GRAPH", "1") == "1"):
             # the captured step is the same work (forward, backward with the bucketed RCCL
             # all-reduces, fused optimizer) replayed with one launch; the per-step input batch is
             # copied into the graph's static input
