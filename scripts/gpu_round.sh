@@ -209,6 +209,21 @@ for s in $STEPS; do
       export TMPDIR=/tmp
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_eager" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-graph > gpurun_out/prof_eager.log 2>&1
       rc=$?; echo "prof eager rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    dpprof)
+      export TMPDIR=/tmp
+      for v in 0 1; do
+        RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=2953$v TFX_DP_FORCE_COLLECTIVE=1 TFX_DP_GRAPH=$v \
+          timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_dp$v" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 > gpurun_out/prof_dp$v.log 2>&1
+        rc=$?; echo "prof dp graph=$v rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/prof_dp$v.log; exit $rc; }
+      done ;;
+    tunebig)
+      timeout -k 10 900 python scripts/tune_convs.py --passes wgrad --merge tensorflow_examples_amd/tune/igemm_gfx950.json --out gpurun_out/igemm_gfx950.json --report gpurun_out/tune_report_big.json > gpurun_out/tune_big.log 2>&1
+      rc=$?; echo "tune rc=$rc"; tail -25 gpurun_out/tune_big.log; [ $rc -eq 0 ] || exit $rc
+      for i in 1 2 3; do
+        timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_tb0_$i.log 2>&1 || exit 1
+        TFX_TUNE_FILE=gpurun_out/igemm_gfx950.json timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_tb1_$i.log 2>&1 || exit 1
+      done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_tb*.log ;;
     pmcbench)
       # PMC passes over a short eager bench (each pass its own run; <= 8 SQ, 4 TCC, 2 GRBM counters)
       export TMPDIR=/tmp

@@ -66,7 +66,11 @@ def main():
     ap.add_argument("--margin", type=float, default=0.03)
     ap.add_argument("--out", default=tuning.TABLE)
     ap.add_argument("--report", default="gpurun_out/tune_report.json")
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad", help="comma list of passes to tune")
+    ap.add_argument("--merge", default=None,
+                    help="existing table: keep its entries for the passes not tuned now, replace the rest")
     a = ap.parse_args()
+    want_passes = set(a.passes.split(","))
     os.environ["TFX_TUNE"] = "0"
     assert _native.load()
     tuning.clear()
@@ -98,6 +102,8 @@ def main():
         if C == 8:  # the stem: its input needs no gradient, so the model never runs its dgrad
             del passes["dgrad"]
         for name, fn in passes.items():
+            if name not in want_passes:
+                continue
             launches = traced(fn)
             fams = sorted({r[0] for r in launches})
             atomic = any(f in tuning.ATOMIC_FAMILIES for f in fams)
@@ -131,6 +137,11 @@ def main():
         del x, w, y, gy, dw
     # a GEMM shape reached from two convs keeps its first (larger-count-first order is not needed:
     # identical (family, M, N, K) means an identical GEMM)
+    if a.merge:
+        # keep the merged table's entries of the passes not re-tuned now (dgrad_flip rows included)
+        with open(a.merge) as f:
+            old = json.load(f)["entries"]
+        entries += [e for e in old if e.get("pass", "").split(" ")[0] not in want_passes]
     seen, uniq_entries = set(), []
     for e in entries:
         k = (e["fam"], e["M"], e["N"], e["K"])
