@@ -39,6 +39,9 @@ flags.DEFINE_float("bucket_mb", 32.0, "all-reduce bucket size (MB)")
 flags.DEFINE_string("logdir", "", "checkpoint directory (resume from the latest checkpoint in it)")
 flags.DEFINE_integer("synthetic_train", 50000, "synthetic training-set size when no data is found")
 flags.DEFINE_integer("eval_examples", 0, "evaluate on the first N test images (0 = all)")
+flags.DEFINE_boolean("graph", True, "GPU: capture the training step (forward, backward with the bucketed RCCL "
+                     "all-reduces, optimizer) in a HIP graph on the first batch and replay it (the capture's "
+                     "warm-up trains on that batch 3 extra times); --nograph runs eager launches")
 FLAGS = flags.FLAGS
 
 
@@ -64,12 +67,30 @@ def main(_):
     total = FLAGS.max_steps or steps_per_epoch * FLAGS.epochs
     bounds = [int(float(f) * total) for f in FLAGS.lr_boundaries.split(",") if f]
     step, t0, seen = start_step, time.time(), 0
+    want_graph = FLAGS.graph and dev.type == "cuda"
     for ep in range(FLAGS.epochs):
         src = batches([xtr[shard], ytr[shard]], FLAGS.batch_size, seed=ep * 1000 + rank)
         for img, lab in DevicePrefetcher(src, dev):
             lr = FLAGS.learning_rate * world * (0.1 ** sum(step >= b for b in bounds))
-            opt.set_learning_rate(lr)
-            loss = trainer.step(to_model_input(augment(img), dtype), lab)
+            opt.set_learning_rate(lr)  # a device scalar: a replayed graph reads the new value
+            x = to_model_input(augment(img), dtype)
+            if want_graph:
+                want_graph = False
+                ok = True
+                try:
+                    trainer.capture(x, lab)
+                except Exception as e:  # eager fallback
+                    print("rank %d: hip graph capture failed (%s)" % (rank, e), file=sys.stderr)
+                    ok = False
+                if world > 1:  # every rank replays or none does (collective order must match)
+                    agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+                    dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+                    ok = bool(agree.item())
+                if not ok:
+                    trainer.graph = None
+                if rank == 0:
+                    print("hip graph: %s" % ("replaying the captured step" if ok else "eager launches"), flush=True)
+            loss = trainer.step(x, lab)
             step += 1
             seen += img.shape[0]
             if rank == 0 and step % 50 == 0:
