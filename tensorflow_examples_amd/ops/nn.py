@@ -415,6 +415,21 @@ _DEFER_RES_BN = os.environ.get("TFX_DEFER_RES_BN", "1") != "0"
 _FUSE_RES_BN_MASK = os.environ.get("TFX_FUSE_RES_BN_MASK", "1") != "0"
 
 
+_ZERO = {}
+
+
+def _zero_scalar(dtype, device) -> torch.Tensor:
+    """A persistent 0-d zero (the never-read placeholder of a BN output that is not written): no fill
+    launch per step, and safe inside a captured graph (allocated once, outside any capture)."""
+    key = (dtype, str(device))
+    t = _ZERO.get(key)
+    if t is None:
+        t = torch.zeros((), dtype=dtype, device=device)
+        if not (t.is_cuda and torch.cuda.is_current_stream_capturing()):  # never cache a graph-pool tensor
+            _ZERO[key] = t
+    return t
+
+
 def _vec_ok(C):
     return C % 8 == 0 and C // 8 <= 256 and 256 % (C // 8) == 0
 
@@ -480,7 +495,7 @@ class _BatchNorm(torch.autograd.Function):
                 if fuse_res:
                     y, mask = torch.ops.tfx.bn_apply_res_bn(x, res_bnb.x, save, res_bnb.save, relu)
                 elif defer_out:
-                    y = torch.zeros((), dtype=x.dtype, device=x.device).expand(x.shape)
+                    y = _zero_scalar(x.dtype, x.device).expand(x.shape)
                 else:
                     y, mask = torch.ops.tfx.bn_apply_train(x, res, save, relu)
             elif training:

@@ -63,7 +63,8 @@ class Optimizer:
         ||g||^2) enables clip-by-global-norm at ``max_norm``."""
         st = self.store
         self.iterations += 1
-        self.step_t.add_(1.0)
+        if self.kind >= ADAM:  # only the bias corrections read the device step counter (one launch less)
+            self.step_t.add_(1.0)
         if st.sparse:
             self.apply_sparse(grad_scale)
         if not st.vars:

@@ -26,6 +26,7 @@ class ClassifierTrainer:
         self.naive = naive_xent
         self.graph = None
         self._static = None
+        self._one = None
 
     def _step(self, x, y):
         # roctx ranges (TFX_ROCTX=1) label the phases on a rocprofv3 --marker-trace timeline
@@ -34,7 +35,13 @@ class ClassifierTrainer:
             logits = self.model(x, training=True)
             loss = ops.softmax_cross_entropy(logits, y, naive=self.naive)
         with trace.range("backward"):
-            loss.backward()
+            # a persistent unit seed gradient: no ones-fill launch per step (graph-safe: never written)
+            one = self._one
+            if one is None or one.device != loss.device or one.dtype != loss.dtype:
+                one = torch.ones((), dtype=loss.dtype, device=loss.device)
+                if not (one.is_cuda and torch.cuda.is_current_stream_capturing()):  # not from a graph pool
+                    self._one = one
+            loss.backward(one)
         scale = 1.0
         if self.dp is not None:
             with trace.range("allreduce_wait"):
