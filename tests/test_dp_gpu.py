@@ -45,27 +45,37 @@ dist.broadcast(w, 0)
 diff = (w - store.master).abs().max().item()
 # single-process reference from the same (rank-0) initial weights: the gradient of each rank's
 # half-batch accumulated into one buffer, averaged -- exactly what bucketed DP must compute
-rs, rm = build_resnet_cifar(device=dev, depth=depth, dtype=torch.bfloat16, seed=0)
-assert torch.equal(rs.master, w0)
-ropt = MomentumOptimizer(rs, 0.01, momentum=0.9)
-for _ in range(STEPS):
-    rs.zero_grad()
-    for r in range(world):
-        xr, yr = batch(r)
-        ops.softmax_cross_entropy(rm(xr, training=True), yr).backward()
-    ropt.apply_gradients(grad_scale=1.0 / world)
-torch.cuda.synchronize()
-d_dp, d_ref = store.master - w0, rs.master - w0
-rel = ((d_dp - d_ref).norm() / d_ref.norm()).item()
-worst = 0.0
-for lo, hi in dp.buckets:
-    n = d_ref[lo:hi].norm().item()
-    if n > 0:
-        worst = max(worst, (d_dp[lo:hi] - d_ref[lo:hi]).norm().item() / n)
-print(f"RANK{rank} buckets={len(dp.buckets)} diff={diff} rel={rel:.3e} worst_bucket={worst:.3e} losses={losses}",
-      flush=True)
+def reference():
+    rs, rm = build_resnet_cifar(device=dev, depth=depth, dtype=torch.bfloat16, seed=0)
+    assert torch.equal(rs.master, w0)
+    ropt = MomentumOptimizer(rs, 0.01, momentum=0.9)
+    for _ in range(STEPS):
+        rs.zero_grad()
+        for r in range(world):
+            xr, yr = batch(r)
+            ops.softmax_cross_entropy(rm(xr, training=True), yr).backward()
+        ropt.apply_gradients(grad_scale=1.0 / world)
+    torch.cuda.synchronize()
+    return rs.master - w0
+
+def compare(a, b):
+    rel = ((a - b).norm() / b.norm()).item()
+    worst = 0.0
+    for lo, hi in dp.buckets:
+        n = b[lo:hi].norm().item()
+        if n > 0:
+            worst = max(worst, (a[lo:hi] - b[lo:hi]).norm().item() / n)
+    return rel, worst
+
+d_dp, d_ref = store.master - w0, reference()
+rel, worst = compare(d_dp, d_ref)
+# noise floor: two single-process references differ by the f32-atomic summation order of the
+# split-K weight gradients and fused BN reductions (bf16 activations amplify it)
+rel_n, worst_n = compare(reference(), d_ref)
+print(f"RANK{rank} buckets={len(dp.buckets)} diff={diff} rel={rel:.3e} worst_bucket={worst:.3e} "
+      f"noise rel={rel_n:.3e} worst={worst_n:.3e} losses={losses}", flush=True)
 assert diff == 0.0, diff
-assert rel < 2e-3 and worst < 1e-2, (rel, worst)
+assert rel < max(2e-3, 4 * rel_n) and worst < max(1e-2, 4 * worst_n), (rel, worst, rel_n, worst_n)
 dist.destroy_process_group()
 """
 
