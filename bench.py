@@ -128,8 +128,10 @@ def run(a):
         def step(i):
             img, lab = batch(i)
             if img.device.type == "cpu" and cuda:  # zero-copy ring: pinned host tensors
-                return trainer.step(to_model_input(img, dtype=dtype, device=dev), lab.to(dev, non_blocking=True))
-            return trainer.step(to_model_input(img, dtype=dtype), lab)
+                lab = lab.to(dev, non_blocking=True)
+            # graphed: the input kernel writes straight into the graph's static input buffer
+            x = to_model_input(img, dtype=dtype, device=dev, out=trainer.input_buffer())
+            return trainer.step(x, lab)
 
         if cuda and a.graph and ((world == 1 and not forced) or os.environ.get("TFX_DP_GRAPH", "1") == "1"):
             # the captured step is the same work (forward, backward with the bucketed RCCL

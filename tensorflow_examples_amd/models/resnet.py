@@ -196,11 +196,17 @@ def build_resnet_cifar(device="cuda", depth=50, num_classes=10, dtype=torch.bflo
     return store, model
 
 
-def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16, device=None) -> torch.Tensor:
+def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16, device=None,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[N,32,32,3] images -> [N,32,32,8] normalised NHWC compute tensor (channels 3..7 zero).
     GPU uint8 input: one fused HIP kernel (csrc/kernels/image.hip).  A pinned host uint8 batch with
-    ``device`` = a GPU: the same kernel reads it over the host link (zero-copy input)."""
+    ``device`` = a GPU: the same kernel reads it over the host link (zero-copy input).  ``out``: a bf16
+    GPU tensor of the output shape to write into (e.g. a captured graph's static input buffer)."""
     x = images_nhwc_u8_or_f
+    if out is not None and x.dtype == torch.uint8 and out.is_cuda and out.dtype == torch.bfloat16 and \
+            (x.is_cuda or x.is_pinned()) and _native.use_native_device(out.device):
+        torch.ops.tfx.image_normalize_into(x.contiguous(), list(_MEAN), list(_STD), out)
+        return out
     if x.dtype == torch.uint8 and dtype == torch.bfloat16 and x.device.type == "cuda" and _native.use_native(x):
         return torch.ops.tfx.image_normalize(x.contiguous(), list(_MEAN), list(_STD), IN_CH_PAD)
     if device is not None and torch.device(device).type == "cuda" and x.device.type == "cpu" and \

@@ -51,10 +51,17 @@ class ClassifierTrainer:
             self.opt.apply_gradients(grad_scale=scale)
         return loss.detach()
 
+    def input_buffer(self):
+        """The captured graph's static input tensor (None when eager): a producer may write the next
+        batch into it directly, and :meth:`step` then skips the copy."""
+        return self._static[0] if self.graph is not None else None
+
     def step(self, x, y):
         if self.graph is not None:
-            self._static[0].copy_(x, non_blocking=True)
-            self._static[1].copy_(y, non_blocking=True)
+            if x is not self._static[0]:
+                self._static[0].copy_(x, non_blocking=True)
+            if y is not self._static[1]:
+                self._static[1].copy_(y, non_blocking=True)
             self.graph.replay()
             return self._static[2]
         return self._step(x, y)
