@@ -2,6 +2,10 @@
 #include "igemm_impl.h"
 
 namespace tfx {
-void igemm_dgrad_cls_dense(IgemmArgs& a, hipStream_t s) { launch_shape<KM_DENSE, MN_DENSE>(a, s, FAM_DGRAD_CLS_DENSE); }
-void igemm_dgrad_cls(IgemmArgs& a, hipStream_t s) { launch_shape<KM_DGRAD_DY, MN_DGRAD_W2>(a, s, FAM_DGRAD_CLS); }
+// (+ the fused BN-backward partials: the four class launches add into the same slots, each output pixel
+// belongs to exactly one class -- conv_dgrad_bn at stride 2)
+void igemm_dgrad_cls_dense(IgemmArgs& a, hipStream_t s) {
+  launch_epi<KM_DENSE, MN_DENSE, EPI_BNB>(a, s, FAM_DGRAD_CLS_DENSE);
+}
+void igemm_dgrad_cls(IgemmArgs& a, hipStream_t s) { launch_epi<KM_DGRAD_DY, MN_DGRAD_W2, EPI_BNB>(a, s, FAM_DGRAD_CLS); }
 }  // namespace tfx

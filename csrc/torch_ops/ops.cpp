@@ -150,6 +150,26 @@ int dgrad_setup(tfx::IgemmArgs& a, const ConvGeom& g, const Tensor& dy, const Te
   return tfx::MODE_DGRAD;
 }
 
+// output-parity class (cph, cpw) of a stride-2 data gradient as a dense stride-1 implicit GEMM over
+// its own taps r = r0 + 2 ri, s = s0 + 2 si (see conv_dgrad); rows = the class's sub-grid pixels
+void cls_setup(tfx::IgemmArgs& a, const ConvGeom& g, const Tensor& dy, const Tensor& w, int64_t pad, int cph,
+               int cpw) {
+  const int r0 = (cph + pad) % 2, s0 = (cpw + pad) % 2;
+  const int Rc = (int)(g.R - r0 + 1) / 2, Sc = (int)(g.S - s0 + 1) / 2;
+  const int Hc = (int)(g.H - cph + 1) / 2, Wc = (int)(g.W - cpw + 1) / 2;
+  a.Nb = g.N; a.H = Hc; a.W = Wc; a.C = g.C; a.Ko = g.Ko; a.R = Rc; a.S = Sc; a.P = g.P; a.Q = g.Q;
+  a.sh = a.sw = 1; a.sh_log2 = a.sw_log2 = 0; a.dh = a.dw = 1;
+  a.ph = (cph + pad - r0) / 2; a.pw = (cpw + pad - s0) / 2;  // p = y + ph - ri
+  a.fd_C = tfx::FastDiv(g.C); a.fd_S = tfx::FastDiv(Sc); a.fd_Ko = tfx::FastDiv(g.Ko);
+  a.fd_PQ = tfx::FastDiv(g.P * g.Q); a.fd_Q = tfx::FastDiv(g.Q);
+  a.cls = 1; a.cph = cph; a.cpw = cpw; a.cr0 = r0; a.cs0 = s0; a.wR = g.R; a.wS = g.S;
+  a.out_H = g.H; a.out_W = g.W;
+  a.fd_cHW = tfx::FastDiv(Hc * Wc); a.fd_cW = tfx::FastDiv(Wc);
+  a.A = bf(dy); a.B = bf(w);
+  a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
+  a.M = g.N * Hc * Wc; a.N = g.C; a.K = Rc * Sc * g.Ko; a.ldc = g.C;
+}
+
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stride, int64_t pad, int64_t dil,
                   optional<Tensor> addend, optional<Tensor> addend_mask, bool addend_s2,
                   optional<Tensor> wflip) {
@@ -202,17 +222,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
         const int Hc = (int)(g.H - cph + 1) / 2, Wc = (int)(g.W - cpw + 1) / 2;
         if (Rc <= 0 || Sc <= 0 || Hc <= 0 || Wc <= 0) continue;  // dx keeps addend / zeros there
         tfx::IgemmArgs a;
-        a.Nb = g.N; a.H = Hc; a.W = Wc; a.C = g.C; a.Ko = g.Ko; a.R = Rc; a.S = Sc; a.P = g.P; a.Q = g.Q;
-        a.sh = a.sw = 1; a.sh_log2 = a.sw_log2 = 0; a.dh = a.dw = 1;
-        a.ph = (cph + pad - r0) / 2; a.pw = (cpw + pad - s0) / 2;  // p = y + ph - ri
-        a.fd_C = tfx::FastDiv(g.C); a.fd_S = tfx::FastDiv(Sc); a.fd_Ko = tfx::FastDiv(g.Ko);
-        a.fd_PQ = tfx::FastDiv(g.P * g.Q); a.fd_Q = tfx::FastDiv(g.Q);
-        a.cls = 1; a.cph = cph; a.cpw = cpw; a.cr0 = r0; a.cs0 = s0; a.wR = g.R; a.wS = g.S;
-        a.out_H = g.H; a.out_W = g.W;
-        a.fd_cHW = tfx::FastDiv(Hc * Wc); a.fd_cW = tfx::FastDiv(Wc);
-        a.A = bf(dy); a.B = bf(w); a.Cp = dx.data_ptr();
-        a.a_bytes = dy.nbytes(); a.b_bytes = w.nbytes();
-        a.M = g.N * Hc * Wc; a.N = g.C; a.K = Rc * Sc * g.Ko; a.ldc = g.C;
+        cls_setup(a, g, dy, w, pad, cph, cpw);
+        a.Cp = dx.data_ptr();
         a.out_mode = tfx::OUT_BF16;
         if (acc) a.addend = bf(*addend);
         tfx::igemm_launch(a, tfx::MODE_DGRAD_CLS, cur_stream());
@@ -293,7 +304,8 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
                                          optional<Tensor> addend_mask, bool reduce, bool addend_s2,
                                          optional<Tensor> wflip) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
-  TORCH_CHECK(stride == 1, "conv_dgrad_bn: stride-1 convs only (stride 2 runs per parity class)");
+  TORCH_CHECK(stride == 1 || (stride == 2 && dil == 1 && dgrad_classes_enabled()),
+              "conv_dgrad_bn: stride-1 convs, or stride 2 by output-parity class");
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
   CHECK_BF16(bn_x); CHECK_CONTIG(bn_x); CHECK_F32(bn_save);
@@ -310,6 +322,39 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   auto dx = (acc && !amask && !addend_s2) ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
   // reduce = false: the partials stay in the slots for bn_bwd_slots (no red, no slot reduce)
   auto red = reduce ? at::empty({2 * g.C}, dy.options().dtype(at::kFloat)) : Tensor();
+  const uint8_t* bmask = nullptr;
+  if (bn_mask.has_value() && bn_mask->defined()) {
+    TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == bn_x.numel(), "bn_mask size");
+    bmask = bn_mask->data_ptr<uint8_t>();
+  }
+  if (stride == 2) {
+    // the four output-parity classes (conv_dgrad's stride-2 path), each with the BN-backward
+    // epilogue: every pixel of dx is written by exactly one class, so their per-column partials
+    // add up in the slots to the full reduction; one slot reduce after the last class
+    TORCH_CHECK(!acc && !amask && !addend_s2, "conv_dgrad_bn stride 2: no addend");
+    for (int cph = 0; cph < 2; ++cph)
+      for (int cpw = 0; cpw < 2; ++cpw)
+        TORCH_CHECK((g.R - (cph + pad) % 2 + 1) / 2 > 0 && (g.S - (cpw + pad) % 2 + 1) / 2 > 0 &&
+                        (g.H - cph + 1) / 2 > 0 && (g.W - cpw + 1) / 2 > 0,
+                    "conv_dgrad_bn stride 2: every parity class must have taps and pixels");
+    bn_counters(ws, g.C);  // workspace size check
+    for (int cph = 0; cph < 2; ++cph) {
+      for (int cpw = 0; cpw < 2; ++cpw) {
+        tfx::IgemmArgs a;
+        cls_setup(a, g, dy, w, pad, cph, cpw);
+        a.Cp = dx.data_ptr();
+        a.out_mode = tfx::OUT_BF16;
+        a.bnb_x = bf(bn_x); a.bnb_save = bn_save.data_ptr<float>(); a.bnb_mask = bmask;
+        a.bnb_relu = relu ? 1 : 0;
+        a.bnb_slots = ws.data_ptr<float>();
+        a.bn_final = 0;
+        tfx::igemm_launch(a, tfx::MODE_DGRAD_CLS, cur_stream());
+      }
+    }
+    if (reduce)
+      tfx::bn_slot_reduce(ws.data_ptr<float>(), g.C, red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), cur_stream());
+    return {dx, red};
+  }
   tfx::IgemmArgs a;
   const int mode = dgrad_setup(a, g, dy, w, wflip, stride, pad, dil);
   a.Cp = dx.data_ptr();
@@ -318,10 +363,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   if (addend_s2) set_addend_s2(a, *addend, g.N, g.H, g.W, g.C);
   a.addend_mask = amask;
   a.bnb_x = bf(bn_x); a.bnb_save = bn_save.data_ptr<float>();
-  if (bn_mask.has_value() && bn_mask->defined()) {
-    TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == bn_x.numel(), "bn_mask size");
-    a.bnb_mask = bn_mask->data_ptr<uint8_t>();
-  }
+  a.bnb_mask = bmask;
   a.bnb_relu = relu ? 1 : 0;
   a.bnb_slots = ws.data_ptr<float>();
   a.bn_cnt = bn_counters(ws, g.C);

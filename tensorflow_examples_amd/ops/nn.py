@@ -121,6 +121,13 @@ _BNB_MAX_BYTES = int(os.environ.get("TFX_BNB_MAX_MB", "256")) << 20
 _DGRAD_FLIP = os.environ.get("TFX_DGRAD_FLIP", "1") != "0"
 
 
+# opt-in (TFX_S2_BNB=1): fuse the BN-backward reduction into stride-2 (parity-class) data gradients
+# too.  Measured a wash in the step (8.152 vs 8.139 ms/step, profiles/r02_s2bnb): the four class
+# GEMMs' epilogue cost matches the reduce kernel it removes.  (The C++ side runs stride-2 data
+# gradients per class unless TFX_DGRAD_CLASSES=0.)
+_S2_BNB = os.environ.get("TFX_S2_BNB", "0") == "1" and os.environ.get("TFX_DGRAD_CLASSES", "1") != "0"
+
+
 def _flip_ok(w, stride, pad, dil):
     sh = w.shape
     return _DGRAD_FLIP and stride == 1 and pad == 1 and dil == 1 and len(sh) == 4 and sh[1] == 3 and sh[2] == 3 \
@@ -177,7 +184,11 @@ class _Conv2d(torch.autograd.Function):
             dx = None
             if need_dx:
                 bnb = ctx.bnb
-                if bnb is not None and stride == 1 and (sink is None or sink.mode == "consume") \
+                # stride 2: the data gradient runs per output-parity class, each class launch with
+                # the same BN-backward epilogue (no sink there: a stride-2 conv2 is its input's sole
+                # consumer)
+                s2_ok = stride == 2 and dil == 1 and sink is None and _S2_BNB
+                if bnb is not None and (stride == 1 or s2_ok) and (sink is None or sink.mode == "consume") \
                         and x.numel() * x.element_size() <= _BNB_MAX_BYTES:
                     # dx is the complete gradient of the BN output x: the epilogue also reduces
                     # that BN's backward (sum g', sum g' xhat, dgamma, dbeta) -- see BNBackwardFusion
