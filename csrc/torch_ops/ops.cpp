@@ -1257,6 +1257,23 @@ Tensor image_normalize(Tensor x, std::vector<double> mean, std::vector<double> s
 // straight over the host link (zero-copy input: no H2D staging copy, no copy stream, no device
 // staging buffer).  The caller keeps the pinned buffer unmodified until the kernel has run
 // (data/pipeline.py PinnedRing(zero_copy=True) orders that with an event per slot).
+// End a capture left open on `stream` (a side stream forked into a HIP-graph capture that failed
+// before the join): its partial graph is discarded.  Returns true if a capture was open.  While any
+// stream of a thread stays capturing, that thread cannot run synchronous work at all.
+bool end_stream_capture(int64_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st == hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return false;
+  }
+  hipGraph_t g = nullptr;
+  (void)hipStreamEndCapture(s, &g);
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  return true;
+}
+
 void image_normalize_into(Tensor x, std::vector<double> mean, std::vector<double> stdv, Tensor out) {
   CHECK_CONTIG(x); CHECK_DEV(out); CHECK_CONTIG(out); CHECK_BF16(out);
   TORCH_CHECK(x.scalar_type() == at::kByte, "image_normalize_into: uint8 images");
@@ -1287,6 +1304,7 @@ void image_normalize_into(Tensor x, std::vector<double> mean, std::vector<double
 TORCH_LIBRARY(tfx, m) {
   m.def("image_normalize", &image_normalize);
   m.def("image_normalize_into", &image_normalize_into);
+  m.def("end_stream_capture", &end_stream_capture);
   m.def("philox_fill", &philox_fill);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

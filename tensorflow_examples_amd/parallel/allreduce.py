@@ -139,6 +139,12 @@ class GradAllReduce:
         self._launched[b] = True
         lo, hi = self.buckets[b]
         view = self.store.grad[lo:hi]
+        if view.is_cuda and torch.cuda.is_current_stream_capturing() and \
+                dist.get_backend(self.group) != dist.Backend.NCCL:
+            # only RCCL collectives are stream-ordered device work a HIP graph can record; refuse
+            # before forking the launch stream (a forked, never-joined stream would stay capturing)
+            raise RuntimeError("HIP graph capture of the DP step needs the nccl (RCCL) backend, not %s"
+                               % dist.get_backend(self.group))
         op = dist.ReduceOp.SUM if self.premul is None else dist._make_nccl_premul_sum(float(self.premul))
         # a bucket's gradients come from the compute stream AND the side stream of the weight
         # gradients (ops/nn.py): issue the collective from a launch stream that waits on both, so it

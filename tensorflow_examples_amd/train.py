@@ -13,6 +13,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
+from .ops import _native
 from .optim import Optimizer
 from .parallel.allreduce import GradAllReduce
 from .utils import trace
@@ -94,6 +95,12 @@ class ClassifierTrainer:
             # Reset it so the eager fallback reduces every bucket exactly once.
             self.graph, self._static = None, None
             if self.dp is not None:
+                # a side stream forked into the failed capture and never joined stays capturing (and
+                # then blocks every synchronous call of this thread): end it, drop the stream
+                ls = getattr(self.dp, "_launch_stream", None)
+                if ls is not None and _native.use_native_device(ls.device):
+                    torch.ops.tfx.end_stream_capture(ls.cuda_stream)
+                self.dp._launch_stream = None
                 self.dp.reset()
             raise
         self.graph = g

@@ -37,7 +37,13 @@ def test_dp_capture_failure_falls_back_to_eager_on_every_rank():
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    assert all(p.returncode == 0 for p in procs), [o[1][-3000:] for o in outs]
+    if any(p.returncode != 0 for p in procs):
+        log = os.path.join(ROOT, "gpurun_out", "dp_fallback_stderr.log")
+        if os.path.isdir(os.path.dirname(log)):
+            with open(log, "w") as f:
+                for r, o in enumerate(outs):
+                    f.write("==== rank %d rc=%s\n%s\n%s\n" % (r, procs[r].returncode, o[0], o[1]))
+    assert all(p.returncode == 0 for p in procs), [o[1][-6000:] for o in outs]
     rec = json.loads([ln for ln in outs[0][0].splitlines() if ln.startswith("{")][0])
     assert rec["n_gpus"] == 2 and rec["config"]["backend"] == "gloo"
     assert rec["config"]["hip_graph"] is False
