@@ -216,6 +216,14 @@ for s in $STEPS; do
           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_dp$v" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 > gpurun_out/prof_dp$v.log 2>&1
         rc=$?; echo "prof dp graph=$v rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/prof_dp$v.log; exit $rc; }
       done ;;
+    retune)
+      timeout -k 10 1000 python scripts/tune_convs.py --passes fwd,dgrad --merge tensorflow_examples_amd/tune/igemm_gfx950.json --out gpurun_out/igemm_gfx950.json --report gpurun_out/tune_report_fd.json > gpurun_out/tune_fd.log 2>&1
+      rc=$?; echo "tune rc=$rc"; tail -40 gpurun_out/tune_fd.log; [ $rc -eq 0 ] || exit $rc
+      for i in 1 2 3; do
+        timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_rt0_$i.log 2>&1 || exit 1
+        TFX_TUNE_FILE=gpurun_out/igemm_gfx950.json timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_rt1_$i.log 2>&1 || exit 1
+      done
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_rt*.log ;;
     tunebig)
       timeout -k 10 900 python scripts/tune_convs.py --passes wgrad --merge tensorflow_examples_amd/tune/igemm_gfx950.json --out gpurun_out/igemm_gfx950.json --report gpurun_out/tune_report_big.json > gpurun_out/tune_big.log 2>&1
       rc=$?; echo "tune rc=$rc"; tail -25 gpurun_out/tune_big.log; [ $rc -eq 0 ] || exit $rc
