@@ -109,6 +109,46 @@ __global__ void __launch_bounds__(256) accuracy_kernel(const TIN* __restrict__ z
 }
 
 // Global average pool NHWC: x [N][HW][C] bf16 -> y [N][C] (bf16 or f32)
+// 8 channels per thread: 16-byte loads over the HW pixels, one 16-byte (bf16) / 2x16-byte (f32) store
+__global__ void __launch_bounds__(256) gap_fwd_vec_kernel(const uint16_t* __restrict__ x, int N, int HW, int C,
+                                                          uint16_t* __restrict__ y16, float* __restrict__ y32) {
+  const int C8 = C >> 3;
+  const int v = blockIdx.x * 256 + threadIdx.x;  // (n, c8)
+  if (v >= N * C8) return;
+  const int n = v / C8, c = (v - n * C8) * 8;
+  const U4* xp = reinterpret_cast<const U4*>(x + (int64_t)n * HW * C + c);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < HW; ++i) {
+    float f[8];
+    unpack8(xp[(int64_t)i * C8], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] += f[k];
+  }
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] *= inv;
+  if (y16) reinterpret_cast<U4*>(y16)[v] = pack8(s);
+  if (y32) {
+    float4* o = reinterpret_cast<float4*>(y32 + (int64_t)n * C + c);
+    o[0] = make_float4(s[0], s[1], s[2], s[3]);
+    o[1] = make_float4(s[4], s[5], s[6], s[7]);
+  }
+}
+
+// dx[n][p][c] = dy[n][c] / HW, 8 channels per thread (16-byte stores), 32-bit index math
+template <typename TG>
+__global__ void __launch_bounds__(256) gap_bwd_vec_kernel(const TG* __restrict__ dy, int nvec, int HWC8, int C8,
+                                                          float inv, uint16_t* __restrict__ dx) {
+  for (int v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+    const int n = v / HWC8, c8 = (v - n * HWC8) % C8;
+    const TG* g = dy + ((int64_t)n * C8 + c8) * 8;
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = ld(g, k) * inv;
+    reinterpret_cast<U4*>(dx)[v] = pack8(f);
+  }
+}
+
 __global__ void __launch_bounds__(256) gap_fwd_kernel(const uint16_t* __restrict__ x, int N, int HW, int C,
                                                       uint16_t* __restrict__ y16, float* __restrict__ y32) {
   const int n = blockIdx.y;
@@ -157,12 +197,27 @@ void accuracy_count(const void* z, bool z_bf16, int B, int C, const int64_t* lab
 }
 
 void gap_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y16, float* y32, hipStream_t s) {
+  if (C % 8 == 0 && (int64_t)N * HW * C < (1ll << 31)) {
+    gap_fwd_vec_kernel<<<(N * (C / 8) + 255) / 256, 256, 0, s>>>(x, N, HW, C, y16, y32);
+    return;
+  }
   dim3 grid((C + 255) / 256, N);
   gap_fwd_kernel<<<grid, 256, 0, s>>>(x, N, HW, C, y16, y32);
 }
 
 void gap_bwd(const void* dy, bool dy_bf16, int N, int HW, int C, uint16_t* dx, hipStream_t s) {
   const int64_t total = (int64_t)N * HW * C;
+  if (C % 8 == 0 && total < (1ll << 31)) {
+    const int nvec = (int)(total / 8);
+    const int gv = std::min((nvec + 255) / 256, 8192);
+    if (dy_bf16)
+      gap_bwd_vec_kernel<uint16_t><<<gv, 256, 0, s>>>((const uint16_t*)dy, nvec, HW * (C / 8), C / 8,
+                                                      1.f / (float)HW, dx);
+    else
+      gap_bwd_vec_kernel<float><<<gv, 256, 0, s>>>((const float*)dy, nvec, HW * (C / 8), C / 8, 1.f / (float)HW,
+                                                   dx);
+    return;
+  }
   int g = (int)std::min<int64_t>((total + 1023) / 1024, 4096);
   if (dy_bf16)
     gap_bwd_kernel<uint16_t><<<g, 256, 0, s>>>((const uint16_t*)dy, N, HW, C, dx);

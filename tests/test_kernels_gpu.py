@@ -205,13 +205,18 @@ def test_softmax_xent(gpu, naive, dense):
     assert cnt.item() == (z.argmax(1) == lab).sum().item()
 
 
-def test_global_avg_pool(gpu):
-    x = _bf(torch.randn(4, 4, 4, 2048, device=gpu))
+@pytest.mark.parametrize("shape", [(4, 4, 4, 2048), (256, 4, 4, 2048), (3, 5, 3, 12), (2, 8, 8, 64)])
+def test_global_avg_pool(gpu, shape):
+    """8-channel vector kernels (C % 8 == 0) and the scalar fallback, bf16 / f32 in and out."""
+    N, H, W, C = shape
+    x = _bf(torch.randn(N, H, W, C, device=gpu))
     y = torch.ops.tfx.gap_fwd(x, False)
-    assert _rel(y, x.float().mean((1, 2))) < 1e-2
-    g = _bf(torch.randn(4, 2048, device=gpu))
-    dx = torch.ops.tfx.gap_bwd(g, 4, 4)
-    assert _rel(dx, (g.float() / 16)[:, None, None, :].expand(4, 4, 4, 2048)) < 1e-2
+    assert y.dtype == torch.bfloat16 and _rel(y, x.float().mean((1, 2))) < 1e-2
+    y32 = torch.ops.tfx.gap_fwd(x, True)
+    assert y32.dtype == torch.float32 and _rel(y32, x.float().mean((1, 2))) < 1e-5
+    for g in (_bf(torch.randn(N, C, device=gpu)), torch.randn(N, C, device=gpu)):
+        dx = torch.ops.tfx.gap_bwd(g, H, W)
+        assert _rel(dx, (g.float() / (H * W))[:, None, None, :].expand(N, H, W, C)) < 1e-2
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
