@@ -53,8 +53,8 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="capture the whole step in a HIP graph and replay it (default on; for N>1 the bucketed "
-                         "RCCL all-reduces are captured too -- measured on a 1-rank RCCL group: 8.16 ms graph vs "
-                         "9.03 ms eager, profiles/r02_final/dp_graph_ab.txt; TFX_DP_GRAPH=0 keeps N>1 eager)")
+                         "RCCL all-reduces are captured too -- measured on a 1-rank RCCL group: 8.09-8.16 ms graph vs "
+                         "8.27-9.03 ms eager, profiles/r02_final/dp_graph_ab.txt; TFX_DP_GRAPH=0 keeps N>1 eager)")
     ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager step launches")
     ap.add_argument("--host-input", nargs="?", const="zerocopy", default=None, choices=["copy", "zerocopy"],
                     help="batches live in pinned host memory: 'zerocopy' (default when given) = the input kernel "
@@ -97,6 +97,10 @@ def run(a):
     if "RANK" in os.environ or a.gpus > 1:
         verify_world(a.gpus if not forced else 1, dev)
     rank = dist.get_rank() if dist.is_initialized() else 0
+    # host-side control collectives (capture agreement, timing barriers, elapsed-time MAX) run on a
+    # gloo group: the RCCL communicator then carries only the gradient all-reduces, and no eager RCCL
+    # call is ever interleaved with replays of a graph that holds captured RCCL collectives
+    ctl = dist.new_group(backend="gloo") if dist.is_initialized() else None
     torch.manual_seed(1234 + rank)
     host = synthetic_batches(a.nbatches, a.batch, seed=1000 + rank)
     dtype = torch.bfloat16 if cuda else torch.float32
@@ -146,8 +150,8 @@ def run(a):
             if world > 1 or forced:
                 # every rank replays its graph or none does: a rank left eager would issue its
                 # collectives in a different order from the graph replays of the others
-                agree = torch.tensor([1 if graphed else 0], dtype=torch.int32, device=dev)
-                dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+                agree = torch.tensor([1 if graphed else 0], dtype=torch.int32)
+                dist.all_reduce(agree, op=dist.ReduceOp.MIN, group=ctl)
                 graphed = bool(agree.item())
             if not graphed:
                 if rank == 0:
@@ -181,19 +185,19 @@ def run(a):
         loss = step(i)
     sync()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=ctl)
     sync()
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(i)
     sync()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=ctl)
     sync()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=ctl)
     elapsed = float(el.item())
     final_loss = float(loss.float().item())
     images = a.batch * world * a.steps

@@ -49,6 +49,9 @@ def main(_):
     dev = init_distributed(device="cuda" if torch.cuda.is_available() else "cpu")
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
+    # host-side control collectives on gloo: after the graph is captured, the RCCL communicator only
+    # ever runs the captured gradient all-reduces (no eager RCCL call between replays)
+    ctl = dist.new_group(backend="gloo") if dist.is_initialized() else None
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     xtr, ytr, xte, yte, synth = load_cifar10(FLAGS.data_dir or None, synthetic_train=FLAGS.synthetic_train)
     if rank == 0:
@@ -83,8 +86,8 @@ def main(_):
                     print("rank %d: hip graph capture failed (%s)" % (rank, e), file=sys.stderr)
                     ok = False
                 if world > 1:  # every rank replays or none does (collective order must match)
-                    agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-                    dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+                    agree = torch.tensor([1 if ok else 0], dtype=torch.int32)
+                    dist.all_reduce(agree, op=dist.ReduceOp.MIN, group=ctl)
                     ok = bool(agree.item())
                 if not ok:
                     trainer.graph = None
@@ -102,9 +105,9 @@ def main(_):
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.time() - t0
-    ips = torch.tensor([seen / dt], dtype=torch.float64, device=dev)
+    ips = torch.tensor([seen / dt], dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(ips)
+        dist.all_reduce(ips, group=ctl)
     if FLAGS.eval_examples:
         xte, yte = xte[:FLAGS.eval_examples], yte[:FLAGS.eval_examples]
     correct = 0.0
