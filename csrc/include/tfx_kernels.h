@@ -102,6 +102,15 @@ struct IgemmArgs {
   float* bnb_red = nullptr;
   float* bnb_dgamma = nullptr;
   float* bnb_dbeta = nullptr;
+  // optional tail blocks (weight-gradient launches): reduce ANOTHER BN layer's backward slots
+  // ([NSLOT][2][sr_C], filled by an earlier data-gradient epilogue) into sr_red = [sum g' | sum g'
+  // xhat] and dgamma / dbeta += -- bn_slot_reduce folded into this launch (16 channels per block,
+  // after the GEMM's blocks: they fill CUs the GEMM's tail leaves idle).  sr_C == 0: none.
+  float* sr_slots = nullptr;
+  float* sr_red = nullptr;
+  float* sr_dgamma = nullptr;
+  float* sr_dbeta = nullptr;
+  int sr_C = 0;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;
 };

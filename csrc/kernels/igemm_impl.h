@@ -461,6 +461,52 @@ __device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n
 // what keeps enough loads and stores in flight.
 // EPI: compile-time epilogue extras (so the plain GEMM / wgrad kernels carry none of their code or
 // registers): EPI_STATS = fused BN statistics (+ last-arriver finalize) of a conv forward,
+// bn_slot_reduce_kernel's math for channels [16 sb, 16 sb + 16) of the sr_* layer, 256 threads:
+// 16 slot-lanes x 4 slots each per channel, all loads in flight before the re-zeroing stores, then an
+// LDS reduction over the 16 slot-lanes.  dbeta / dgamma are loaded before the slot round trip.
+__device__ __forceinline__ void sr_block(const IgemmArgs& a, int sb, float* red2) {
+  const int C = a.sr_C, tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = sb * 16 + tx;
+  const bool own = ty == 0 && c < C;
+  float db = 0.f, dg = 0.f;
+  if (own) {
+    if (a.sr_dbeta) db = a.sr_dbeta[c];
+    if (a.sr_dgamma) dg = a.sr_dgamma[c];
+  }
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    float vs[NSLOT / 16], vq[NSLOT / 16];
+#pragma unroll
+    for (int i = 0; i < NSLOT / 16; ++i) {
+      const float* p = a.sr_slots + (size_t)(ty + 16 * i) * 2 * C;
+      vs[i] = p[c];
+      vq[i] = p[C + c];
+    }
+#pragma unroll
+    for (int i = 0; i < NSLOT / 16; ++i) {
+      s += vs[i];
+      q += vq[i];
+      float* p = a.sr_slots + (size_t)(ty + 16 * i) * 2 * C;
+      p[c] = 0.f;  // the workspace is zero again for its next use
+      p[C + c] = 0.f;
+    }
+  }
+  red2[threadIdx.x] = s;
+  red2[256 + threadIdx.x] = q;
+  __syncthreads();  // the waves still running: threads >= 256 of an 8-wave block have exited
+  if (own) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      s += red2[threadIdx.x + 16 * k];
+      q += red2[256 + threadIdx.x + 16 * k];
+    }
+    a.sr_red[c] = s;
+    a.sr_red[C + c] = q;
+    if (a.sr_dbeta) a.sr_dbeta[c] = db + s;
+    if (a.sr_dgamma) a.sr_dgamma[c] = dg + q;
+  }
+}
+
 // EPI_BNB = fused BN-backward partials (+ last-arriver reduce) of a conv data gradient.
 // KS = 2: in-block split-K for the f32-atomic weight gradients.  512 threads = two 4-wave groups
 // on the SAME output tile, each running the pipelined K loop over half of the block's k-tiles in its
@@ -536,7 +582,16 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   };
   const int t = threadIdx.x & 255, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
 
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  // tail blocks past the GEMM's grid: another BN layer's backward slot reduction (IgemmArgs sr_*)
+  const int gemm_blocks = (int)gridDim.x - (a.sr_C ? (a.sr_C + 15) / 16 : 0);
+  if ((int)blockIdx.x >= gemm_blocks) {
+    if (threadIdx.x < 256) {
+      float* scratch = reinterpret_cast<float*>(GL ? ga0 : smem_all);  // >= 2 KB, unused by this block
+      sr_block(a, (int)blockIdx.x - gemm_blocks, scratch);
+    }
+    return;
+  }
+  const int bid = xcd_remap(blockIdx.x, gemm_blocks);
   const int tiles_mn = a.tiles_m * a.tiles_n;
   const int split = bid / tiles_mn;
   const int rem = bid - split * tiles_mn;
@@ -1277,8 +1332,8 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
     a.kps += a.kps & 1;  // even k-tiles per split: no zero step in the loop
   }
   splits = (nkt + a.kps - 1) / a.kps;
-  const int grid = tiles * splits;
-  if (grid == 0) return;
+  if (tiles * splits == 0) return;
+  const int grid = tiles * splits + (a.sr_C ? (a.sr_C + 15) / 16 : 0);  // + slot-reduce tail blocks
   // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
   constexpr int STAGE_B = (BM + BN) * BKT * 2;

@@ -377,11 +377,16 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
 }
 
 // dW (f32, [Ko][R][S][C]) = or += conv weight gradient
-void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t dil, bool accumulate) {
+void conv_wgrad_impl(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t dil, bool accumulate,
+                     const tfx::IgemmArgs* sr) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   auto g = geom(x.sizes().vec(), dw.sizes().vec(), stride, pad, dil);
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
   auto a = conv_args(g, stride, pad, dil);
+  if (sr) {
+    a.sr_slots = sr->sr_slots; a.sr_red = sr->sr_red; a.sr_dgamma = sr->sr_dgamma; a.sr_dbeta = sr->sr_dbeta;
+    a.sr_C = sr->sr_C;
+  }
   const int64_t RSC = g.R * g.S * g.C;
   a.K = g.N * g.P * g.Q;
   a.out_mode = tfx::OUT_F32_ATOMIC;
@@ -398,6 +403,26 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int
     a.M = g.Ko; a.N = RSC; a.lda = g.Ko;
     tfx::igemm_launch(a, tfx::MODE_WGRAD, cur_stream());
   }
+}
+
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t dil, bool accumulate) {
+  conv_wgrad_impl(dy, x, dw, stride, pad, dil, accumulate, nullptr);
+}
+
+// conv_wgrad + the backward slot reduction of the BN that produced x (its partials left in `slots` by
+// conv_dgrad_bn(reduce=False)), in ONE launch: the reduction runs as tail blocks of the weight-gradient
+// grid (no separate bn_slot_reduce launch).  Returns red = [sum g' | sum g' xhat]; dgamma / dbeta +=.
+Tensor conv_wgrad_sr(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t dil, bool accumulate,
+                     Tensor slots, optional<Tensor> dgamma, optional<Tensor> dbeta) {
+  CHECK_DEV(slots); CHECK_F32(slots); CHECK_CONTIG(slots);
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(slots.numel() >= tfx::NSLOT * 2 * C, "conv_wgrad_sr: slot workspace too small");
+  auto red = at::empty({2 * C}, slots.options());
+  tfx::IgemmArgs sr;
+  sr.sr_slots = slots.data_ptr<float>(); sr.sr_red = red.data_ptr<float>();
+  sr.sr_dgamma = fpm(dgamma); sr.sr_dbeta = fpm(dbeta); sr.sr_C = (int)C;
+  conv_wgrad_impl(dy, x, dw, stride, pad, dil, accumulate, &sr);
+  return red;
 }
 
 // ------------------------------------------------------------------ dense bf16 GEMM
@@ -1331,6 +1356,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
         "Tensor? addend_mask=None, bool addend_s2=False, Tensor? wflip=None) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad_sr", &conv_wgrad_sr);
   m.def("gemm", &gemm);
   m.def("gemm_into", &gemm_into);
   m.def("sgemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, int act, bool split=False) -> Tensor", &sgemm);

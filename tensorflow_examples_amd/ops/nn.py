@@ -121,6 +121,9 @@ _BNB_MAX_BYTES = int(os.environ.get("TFX_BNB_MAX_MB", "256")) << 20
 _DGRAD_FLIP = os.environ.get("TFX_DGRAD_FLIP", "1") != "0"
 
 
+# A/B switch: the BN-backward slot reduction of a fused data gradient runs as tail blocks of the same
+# conv's weight-gradient launch (conv_wgrad_sr) instead of its own bn_slot_reduce launch
+_SR_FUSE = os.environ.get("TFX_SR_FUSE", "1") != "0"
 # opt-in (TFX_S2_BNB=1): fuse the BN-backward reduction into stride-2 (parity-class) data gradients
 # too.  Measured a wash in the step (8.152 vs 8.139 ms/step, profiles/r02_s2bnb): the four class
 # GEMMs' epilogue cost matches the reduce kernel it removes.  (The C++ side runs stride-2 data
@@ -182,6 +185,7 @@ class _Conv2d(torch.autograd.Function):
             gy = gy.contiguous()
             sink = ctx.sink
             dx = None
+            sr_bnb = None
             if need_dx:
                 bnb = ctx.bnb
                 # stride 2: the data gradient runs per output-parity class, each class launch with
@@ -204,6 +208,13 @@ class _Conv2d(torch.autograd.Function):
                             gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
                             sb, None, None, amask, False, s2, _wflip(w, stride, pad, dil))
                         bnb.red = BNBackwardFusion.IN_SLOTS
+                    elif _SR_FUSE and w.trainable and wgrad_side_stream(gy.device) is None:
+                        # partials stay in the slots; the weight-gradient launch below reduces them in
+                        # tail blocks of its grid (conv_wgrad_sr): no bn_slot_reduce launch
+                        dx, _ = torch.ops.tfx.conv_dgrad_bn(
+                            gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
+                            bnb.ws, None, None, amask, False, s2, _wflip(w, stride, pad, dil))
+                        sr_bnb = bnb
                     else:
                         dx, bnb.red = torch.ops.tfx.conv_dgrad_bn(
                             gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
@@ -236,6 +247,10 @@ class _Conv2d(torch.autograd.Function):
                         _grad_ready(w)
                     gy.record_stream(ss)
                     x.record_stream(ss)
+                elif sr_bnb is not None:
+                    sr_bnb.red = torch.ops.tfx.conv_wgrad_sr(gy, x, w.grad, stride, pad, dil, True, sr_bnb.ws,
+                                                             sr_bnb.dgamma, sr_bnb.dbeta)
+                    _grad_ready(w)
                 else:
                     torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
                     _grad_ready(w)

@@ -463,3 +463,35 @@ def test_conv_dgrad_bn_stride2_classes(gpu, shape, variant):
     assert _rel(dg, dgr) < 1e-3 and _rel(db, dbr) < 1e-3
     bx, _ = torch.ops.tfx.bn_bwd_apply(dx, xb, None, save, red, relu, None)
     assert _rel(bx, ref_bx) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(256, 32, 32, 64, 64, 1, 1), (256, 32, 32, 64, 64, 3, 1),
+                                   (256, 16, 16, 128, 128, 3, 1), (256, 8, 8, 1024, 256, 1, 1),
+                                   (256, 4, 4, 512, 2048, 1, 1), (256, 16, 16, 256, 256, 3, 2), (4, 5, 5, 24, 40, 3, 1)])
+def test_conv_wgrad_slot_reduce_tail_blocks(gpu, shape):
+    """conv_wgrad_sr: the weight gradient plus, in tail blocks of the same grid, another BN layer's
+    backward slot reduction (red = slot sums, dgamma / dbeta +=, slots re-zeroed) -- every wgrad
+    family (dense pair, im2col, transposed) at production shapes, vs conv_wgrad + a torch reduction."""
+    N, H, W, C, K, R, st = shape
+    pad = R // 2
+    torch.manual_seed(23)
+    x = _bf(torch.randn(N, H, W, C, device=gpu))
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    gy = _bf(torch.randn(N, P, Q, K, device=gpu))
+    dw_ref = torch.zeros(K, R, R, C, device=gpu)
+    torch.ops.tfx.conv_wgrad(gy, x, dw_ref, st, pad, 1, True)
+    slots = torch.zeros(64 * 2 * C + 64, device=gpu)
+    slots[: 64 * 2 * C] = torch.randn(64 * 2 * C, device=gpu)
+    red_ref = slots[: 64 * 2 * C].view(64, 2, C).sum(0).reshape(-1)
+    dg, db = torch.full((C,), 0.5, device=gpu), torch.full((C,), -0.25, device=gpu)
+    dw = torch.zeros(K, R, R, C, device=gpu)
+    red = torch.ops.tfx.conv_wgrad_sr(gy, x, dw, st, pad, 1, True, slots, dg, db)
+    torch.cuda.synchronize()
+    assert _rel(dw, dw_ref) < 1e-5
+    assert torch.allclose(red, red_ref, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(db, red_ref[:C] - 0.25, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(dg, red_ref[C:] + 0.5, rtol=1e-5, atol=1e-4)
+    assert slots.abs().max().item() == 0.0, "slots not re-zeroed"
+    red2 = torch.ops.tfx.conv_wgrad_sr(gy, x, dw, st, pad, 1, True, slots, None, None)  # no parameter grads
+    torch.cuda.synchronize()
+    assert red2.abs().max().item() == 0.0 and _rel(dw, 2 * dw_ref) < 1e-5
