@@ -111,6 +111,12 @@ struct IgemmArgs {
   float* sr_dgamma = nullptr;
   float* sr_dbeta = nullptr;
   int sr_C = 0;
+  // a second such reduction in the same tail (blocks after the first one's)
+  float* sr2_slots = nullptr;
+  float* sr2_red = nullptr;
+  float* sr2_dgamma = nullptr;
+  float* sr2_dbeta = nullptr;
+  int sr2_C = 0;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;
 };

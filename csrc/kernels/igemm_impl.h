@@ -464,21 +464,22 @@ __device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n
 // bn_slot_reduce_kernel's math for channels [16 sb, 16 sb + 16) of the sr_* layer, 256 threads:
 // 16 slot-lanes x 4 slots each per channel, all loads in flight before the re-zeroing stores, then an
 // LDS reduction over the 16 slot-lanes.  dbeta / dgamma are loaded before the slot round trip.
-__device__ __forceinline__ void sr_block(const IgemmArgs& a, int sb, float* red2) {
-  const int C = a.sr_C, tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+__device__ __forceinline__ void sr_block(float* __restrict__ slots, float* __restrict__ red, float* __restrict__ dgamma,
+                                         float* __restrict__ dbeta, int C, int sb, float* red2) {
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int c = sb * 16 + tx;
   const bool own = ty == 0 && c < C;
   float db = 0.f, dg = 0.f;
   if (own) {
-    if (a.sr_dbeta) db = a.sr_dbeta[c];
-    if (a.sr_dgamma) dg = a.sr_dgamma[c];
+    if (dbeta) db = dbeta[c];
+    if (dgamma) dg = dgamma[c];
   }
   float s = 0.f, q = 0.f;
   if (c < C) {
     float vs[NSLOT / 16], vq[NSLOT / 16];
 #pragma unroll
     for (int i = 0; i < NSLOT / 16; ++i) {
-      const float* p = a.sr_slots + (size_t)(ty + 16 * i) * 2 * C;
+      const float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
       vs[i] = p[c];
       vq[i] = p[C + c];
     }
@@ -486,7 +487,7 @@ __device__ __forceinline__ void sr_block(const IgemmArgs& a, int sb, float* red2
     for (int i = 0; i < NSLOT / 16; ++i) {
       s += vs[i];
       q += vq[i];
-      float* p = a.sr_slots + (size_t)(ty + 16 * i) * 2 * C;
+      float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
       p[c] = 0.f;  // the workspace is zero again for its next use
       p[C + c] = 0.f;
     }
@@ -500,10 +501,10 @@ __device__ __forceinline__ void sr_block(const IgemmArgs& a, int sb, float* red2
       s += red2[threadIdx.x + 16 * k];
       q += red2[256 + threadIdx.x + 16 * k];
     }
-    a.sr_red[c] = s;
-    a.sr_red[C + c] = q;
-    if (a.sr_dbeta) a.sr_dbeta[c] = db + s;
-    if (a.sr_dgamma) a.sr_dgamma[c] = dg + q;
+    red[c] = s;
+    red[C + c] = q;
+    if (dbeta) dbeta[c] = db + s;
+    if (dgamma) dgamma[c] = dg + q;
   }
 }
 
@@ -583,11 +584,14 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   const int t = threadIdx.x & 255, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
 
   // tail blocks past the GEMM's grid: another BN layer's backward slot reduction (IgemmArgs sr_*)
-  const int gemm_blocks = (int)gridDim.x - (a.sr_C ? (a.sr_C + 15) / 16 : 0);
+  const int nsr1 = a.sr_C ? (a.sr_C + 15) / 16 : 0, nsr2 = a.sr2_C ? (a.sr2_C + 15) / 16 : 0;
+  const int gemm_blocks = (int)gridDim.x - nsr1 - nsr2;
   if ((int)blockIdx.x >= gemm_blocks) {
     if (threadIdx.x < 256) {
       float* scratch = reinterpret_cast<float*>(GL ? ga0 : smem_all);  // >= 2 KB, unused by this block
-      sr_block(a, (int)blockIdx.x - gemm_blocks, scratch);
+      const int sb = (int)blockIdx.x - gemm_blocks;
+      if (sb < nsr1) sr_block(a.sr_slots, a.sr_red, a.sr_dgamma, a.sr_dbeta, a.sr_C, sb, scratch);
+      else sr_block(a.sr2_slots, a.sr2_red, a.sr2_dgamma, a.sr2_dbeta, a.sr2_C, sb - nsr1, scratch);
     }
     return;
   }
@@ -1333,7 +1337,8 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   }
   splits = (nkt + a.kps - 1) / a.kps;
   if (tiles * splits == 0) return;
-  const int grid = tiles * splits + (a.sr_C ? (a.sr_C + 15) / 16 : 0);  // + slot-reduce tail blocks
+  const int grid = tiles * splits + (a.sr_C ? (a.sr_C + 15) / 16 : 0) +
+                   (a.sr2_C ? (a.sr2_C + 15) / 16 : 0);  // + slot-reduce tail blocks
   // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
   constexpr int STAGE_B = (BM + BN) * BKT * 2;

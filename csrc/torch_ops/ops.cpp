@@ -386,6 +386,8 @@ void conv_wgrad_impl(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad
   if (sr) {
     a.sr_slots = sr->sr_slots; a.sr_red = sr->sr_red; a.sr_dgamma = sr->sr_dgamma; a.sr_dbeta = sr->sr_dbeta;
     a.sr_C = sr->sr_C;
+    a.sr2_slots = sr->sr2_slots; a.sr2_red = sr->sr2_red; a.sr2_dgamma = sr->sr2_dgamma; a.sr2_dbeta = sr->sr2_dbeta;
+    a.sr2_C = sr->sr2_C;
   }
   const int64_t RSC = g.R * g.S * g.C;
   a.K = g.N * g.P * g.Q;
@@ -422,6 +424,60 @@ Tensor conv_wgrad_sr(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad
   sr.sr_slots = slots.data_ptr<float>(); sr.sr_red = red.data_ptr<float>();
   sr.sr_dgamma = fpm(dgamma); sr.sr_dbeta = fpm(dbeta); sr.sr_C = (int)C;
   conv_wgrad_impl(dy, x, dw, stride, pad, dil, accumulate, &sr);
+  return red;
+}
+
+// conv_wgrad with up to two pending BN-backward slot reductions in the tail (either may be absent:
+// an undefined slots tensor).  Returns (red1, red2), empty where absent.
+std::tuple<Tensor, Tensor> conv_wgrad_sr2(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t dil,
+                                          bool accumulate, optional<Tensor> slots, optional<Tensor> dgamma,
+                                          optional<Tensor> dbeta, optional<Tensor> slots2, int64_t C2,
+                                          optional<Tensor> dgamma2, optional<Tensor> dbeta2) {
+  tfx::IgemmArgs sr;
+  auto opts = dy.options().dtype(at::kFloat);
+  Tensor red1 = at::empty({0}, opts), red2 = at::empty({0}, opts);
+  if (slots.has_value() && slots->defined()) {
+    CHECK_DEV(*slots); CHECK_F32(*slots); CHECK_CONTIG(*slots);
+    const int64_t C = x.size(-1);
+    TORCH_CHECK(slots->numel() >= tfx::NSLOT * 2 * C, "conv_wgrad_sr2: slot workspace too small");
+    red1 = at::empty({2 * C}, opts);
+    sr.sr_slots = slots->data_ptr<float>(); sr.sr_red = red1.data_ptr<float>();
+    sr.sr_dgamma = fpm(dgamma); sr.sr_dbeta = fpm(dbeta); sr.sr_C = (int)C;
+  }
+  if (slots2.has_value() && slots2->defined()) {
+    CHECK_DEV(*slots2); CHECK_F32(*slots2); CHECK_CONTIG(*slots2);
+    TORCH_CHECK(C2 > 0 && slots2->numel() >= tfx::NSLOT * 2 * C2, "conv_wgrad_sr2: second slot workspace");
+    red2 = at::empty({2 * C2}, opts);
+    sr.sr2_slots = slots2->data_ptr<float>(); sr.sr2_red = red2.data_ptr<float>();
+    sr.sr2_dgamma = fpm(dgamma2); sr.sr2_dbeta = fpm(dbeta2); sr.sr2_C = (int)C2;
+  }
+  conv_wgrad_impl(dy, x, dw, stride, pad, dil, accumulate, &sr);
+  return {red1, red2};
+}
+
+// the reduce half of a BN backward only (no residual): per-column partials [sum g' | sum g' xhat] of
+// the output gradient g into the layer's zeroed slot workspace -- a later launch reduces the slots
+// (conv_wgrad_sr2 tail blocks, or bn_slots_reduce)
+void bn_bwd_reduce_into(Tensor g, Tensor x, Tensor save, bool relu, optional<Tensor> mask, Tensor slots) {
+  CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(slots);
+  TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd_reduce_into: grad shape");
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(slots.numel() >= tfx::NSLOT * 2 * C, "bn_bwd_reduce_into: slot workspace");
+  const uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() * 8 == x.numel(), "relu mask size");
+    mk = mask->data_ptr<uint8_t>();
+  }
+  tfx::bn_bwd_reduce(bf(g), bf(x), mk, false, save.data_ptr<float>(), M, C, relu, slots.data_ptr<float>(),
+                     cur_stream());
+}
+
+// the slot reduction alone: red = [sum g' | sum g' xhat] from the slots (re-zeroed), dgamma/dbeta +=
+Tensor bn_slots_reduce(Tensor slots, int64_t C, optional<Tensor> dgamma, optional<Tensor> dbeta) {
+  CHECK_DEV(slots); CHECK_F32(slots); CHECK_CONTIG(slots);
+  TORCH_CHECK(slots.numel() >= tfx::NSLOT * 2 * C, "bn_slots_reduce: slot workspace");
+  auto red = at::empty({2 * C}, slots.options());
+  tfx::bn_slot_reduce(slots.data_ptr<float>(), (int)C, red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), cur_stream());
   return red;
 }
 
@@ -633,7 +689,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(Tensor g, Tensor x, optional<Tensor> r
 std::tuple<Tensor, Tensor, Tensor> bn_bwd_apply_sec(Tensor g, Tensor x, Tensor save, Tensor red, bool relu,
                                                     optional<Tensor> mask, Tensor x2, Tensor save2, Tensor slots2,
                                                     optional<Tensor> dgamma2, optional<Tensor> dbeta2,
-                                                    bool want_dres) {
+                                                    bool want_dres, bool reduce2) {
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(red);
   CHECK_BF16(x2); CHECK_CONTIG(x2); CHECK_F32(save2); CHECK_F32(slots2);
   const int64_t C = x.size(-1), M = x.numel() / C;
@@ -650,12 +706,15 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd_apply_sec(Tensor g, Tensor x, Tensor s
   auto dx = at::empty_like(x);
   Tensor dres;
   if (want_dres) dres = at::empty_like(x);
-  auto red2 = at::empty({2 * C}, x.options().dtype(at::kFloat));
+  // reduce2 = false: the residual BN's partials stay in slots2 for a later launch to reduce
+  // (conv_wgrad_sr2 tail blocks / bn_slots_reduce); red2 is then empty
+  auto red2 = at::empty({reduce2 ? 2 * C : 0}, x.options().dtype(at::kFloat));
   tfx::bn_backward_apply_sec(bf(g), bf(x), mk, save.data_ptr<float>(), red.data_ptr<float>(), M, (int)C, relu,
                              bfm(dx), want_dres ? bfm(dres) : nullptr, bf(x2), save2.data_ptr<float>(), slots2.data_ptr<float>(),
                              cur_stream());
-  tfx::bn_slot_reduce(slots2.data_ptr<float>(), (int)C, red2.data_ptr<float>(), fpm(dgamma2), fpm(dbeta2),
-                      cur_stream());
+  if (reduce2)
+    tfx::bn_slot_reduce(slots2.data_ptr<float>(), (int)C, red2.data_ptr<float>(), fpm(dgamma2), fpm(dbeta2),
+                        cur_stream());
   return {dx, dres, red2};
 }
 
@@ -1357,6 +1416,9 @@ TORCH_LIBRARY(tfx, m) {
         "Tensor? addend_mask=None, bool addend_s2=False, Tensor? wflip=None) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_wgrad_sr", &conv_wgrad_sr);
+  m.def("conv_wgrad_sr2", &conv_wgrad_sr2);
+  m.def("bn_bwd_reduce_into", &bn_bwd_reduce_into);
+  m.def("bn_slots_reduce", &bn_slots_reduce);
   m.def("gemm", &gemm);
   m.def("gemm_into", &gemm_into);
   m.def("sgemm(Tensor a, Tensor b, bool ta, bool tb, Tensor? bias, int act, bool split=False) -> Tensor", &sgemm);
@@ -1368,8 +1430,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_apply_res_bn(Tensor x, Tensor res_x, Tensor save, Tensor res_save, bool relu) -> (Tensor, Tensor)",
         &bn_apply_res_bn);
   m.def("bn_bwd_apply_sec(Tensor g, Tensor x, Tensor save, Tensor red, bool relu, Tensor? mask, Tensor x2, "
-        "Tensor save2, Tensor slots2, Tensor? dgamma2=None, Tensor? dbeta2=None, bool want_dres=True) -> "
-        "(Tensor, Tensor, Tensor)",
+        "Tensor save2, Tensor slots2, Tensor? dgamma2=None, Tensor? dbeta2=None, bool want_dres=True, "
+        "bool reduce2=True) -> (Tensor, Tensor, Tensor)",
         &bn_bwd_apply_sec);
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);

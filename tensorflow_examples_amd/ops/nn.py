@@ -15,7 +15,7 @@ launch a bucket's all-reduce as soon as its last gradient lands.
 from __future__ import annotations
 
 import os
-from typing import Optional
+from typing import List, Optional
 
 import torch
 import torch.nn.functional as F
@@ -124,6 +124,9 @@ _DGRAD_FLIP = os.environ.get("TFX_DGRAD_FLIP", "1") != "0"
 # A/B switch: the BN-backward slot reduction of a fused data gradient runs as tail blocks of the same
 # conv's weight-gradient launch (conv_wgrad_sr) instead of its own bn_slot_reduce launch
 _SR_FUSE = os.environ.get("TFX_SR_FUSE", "1") != "0"
+# ... and also the reductions of the stride-2 conv2's input BN and of the projection-shortcut BN
+# (deferred to the next weight-gradient launch's tail; TFX_SR_FUSE2=0 keeps their own launches)
+_SR_FUSE2 = _SR_FUSE and os.environ.get("TFX_SR_FUSE2", "1") != "0"
 # opt-in (TFX_S2_BNB=1): fuse the BN-backward reduction into stride-2 (parity-class) data gradients
 # too.  Measured a wash in the step (8.152 vs 8.139 ms/step, profiles/r02_s2bnb): the four class
 # GEMMs' epilogue cost matches the reduce kernel it removes.  (The C++ side runs stride-2 data
@@ -238,6 +241,14 @@ class _Conv2d(torch.autograd.Function):
                     if sink is not None:  # mode "produce": park it for the last consumer
                         sink.put(dx)
                         dx = None
+                    elif bnb is not None and stride == 2 and _SR_FUSE2 and w.trainable and bnb.mask is None \
+                            and not bnb.deferred and bnb.wsobj is None and bnb.red is None \
+                            and wgrad_side_stream(gy.device) is None:
+                        # dx is the complete output gradient of the BN that produced x: its backward
+                        # partials go into the BN's slots now, their reduction rides in the tail of the
+                        # weight-gradient launch below (no bn_bwd reduce + slot-reduce pair later)
+                        torch.ops.tfx.bn_bwd_reduce_into(dx, bnb.x, bnb.save, bnb.relu, None, bnb.ws)
+                        sr_bnb = bnb
             if w.trainable:
                 ss = _enter_side(gy.device)
                 if ss is not None:
@@ -247,9 +258,18 @@ class _Conv2d(torch.autograd.Function):
                         _grad_ready(w)
                     gy.record_stream(ss)
                     x.record_stream(ss)
-                elif sr_bnb is not None:
-                    sr_bnb.red = torch.ops.tfx.conv_wgrad_sr(gy, x, w.grad, stride, pad, dil, True, sr_bnb.ws,
-                                                             sr_bnb.dgamma, sr_bnb.dbeta)
+                elif sr_bnb is not None or (_PENDING_SR and _PENDING_SR[0].ws.device == gy.device):
+                    t2 = _PENDING_SR.pop(0) if (_PENDING_SR and _PENDING_SR[0].ws.device == gy.device) else None
+                    t1 = sr_bnb
+                    r1, r2 = torch.ops.tfx.conv_wgrad_sr2(
+                        gy, x, w.grad, stride, pad, dil, True, t1.ws if t1 is not None else None,
+                        t1.dgamma if t1 is not None else None, t1.dbeta if t1 is not None else None,
+                        t2.ws if t2 is not None else None, t2.x.shape[-1] if t2 is not None else 0,
+                        t2.dgamma if t2 is not None else None, t2.dbeta if t2 is not None else None)
+                    if t1 is not None:
+                        t1.red = r1
+                    if t2 is not None:
+                        t2.red, t2.sr_pending = r2, False
                     _grad_ready(w)
                 else:
                     torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
@@ -395,7 +415,8 @@ class BNBackwardFusion:
     ``red`` ([sum g' | sum g' xhat]), or -- two-slot-set workspaces (``wsobj``) -- leaves the
     partials in the layer's backward slots and sets ``red = IN_SLOTS``; the BN backward then runs
     only its apply pass."""
-    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "wsobj", "in_mask", "deferred")
+    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "wsobj", "in_mask", "deferred",
+                 "sr_pending")
     IN_SLOTS = "slots"
 
     def __init__(self, x, save, mask, relu, ws, dgamma, dbeta, wsobj=None):
@@ -407,6 +428,8 @@ class BNBackwardFusion:
         # the BN's output was never written (batch_norm(defer_output=True)): its only consumer, a
         # residual BN, normalizes ``x`` with ``save`` on the fly
         self.deferred = False
+        # backward partials sit in ``ws`` waiting for a later launch to reduce them (_PENDING_SR)
+        self.sr_pending = False
 
 
 # ====================================================================== batch norm (+res, +relu)
@@ -439,6 +462,27 @@ _FUSE_RES_BN = os.environ.get("TFX_FUSE_RES_BN", "1") != "0"
 _DEFER_RES_BN = os.environ.get("TFX_DEFER_RES_BN", "1") != "0"
 # ... and with the tail's ReLU, pass gy + mask bits instead of writing gy * mask
 _FUSE_RES_BN_MASK = os.environ.get("TFX_FUSE_RES_BN_MASK", "1") != "0"
+
+
+# BN layers whose backward partials wait in their slot workspace for the next weight-gradient
+# launch to reduce them in its tail blocks (conv_wgrad_sr2) -- or for their own backward to reduce
+# them (bn_slots_reduce) if no such launch came first
+_PENDING_SR: List["BNBackwardFusion"] = []
+
+
+def reset_pending_slot_reductions() -> None:
+    """Forget deferred reductions of an abandoned step (an exception part-way through backward)."""
+    for b in _PENDING_SR:
+        b.sr_pending = False
+    _PENDING_SR.clear()
+
+
+def _resolve_pending(b: "BNBackwardFusion") -> None:
+    if b.sr_pending:
+        if b in _PENDING_SR:
+            _PENDING_SR.remove(b)
+        b.red = torch.ops.tfx.bn_slots_reduce(b.ws, b.x.shape[-1], b.dgamma, b.dbeta)
+        b.sr_pending = False
 
 
 _ZERO = {}
@@ -554,6 +598,8 @@ class _BatchNorm(torch.autograd.Function):
             x, res, save, mask = ctx.saved_tensors
             if not training:
                 raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
+            if ctx.bnb is not None:
+                _resolve_pending(ctx.bnb)  # no weight-gradient launch took its deferred reduction
             train_p = gamma is not None and gamma.trainable
             gy = gy.contiguous()
             # residual gradient g' = gy * relu_mask: when the sink's consumer applies the mask itself
@@ -581,9 +627,17 @@ class _BatchNorm(torch.autograd.Function):
                 # with a ReLU the residual gradient is gy * mask: hand the residual BN gy itself and
                 # the mask bits instead of writing the masked copy
                 pass_mask = relu and _FUSE_RES_BN_MASK
-                dx, dres, rb.red = torch.ops.tfx.bn_bwd_apply_sec(gy, x, save, ctx.bnb.red, relu, mask, rb.x, rb.save,
-                                                                   rb.ws, rb.dgamma if p_t else None,
-                                                                   rb.dbeta if p_t else None, not pass_mask)
+                # _SR_FUSE: the residual BN's slot reduction is deferred to the tail of the next weight-
+                # gradient launch (this block's conv3, which autograd runs before the residual BN)
+                defer = _SR_FUSE2 and wgrad_side_stream(gy.device) is None
+                dx, dres, red2 = torch.ops.tfx.bn_bwd_apply_sec(gy, x, save, ctx.bnb.red, relu, mask, rb.x, rb.save,
+                                                                 rb.ws, rb.dgamma if p_t else None,
+                                                                 rb.dbeta if p_t else None, not pass_mask, not defer)
+                if defer:
+                    rb.red, rb.sr_pending = None, True
+                    _PENDING_SR.append(rb)
+                else:
+                    rb.red = red2
                 if pass_mask:
                     rb.in_mask, dres = mask, gy
                 ctx.bnb.red = None

@@ -14,6 +14,7 @@ import torch.distributed as dist
 
 from . import ops
 from .ops import _native
+from .ops.nn import reset_pending_slot_reductions
 from .optim import Optimizer
 from .parallel.allreduce import GradAllReduce
 from .utils import trace
@@ -31,6 +32,7 @@ class ClassifierTrainer:
 
     def _step(self, x, y):
         # roctx ranges (TFX_ROCTX=1) label the phases on a rocprofv3 --marker-trace timeline
+        reset_pending_slot_reductions()  # nothing deferred survives an abandoned step
         self.store.zero_grad()
         with trace.range("forward"):
             logits = self.model(x, training=True)

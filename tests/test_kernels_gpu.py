@@ -495,3 +495,54 @@ def test_conv_wgrad_slot_reduce_tail_blocks(gpu, shape):
     red2 = torch.ops.tfx.conv_wgrad_sr(gy, x, dw, st, pad, 1, True, slots, None, None)  # no parameter grads
     torch.cuda.synchronize()
     assert red2.abs().max().item() == 0.0 and _rel(dw, 2 * dw_ref) < 1e-5
+
+
+@pytest.mark.parametrize("shape,C2", [((256, 16, 16, 128, 128, 3, 2), 512), ((256, 8, 8, 256, 1024, 1, 1), 1024),
+                                      ((256, 4, 4, 512, 2048, 1, 1), 2048)])
+def test_conv_wgrad_two_tail_reductions(gpu, shape, C2):
+    """conv_wgrad_sr2: two BN layers' deferred slot reductions in one weight-gradient grid's tail
+    (the conv's own input BN, and a pending one: a projection-shortcut BN), vs torch; plus the
+    reduce-only BN backward (bn_bwd_reduce_into) and the standalone bn_slots_reduce it pairs with."""
+    N, H, W, C, K, R, st = shape
+    pad = R // 2
+    torch.manual_seed(29)
+    x = _bf(torch.randn(N, H, W, C, device=gpu))
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    gy = _bf(torch.randn(N, P, Q, K, device=gpu))
+    dw_ref = torch.zeros(K, R, R, C, device=gpu)
+    torch.ops.tfx.conv_wgrad(gy, x, dw_ref, st, pad, 1, True)
+    # set 1: partials written by bn_bwd_reduce_into from a BN with ReLU (checked against bn_bwd's red)
+    xb = _bf(torch.randn(N, H, W, C, device=gpu) + 0.2)
+    gamma, beta = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
+    ws = torch.zeros(64 * 2 * C + 64, device=gpu)
+    _, save, _ = torch.ops.tfx.bn_fwd_train(xb, gamma, beta, None, None, 0.1, 1e-5, None, True, ws, False)
+    g = _bf(torch.randn(N, H, W, C, device=gpu))
+    wsr = torch.zeros(64 * 2 * C, device=gpu)
+    _, _, red_ref = torch.ops.tfx.bn_bwd(g, xb, None, save, True, wsr, None, None, None)
+    slots1 = torch.zeros(64 * 2 * C + 64, device=gpu)
+    torch.ops.tfx.bn_bwd_reduce_into(g, xb, save, True, None, slots1)
+    # set 2: arbitrary partials
+    slots2 = torch.zeros(64 * 2 * C2 + 64, device=gpu)
+    slots2[: 64 * 2 * C2] = torch.randn(64 * 2 * C2, device=gpu)
+    red2_ref = slots2[: 64 * 2 * C2].view(64, 2, C2).sum(0).reshape(-1)
+    dg1, db1 = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+    dg2, db2 = torch.zeros(C2, device=gpu), torch.zeros(C2, device=gpu)
+    dw = torch.zeros(K, R, R, C, device=gpu)
+    r1, r2 = torch.ops.tfx.conv_wgrad_sr2(gy, x, dw, st, pad, 1, True, slots1, dg1, db1, slots2, C2, dg2, db2)
+    torch.cuda.synchronize()
+    assert _rel(dw, dw_ref) < 1e-5
+    assert _rel(r1, red_ref) < 1e-4 and _rel(db1, red_ref[:C]) < 1e-4 and _rel(dg1, red_ref[C:]) < 1e-4
+    assert torch.allclose(r2, red2_ref, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(db2, red2_ref[:C2], rtol=1e-5, atol=1e-4)
+    assert slots1.abs().max().item() == 0.0 and slots2.abs().max().item() == 0.0
+    # only the second set; then the standalone reduction
+    slots2[: 64 * 2 * C2] = torch.randn(64 * 2 * C2, device=gpu)
+    ref = slots2[: 64 * 2 * C2].view(64, 2, C2).sum(0).reshape(-1)
+    r1b, r2b = torch.ops.tfx.conv_wgrad_sr2(gy, x, dw, st, pad, 1, True, None, None, None, slots2, C2, None, None)
+    torch.cuda.synchronize()
+    assert r1b.numel() == 0 and torch.allclose(r2b, ref, rtol=1e-5, atol=1e-4)
+    slots2[: 64 * 2 * C2] = torch.randn(64 * 2 * C2, device=gpu)
+    ref = slots2[: 64 * 2 * C2].view(64, 2, C2).sum(0).reshape(-1)
+    r3 = torch.ops.tfx.bn_slots_reduce(slots2, C2, None, None)
+    torch.cuda.synchronize()
+    assert torch.allclose(r3, ref, rtol=1e-5, atol=1e-4) and slots2.abs().max().item() == 0.0
