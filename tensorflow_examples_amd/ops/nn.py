@@ -127,6 +127,8 @@ _SR_FUSE = os.environ.get("TFX_SR_FUSE", "1") != "0"
 # ... and also the reductions of the stride-2 conv2's input BN and of the projection-shortcut BN
 # (deferred to the next weight-gradient launch's tail; TFX_SR_FUSE2=0 keeps their own launches)
 _SR_FUSE2 = _SR_FUSE and os.environ.get("TFX_SR_FUSE2", "1") != "0"
+# test hook: False leaves every deferred reduction to its own BN's backward (the fallback path)
+_SR_TAKE_PENDING = True
 # opt-in (TFX_S2_BNB=1): fuse the BN-backward reduction into stride-2 (parity-class) data gradients
 # too.  Measured a wash in the step (8.152 vs 8.139 ms/step, profiles/r02_s2bnb): the four class
 # GEMMs' epilogue cost matches the reduce kernel it removes.  (The C++ side runs stride-2 data
@@ -258,8 +260,9 @@ class _Conv2d(torch.autograd.Function):
                         _grad_ready(w)
                     gy.record_stream(ss)
                     x.record_stream(ss)
-                elif sr_bnb is not None or (_PENDING_SR and _PENDING_SR[0].ws.device == gy.device):
-                    t2 = _PENDING_SR.pop(0) if (_PENDING_SR and _PENDING_SR[0].ws.device == gy.device) else None
+                elif sr_bnb is not None or (_SR_TAKE_PENDING and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device):
+                    take = _SR_TAKE_PENDING and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device
+                    t2 = _PENDING_SR.pop(0) if take else None
                     t1 = sr_bnb
                     r1, r2 = torch.ops.tfx.conv_wgrad_sr2(
                         gy, x, w.grad, stride, pad, dil, True, t1.ws if t1 is not None else None,
