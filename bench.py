@@ -87,7 +87,7 @@ def run(a):
     from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
     from tensorflow_examples_amd.optim import MomentumOptimizer
     from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed
-    from tensorflow_examples_amd.parallel.launch import verify_world
+    from tensorflow_examples_amd.parallel.launch import control_device, control_group as _control_group, verify_world
     from tensorflow_examples_amd.train import ClassifierTrainer
 
     cuda = a.device == "cuda"
@@ -100,7 +100,8 @@ def run(a):
     # host-side control collectives (capture agreement, timing barriers, elapsed-time MAX) run on a
     # gloo group: the RCCL communicator then carries only the gradient all-reduces, and no eager RCCL
     # call is ever interleaved with replays of a graph that holds captured RCCL collectives
-    ctl = dist.new_group(backend="gloo") if dist.is_initialized() else None
+    ctl = _control_group() if dist.is_initialized() else None
+    cdev = control_device(ctl, dev)
     torch.manual_seed(1234 + rank)
     host = synthetic_batches(a.nbatches, a.batch, seed=1000 + rank)
     dtype = torch.bfloat16 if cuda else torch.float32
@@ -150,7 +151,7 @@ def run(a):
             if world > 1 or forced:
                 # every rank replays its graph or none does: a rank left eager would issue its
                 # collectives in a different order from the graph replays of the others
-                agree = torch.tensor([1 if graphed else 0], dtype=torch.int32)
+                agree = torch.tensor([1 if graphed else 0], dtype=torch.int32, device=cdev)
                 dist.all_reduce(agree, op=dist.ReduceOp.MIN, group=ctl)
                 graphed = bool(agree.item())
             if not graphed:
@@ -195,7 +196,7 @@ def run(a):
         dist.barrier(group=ctl)
     sync()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX, group=ctl)
     elapsed = float(el.item())

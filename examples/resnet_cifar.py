@@ -24,6 +24,7 @@ from tensorflow_examples_amd.data.pipeline import DevicePrefetcher, batches  # n
 from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
 from tensorflow_examples_amd.optim import MomentumOptimizer  # noqa: E402
 from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed  # noqa: E402
+from tensorflow_examples_amd.parallel.launch import control_device, control_group as _control_group  # noqa: E402
 from tensorflow_examples_amd.train import ClassifierTrainer  # noqa: E402
 
 flags = app.flags
@@ -51,7 +52,8 @@ def main(_):
     rank = dist.get_rank() if dist.is_initialized() else 0
     # host-side control collectives on gloo: after the graph is captured, the RCCL communicator only
     # ever runs the captured gradient all-reduces (no eager RCCL call between replays)
-    ctl = dist.new_group(backend="gloo") if dist.is_initialized() else None
+    ctl = _control_group() if dist.is_initialized() else None
+    cdev = control_device(ctl, dev)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     xtr, ytr, xte, yte, synth = load_cifar10(FLAGS.data_dir or None, synthetic_train=FLAGS.synthetic_train)
     if rank == 0:
@@ -86,7 +88,7 @@ def main(_):
                     print("rank %d: hip graph capture failed (%s)" % (rank, e), file=sys.stderr)
                     ok = False
                 if world > 1:  # every rank replays or none does (collective order must match)
-                    agree = torch.tensor([1 if ok else 0], dtype=torch.int32)
+                    agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
                     dist.all_reduce(agree, op=dist.ReduceOp.MIN, group=ctl)
                     ok = bool(agree.item())
                 if not ok:
@@ -105,7 +107,7 @@ def main(_):
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.time() - t0
-    ips = torch.tensor([seen / dt], dtype=torch.float64)
+    ips = torch.tensor([seen / dt], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(ips, group=ctl)
     if FLAGS.eval_examples:

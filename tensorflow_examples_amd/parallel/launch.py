@@ -144,6 +144,33 @@ def init_distributed(backend: Optional[str] = None, device: str = "cuda", timeou
     return dev
 
 
+def control_group():
+    """A gloo process group for host-side control collectives (agreement flags, barriers, timing
+    reductions), so the RCCL communicator carries only the (possibly graph-captured) gradient
+    collectives.  Falls back to the default group if gloo cannot be brought up on this host."""
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return None
+    if dist.get_backend() == "gloo":
+        return None  # the default group already is gloo
+    try:
+        return dist.new_group(backend="gloo")
+    except Exception as e:  # pragma: no cover - host networking dependent
+        print(f"control group: gloo unavailable ({e}); using the default group", file=sys.stderr)
+        return None
+
+
+def control_device(group, device):
+    """Where a control collective's tensor lives: the host for a gloo group, else ``device``."""
+    import torch
+    import torch.distributed as dist
+
+    if group is not None or (dist.is_initialized() and dist.get_backend() == "gloo"):
+        return torch.device("cpu")
+    return device
+
+
 def verify_world(expected: int, device) -> int:
     """Check the process group really spans ``expected`` ranks: the group size must match and an
     all-reduce of ones must sum to it (a collective that every rank completes).  Returns the size."""
