@@ -246,6 +246,9 @@ void lstm_seq_bwd(const float* act, const float* cbuf, const uint16_t* dH, const
 
 // ---------------------------------------------------------------- input pipeline
 // uint8 NHWC [npix][cin] (cin <= 4) -> bf16 NHWC [npix][cout] (cout 4 or 8): (x/255 - mean)/std, zero pad
+// pad-P random crop + flip (per-image off[n] = {ox, oy, flip}) fused with image_normalize
+void augment_normalize(const uint8_t* x, int N, int H, int W, int cin, int cout, int pad, const int32_t* off,
+                       const float* mean, const float* stdv, uint16_t* y, hipStream_t s);
 void image_normalize(const uint8_t* x, int64_t npix, int cin, int cout, const float* mean, const float* stdv,
                      uint16_t* y, hipStream_t s);
 

@@ -1341,6 +1341,30 @@ Tensor image_normalize(Tensor x, std::vector<double> mean, std::vector<double> s
 // straight over the host link (zero-copy input: no H2D staging copy, no copy stream, no device
 // staging buffer).  The caller keeps the pinned buffer unmodified until the kernel has run
 // (data/pipeline.py PinnedRing(zero_copy=True) orders that with an event per slot).
+// Training augmentation (pad-`pad` random crop + flip; offsets [N][3] int32 = ox, oy, flip on the
+// device) fused with the uint8 -> normalised bf16 conversion: returns [N][H][W][cout]
+Tensor augment_normalize(Tensor x, Tensor offsets, std::vector<double> mean, std::vector<double> stdv, int64_t cout,
+                         int64_t pad) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_DEV(offsets); CHECK_CONTIG(offsets);
+  TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4, "augment_normalize: uint8 NHWC images");
+  TORCH_CHECK(offsets.scalar_type() == at::kInt && offsets.dim() == 2 && offsets.size(0) == x.size(0) &&
+                  offsets.size(1) == 3, "augment_normalize: offsets [N][3] int32");
+  const int64_t cin = x.size(3);
+  TORCH_CHECK(cin >= 1 && cin <= 4 && (int64_t)mean.size() == cin && (int64_t)stdv.size() == cin,
+              "augment_normalize: 1..4 channels with per-channel mean/std");
+  TORCH_CHECK(cout == 4 || cout == 8, "augment_normalize: cout 4 or 8");
+  TORCH_CHECK(pad >= 0 && pad < 64, "augment_normalize: pad");
+  auto y = at::empty({x.size(0), x.size(1), x.size(2), cout}, x.options().dtype(at::kBFloat16));
+  float m[4] = {0, 0, 0, 0}, sd[4] = {1, 1, 1, 1};
+  for (int64_t c = 0; c < cin; ++c) {
+    m[c] = (float)mean[c];
+    sd[c] = (float)stdv[c];
+  }
+  tfx::augment_normalize(x.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)cin, (int)cout,
+                         (int)pad, offsets.data_ptr<int32_t>(), m, sd, bfm(y), cur_stream());
+  return y;
+}
+
 // End a capture left open on `stream` (a side stream forked into a HIP-graph capture that failed
 // before the join): its partial graph is discarded.  Returns true if a capture was open.  While any
 // stream of a thread stays capturing, that thread cannot run synchronous work at all.
@@ -1388,6 +1412,7 @@ void image_normalize_into(Tensor x, std::vector<double> mean, std::vector<double
 TORCH_LIBRARY(tfx, m) {
   m.def("image_normalize", &image_normalize);
   m.def("image_normalize_into", &image_normalize_into);
+  m.def("augment_normalize", &augment_normalize);
   m.def("end_stream_capture", &end_stream_capture);
   m.def("philox_fill", &philox_fill);
   m.def("maxpool_fwd", &maxpool_fwd);

@@ -19,7 +19,7 @@ import torch.distributed as dist  # noqa: E402
 
 from tensorflow_examples_amd import app, ops  # noqa: E402
 from tensorflow_examples_amd.ckpt import Saver, latest_checkpoint  # noqa: E402
-from tensorflow_examples_amd.data.cifar import augment, load_cifar10  # noqa: E402
+from tensorflow_examples_amd.data.cifar import augment_model_input, load_cifar10  # noqa: E402
 from tensorflow_examples_amd.data.pipeline import DevicePrefetcher, batches  # noqa: E402
 from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
 from tensorflow_examples_amd.optim import MomentumOptimizer  # noqa: E402
@@ -78,7 +78,7 @@ def main(_):
         for img, lab in DevicePrefetcher(src, dev):
             lr = FLAGS.learning_rate * world * (0.1 ** sum(step >= b for b in bounds))
             opt.set_learning_rate(lr)  # a device scalar: a replayed graph reads the new value
-            x = to_model_input(augment(img), dtype)
+            x = augment_model_input(img, dtype)  # crop + flip + normalise: one fused kernel on the GPU
             if want_graph:
                 want_graph = False
                 ok = True

@@ -54,16 +54,41 @@ def load_cifar10(data_dir: Optional[str], synthetic_train: int = 50000, syntheti
     return xtr, ytr, xte, yte, True
 
 
-def augment(images: torch.Tensor, generator: Optional[torch.Generator] = None) -> torch.Tensor:
-    """Random 4-pixel-padded crop + horizontal flip of an NHWC uint8 batch (on its device)."""
+def augment_offsets(n: int, device, generator: Optional[torch.Generator] = None, pad: int = 4) -> torch.Tensor:
+    """Per-image crop origin in the padded image and flip bit: int32 [n, 3] = (ox, oy, flip)."""
+    r = torch.randint(0, 2 * pad + 1, (n, 3), device=device, generator=generator, dtype=torch.int32)
+    r[:, 2] %= 2
+    return r
+
+
+def augment(images: torch.Tensor, generator: Optional[torch.Generator] = None,
+            offsets: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Random 4-pixel-padded crop + horizontal flip of an NHWC uint8 batch (on its device).
+    ``offsets``: explicit :func:`augment_offsets` (else drawn from ``generator``)."""
     n = images.shape[0]
     dev = images.device
     padded = torch.nn.functional.pad(images.permute(0, 3, 1, 2), (4, 4, 4, 4)).permute(0, 2, 3, 1)
-    ox = torch.randint(0, 9, (n,), device=dev, generator=generator)
-    oy = torch.randint(0, 9, (n,), device=dev, generator=generator)
-    flip = torch.randint(0, 2, (n,), device=dev, generator=generator).bool()
+    if offsets is None:
+        offsets = augment_offsets(n, dev, generator)
+    ox, oy, flip = offsets[:, 0].long(), offsets[:, 1].long(), offsets[:, 2].bool()
     ar = torch.arange(32, device=dev)
     rows = (oy[:, None] + ar[None, :])                                  # [n,32]
     cols = ox[:, None] + torch.where(flip[:, None], 31 - ar[None, :], ar[None, :])
     bidx = torch.arange(n, device=dev)[:, None, None]
     return padded[bidx, rows[:, :, None], cols[:, None, :]]
+
+
+def augment_model_input(images: torch.Tensor, dtype=torch.bfloat16, generator: Optional[torch.Generator] = None,
+                        offsets: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """:func:`augment` + ``models.resnet.to_model_input`` -- on the GPU one fused HIP kernel
+    (csrc/kernels/image.hip ``augment_norm_kernel``: crop, flip, normalise, pad to 8 channels) after
+    one offsets draw, instead of ~10 elementwise/gather launches; elsewhere the two-step path."""
+    from ..models.resnet import IN_CH_PAD, _MEAN, _STD, to_model_input
+    from ..ops import _native
+    if offsets is None:
+        offsets = augment_offsets(images.shape[0], images.device, generator)
+    if images.is_cuda and images.dtype == torch.uint8 and dtype == torch.bfloat16 and images.shape[1:] == (32, 32, 3) \
+            and _native.use_native(images):
+        return torch.ops.tfx.augment_normalize(images.contiguous(), offsets.contiguous(), list(_MEAN), list(_STD),
+                                               IN_CH_PAD, 4)
+    return to_model_input(augment(images, offsets=offsets), dtype)

@@ -109,3 +109,22 @@ def test_bench_host_input_copy_mode_runs(gpu):
     assert p.returncode == 0, p.stderr[-3000:]
     rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert rec["config"]["host_input"] == "copy" and rec["value"] > 0
+
+
+def test_fused_augment_normalize_matches_two_step(gpu):
+    """augment_model_input: crop + flip + normalise in one HIP kernel == augment() then
+    to_model_input() with the same per-image offsets (bit-exact: same fma), incl. padding pixels."""
+    from tensorflow_examples_amd.data.cifar import augment, augment_model_input, augment_offsets
+    from tensorflow_examples_amd.models.resnet import to_model_input
+    g = torch.Generator(device=gpu).manual_seed(11)
+    img = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, device=gpu)
+    off = augment_offsets(64, gpu, g)
+    off[0] = torch.tensor([0, 0, 1], dtype=torch.int32, device=gpu)  # corner crop + flip: padding visible
+    off[1] = torch.tensor([8, 8, 0], dtype=torch.int32, device=gpu)
+    fused = augment_model_input(img, offsets=off)
+    ref = to_model_input(augment(img, offsets=off))
+    torch.cuda.synchronize()
+    assert fused.shape == (64, 32, 32, 8) and fused.dtype == torch.bfloat16
+    assert torch.equal(fused, ref)
+    cpu = augment_model_input(img.cpu(), dtype=torch.float32, offsets=off.cpu())  # the CPU reference path
+    assert (cpu - fused.float().cpu()).abs().max().item() < 2e-2
