@@ -117,6 +117,18 @@ struct IgemmArgs {
   float* sr2_dgamma = nullptr;
   float* sr2_dbeta = nullptr;
   int sr2_C = 0;
+  // optional tail blocks (forward launches): finalize ANOTHER BN layer's statistics ([NSLOT][2][fin_C]
+  // slots filled by an earlier conv epilogue) into fin_save = [mean | invstd | scale | shift] and its
+  // running statistics -- bn_finalize folded into an independent later launch.  fin_C == 0: none.
+  float* fin_slots = nullptr;
+  const float* fin_gamma = nullptr;
+  const float* fin_beta = nullptr;
+  float* fin_rmean = nullptr;
+  float* fin_rvar = nullptr;
+  float* fin_save = nullptr;
+  int64_t fin_M = 0;
+  float fin_eps = 1e-5f, fin_momentum = 0.1f;
+  int fin_C = 0;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;
 };

@@ -508,6 +508,63 @@ __device__ __forceinline__ void sr_block(float* __restrict__ slots, float* __res
   }
 }
 
+// bn_finalize_kernel's math for channels [16 sb, 16 sb + 16) of the fin_* layer, 256 threads
+__device__ __forceinline__ void fin_block(const IgemmArgs& a, int sb, float* red2) {
+  const int C = a.fin_C, tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = sb * 16 + tx;
+  const bool own = ty == 0 && c < C;
+  float g = 1.f, b = 0.f, rm = 0.f, rv = 0.f;
+  if (own) {
+    if (a.fin_gamma) g = a.fin_gamma[c];
+    if (a.fin_beta) b = a.fin_beta[c];
+    if (a.fin_rmean) {
+      rm = a.fin_rmean[c];
+      rv = a.fin_rvar[c];
+    }
+  }
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    float vs[NSLOT / 16], vq[NSLOT / 16];
+#pragma unroll
+    for (int i = 0; i < NSLOT / 16; ++i) {
+      const float* p = a.fin_slots + (size_t)(ty + 16 * i) * 2 * C;
+      vs[i] = p[c];
+      vq[i] = p[C + c];
+    }
+#pragma unroll
+    for (int i = 0; i < NSLOT / 16; ++i) {
+      s += vs[i];
+      q += vq[i];
+      float* p = a.fin_slots + (size_t)(ty + 16 * i) * 2 * C;
+      p[c] = 0.f;
+      p[C + c] = 0.f;
+    }
+  }
+  red2[threadIdx.x] = s;
+  red2[256 + threadIdx.x] = q;
+  __syncthreads();
+  if (!own) return;
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    s += red2[threadIdx.x + 16 * k];
+    q += red2[256 + threadIdx.x + 16 * k];
+  }
+  const float inv_m = 1.f / (float)a.fin_M;
+  const float mean = s * inv_m;
+  const float var = fmaxf(q * inv_m - mean * mean, 0.f);
+  const float invstd = rsqrtf(var + a.fin_eps);
+  const float scale = g * invstd;
+  a.fin_save[c] = mean;
+  a.fin_save[C + c] = invstd;
+  a.fin_save[2 * C + c] = scale;
+  a.fin_save[3 * C + c] = b - mean * scale;
+  if (a.fin_rmean) {
+    const float unb = a.fin_M > 1 ? var * (float)a.fin_M / (float)(a.fin_M - 1) : var;
+    a.fin_rmean[c] = (1.f - a.fin_momentum) * rm + a.fin_momentum * mean;
+    a.fin_rvar[c] = (1.f - a.fin_momentum) * rv + a.fin_momentum * unb;
+  }
+}
+
 // EPI_BNB = fused BN-backward partials (+ last-arriver reduce) of a conv data gradient.
 // KS = 2: in-block split-K for the f32-atomic weight gradients.  512 threads = two 4-wave groups
 // on the SAME output tile, each running the pipelined K loop over half of the block's k-tiles in its
@@ -585,13 +642,15 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
 
   // tail blocks past the GEMM's grid: another BN layer's backward slot reduction (IgemmArgs sr_*)
   const int nsr1 = a.sr_C ? (a.sr_C + 15) / 16 : 0, nsr2 = a.sr2_C ? (a.sr2_C + 15) / 16 : 0;
-  const int gemm_blocks = (int)gridDim.x - nsr1 - nsr2;
+  const int nfin = a.fin_C ? (a.fin_C + 15) / 16 : 0;
+  const int gemm_blocks = (int)gridDim.x - nsr1 - nsr2 - nfin;
   if ((int)blockIdx.x >= gemm_blocks) {
     if (threadIdx.x < 256) {
       float* scratch = reinterpret_cast<float*>(GL ? ga0 : smem_all);  // >= 2 KB, unused by this block
       const int sb = (int)blockIdx.x - gemm_blocks;
       if (sb < nsr1) sr_block(a.sr_slots, a.sr_red, a.sr_dgamma, a.sr_dbeta, a.sr_C, sb, scratch);
-      else sr_block(a.sr2_slots, a.sr2_red, a.sr2_dgamma, a.sr2_dbeta, a.sr2_C, sb - nsr1, scratch);
+      else if (sb < nsr1 + nsr2) sr_block(a.sr2_slots, a.sr2_red, a.sr2_dgamma, a.sr2_dbeta, a.sr2_C, sb - nsr1, scratch);
+      else fin_block(a, sb - nsr1 - nsr2, scratch);
     }
     return;
   }
@@ -1337,8 +1396,8 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   }
   splits = (nkt + a.kps - 1) / a.kps;
   if (tiles * splits == 0) return;
-  const int grid = tiles * splits + (a.sr_C ? (a.sr_C + 15) / 16 : 0) +
-                   (a.sr2_C ? (a.sr2_C + 15) / 16 : 0);  // + slot-reduce tail blocks
+  const int grid = tiles * splits + (a.sr_C ? (a.sr_C + 15) / 16 : 0) + (a.sr2_C ? (a.sr2_C + 15) / 16 : 0) +
+                   (a.fin_C ? (a.fin_C + 15) / 16 : 0);  // + slot-reduce / finalize tail blocks
   // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
   constexpr int STAGE_B = (BM + BN) * BKT * 2;

@@ -292,6 +292,57 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   return {y, save};
 }
 
+// conv_fwd_bn with two deferral hooks: `defer` = do NOT finalize this conv's BN here (the returned save
+// is filled later: a finalize folded into another launch's tail, or bn_finalize_into); and the
+// fin_* arguments = finalize ANOTHER, earlier-deferred BN in the tail blocks of this launch.
+std::tuple<Tensor, Tensor> conv_fwd_bn2(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor ws,
+                                        optional<Tensor> gamma, optional<Tensor> beta, optional<Tensor> run_mean,
+                                        optional<Tensor> run_var, double momentum, double eps, bool defer,
+                                        optional<Tensor> fin_slots, int64_t fin_C, int64_t fin_M,
+                                        optional<Tensor> fin_gamma, optional<Tensor> fin_beta,
+                                        optional<Tensor> fin_rmean, optional<Tensor> fin_rvar, double fin_momentum,
+                                        double fin_eps, optional<Tensor> fin_save) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
+  auto g = geom(x.sizes().vec(), w.sizes().vec(), stride, pad, dil);
+  auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
+  auto save = at::empty({4 * g.Ko}, x.options().dtype(at::kFloat));
+  auto a = conv_args(g, stride, pad, dil);
+  a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
+  a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
+  a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
+  a.out_mode = tfx::OUT_BF16;
+  a.stats = ws.data_ptr<float>();
+  a.bn_cnt = bn_counters(ws, g.Ko);
+  a.bn_final = 0;
+  a.bn_gamma = fp(gamma); a.bn_beta = fp(beta); a.bn_rmean = fpm(run_mean); a.bn_rvar = fpm(run_var);
+  a.bn_save = save.data_ptr<float>();
+  a.bn_eps = (float)eps; a.bn_momentum = (float)momentum;
+  if (fin_slots.has_value() && fin_slots->defined()) {
+    CHECK_DEV(*fin_slots); CHECK_F32(*fin_slots);
+    TORCH_CHECK(fin_C > 0 && fin_slots->numel() >= tfx::NSLOT * 2 * fin_C && fin_save.has_value() &&
+                    fin_save->defined() && fin_save->numel() == 4 * fin_C && fin_M > 0,
+                "conv_fwd_bn2: deferred finalize arguments");
+    a.fin_slots = fin_slots->data_ptr<float>(); a.fin_C = (int)fin_C; a.fin_M = fin_M;
+    a.fin_gamma = fp(fin_gamma); a.fin_beta = fp(fin_beta); a.fin_rmean = fpm(fin_rmean); a.fin_rvar = fpm(fin_rvar);
+    a.fin_save = fin_save->data_ptr<float>();
+    a.fin_eps = (float)fin_eps; a.fin_momentum = (float)fin_momentum;
+  }
+  tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
+  if (!defer)
+    tfx::bn_finalize(a.stats, a.M, g.Ko, a.bn_gamma, a.bn_beta, a.bn_eps, a.bn_momentum, a.bn_rmean, a.bn_rvar,
+                     a.bn_save, cur_stream());
+  return {y, save};
+}
+
+// the finalize of a deferred BN on its own (no later forward launch took it): slots -> save + running stats
+void bn_finalize_into(Tensor slots, int64_t C, int64_t M, optional<Tensor> gamma, optional<Tensor> beta,
+                      optional<Tensor> run_mean, optional<Tensor> run_var, double momentum, double eps, Tensor save) {
+  CHECK_DEV(slots); CHECK_F32(slots); CHECK_F32(save);
+  TORCH_CHECK(slots.numel() >= tfx::NSLOT * 2 * C && save.numel() == 4 * C, "bn_finalize_into: sizes");
+  tfx::bn_finalize(slots.data_ptr<float>(), M, (int)C, fp(gamma), fp(beta), (float)eps, (float)momentum,
+                   fpm(run_mean), fpm(run_var), save.data_ptr<float>(), cur_stream());
+}
+
 // stride-1 conv data gradient whose epilogue also reduces the backward of the BN that produced
 // the conv's input (the gradient written here is that BN's complete output gradient): returns
 // (dx, red = [sum g' | sum g' xhat]) with dgamma / dbeta accumulated -- the BN then only applies
@@ -1461,6 +1512,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);
+  m.def("conv_fwd_bn2", &conv_fwd_bn2);
+  m.def("bn_finalize_into", &bn_finalize_into);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
         "Tensor bn_x, Tensor bn_save, Tensor? bn_mask, bool relu, Tensor ws, Tensor? dgamma, Tensor? dbeta, "
         "Tensor? addend_mask=None, bool reduce=True, bool addend_s2=False, Tensor? wflip=None) -> (Tensor, Tensor)",

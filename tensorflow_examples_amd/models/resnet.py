@@ -69,6 +69,9 @@ class _BN:
         fused = training and x.device.type == "cuda"
         if fused and _FUSE_BN:
             self.ws.finalize_args = (self.gamma.master, self.beta.master, self.mean, self.var, 0.1, 1e-5)
+            # a BN whose output is never written (read only by the tail BN) can finalize late: in the
+            # tail blocks of the next conv's forward launch (ops/nn.py _PENDING_FIN)
+            self.ws.defer_finalize = bool(defer_output)
             y = conv(x, self.ws, sink, fuse_input_bn_backward and _FUSE_BN)
             return self(y, training, relu=relu, residual=residual, stats_ready=True, residual_sink=residual_sink,
                         ws_obj=True, residual_is_bn=residual_is_bn, defer_output=defer_output)

@@ -171,6 +171,24 @@ class _Conv2d(torch.autograd.Function):
                     y = torch.ops.tfx.conv_fwd_stats(x.contiguous(), w.value, stride, pad, dil, sf)
                     ws.stats_ready = True
                     return y
+                if _FIN_DEFER:
+                    # this conv's BN finalize may be deferred (ws.defer_finalize: a shortcut BN read only
+                    # by the tail BN), and a previously deferred one rides in this launch's tail blocks
+                    defer = bool(getattr(ws, "defer_finalize", False))
+                    fin = _PENDING_FIN.pop(0) if (_PENDING_FIN and _PENDING_FIN[0]["slots"].device == x.device) \
+                        else None
+                    fa = fin["args"] if fin is not None else (None,) * 6
+                    y, save = torch.ops.tfx.conv_fwd_bn2(
+                        x.contiguous(), w.value, stride, pad, dil, ws.get(x.device), *ws.finalize_args, defer,
+                        fin["slots"] if fin is not None else None, fin["C"] if fin is not None else 0,
+                        fin["M"] if fin is not None else 0, fa[0], fa[1], fa[2], fa[3],
+                        fa[4] if fin is not None else 0.1, fa[5] if fin is not None else 1e-5,
+                        fin["save"] if fin is not None else None)
+                    ws.pending_save = save
+                    if defer:
+                        _PENDING_FIN.append({"slots": ws.get(x.device), "C": y.shape[-1], "M": y.numel() // y.shape[-1],
+                                             "args": ws.finalize_args, "save": save})
+                    return y
                 # epilogue statistics + last-arriver finalize: the BN only applies
                 y, ws.pending_save = torch.ops.tfx.conv_fwd_bn(x.contiguous(), w.value, stride, pad, dil,
                                                                ws.get(x.device), *ws.finalize_args)
@@ -473,11 +491,30 @@ _FUSE_RES_BN_MASK = os.environ.get("TFX_FUSE_RES_BN_MASK", "1") != "0"
 _PENDING_SR: List["BNBackwardFusion"] = []
 
 
+# deferred forward finalizes (a projection-shortcut BN whose output is consumed only by the block's
+# tail BN): the next conv forward launch runs them in its tail blocks (conv_fwd_bn2)
+_PENDING_FIN: List[dict] = []
+# A/B switch for the deferred finalize
+_FIN_DEFER = os.environ.get("TFX_FIN_DEFER", "0") == "1"
+
+
 def reset_pending_slot_reductions() -> None:
-    """Forget deferred reductions of an abandoned step (an exception part-way through backward)."""
+    """Forget deferred reductions / finalizes of an abandoned step (an exception part-way through)."""
     for b in _PENDING_SR:
         b.sr_pending = False
     _PENDING_SR.clear()
+    _PENDING_FIN.clear()
+
+
+def _resolve_pending_fin(save: torch.Tensor) -> None:
+    """Make sure the deferred finalize that fills ``save`` has been issued (else issue it now)."""
+    for i, r in enumerate(_PENDING_FIN):
+        if r["save"] is save:
+            _PENDING_FIN.pop(i)
+            ga = r["args"]
+            torch.ops.tfx.bn_finalize_into(r["slots"], r["C"], r["M"], ga[0], ga[1], ga[2], ga[3], ga[4], ga[5],
+                                           r["save"])
+            return
 
 
 def _resolve_pending(b: "BNBackwardFusion") -> None:
@@ -547,6 +584,8 @@ class _BatchNorm(torch.autograd.Function):
             # (bn_apply_res_bn), or materialize it for the other paths (autograd still routes its
             # gradient to that BN: the lazy tensor stays this Function's input)
             res_lazy = res is not None and res_bnb is not None and res_bnb.deferred
+            if res_lazy:
+                _resolve_pending_fin(res_bnb.save)  # no conv launch took its deferred finalize
             fuse_res = res_lazy and pending and relu
             if res_lazy and not fuse_res:
                 res = torch.ops.tfx.bn_apply_train(res_bnb.x, None, res_bnb.save, False)[0]
@@ -565,6 +604,8 @@ class _BatchNorm(torch.autograd.Function):
             elif pending:
                 # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
                 save, wsobj.pending_save = wsobj.pending_save, None
+                if not defer_out:
+                    _resolve_pending_fin(save)  # this BN applies now: its deferred finalize must have run
                 if fuse_res:
                     y, mask = torch.ops.tfx.bn_apply_res_bn(x, res_bnb.x, save, res_bnb.save, relu)
                 elif defer_out:

@@ -156,3 +156,38 @@ def test_deferred_slot_reductions_fallback_and_off_agree(gpu):
         for gx, tag in ((g2, "fallback"), (g3, "off")):
             e = (gx[sl] - g0[sl]).norm().item() / n
             assert e <= max(4 * noise, 1e-3), (tag, v.name, e, noise)
+
+
+def test_deferred_shortcut_finalize_matches_immediate(gpu):
+    """The projection-shortcut BN's forward finalize deferred into the tail blocks of the next conv
+    launch (conv_fwd_bn2 fin_*), or resolved late by its consumer (bn_finalize_into), gives the same
+    loss, running statistics and gradients as the immediate finalize."""
+    from tensorflow_examples_amd import ops
+    from tensorflow_examples_amd.ops import nn as nnops
+
+    g = torch.Generator().manual_seed(6)
+    img = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 10, (32,), generator=g).to(gpu)
+    xin = to_model_input(img.to(gpu))
+
+    def run():
+        st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=4)
+        st.zero_grad()
+        loss = ops.softmax_cross_entropy(m(xin, training=True), lab)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert not nnops._PENDING_FIN, "a deferred finalize was never issued"
+        return float(loss), st.grad.clone(), {k: t.clone() for k, t in st.state.items()}
+
+    saved = nnops._FIN_DEFER
+    try:
+        nnops._FIN_DEFER = False
+        l0, g0, s0 = run()
+        nnops._FIN_DEFER = True
+        l1, g1, s1 = run()
+    finally:
+        nnops._FIN_DEFER = saved
+    assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0)), (l0, l1)
+    for k in s0:
+        assert torch.allclose(s0[k], s1[k], rtol=1e-4, atol=1e-5), k
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
