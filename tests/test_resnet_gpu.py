@@ -183,11 +183,15 @@ def test_deferred_shortcut_finalize_matches_immediate(gpu):
     try:
         nnops._FIN_DEFER = False
         l0, g0, s0 = run()
+        la, ga, sa = run()  # noise floor: the epilogue's f32-atomic statistics sum in any order
         nnops._FIN_DEFER = True
         l1, g1, s1 = run()
     finally:
         nnops._FIN_DEFER = saved
-    assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0)), (l0, l1)
+    assert abs(l1 - l0) <= 4 * abs(la - l0) + 2e-3 * abs(l0), (l0, la, l1)
     for k in s0:
-        assert torch.allclose(s0[k], s1[k], rtol=1e-4, atol=1e-5), k
-    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
+        noise = (sa[k] - s0[k]).abs().max().item()
+        assert (s1[k] - s0[k]).abs().max().item() <= 4 * noise + 1e-4 * s0[k].abs().max().item() + 1e-6, k
+    eg = ((g1 - g0).norm() / g0.norm()).item()
+    en = ((ga - g0).norm() / g0.norm()).item()
+    assert eg <= 4 * en + 1e-3, (eg, en)
