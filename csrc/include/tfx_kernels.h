@@ -189,6 +189,9 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
 // ---------------------------------------------------------------- loss / pooling
 void softmax_xent(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,
                   bool naive, float gscale, float* loss_rows, float* dz, float* probs, hipStream_t s);
+// single-block variant for small batches: batch-mean loss + dz (f32 or bf16) in one launch
+void softmax_xent_mean(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,
+                       bool naive, float gscale, float* loss_mean, void* dz, bool dz_bf16, hipStream_t s);
 void accuracy_count(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,
                     float* count, hipStream_t s);
 void gap_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y16, float* y32, hipStream_t s);

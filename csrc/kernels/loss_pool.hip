@@ -18,15 +18,18 @@ __device__ __forceinline__ float ld<float>(const float* p, int64_t i) { return p
 template <>
 __device__ __forceinline__ float ld<uint16_t>(const uint16_t* p, int64_t i) { return bf16_to_f32(p[i]); }
 
-template <typename TIN>
-__global__ void __launch_bounds__(256) softmax_xent_kernel(const TIN* __restrict__ z, int B, int C,
-                                                           const int64_t* __restrict__ lab_idx,
-                                                           const float* __restrict__ lab_dense, int naive,
-                                                           float gscale, float* __restrict__ loss_rows,
-                                                           float* __restrict__ dz, float* __restrict__ probs) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;
+template <typename T>
+__device__ __forceinline__ void st_dz(T* p, int64_t i, float v);
+template <>
+__device__ __forceinline__ void st_dz<float>(float* p, int64_t i, float v) { p[i] = v; }
+template <>
+__device__ __forceinline__ void st_dz<uint16_t>(uint16_t* p, int64_t i, float v) { p[i] = f32_to_bf16(v); }
+
+// One row on one wave; returns the row's loss (every lane holds it).
+template <typename TIN, typename TDZ>
+__device__ __forceinline__ float xent_row(const TIN* __restrict__ z, int row, int C, int lane,
+                                          const int64_t* __restrict__ lab_idx, const float* __restrict__ lab_dense,
+                                          int naive, float gscale, TDZ* __restrict__ dz, float* __restrict__ probs) {
   const TIN* zr = z + (int64_t)row * C;
   float m = -INFINITY;
   for (int c = lane; c < C; c += 64) m = fmaxf(m, ld(zr, c));
@@ -53,8 +56,7 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(const TIN* __restrict
   }
   loss = wave_sum(loss);
   if (naive) gp = wave_sum(gp);
-  if (lane == 0 && loss_rows) loss_rows[row] = loss;
-  if (!dz && !probs) return;
+  if (!dz && !probs) return loss;
   for (int c = lane; c < C; c += 64) {
     const float zc = ld(zr, c);
     const float p = __expf(zc - m) * inv_s;
@@ -68,8 +70,45 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(const TIN* __restrict
       } else {
         d = (p - y) * gscale;
       }
-      dz[(int64_t)row * C + c] = d;
+      st_dz(dz, (int64_t)row * C + c, d);
     }
+  }
+  return loss;
+}
+
+template <typename TIN>
+__global__ void __launch_bounds__(256) softmax_xent_kernel(const TIN* __restrict__ z, int B, int C,
+                                                           const int64_t* __restrict__ lab_idx,
+                                                           const float* __restrict__ lab_dense, int naive,
+                                                           float gscale, float* __restrict__ loss_rows,
+                                                           float* __restrict__ dz, float* __restrict__ probs) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float loss = xent_row(z, row, C, lane, lab_idx, lab_dense, naive, gscale, dz, probs);
+  if (lane == 0 && loss_rows) loss_rows[row] = loss;
+}
+
+// Small batches (the training step's loss): one block of 16 waves walks every row and also writes
+// the batch-mean loss (fixed-order LDS sum: deterministic), with dz stored in the logits' dtype --
+// the separate mean-reduction and scale/cast launches of the training step's loss are gone.
+template <typename TIN, typename TDZ>
+__global__ void __launch_bounds__(1024) softmax_xent_mean_kernel(const TIN* __restrict__ z, int B, int C,
+                                                                 const int64_t* __restrict__ lab_idx,
+                                                                 const float* __restrict__ lab_dense, int naive,
+                                                                 float gscale, float* __restrict__ loss_mean,
+                                                                 TDZ* __restrict__ dz) {
+  __shared__ float part[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int row = w; row < B; row += 16) acc += xent_row(z, row, C, lane, lab_idx, lab_dense, naive, gscale, dz,
+                                                        (float*)nullptr);
+  if (lane == 0) part[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < 16; ++i) t += part[i];
+    loss_mean[0] = t / (float)B;
   }
 }
 
@@ -184,6 +223,22 @@ void softmax_xent(const void* z, bool z_bf16, int B, int C, const int64_t* lab_i
   else
     softmax_xent_kernel<float><<<grid, 256, 0, s>>>((const float*)z, B, C, lab_idx, lab_dense, naive, gscale,
                                                     loss_rows, dz, probs);
+}
+
+void softmax_xent_mean(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,
+                       bool naive, float gscale, float* loss_mean, void* dz, bool dz_bf16, hipStream_t s) {
+  if (z_bf16 && dz_bf16)
+    softmax_xent_mean_kernel<uint16_t, uint16_t><<<1, 1024, 0, s>>>((const uint16_t*)z, B, C, lab_idx, lab_dense,
+                                                                  naive, gscale, loss_mean, (uint16_t*)dz);
+  else if (z_bf16)
+    softmax_xent_mean_kernel<uint16_t, float><<<1, 1024, 0, s>>>((const uint16_t*)z, B, C, lab_idx, lab_dense,
+                                                               naive, gscale, loss_mean, (float*)dz);
+  else if (dz_bf16)
+    softmax_xent_mean_kernel<float, uint16_t><<<1, 1024, 0, s>>>((const float*)z, B, C, lab_idx, lab_dense, naive,
+                                                               gscale, loss_mean, (uint16_t*)dz);
+  else
+    softmax_xent_mean_kernel<float, float><<<1, 1024, 0, s>>>((const float*)z, B, C, lab_idx, lab_dense, naive,
+                                                            gscale, loss_mean, (float*)dz);
 }
 
 void accuracy_count(const void* z, bool z_bf16, int B, int C, const int64_t* lab_idx, const float* lab_dense,

@@ -888,6 +888,37 @@ std::tuple<Tensor, Tensor> softmax_xent(Tensor z, optional<Tensor> lab_idx, opti
   return {loss, dz};
 }
 
+// Batch-mean loss (0-dim f32) and dz = d(mean)/dz in one single-block launch, dz in the logits'
+// dtype when dz_native (bf16 logits get a bf16 gradient: no scale/cast launch in backward).
+std::tuple<Tensor, Tensor> softmax_xent_mean(Tensor z, optional<Tensor> lab_idx, optional<Tensor> lab_dense,
+                                             bool naive, bool want_grad, bool dz_native) {
+  CHECK_DEV(z); CHECK_CONTIG(z);
+  TORCH_CHECK(z.dim() == 2, "logits must be [B,C]");
+  const bool zb = z.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(zb || z.scalar_type() == at::kFloat, "logits dtype");
+  const int64_t B = z.size(0), C = z.size(1);
+  TORCH_CHECK(B >= 1 && B * ((C + 63) / 64) <= 1024, "softmax_xent_mean: batch too large for one block");
+  const int64_t* li = nullptr;
+  const float* ld = nullptr;
+  if (lab_idx.has_value() && lab_idx->defined()) {
+    CHECK_DEV(*lab_idx);
+    TORCH_CHECK(lab_idx->scalar_type() == at::kLong && lab_idx->numel() == B && lab_idx->is_contiguous(), "labels");
+    li = lab_idx->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(lab_dense.has_value() && lab_dense->defined(), "need labels");
+    CHECK_F32(*lab_dense); CHECK_CONTIG(*lab_dense);
+    TORCH_CHECK(lab_dense->size(0) == B && lab_dense->size(1) == C, "dense labels shape");
+    ld = lab_dense->data_ptr<float>();
+  }
+  auto loss = at::empty({}, z.options().dtype(at::kFloat));
+  const bool db = dz_native && zb;
+  Tensor dz;
+  if (want_grad) dz = at::empty({B, C}, z.options().dtype(db ? at::kBFloat16 : at::kFloat));
+  tfx::softmax_xent_mean(z.data_ptr(), zb, (int)B, (int)C, li, ld, naive, 1.0f / (float)B, loss.data_ptr<float>(),
+                         want_grad ? dz.data_ptr() : nullptr, db, cur_stream());
+  return {loss, dz};
+}
+
 Tensor accuracy_count(Tensor z, optional<Tensor> lab_idx, optional<Tensor> lab_dense) {
   CHECK_DEV(z); CHECK_CONTIG(z);
   const bool zb = z.scalar_type() == at::kBFloat16;
@@ -1526,6 +1557,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_bwd(Tensor g, Tensor x, Tensor? res, Tensor save, bool relu, Tensor slots, Tensor? dgamma, "
         "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);
   m.def("softmax_xent", &softmax_xent);
+  m.def("softmax_xent_mean", &softmax_xent_mean);
   m.def("accuracy_count", &accuracy_count);
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);

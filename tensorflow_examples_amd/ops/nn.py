@@ -938,16 +938,25 @@ def avg_pool2d(x, ksize: int = 2, stride: Optional[int] = None, pad: int = 0):
 # ====================================================================== losses / metrics
 class _SoftmaxXent(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, labels, naive):
+    def forward(ctx, logits, labels, naive, unit_seed=False):
         ctx.native = _native.use_native(logits)
+        ctx.unit_seed = False
         B, C = logits.shape
         if ctx.native:
-            idx = labels if labels.dtype == torch.long else None
+            idx = labels.contiguous() if labels.dtype == torch.long else None
             dense = labels.float().contiguous() if labels.dtype != torch.long else None
+            ctx.dtype = logits.dtype
+            if B * ((C + 63) // 64) <= 1024:
+                # one launch: the mean loss and dz (already in the logits' dtype when the caller
+                # promises a unit seed gradient, so backward launches nothing)
+                loss, dz = torch.ops.tfx.softmax_xent_mean(logits.contiguous(), idx, dense, naive,
+                                                           bool(ctx.needs_input_grad[0]), bool(unit_seed))
+                ctx.unit_seed = bool(unit_seed) and dz is not None and dz.dtype == logits.dtype
+                ctx.save_for_backward(dz)
+                return loss
             loss_rows, dz = torch.ops.tfx.softmax_xent(logits.contiguous(), idx, dense, naive, 1.0 / B,
                                                        bool(ctx.needs_input_grad[0]))
             ctx.save_for_backward(dz)
-            ctx.dtype = logits.dtype
             return loss_rows.mean()
         ctx.save_for_backward(logits, labels)
         ctx.naive = naive
@@ -957,15 +966,17 @@ class _SoftmaxXent(torch.autograd.Function):
     def backward(ctx, g):
         if ctx.native:
             (dz,) = ctx.saved_tensors
+            if ctx.unit_seed:
+                return dz, None, None, None
             # upstream scale (1.0 for loss.backward()) + cast in one HIP launch
             gs = g.reshape(1).float().contiguous()
-            return torch.ops.tfx.scale_by_scalar(dz, gs, ctx.dtype == torch.bfloat16), None, None
+            return torch.ops.tfx.scale_by_scalar(dz, gs, ctx.dtype == torch.bfloat16), None, None, None
         logits, labels = ctx.saved_tensors
         with torch.enable_grad():
             z = logits.detach().requires_grad_(True)
             loss = _xent_ref(z, labels, ctx.naive)
             (dz,) = torch.autograd.grad(loss, [z], g)
-        return dz, None, None
+        return dz, None, None, None
 
 
 def _xent_ref(logits, labels, naive):
@@ -980,10 +991,12 @@ def _xent_ref(logits, labels, naive):
     return (-(y * torch.log_softmax(z, dim=1)).sum(1)).mean()
 
 
-def softmax_cross_entropy(logits, labels, naive: bool = False):
+def softmax_cross_entropy(logits, labels, naive: bool = False, unit_seed: bool = False):
     """Mean softmax cross-entropy. ``labels``: int64 class ids or dense [B,C] targets.
-    ``naive=True`` reproduces TF1's ``reduce_mean(-reduce_sum(y_*log(softmax(z))))``."""
-    return _SoftmaxXent.apply(logits, labels, naive)
+    ``naive=True`` reproduces TF1's ``reduce_mean(-reduce_sum(y_*log(softmax(z))))``.
+    ``unit_seed=True`` is the caller's promise that backward is seeded with exactly 1 (the loss is
+    the root, ``loss.backward()``): the gradient then leaves the forward launch ready to use."""
+    return _SoftmaxXent.apply(logits, labels, naive, unit_seed)
 
 
 def accuracy(logits, labels) -> torch.Tensor:

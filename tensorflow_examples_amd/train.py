@@ -36,7 +36,7 @@ class ClassifierTrainer:
         self.store.zero_grad()
         with trace.range("forward"):
             logits = self.model(x, training=True)
-            loss = ops.softmax_cross_entropy(logits, y, naive=self.naive)
+            loss = ops.softmax_cross_entropy(logits, y, naive=self.naive, unit_seed=True)  # seeded by _one
         with trace.range("backward"):
             # a persistent unit seed gradient: no ones-fill launch per step (graph-safe: never written)
             one = self._one

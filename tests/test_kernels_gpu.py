@@ -8,6 +8,7 @@ import math
 import pytest
 import torch
 import torch.nn.functional as F
+from tensorflow_examples_amd import ops
 
 pytestmark = pytest.mark.gpu
 
@@ -203,6 +204,40 @@ def test_softmax_xent(gpu, naive, dense):
     assert torch.allclose(dz, zr.grad, atol=1e-5, rtol=1e-3)
     cnt = torch.ops.tfx.accuracy_count(z, lab, None)
     assert cnt.item() == (z.argmax(1) == lab).sum().item()
+
+
+@pytest.mark.parametrize("naive", [False, True])
+@pytest.mark.parametrize("dense", [False, True])
+@pytest.mark.parametrize("B,C,bf16", [(256, 10, True), (100, 10, False), (1024, 10, True), (7, 130, True)])
+def test_softmax_xent_mean(gpu, naive, dense, B, C, bf16):
+    """Single-launch mean loss + dz (the training step's loss): fp32 reference of the same op, and
+    the unit-seed autograd path returns the same gradient as the scaled one."""
+    torch.manual_seed(5)
+    z = (torch.randn(B, C, device=gpu) * 3)
+    if bf16:
+        z = z.bfloat16()
+    lab = torch.randint(0, C, (B,), device=gpu)
+    y = F.one_hot(lab, C).float()
+    for native_dz in (False, True):
+        loss, dz = torch.ops.tfx.softmax_xent_mean(z, None if dense else lab, y if dense else None, naive, True,
+                                                   native_dz)
+        assert loss.dim() == 0 and dz.dtype == (z.dtype if native_dz else torch.float32)
+        zr = z.float().clone().requires_grad_(True)
+        if naive:
+            lr = (-(y * torch.log(torch.softmax(zr, 1))).sum(1)).mean()
+        else:
+            lr = (-(y * torch.log_softmax(zr, 1)).sum(1)).mean()
+        lr.backward()
+        assert abs(loss.item() - lr.item()) < 1e-4 * max(1.0, abs(lr.item()))
+        tol = 4e-3 if dz.dtype == torch.bfloat16 else 1e-3
+        assert torch.allclose(dz.float(), zr.grad, atol=1e-5, rtol=tol)
+    # autograd: unit-seed gradient (ready in the forward) == the scaled/cast backward
+    grads = []
+    for unit in (False, True):
+        zz = z.clone().requires_grad_(True)
+        ops.softmax_cross_entropy(zz, y if dense else lab, naive=naive, unit_seed=unit).backward()
+        grads.append(zz.grad.float())
+    assert torch.allclose(grads[0], grads[1], atol=1e-6, rtol=1e-2)
 
 
 @pytest.mark.parametrize("shape", [(4, 4, 4, 2048), (256, 4, 4, 2048), (3, 5, 3, 12), (2, 8, 8, 64)])
