@@ -84,7 +84,7 @@ def run(a):
     import torch.distributed as dist
 
     from tensorflow_examples_amd.data.pipeline import PinnedRing
-    from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
+    from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_batch, to_model_input
     from tensorflow_examples_amd.optim import MomentumOptimizer
     from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed
     from tensorflow_examples_amd.parallel.launch import control_device, control_group as _control_group, verify_world
@@ -132,11 +132,11 @@ def run(a):
 
         def step(i):
             img, lab = batch(i)
-            if img.device.type == "cpu" and cuda:  # zero-copy ring: pinned host tensors
-                lab = lab.to(dev, non_blocking=True)
-            # graphed: the input kernel writes straight into the graph's static input buffer
-            x = to_model_input(img, dtype=dtype, device=dev, out=trainer.input_buffer())
-            return trainer.step(x, lab)
+            # graphed: the input kernel writes straight into the graph's static input and label
+            # buffers (zero-copy ring: reading the pinned host slot over the host link)
+            x, y = to_model_batch(img, lab, dtype=dtype, device=dev, out=trainer.input_buffer(),
+                                  labels_out=trainer.label_buffer())
+            return trainer.step(x, y)
 
         if cuda and a.graph and ((world == 1 and not forced) or os.environ.get("TFX_DP_GRAPH", "1") == "1"):
             # the captured step is the same work (forward, backward with the bucketed RCCL

@@ -265,7 +265,8 @@ void lstm_seq_bwd(const float* act, const float* cbuf, const uint16_t* dH, const
 void augment_normalize(const uint8_t* x, int N, int H, int W, int cin, int cout, int pad, const int32_t* off,
                        const float* mean, const float* stdv, uint16_t* y, hipStream_t s);
 void image_normalize(const uint8_t* x, int64_t npix, int cin, int cout, const float* mean, const float* stdv,
-                     uint16_t* y, hipStream_t s);
+                     uint16_t* y, hipStream_t s,
+                     const int64_t* lab = nullptr, int64_t* lab_out = nullptr, int nlab = 0);
 
 // ---------------------------------------------------------------- ps transport over xGMI peer memory
 // p -= lr*g on a (peer-mapped) arena range (g zeroed as consumed if zero_g); then, if step != null,

@@ -3,7 +3,9 @@
 // y[p][c] = (x[p][c] / 255 - mean[c]) / std[c] for c < cin, 0 for cin <= c < cout (the stem's padded
 // channels, which must stay exactly zero).  One thread per pixel: cin byte loads, one 16-byte store
 // for cout = 8.  Replaces the ~8 elementwise launches (cast, scale, subtract, divide, zero-fill,
-// slice copy) of the PyTorch formulation at the head of every training step.
+// slice copy) of the PyTorch formulation at the head of every training step.  Optionally the batch's
+// int64 labels ride along (lab -> lab_out), so a captured step's static label buffer is filled by the
+// same launch instead of a separate copy.
 #include "tfx_common.h"
 #include "tfx_kernels.h"
 
@@ -17,7 +19,10 @@ struct Norm4 {
 
 template <int COUT>
 __global__ void __launch_bounds__(256) image_norm_kernel(const uint8_t* __restrict__ x, int64_t npix, int cin,
-                                                         Norm4 nm, uint16_t* __restrict__ y) {
+                                                         Norm4 nm, uint16_t* __restrict__ y,
+                                                         const int64_t* __restrict__ lab, int64_t* __restrict__ lab_out,
+                                                         int nlab) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nlab; i += gridDim.x * 256) lab_out[i] = lab[i];
   for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < npix; p += (int64_t)gridDim.x * 256) {
     float f[COUT];
 #pragma unroll
@@ -82,7 +87,7 @@ void augment_normalize(const uint8_t* x, int N, int H, int W, int cin, int cout,
 }
 
 void image_normalize(const uint8_t* x, int64_t npix, int cin, int cout, const float* mean, const float* stdv,
-                     uint16_t* y, hipStream_t s) {
+                     uint16_t* y, hipStream_t s, const int64_t* lab, int64_t* lab_out, int nlab) {
   Norm4 nm{};
   for (int c = 0; c < 4; ++c) {
     const float m = c < cin ? mean[c] : 0.f, sd = c < cin ? stdv[c] : 1.f;
@@ -92,8 +97,8 @@ void image_normalize(const uint8_t* x, int64_t npix, int cin, int cout, const fl
   int64_t g = (npix + 255) / 256;
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
-  if (cout == 8) image_norm_kernel<8><<<(int)g, 256, 0, s>>>(x, npix, cin, nm, y);
-  else image_norm_kernel<4><<<(int)g, 256, 0, s>>>(x, npix, cin, nm, y);
+  if (cout == 8) image_norm_kernel<8><<<(int)g, 256, 0, s>>>(x, npix, cin, nm, y, lab, lab_out, nlab);
+  else image_norm_kernel<4><<<(int)g, 256, 0, s>>>(x, npix, cin, nm, y, lab, lab_out, nlab);
 }
 
 }  // namespace tfx

@@ -101,8 +101,99 @@ __global__ void __launch_bounds__(1024) softmax_xent_mean_kernel(const TIN* __re
   __shared__ float part[16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float acc = 0.f;
-  for (int row = w; row < B; row += 16) acc += xent_row(z, row, C, lane, lab_idx, lab_dense, naive, gscale, dz,
-                                                        (float*)nullptr);
+  if (C <= 32) {
+    // thread = row: the whole row lives in one thread's registers (no cross-lane reductions, whose
+    // serial shuffle latency -- ~3 per row -- dominates a one-block launch)
+    for (int row = threadIdx.x; row < B; row += 1024) {
+      float zv[32];
+      const int64_t lab = lab_idx ? lab_idx[row] : -1;
+      float m = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 32; ++c)
+        if (c < C) {
+          zv[c] = ld(z, (int64_t)row * C + c);
+          m = fmaxf(m, zv[c]);
+        }
+      float sum = 0.f;
+#pragma unroll
+      for (int c = 0; c < 32; ++c)
+        if (c < C) sum += __expf(zv[c] - m);
+      const float inv_s = 1.f / sum, lse = m + __logf(sum);
+      float l = 0.f, gp = 0.f;
+#pragma unroll
+      for (int c = 0; c < 32; ++c)
+        if (c < C) {
+          const float y = lab_dense ? lab_dense[(int64_t)row * C + c] : (c == lab ? 1.f : 0.f);
+          if (naive) {
+            const float p = __expf(zv[c] - m) * inv_s;
+            if (y != 0.f) {
+              l -= y * logf(p);
+              gp += -y / p * gscale * p;
+            }
+          } else if (y != 0.f) {
+            l += y * (lse - zv[c]);
+          }
+        }
+      if (dz) {
+#pragma unroll
+        for (int c = 0; c < 32; ++c)
+          if (c < C) {
+            const float y = lab_dense ? lab_dense[(int64_t)row * C + c] : (c == lab ? 1.f : 0.f);
+            const float p = __expf(zv[c] - m) * inv_s;
+            float d;
+            if (naive) {
+              const float g = y != 0.f ? -y / p * gscale : 0.f;
+              d = (g - gp) * p;
+            } else {
+              d = (p - y) * gscale;
+            }
+            st_dz(dz, (int64_t)row * C + c, d);
+          }
+      }
+      acc += l;
+    }
+    acc = wave_sum(acc);
+  } else if (C <= 64) {
+    // lane = class: every load of a chunk of RPW rows is issued before any math (one memory round
+    // trip per chunk instead of ~5 dependent ones per row), then the rows reduce from registers
+    constexpr int RPW = 16;
+    for (int base = w; base < B; base += 16 * RPW) {
+      float zc[RPW], yv[RPW];
+#pragma unroll
+      for (int k = 0; k < RPW; ++k) {
+        const int row = base + 16 * k;
+        const bool v = row < B && lane < C;
+        zc[k] = v ? ld(z, (int64_t)row * C + lane) : -INFINITY;
+        if (lab_dense) yv[k] = v ? lab_dense[(int64_t)row * C + lane] : 0.f;
+        else yv[k] = (v && lab_idx[row] == lane) ? 1.f : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < RPW; ++k) {
+        const int row = base + 16 * k;
+        if (row >= B) break;  // wave-uniform
+        const bool v = lane < C;
+        const float m = wave_max(zc[k]);
+        const float e = v ? __expf(zc[k] - m) : 0.f;
+        const float sum = wave_sum(e);
+        const float p = e / sum, y = yv[k];
+        float l, d;
+        if (naive) {
+          l = wave_sum(y != 0.f ? -y * logf(p) : 0.f);
+          const float g = y != 0.f ? -y / p * gscale : 0.f;
+          const float gp = wave_sum(g * p);
+          d = (g - gp) * p;
+        } else {
+          l = wave_sum(y != 0.f ? y * (m + __logf(sum) - zc[k]) : 0.f);
+          d = (p - y) * gscale;
+        }
+        if (dz && v) st_dz(dz, (int64_t)row * C + lane, d);
+        acc += l;
+      }
+    }
+  } else {
+    for (int row = w; row < B; row += 16) acc += xent_row(z, row, C, lane, lab_idx, lab_dense, naive, gscale, dz,
+                                                          (float*)nullptr);
+  }
   if (lane == 0) part[w] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {

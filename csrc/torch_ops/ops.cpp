@@ -1464,7 +1464,19 @@ bool end_stream_capture(int64_t stream) {
   return true;
 }
 
-void image_normalize_into(Tensor x, std::vector<double> mean, std::vector<double> stdv, Tensor out) {
+// Host pointer of a pinned (page-locked) tensor as the GPU sees it (zero-copy reads over the host link).
+static const void* pinned_device_ptr(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_pinned(), what, ": a host input must be pinned (page-locked)");
+  void* dp = nullptr;
+  TORCH_CHECK(hipHostGetDevicePointer(&dp, const_cast<void*>(t.data_ptr()), 0) == hipSuccess && dp, what,
+              ": pinned host buffer is not mapped into the GPU's address space");
+  return dp;
+}
+
+// labels / labels_out (optional, int64 [N]): copied by the same launch (a pinned host source is read
+// zero-copy), e.g. into a captured step's static label buffer.
+void image_normalize_into(Tensor x, std::vector<double> mean, std::vector<double> stdv, Tensor out,
+                          optional<Tensor> labels, optional<Tensor> labels_out) {
   CHECK_CONTIG(x); CHECK_DEV(out); CHECK_CONTIG(out); CHECK_BF16(out);
   TORCH_CHECK(x.scalar_type() == at::kByte, "image_normalize_into: uint8 images");
   const int64_t cin = x.size(-1), cout = out.size(-1);
@@ -1474,19 +1486,27 @@ void image_normalize_into(Tensor x, std::vector<double> mean, std::vector<double
   TORCH_CHECK(x.numel() / cin == out.numel() / cout && x.dim() == out.dim(),
               "image_normalize_into: pixel counts of x and out differ");
   const uint8_t* src = x.data_ptr<uint8_t>();
-  if (!x.is_cuda()) {
-    TORCH_CHECK(x.is_pinned(), "image_normalize_into: a host input must be pinned (page-locked)");
-    void* dp = nullptr;
-    TORCH_CHECK(hipHostGetDevicePointer(&dp, const_cast<uint8_t*>(src), 0) == hipSuccess && dp,
-                "image_normalize_into: pinned host buffer is not mapped into the GPU's address space");
-    src = static_cast<const uint8_t*>(dp);
-  }
+  if (!x.is_cuda()) src = static_cast<const uint8_t*>(pinned_device_ptr(x, "image_normalize_into"));
   float m[4] = {0, 0, 0, 0}, s[4] = {1, 1, 1, 1};
   for (int64_t c = 0; c < cin; ++c) {
     m[c] = (float)mean[c];
     s[c] = (float)stdv[c];
   }
-  tfx::image_normalize(src, x.numel() / cin, (int)cin, (int)cout, m, s, bfm(out), cur_stream());
+  const int64_t* lab = nullptr;
+  int64_t* lab_out = nullptr;
+  int nlab = 0;
+  if (labels.has_value() && labels->defined()) {
+    TORCH_CHECK(labels_out.has_value() && labels_out->defined(), "image_normalize_into: labels need labels_out");
+    const Tensor& l = *labels;
+    const Tensor& lo = *labels_out;
+    CHECK_DEV(lo); CHECK_CONTIG(lo); CHECK_CONTIG(l);
+    TORCH_CHECK(l.scalar_type() == at::kLong && lo.scalar_type() == at::kLong && l.numel() == lo.numel() &&
+                l.numel() < (1 << 30), "image_normalize_into: int64 labels of equal size");
+    lab = l.is_cuda() ? l.data_ptr<int64_t>() : static_cast<const int64_t*>(pinned_device_ptr(l, "labels"));
+    lab_out = lo.data_ptr<int64_t>();
+    nlab = (int)l.numel();
+  }
+  tfx::image_normalize(src, x.numel() / cin, (int)cin, (int)cout, m, s, bfm(out), cur_stream(), lab, lab_out, nlab);
 }
 
 }  // namespace

@@ -199,6 +199,25 @@ def build_resnet_cifar(device="cuda", depth=50, num_classes=10, dtype=torch.bflo
     return store, model
 
 
+def to_model_batch(images: torch.Tensor, labels: torch.Tensor, dtype=torch.bfloat16, device=None,
+                   out: Optional[torch.Tensor] = None, labels_out: Optional[torch.Tensor] = None):
+    """(images, labels) -> (model input, device labels).  With both static buffers (a captured step's
+    :meth:`ClassifierTrainer.input_buffer` / :meth:`label_buffer`) and uint8 images on the GPU or in
+    pinned host memory, the one input kernel writes both (no separate label copy launch); otherwise
+    :func:`to_model_input` plus a label copy."""
+    if out is not None and labels_out is not None and images.dtype == torch.uint8 and out.is_cuda and \
+            out.dtype == torch.bfloat16 and labels.dtype == torch.int64 and labels_out.is_cuda and \
+            (images.is_cuda or images.is_pinned()) and (labels.is_cuda or labels.is_pinned()) and \
+            _native.use_native_device(out.device):
+        torch.ops.tfx.image_normalize_into(images.contiguous(), list(_MEAN), list(_STD), out, labels.contiguous(),
+                                           labels_out)
+        return out, labels_out
+    x = to_model_input(images, dtype=dtype, device=device, out=out)
+    dev = torch.device(device) if device is not None else x.device
+    y = labels.to(dev, non_blocking=True) if labels.device != dev else labels
+    return x, y
+
+
 def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16, device=None,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[N,32,32,3] images -> [N,32,32,8] normalised NHWC compute tensor (channels 3..7 zero).
@@ -208,7 +227,7 @@ def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16, devi
     x = images_nhwc_u8_or_f
     if out is not None and x.dtype == torch.uint8 and out.is_cuda and out.dtype == torch.bfloat16 and \
             (x.is_cuda or x.is_pinned()) and _native.use_native_device(out.device):
-        torch.ops.tfx.image_normalize_into(x.contiguous(), list(_MEAN), list(_STD), out)
+        torch.ops.tfx.image_normalize_into(x.contiguous(), list(_MEAN), list(_STD), out, None, None)
         return out
     if x.dtype == torch.uint8 and dtype == torch.bfloat16 and x.device.type == "cuda" and _native.use_native(x):
         return torch.ops.tfx.image_normalize(x.contiguous(), list(_MEAN), list(_STD), IN_CH_PAD)
@@ -216,7 +235,7 @@ def to_model_input(images_nhwc_u8_or_f: torch.Tensor, dtype=torch.bfloat16, devi
             x.dtype == torch.uint8 and dtype == torch.bfloat16 and x.is_pinned():
         # zero-copy input: the kernel reads the pinned host batch directly (no H2D staging copy)
         out = torch.empty((*x.shape[:-1], IN_CH_PAD), dtype=dtype, device=device)
-        torch.ops.tfx.image_normalize_into(x.contiguous(), list(_MEAN), list(_STD), out)
+        torch.ops.tfx.image_normalize_into(x.contiguous(), list(_MEAN), list(_STD), out, None, None)
         return out
     if x.dtype == torch.uint8:
         x = x.float() / 255.0

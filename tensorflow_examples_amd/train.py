@@ -59,6 +59,10 @@ class ClassifierTrainer:
         batch into it directly, and :meth:`step` then skips the copy."""
         return self._static[0] if self.graph is not None else None
 
+    def label_buffer(self):
+        """The captured graph's static label tensor (None when eager), see :meth:`input_buffer`."""
+        return self._static[1] if self.graph is not None else None
+
     def step(self, x, y):
         if self.graph is not None:
             if x is not self._static[0]:

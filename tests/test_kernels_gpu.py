@@ -208,7 +208,7 @@ def test_softmax_xent(gpu, naive, dense):
 
 @pytest.mark.parametrize("naive", [False, True])
 @pytest.mark.parametrize("dense", [False, True])
-@pytest.mark.parametrize("B,C,bf16", [(256, 10, True), (100, 10, False), (1024, 10, True), (7, 130, True)])
+@pytest.mark.parametrize("B,C,bf16", [(256, 10, True), (100, 10, False), (1024, 10, True), (300, 40, True), (7, 130, True)])
 def test_softmax_xent_mean(gpu, naive, dense, B, C, bf16):
     """Single-launch mean loss + dz (the training step's loss): fp32 reference of the same op, and
     the unit-seed autograd path returns the same gradient as the scaled one."""

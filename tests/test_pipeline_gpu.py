@@ -72,7 +72,29 @@ def test_image_normalize_into_zero_copy_matches_reference(gpu):
     assert (pin_out.float().cpu() - ref).abs().max().item() < 2e-2
     assert float(pin_out[..., 3:].abs().max()) == 0.0
     with pytest.raises(RuntimeError):  # pageable host memory is refused, not silently copied
-        torch.ops.tfx.image_normalize_into(img, list(_MEAN), list(_STD), torch.empty_like(dev_out))
+        torch.ops.tfx.image_normalize_into(img, list(_MEAN), list(_STD), torch.empty_like(dev_out), None, None)
+
+
+def test_input_kernel_carries_labels(gpu):
+    """The input kernel copies the batch's labels (pinned host or device) into a label buffer in the
+    same launch; to_model_batch falls back to a plain copy without static buffers."""
+    from tensorflow_examples_amd.models.resnet import _MEAN, _STD, to_model_batch, to_model_input
+    g = torch.Generator().manual_seed(3)
+    img = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, generator=g).pin_memory()
+    lab = torch.randint(0, 10, (16,), dtype=torch.int64, generator=g).pin_memory()
+    ref = to_model_input(img.to(gpu))
+    xo = torch.empty_like(ref)
+    yo = torch.full((16,), -1, dtype=torch.int64, device=gpu)
+    x, y = to_model_batch(img, lab, device=gpu, out=xo, labels_out=yo)
+    torch.cuda.synchronize()
+    assert x is xo and y is yo and torch.equal(x, ref) and torch.equal(y.cpu(), lab)
+    yo2 = torch.full((16,), -1, dtype=torch.int64, device=gpu)
+    x2, y2 = to_model_batch(img.to(gpu), lab.to(gpu), device=gpu, out=torch.empty_like(ref), labels_out=yo2)
+    assert torch.equal(x2, ref) and torch.equal(y2.cpu(), lab)
+    x3, y3 = to_model_batch(img, lab, device=gpu)  # no static buffers: zero-copy image, copied labels
+    assert torch.equal(x3, ref) and y3.is_cuda and torch.equal(y3.cpu(), lab)
+    with pytest.raises(RuntimeError):  # pageable host labels are refused, not silently copied
+        torch.ops.tfx.image_normalize_into(img, list(_MEAN), list(_STD), torch.empty_like(ref), lab.clone(), yo)
 
 
 def test_zero_copy_ring_never_overwrites_a_queued_batch(gpu):
