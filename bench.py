@@ -130,12 +130,14 @@ def run(a):
         dp = GradAllReduce(store, bucket_bytes=int(a.bucket_mb * (1 << 20))) if dist.is_initialized() else None
         trainer = ClassifierTrainer(store, model, opt, dp)
 
+        label_fuse = os.environ.get("TFX_LABEL_FUSE", "1") == "1"  # 0: separate label copy (A/B)
+
         def step(i):
             img, lab = batch(i)
             # graphed: the input kernel writes straight into the graph's static input and label
             # buffers (zero-copy ring: reading the pinned host slot over the host link)
             x, y = to_model_batch(img, lab, dtype=dtype, device=dev, out=trainer.input_buffer(),
-                                  labels_out=trainer.label_buffer())
+                                  labels_out=trainer.label_buffer() if label_fuse else None)
             return trainer.step(x, y)
 
         if cuda and a.graph and ((world == 1 and not forced) or os.environ.get("TFX_DP_GRAPH", "1") == "1"):

@@ -496,6 +496,8 @@ _PENDING_SR: List["BNBackwardFusion"] = []
 _PENDING_FIN: List[dict] = []
 # A/B switch for the deferred finalize
 _FIN_DEFER = os.environ.get("TFX_FIN_DEFER", "0") == "1"
+# single-launch mean loss for small batches (TFX_XENT_MEAN=0: per-row kernel + mean + scale launches)
+_XENT_MEAN = os.environ.get("TFX_XENT_MEAN", "1") == "1"
 
 
 def reset_pending_slot_reductions() -> None:
@@ -946,7 +948,7 @@ class _SoftmaxXent(torch.autograd.Function):
             idx = labels.contiguous() if labels.dtype == torch.long else None
             dense = labels.float().contiguous() if labels.dtype != torch.long else None
             ctx.dtype = logits.dtype
-            if B * ((C + 63) // 64) <= 1024:
+            if _XENT_MEAN and B * ((C + 63) // 64) <= 1024:
                 # one launch: the mean loss and dz (already in the logits' dtype when the caller
                 # promises a unit seed gradient, so backward launches nothing)
                 loss, dz = torch.ops.tfx.softmax_xent_mean(logits.contiguous(), idx, dense, naive,
