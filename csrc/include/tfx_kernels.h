@@ -11,7 +11,6 @@ namespace tfx {
 
 // Cross-block reduction slots for per-channel statistics ([NSLOT][2][C] f32, see batchnorm.hip)
 constexpr int NSLOT = 64;
-constexpr int BN_CNT = 64;  // per-column-tile counters after the slots (N <= 64 * 64 columns)
 
 // Division by a runtime-invariant divisor via multiply-high (valid for n < 2^31).
 struct FastDiv {
@@ -78,19 +77,7 @@ struct IgemmArgs {
   int cls = 0, cph = 0, cpw = 0, cr0 = 0, cs0 = 0, wR = 1, wS = 1, out_H = 0, out_W = 0;
   FastDiv fd_cHW, fd_cW;
   // ---- fused batch-norm epilogues (per output column c; the BN layer's workspace holds the
-  // [NSLOT][2][N] slots and, after them, BN_CNT per-column-tile arrival counters, zero between uses)
-  // bn_final: the LAST block to finish each column tile (agent-scope release / acquire on its
-  //   counter) reduces that tile's slots -- forward (stats != nullptr): BN finalize into bn_save
-  //   [mean | invstd | scale | shift] + running stats; backward (bnb_x != nullptr): red = [sum g' |
-  //   sum g' xhat] and dbeta / dgamma += -- so no separate finalize / slot-reduce launch.
-  unsigned* bn_cnt = nullptr;
-  int bn_final = 0;
-  const float* bn_gamma = nullptr;
-  const float* bn_beta = nullptr;
-  float* bn_rmean = nullptr;
-  float* bn_rvar = nullptr;
-  float* bn_save = nullptr;
-  float bn_eps = 1e-5f, bn_momentum = 0.1f;
+  // [NSLOT][2][N] slots, zero between uses: the finalize / slot-reduce that consumes them re-zeroes)
   // backward partials of the BN whose OUTPUT gradient this dgrad produces: g' = bf16(out) * relu
   // mask (from x*scale+shift > 0, or the residual layer's mask bits), accumulated per column:
   // sum g' and sum g' * (x - mean) * invstd into bnb_slots
@@ -99,9 +86,6 @@ struct IgemmArgs {
   const uint8_t* bnb_mask = nullptr;
   int bnb_relu = 0;
   float* bnb_slots = nullptr;
-  float* bnb_red = nullptr;
-  float* bnb_dgamma = nullptr;
-  float* bnb_dbeta = nullptr;
   // optional tail blocks (weight-gradient launches): reduce ANOTHER BN layer's backward slots
   // ([NSLOT][2][sr_C], filled by an earlier data-gradient epilogue) into sr_red = [sum g' | sum g'
   // xhat] and dgamma / dbeta += -- bn_slot_reduce folded into this launch (16 channels per block,
@@ -117,18 +101,6 @@ struct IgemmArgs {
   float* sr2_dgamma = nullptr;
   float* sr2_dbeta = nullptr;
   int sr2_C = 0;
-  // optional tail blocks (forward launches): finalize ANOTHER BN layer's statistics ([NSLOT][2][fin_C]
-  // slots filled by an earlier conv epilogue) into fin_save = [mean | invstd | scale | shift] and its
-  // running statistics -- bn_finalize folded into an independent later launch.  fin_C == 0: none.
-  float* fin_slots = nullptr;
-  const float* fin_gamma = nullptr;
-  const float* fin_beta = nullptr;
-  float* fin_rmean = nullptr;
-  float* fin_rvar = nullptr;
-  float* fin_save = nullptr;
-  int64_t fin_M = 0;
-  float fin_eps = 1e-5f, fin_momentum = 0.1f;
-  int fin_C = 0;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;
 };
@@ -167,18 +139,6 @@ void bn_backward_apply_sec(const uint16_t* g, const uint16_t* x, const uint8_t* 
 void bn_backward_apply(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask,
                        const float* save, const float* red, int64_t M, int C, bool relu, uint16_t* dx,
                        uint16_t* dres, hipStream_t s);
-// slot-consuming passes (batchnorm.hip "slot-consuming passes"): the forward apply reduces the
-// forward statistics slots S_f itself (row group 0 writes save / running stats and zeroes
-// slots_zero = the layer's backward slots S_b); the backward apply reduces S_b itself (row group 0
-// accumulates dgamma / dbeta and zeroes slots_zero = S_f).  bn_slots_ok(C): C in {64,128,256} or a
-// multiple of 256.
-bool bn_slots_ok(int C);
-void bn_apply_slots(const uint16_t* x, const uint16_t* res, const float* slots_f, float* slots_zero, int64_t M, int C,
-                    const float* gamma, const float* beta, float eps, float momentum, float* run_mean, float* run_var,
-                    float* save, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s);
-void bn_bwd_apply_slots(const uint16_t* g, const uint16_t* x, const uint8_t* mask, bool has_res, const float* save,
-                        const float* slots_b, float* slots_zero, int64_t M, int C, bool relu, float* dgamma,
-                        float* dbeta, uint16_t* dx, uint16_t* dres, hipStream_t s);
 // backward partials (sum g', sum g' xhat) of the vector path into slots (no slot reduce)
 void bn_bwd_reduce(const uint16_t* g, const uint16_t* x, const uint8_t* mask, bool has_res, const float* save,
                    int64_t M, int C, bool relu, float* slots, hipStream_t s);

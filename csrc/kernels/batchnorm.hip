@@ -500,279 +500,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_gen_kernel(const uint16_t* _
   }
 }
 
-// ================================================================== slot-consuming passes
-// The forward apply and the backward apply reduce the layer's statistics slots THEMSELVES, so a
-// BN layer costs one launch per direction instead of two (no bn_finalize / bn_slot_reduce: those
-// were 106 launches of ~5 us per ResNet-50 step, profiles/r02_head).  Grid = (C / CS channel slabs)
-// x row groups, CS = min(C, 256): every block sums the NSLOT slot rows of its slab's channels (one
-// round trip, issued together with its first tensor loads), derives the per-channel coefficients
-// into LDS, then streams rows with a fixed 8-channel vector per thread.
-//
-// Slot lifetime (two slot sets per layer, S_f = forward statistics, S_b = backward partials):
-//   S_f: producer conv epilogue (atomics) -> read by every block of bn_apply_slots -> zeroed by
-//        row group 0 of the SAME layer's bn_bwd_apply_slots (it runs later in the step);
-//   S_b: producer dgrad epilogue / bn_bwd_reduce -> read by bn_bwd_apply_slots -> zeroed by row
-//        group 0 of the layer's next bn_apply_slots (next step's forward).
-// No block zeroes slots another block of its own launch still reads.  Row group 0 alone also
-// writes save = [mean | invstd | scale | shift] and the running statistics (forward) or
-// accumulates dgamma / dbeta (backward).
-constexpr int SLAB = 256;
-constexpr int SU = 4;  // rows per thread in flight in the slot-consuming passes
-
-// sums of the slab's NSLOT slot rows per channel -> (s, q) of channel c_base + t for t < CS
-__device__ __forceinline__ void slab_slot_sums(const float* __restrict__ slots, int C, int c_base, int CS,
-                                               float* lds2x256, float& s, float& q) {
-  const int t = threadIdx.x, G = 256 / CS, cl = t % CS, grp = t / CS;
-  const int per = NSLOT / G;  // G in {1, 2, 4}: slot rows per thread, 16 in flight at a time
-  s = 0.f;
-  q = 0.f;
-  for (int k0 = 0; k0 < per; k0 += 16) {
-    float vs[16], vq[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const float* row = slots + (size_t)(grp + (k0 + k) * G) * 2 * C + c_base + cl;
-      vs[k] = row[0];
-      vq[k] = row[C];
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      s += vs[k];
-      q += vq[k];
-    }
-  }
-  lds2x256[t] = s;
-  lds2x256[256 + t] = q;
-  __syncthreads();
-  if (t < CS) {
-    for (int g = 1; g < G; ++g) {
-      s += lds2x256[g * CS + t];
-      q += lds2x256[256 + g * CS + t];
-    }
-  }
-}
-
-__device__ __forceinline__ void slab_zero(float* __restrict__ slots, int C, int c_base, int CS) {
-  for (int i = threadIdx.x; i < NSLOT * 2 * CS; i += 256) {
-    const int row = i / CS, cl = i - row * CS;
-    slots[(size_t)row * C + c_base + cl] = 0.f;
-  }
-}
-
-template <bool RES, bool RELU>
-__global__ void __launch_bounds__(256) bn_apply_slots_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const float* __restrict__ slots_f,
-    float* __restrict__ slots_zero, int64_t M, int C, const float* __restrict__ gamma, const float* __restrict__ beta,
-    float eps, float momentum, float* __restrict__ run_mean, float* __restrict__ run_var, float* __restrict__ save,
-    uint16_t* __restrict__ y, uint8_t* __restrict__ mask) {
-  const int CS = C < SLAB ? C : SLAB;
-  const int c_base = blockIdx.x * CS, t = threadIdx.x;
-  const int tpr = CS >> 3, rpb = 256 / tpr, cv = t % tpr, r0 = t / tpr;
-  const int64_t stride = (int64_t)gridDim.y * rpb;
-  const int64_t rstart = (int64_t)blockIdx.y * rpb + r0;
-  const int64_t col = c_base + cv * 8;
-  // SU rows per thread in flight; the first batch goes out together with the slot loads (both one
-  // round trip away).  Loads clamp the row (always in bounds, no branches); stores skip rows >= M.
-  U4 xv[SU], rv[SU];
-  auto load = [&](int64_t r) {
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const int64_t o = min(r + u * stride, M - 1) * C + col;
-      xv[u] = *reinterpret_cast<const U4*>(x + o);
-      if (RES) rv[u] = *reinterpret_cast<const U4*>(res + o);
-    }
-  };
-  load(rstart);
-  __shared__ float red[512];
-  __shared__ float lsc[SLAB], lsh[SLAB];
-  const bool lead = blockIdx.y == 0;
-  float gm = 1.f, bt = 0.f, rmv = 0.f, rvv = 0.f;
-  if (t < CS) {
-    const int c = c_base + t;
-    if (gamma) gm = gamma[c];
-    if (beta) bt = beta[c];
-    if (lead && run_mean) {
-      rmv = run_mean[c];
-      rvv = run_var[c];
-    }
-  }
-  float s, q;
-  slab_slot_sums(slots_f, C, c_base, CS, red, s, q);
-  if (t < CS) {
-    const int c = c_base + t;
-    const float inv_m = 1.f / (float)M;
-    const float mean = s * inv_m;
-    const float var = fmaxf(q * inv_m - mean * mean, 0.f);
-    const float invstd = rsqrtf(var + eps);
-    const float sc = gm * invstd, sh = bt - mean * sc;
-    lsc[t] = sc;
-    lsh[t] = sh;
-    if (lead) {
-      save[c] = mean;
-      save[C + c] = invstd;
-      save[2 * C + c] = sc;
-      save[3 * C + c] = sh;
-      if (run_mean) {
-        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-        run_mean[c] = (1.f - momentum) * rmv + momentum * mean;
-        run_var[c] = (1.f - momentum) * rvv + momentum * unb;
-      }
-    }
-  }
-  if (lead && slots_zero) slab_zero(slots_zero, C, c_base, CS);
-  __syncthreads();
-  float sc[8], sh[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    sc[k] = lsc[cv * 8 + k];
-    sh[k] = lsh[cv * 8 + k];
-  }
-  for (int64_t r = rstart; r < M; r += SU * stride) {
-    U4 xc[SU], rc[SU];
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      xc[u] = xv[u];
-      if (RES) rc[u] = rv[u];
-    }
-    if (r + SU * stride < M) load(r + SU * stride);  // next batch in flight while this one is stored
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const int64_t ru = r + u * stride;
-      if (ru < M) {
-        float f[8], rr[8];
-        unpack8(xc[u], f);
-        if (RES) unpack8(rc[u], rr);
-        uint32_t bits = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float z = fmaf(f[k], sc[k], sh[k]);
-          if (RES) z += rr[k];
-          bits |= (z > 0.f ? 1u : 0u) << k;
-          f[k] = RELU ? fmaxf(z, 0.f) : z;
-        }
-        const int64_t o = ru * C + col;
-        *reinterpret_cast<U4*>(y + o) = pack8(f);
-        if (RES && RELU && mask) mask[o >> 3] = (uint8_t)bits;
-      }
-    }
-  }
-}
-
-// dx = A*g' + B*x + D (bn_bwd_apply_vec_kernel's math) with red = the reduced S_b slots
-template <bool RES, bool RELU>
-__global__ void __launch_bounds__(256) bn_bwd_apply_slots_kernel(
-    const uint16_t* __restrict__ g, const uint16_t* __restrict__ x, const uint8_t* __restrict__ mask,
-    const float* __restrict__ save, const float* __restrict__ slots_b, float* __restrict__ slots_zero, int64_t M,
-    int C, float* __restrict__ dgamma, float* __restrict__ dbeta, uint16_t* __restrict__ dx,
-    uint16_t* __restrict__ dres) {
-  const int CS = C < SLAB ? C : SLAB;
-  const int c_base = blockIdx.x * CS, t = threadIdx.x;
-  const int tpr = CS >> 3, rpb = 256 / tpr, cv = t % tpr, r0 = t / tpr;
-  const int64_t stride = (int64_t)gridDim.y * rpb;
-  const int64_t rstart = (int64_t)blockIdx.y * rpb + r0;
-  const int64_t col = c_base + cv * 8;
-  U4 gv[SU], xv[SU];
-  uint32_t mv[SU];
-  auto load = [&](int64_t r) {
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const int64_t o = min(r + u * stride, M - 1) * C + col;
-      gv[u] = *reinterpret_cast<const U4*>(g + o);
-      xv[u] = *reinterpret_cast<const U4*>(x + o);
-      mv[u] = (RES && RELU) ? mask[o >> 3] : 0u;
-    }
-  };
-  load(rstart);
-  __shared__ float red[512];
-  __shared__ float lA[SLAB], lB[SLAB], lD[SLAB], lsc[SLAB], lsh[SLAB];
-  const bool lead = blockIdx.y == 0;
-  float mu = 0.f, is = 0.f, scv = 0.f, shv = 0.f, db = 0.f, dg = 0.f;
-  if (t < CS) {
-    const int c = c_base + t;
-    mu = save[c];
-    is = save[C + c];
-    scv = save[2 * C + c];
-    shv = save[3 * C + c];
-    if (lead) {
-      if (dbeta) db = dbeta[c];
-      if (dgamma) dg = dgamma[c];
-    }
-  }
-  float s, q;
-  slab_slot_sums(slots_b, C, c_base, CS, red, s, q);
-  if (t < CS) {
-    const float inv_m = 1.f / (float)M;
-    const float kg = s * inv_m, kx = q * inv_m * is;
-    lA[t] = scv;
-    lB[t] = -scv * kx;
-    lD[t] = scv * (kx * mu - kg);
-    lsc[t] = scv;
-    lsh[t] = shv;
-    if (lead) {
-      const int c = c_base + t;
-      if (dbeta) dbeta[c] = db + s;
-      if (dgamma) dgamma[c] = dg + q;
-    }
-  }
-  if (lead && slots_zero) slab_zero(slots_zero, C, c_base, CS);
-  __syncthreads();
-  float A[8], B[8], D[8], sc[8], sh[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    A[k] = lA[cv * 8 + k];
-    B[k] = lB[cv * 8 + k];
-    D[k] = lD[cv * 8 + k];
-    sc[k] = lsc[cv * 8 + k];
-    sh[k] = lsh[cv * 8 + k];
-  }
-  for (int64_t r = rstart; r < M; r += SU * stride) {
-    U4 gc[SU], xc[SU];
-    uint32_t mc[SU];
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      gc[u] = gv[u];
-      xc[u] = xv[u];
-      mc[u] = mv[u];
-    }
-    if (r + SU * stride < M) load(r + SU * stride);
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const int64_t ru = r + u * stride;
-      if (ru < M) {
-        float gf[8], xf[8], o[8];
-        unpack8(gc[u], gf);
-        unpack8(xc[u], xf);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float gg = gf[k];
-          if (RES && RELU) {
-            gg = ((mc[u] >> k) & 1u) ? gg : 0.f;
-          } else if (RELU) {
-            gg = fmaf(xf[k], sc[k], sh[k]) > 0.f ? gg : 0.f;
-          }
-          gf[k] = gg;
-          o[k] = fmaf(A[k], gg, fmaf(B[k], xf[k], D[k]));
-        }
-        const int64_t off = ru * C + col;
-        *reinterpret_cast<U4*>(dx + off) = pack8(o);
-        if (RES && dres) *reinterpret_cast<U4*>(dres + off) = pack8(gf);
-      }
-    }
-  }
-}
-
 // ================================================================== launch helpers
-// C in {64, 128, 256} (G = 256 / C <= 4 slot groups per block) or a multiple of 256
-bool slab_ok(int C) { return C <= SLAB ? (C == 64 || C == 128 || C == 256) : C % SLAB == 0; }
-dim3 slab_grid(int64_t M, int C) {
-  const int CS = C < SLAB ? C : SLAB;
-  const int nslab = C / CS, rpb = 256 / (CS / 8);
-  // up to ~8 blocks per CU in all, at least one SU-row batch per thread (the per-block slot
-  // prologue amortises over the batches, the resident waves keep SU x 16 B per lane in flight)
-  int64_t rg = (M + SU * rpb - 1) / (SU * rpb);
-  const int64_t cap = std::max<int64_t>(1, 2048 / nslab);
-  if (rg > cap) rg = cap;
-  return dim3(nslab, (unsigned)std::max<int64_t>(1, rg));
-}
 bool vec_ok(int C) { return (C % 8 == 0) && (C / 8) <= 256 && (256 % (C / 8) == 0); }
 int grid_for(int64_t work, int per_block, int cap = 2048) {
   int64_t g = (work + per_block - 1) / per_block;
@@ -852,22 +580,11 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
   const int64_t n = M * C;
   // the vector kernels take the residual ReLU mask from the forward's mask bits
   if (vec_ok(C) && (!has_res || !relu || mask)) {
+    // one row per thread in flight (U = 1): 2 / 4 rows measured no faster (scripts/bn_bench.py)
     const int rpb = 256 / (C / 8);
-    static const int U = [] {
-      const char* e = getenv("TFX_BN_RED_U");
-      return e ? atoi(e) : 1;
-    }();
-    const int gr = grid_for(M, rpb * (U >= 4 ? 4 : 8));
-    if (U >= 4) {
-      TFX_DISPATCH_RR(has_res, relu,
-                      (bn_bwd_reduce_vec_kernel<R_, L_, 4><<<gr, 256, 0, s>>>(g, x, mask, save, M, C, slots)));
-    } else if (U == 2) {
-      TFX_DISPATCH_RR(has_res, relu,
-                      (bn_bwd_reduce_vec_kernel<R_, L_, 2><<<gr, 256, 0, s>>>(g, x, mask, save, M, C, slots)));
-    } else {
-      TFX_DISPATCH_RR(has_res, relu,
-                      (bn_bwd_reduce_vec_kernel<R_, L_, 1><<<gr, 256, 0, s>>>(g, x, mask, save, M, C, slots)));
-    }
+    const int gr = grid_for(M, rpb * 8);
+    TFX_DISPATCH_RR(has_res, relu,
+                    (bn_bwd_reduce_vec_kernel<R_, L_, 1><<<gr, 256, 0, s>>>(g, x, mask, save, M, C, slots)));
   } else {
     dim3 grid((C + 63) / 64, grid_for(M, 64));
     TFX_DISPATCH_RR(has_res, relu,
@@ -879,25 +596,6 @@ void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, cons
 
 void bn_slot_reduce(float* slots, int C, float* red, float* dgamma, float* dbeta, hipStream_t s) {
   bn_slot_reduce_kernel<<<(C + 15) / 16, 256, 0, s>>>(slots, C, red, dgamma, dbeta);
-}
-
-bool bn_slots_ok(int C) { return slab_ok(C); }
-
-void bn_apply_slots(const uint16_t* x, const uint16_t* res, const float* slots_f, float* slots_zero, int64_t M, int C,
-                    const float* gamma, const float* beta, float eps, float momentum, float* run_mean, float* run_var,
-                    float* save, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s) {
-  const dim3 grid = slab_grid(M, C);
-  TFX_DISPATCH_RR(res != nullptr, relu, (bn_apply_slots_kernel<R_, L_><<<grid, 256, 0, s>>>(
-                                            x, res, slots_f, slots_zero, M, C, gamma, beta, eps, momentum, run_mean,
-                                            run_var, save, y, mask)));
-}
-
-void bn_bwd_apply_slots(const uint16_t* g, const uint16_t* x, const uint8_t* mask, bool has_res, const float* save,
-                        const float* slots_b, float* slots_zero, int64_t M, int C, bool relu, float* dgamma,
-                        float* dbeta, uint16_t* dx, uint16_t* dres, hipStream_t s) {
-  const dim3 grid = slab_grid(M, C);
-  TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_slots_kernel<R_, L_><<<grid, 256, 0, s>>>(
-                                     g, x, mask, save, slots_b, slots_zero, M, C, dgamma, dbeta, dx, dres)));
 }
 
 void bn_bwd_reduce(const uint16_t* g, const uint16_t* x, const uint8_t* mask, bool has_res, const float* save,

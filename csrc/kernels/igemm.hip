@@ -107,7 +107,7 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
   if (a.stats || a.bnb_x) {
     if (!(a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 7) == 0 && (a.N & 7) == 0 &&
           (mode == MODE_FWD ||
-           (a.bnb_x && (mode == MODE_DGRAD || mode == MODE_DGRAD_FLIP || (mode == MODE_DGRAD_CLS && !a.bn_final)))) &&
+           (a.bnb_x && (mode == MODE_DGRAD || mode == MODE_DGRAD_FLIP))) &&
           (a.stats == nullptr || a.bnb_x == nullptr))) {
       fprintf(stderr, "igemm_launch: unsupported fused-BN epilogue configuration\n");
       abort();

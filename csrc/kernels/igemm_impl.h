@@ -362,94 +362,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, n, 0x00020000);
 }
 
-// ------------------------------------------------------------------ fused-BN last arriver
-// Every block of column tile tn has added its per-column partials into the slots.  The payload is
-// written ONLY by agent-scope atomics (performed past the XCD L2, which drops the line), so the
-// hand-off needs no L2 writeback (MI355X_MICROARCH.md "Correctness boundaries", sc1 table row 1):
-// every wave drains vmcnt, barrier, ONE lane bumps the tile's counter; the block whose add returns
-// tiles_m - 1 is last and its waves read the slots with sc1 loads after a barrier.  An agent release
-// (buffer_wbl2) per block here would write back the freshly stored output tile of every block on the
-// XCD: measured 2-6x slower conv kernels.  The host only fuses when the tile's slot columns are whole
-// 128-B lines (N % 32 == 0), so no block ever loads a line holding another tile's pending sums.
-// The last arriver sums the NSLOT slot rows of the tile's columns, re-zeroes them (sc1 stores: the
-// lines leave the L2 again) and resets the counter, so the workspace is zero between uses.
-// FWD: finalize the BN of the columns (bn_finalize_kernel's math); BWD: red + dgamma / dbeta.
-template <int BN, bool BWD>
-__device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n0, char* smem, int t) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  unsigned* flag = reinterpret_cast<unsigned*>(smem + 8192);  // past the [2][BN][2] f32 partials
-  if (t == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(a.bn_cnt + tn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = prev == (unsigned)(a.tiles_m - 1) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*flag == 0) return;
-  constexpr int NPH = 256 / BN;  // slot phases per column
-  const int cl = t % BN, ph = t / BN, c = n0 + cl;
-  float* slots = BWD ? a.bnb_slots : a.stats;
-  float s = 0.f, q = 0.f;
-  if (c < a.N) {
-    // 8 slot rows in flight per step (bounded registers: this runs in every fused-BN kernel)
-    // every slot row in flight at once: the reducer runs on the kernel's critical tail, and the slots
-    // (written by memory-side atomics) are an HBM / MALL round trip away -- one round trip, not four
-    constexpr int CH = NSLOT / NPH;
-    for (int k0 = 0; k0 < NSLOT / NPH; k0 += CH) {
-      float vs[CH], vq[CH];
-#pragma unroll
-      for (int k = 0; k < CH; ++k) {
-        float* row = slots + (size_t)(ph + (k0 + k) * NPH) * 2 * a.N;
-        vs[k] = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vq[k] = __hip_atomic_load(row + a.N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int k = 0; k < CH; ++k) {
-        s += vs[k];
-        q += vq[k];
-        float* row = slots + (size_t)(ph + (k0 + k) * NPH) * 2 * a.N;
-        __hip_atomic_store(row + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(row + a.N + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  float* part = reinterpret_cast<float*>(smem);
-  part[(ph * BN + cl) * 2] = s;
-  part[(ph * BN + cl) * 2 + 1] = q;
-  __syncthreads();
-  if (t < BN && c < a.N) {
-    s = 0.f;
-    q = 0.f;
-#pragma unroll
-    for (int k = 0; k < NPH; ++k) {
-      s += part[(k * BN + t) * 2];
-      q += part[(k * BN + t) * 2 + 1];
-    }
-    const int C = a.N;
-    if constexpr (BWD) {
-      a.bnb_red[c] = s;
-      a.bnb_red[C + c] = q;
-      if (a.bnb_dbeta) a.bnb_dbeta[c] += s;
-      if (a.bnb_dgamma) a.bnb_dgamma[c] += q;
-    } else {
-      const float inv_m = 1.f / (float)a.M;
-      const float mean = s * inv_m;
-      const float var = fmaxf(q * inv_m - mean * mean, 0.f);
-      const float invstd = rsqrtf(var + a.bn_eps);
-      const float scale = (a.bn_gamma ? a.bn_gamma[c] : 1.f) * invstd;
-      a.bn_save[c] = mean;
-      a.bn_save[C + c] = invstd;
-      a.bn_save[2 * C + c] = scale;
-      a.bn_save[3 * C + c] = (a.bn_beta ? a.bn_beta[c] : 0.f) - mean * scale;
-      if (a.bn_rmean) {
-        const float unb = a.M > 1 ? var * (float)a.M / (float)(a.M - 1) : var;
-        a.bn_rmean[c] = (1.f - a.bn_momentum) * a.bn_rmean[c] + a.bn_momentum * mean;
-        a.bn_rvar[c] = (1.f - a.bn_momentum) * a.bn_rvar[c] + a.bn_momentum * unb;
-      }
-    }
-  }
-  if (t == 0) __hip_atomic_store(a.bn_cnt + tn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // (the anonymous namespace continues: kernels get internal linkage per translation unit)
 
 // SWAP: compute the transposed tile (MFMA operands exchanged) so each lane holds 4 CONSECUTIVE
@@ -460,8 +372,9 @@ __device__ __forceinline__ void bn_tile_reduce(const IgemmArgs& a, int tn, int n
 // of 64-channel layers), which then fit 4 blocks per CU -- those are memory-bound, and occupancy is
 // what keeps enough loads and stores in flight.
 // EPI: compile-time epilogue extras (so the plain GEMM / wgrad kernels carry none of their code or
-// registers): EPI_STATS = fused BN statistics (+ last-arriver finalize) of a conv forward,
-// bn_slot_reduce_kernel's math for channels [16 sb, 16 sb + 16) of the sr_* layer, 256 threads:
+// registers): EPI_STATS = fused BN statistics of a conv forward.
+//
+// sr_block: bn_slot_reduce_kernel's math for channels [16 sb, 16 sb + 16) of the sr_* layer, 256 threads:
 // 16 slot-lanes x 4 slots each per channel, all loads in flight before the re-zeroing stores, then an
 // LDS reduction over the 16 slot-lanes.  dbeta / dgamma are loaded before the slot round trip.
 __device__ __forceinline__ void sr_block(float* __restrict__ slots, float* __restrict__ red, float* __restrict__ dgamma,
@@ -508,64 +421,7 @@ __device__ __forceinline__ void sr_block(float* __restrict__ slots, float* __res
   }
 }
 
-// bn_finalize_kernel's math for channels [16 sb, 16 sb + 16) of the fin_* layer, 256 threads
-__device__ __forceinline__ void fin_block(const IgemmArgs& a, int sb, float* red2) {
-  const int C = a.fin_C, tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int c = sb * 16 + tx;
-  const bool own = ty == 0 && c < C;
-  float g = 1.f, b = 0.f, rm = 0.f, rv = 0.f;
-  if (own) {
-    if (a.fin_gamma) g = a.fin_gamma[c];
-    if (a.fin_beta) b = a.fin_beta[c];
-    if (a.fin_rmean) {
-      rm = a.fin_rmean[c];
-      rv = a.fin_rvar[c];
-    }
-  }
-  float s = 0.f, q = 0.f;
-  if (c < C) {
-    float vs[NSLOT / 16], vq[NSLOT / 16];
-#pragma unroll
-    for (int i = 0; i < NSLOT / 16; ++i) {
-      const float* p = a.fin_slots + (size_t)(ty + 16 * i) * 2 * C;
-      vs[i] = p[c];
-      vq[i] = p[C + c];
-    }
-#pragma unroll
-    for (int i = 0; i < NSLOT / 16; ++i) {
-      s += vs[i];
-      q += vq[i];
-      float* p = a.fin_slots + (size_t)(ty + 16 * i) * 2 * C;
-      p[c] = 0.f;
-      p[C + c] = 0.f;
-    }
-  }
-  red2[threadIdx.x] = s;
-  red2[256 + threadIdx.x] = q;
-  __syncthreads();
-  if (!own) return;
-#pragma unroll
-  for (int k = 1; k < 16; ++k) {
-    s += red2[threadIdx.x + 16 * k];
-    q += red2[256 + threadIdx.x + 16 * k];
-  }
-  const float inv_m = 1.f / (float)a.fin_M;
-  const float mean = s * inv_m;
-  const float var = fmaxf(q * inv_m - mean * mean, 0.f);
-  const float invstd = rsqrtf(var + a.fin_eps);
-  const float scale = g * invstd;
-  a.fin_save[c] = mean;
-  a.fin_save[C + c] = invstd;
-  a.fin_save[2 * C + c] = scale;
-  a.fin_save[3 * C + c] = b - mean * scale;
-  if (a.fin_rmean) {
-    const float unb = a.fin_M > 1 ? var * (float)a.fin_M / (float)(a.fin_M - 1) : var;
-    a.fin_rmean[c] = (1.f - a.fin_momentum) * rm + a.fin_momentum * mean;
-    a.fin_rvar[c] = (1.f - a.fin_momentum) * rv + a.fin_momentum * unb;
-  }
-}
-
-// EPI_BNB = fused BN-backward partials (+ last-arriver reduce) of a conv data gradient.
+// EPI_BNB = fused BN-backward partials of a conv data gradient.
 // KS = 2: in-block split-K for the f32-atomic weight gradients.  512 threads = two 4-wave groups
 // on the SAME output tile, each running the pipelined K loop over half of the block's k-tiles in its
 // own LDS stages; group 1 hands its accumulators to group 0 through LDS and only group 0 issues the
@@ -642,15 +498,13 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
 
   // tail blocks past the GEMM's grid: another BN layer's backward slot reduction (IgemmArgs sr_*)
   const int nsr1 = a.sr_C ? (a.sr_C + 15) / 16 : 0, nsr2 = a.sr2_C ? (a.sr2_C + 15) / 16 : 0;
-  const int nfin = a.fin_C ? (a.fin_C + 15) / 16 : 0;
-  const int gemm_blocks = (int)gridDim.x - nsr1 - nsr2 - nfin;
+  const int gemm_blocks = (int)gridDim.x - nsr1 - nsr2;
   if ((int)blockIdx.x >= gemm_blocks) {
     if (threadIdx.x < 256) {
       float* scratch = reinterpret_cast<float*>(GL ? ga0 : smem_all);  // >= 2 KB, unused by this block
       const int sb = (int)blockIdx.x - gemm_blocks;
       if (sb < nsr1) sr_block(a.sr_slots, a.sr_red, a.sr_dgamma, a.sr_dbeta, a.sr_C, sb, scratch);
-      else if (sb < nsr1 + nsr2) sr_block(a.sr2_slots, a.sr2_red, a.sr2_dgamma, a.sr2_dbeta, a.sr2_C, sb - nsr1, scratch);
-      else fin_block(a, sb - nsr1 - nsr2, scratch);
+      else sr_block(a.sr2_slots, a.sr2_red, a.sr2_dgamma, a.sr2_dbeta, a.sr2_C, sb - nsr1, scratch);
     }
     return;
   }
@@ -1230,7 +1084,6 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
             atomicAdd(&slot[a.N + nn], red[t * 2 + 1] + red[(BN + t) * 2 + 1]);
           }
         }
-        if (a.bn_final) bn_tile_reduce<BN, bnb>(a, tn, n0, smem, t);
       }
     } else if (a.out_mode == OUT_BF16 && !a.trans_out && (a.ldc & 3) == 0 && (a.N & 3) == 0) {
       uint16_t* Cb = reinterpret_cast<uint16_t*>(a.Cp);
@@ -1337,26 +1190,10 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
 
 // ============================================================ host launcher
 
-// LDS-DMA ring depth for the main loop (0 = register-staged pipeline, 2 or 3 = ring depth, capped
-// per tile shape by the LDS budget).  Measured per mode on the ResNet-50 batch-256 layers
-// (profiles/r02_glds, scripts/conv_bench.py): in isolation the ring wins on the f32-atomic weight
-// gradients (-7 %, up to +40 % per layer) where a 3-deep ring fits next to the in-block split-K, and
-// loses on the bf16-output forward / data-gradient kernels (1 block per CU at a 3-deep ring vs 2
-// with the register pipeline).  Inside the full training step the wgrad win does not survive
-// (bench.py 9.334 vs 9.266 ms/step, 3 runs each, profiles/r02_glds/step_ab.txt: the ring's
-// 1-block-per-CU occupancy leaves no room for the overlapping kernels), so every mode defaults to
-// the register pipeline.  TFX_GLDS forces one depth everywhere; TFX_GLDS_WGRAD / TFX_GLDS_BF16 per mode.
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-int glds_stages(bool atomic_out, int g3) {
-  static const int all = env_int("TFX_GLDS", -1), wg = env_int("TFX_GLDS_WGRAD", 0), bf = env_int("TFX_GLDS_BF16", 0);
-  if (all >= 0) return all;
-  if (atomic_out) return g3 >= 3 ? wg : 0;
-  return bf;
-}
-
+// LDS-DMA ring depth for the main loop: 0 = register-staged pipeline (the default: in the full
+// training step the ring's 1-block-per-CU occupancy left no room for the overlapping kernels,
+// bench.py 9.334 vs 9.266 ms/step, profiles/r02_glds/step_ab.txt), 2 or 3 = ring depth, capped per
+// tile shape by the LDS budget -- chosen per layer by the measured launch table (TuneCfg.gls).
 // launch configuration of the current launch_shape call (igemm_tune_lookup), read by launch_t
 thread_local TuneCfg g_tc;
 
@@ -1377,10 +1214,7 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   const int nkt = (a.K + BKT - 1) / BKT;
   const int tiles = a.tiles_m * a.tiles_n;
   int splits = 1;
-  static const int want = [] {
-    const char* e = getenv("TFX_SPLITK_BLOCKS");
-    return e ? atoi(e) : 256;  // one block per CU: measured best (fewer f32 atomic partials)
-  }();
+  constexpr int want = 256;  // one block per CU: measured best (fewer f32 atomic partials)
   const int want_blocks = g_tc.want > 0 ? g_tc.want : want * want_mult;
   if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, want_blocks, min_kps);
   a.kps = (nkt + splits - 1) / splits;
@@ -1396,13 +1230,13 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   }
   splits = (nkt + a.kps - 1) / a.kps;
   if (tiles * splits == 0) return;
-  const int grid = tiles * splits + (a.sr_C ? (a.sr_C + 15) / 16 : 0) + (a.sr2_C ? (a.sr2_C + 15) / 16 : 0) +
-                   (a.fin_C ? (a.fin_C + 15) / 16 : 0);  // + slot-reduce / finalize tail blocks
+  const int grid = tiles * splits + (a.sr_C ? (a.sr_C + 15) / 16 : 0) +
+                   (a.sr2_C ? (a.sr2_C + 15) / 16 : 0);  // + slot-reduce tail blocks
   // transposed MFMA orientation for bf16 outputs and transposed stores (see kernel comment)
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
   constexpr int STAGE_B = (BM + BN) * BKT * 2;
   constexpr int G3 = KS * 3 * STAGE_B <= 163840 ? 3 : 2;
-  const int gls = g_tc.gls >= 0 ? g_tc.gls : glds_stages(a.out_mode == OUT_F32_ATOMIC, G3);
+  const int gls = g_tc.gls >= 0 ? g_tc.gls : 0;
   if (gls > 0) {
     // LDS-DMA ring: single k-tile -> GLS 1; otherwise the deepest ring (<= 3) that fits the LDS
     const bool single = nkt == 1 && splits == 1;
@@ -1443,44 +1277,12 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
 
 // tile choice: narrow N -> 256x64 (if M is large) or 128x64; otherwise 128x128, unless that leaves
 // the chip under-filled (fewer than 2 blocks per CU: the small late-stage convs), then 128x64 --
-// twice the blocks for the same K loop.  TFX_TILE_POLICY=0 disables the under-fill rule (A/B).
-int tile_policy() {
-  static const int p = [] {
-    const char* e = getenv("TFX_TILE_POLICY");
-    return e ? atoi(e) : 1;
-  }();
-  return p;
-}
-
-// weight gradients (split-K, f32 atomics): 128x64 tiles at twice the block target keep the same
-// splits (same atomic traffic) but put two blocks on each CU for latency hiding.  Measured: -25 %
-// on the 1x1 (dense x dense) weight gradients, +3..8 % on the im2col-gathered 3x3 ones, so the
-// default (0 = auto) uses it for the dense pair only; TFX_WGRAD_TILE=64/128 forces one (A/B).
-int wgrad_tile() {
-  static const int t = [] {
-    const char* e = getenv("TFX_WGRAD_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  return t;
-}
-
-// in-block split-K for the weight gradients (TFX_WGRAD_KS=1 restores one 4-wave group per block)
-int wgrad_ks() {
-  static const int k = [] {
-    const char* e = getenv("TFX_WGRAD_KS");
-    return e ? atoi(e) : 2;
-  }();
-  return k;
-}
-
-// min k-tiles per split for the skinny GEMM path (TFX_SKINNY_KPS; 0 disables the path)
-int skinny_min_kps() {
-  static const int k = [] {
-    const char* e = getenv("TFX_SKINNY_KPS");
-    return e ? atoi(e) : 2;
-  }();
-  return k;
-}
+// twice the blocks for the same K loop.
+// Weight gradients (split-K, f32 atomics): in-block split-K (8-wave blocks, KS = 2) by default;
+// 128x64 tiles for the dense (1x1) pair -- half the atomic bytes of the 2-blocks-per-CU 128x64 form
+// -- and 128x128 for the im2col-gathered ones (measured: profiles/r01_v10, r02_bigtile).
+// min k-tiles per split for the skinny GEMM path
+constexpr int kSkinnyMinKps = 2;
 
 template <int AK, int BK, bool ALLOW256 = true, int EPI = EPI_PLAIN>
 void launch_shape(IgemmArgs& a, hipStream_t s, int fam = -1) {
@@ -1489,7 +1291,7 @@ void launch_shape(IgemmArgs& a, hipStream_t s, int fam = -1) {
   g_tc = tuned ? tc : TuneCfg{};
   if (tuned && tc.tile > 0) {
     if constexpr (!ALLOW256) {
-      if (tc.ks == 2 || (tc.ks == 0 && wgrad_ks() == 2)) {
+      if (tc.ks == 2 || tc.ks == 0) {
         if (tc.tile == 2) return launch_t<AK, BK, 128, 64, EPI, 2>(a, s);
         return launch_t<AK, BK, 128, 128, EPI, 2>(a, s);
       }
@@ -1509,15 +1311,12 @@ void launch_shape(IgemmArgs& a, hipStream_t s, int fam = -1) {
   }
   if constexpr (!ALLOW256) {
     const bool dense_pair = (AK == MN_DENSE && BK == MN_DENSE) || (a.R == 1 && a.S == 1);  // 1x1 (any stride)
-    const bool ks2 = tuned && tc.ks > 0 ? tc.ks == 2 : wgrad_ks() == 2;
+    const bool ks2 = tuned && tc.ks > 0 ? tc.ks == 2 : true;
     if (ks2) {
-      // 8-wave blocks, one per CU: 128x64 tiles for the dense pair (half the atomic bytes of the
-      // 2-blocks-per-CU 128x64 form), 128x128 for the im2col-gathered ones
-      if (a.N <= 64 || (dense_pair && wgrad_tile() != 128) || wgrad_tile() == 64)
-        return launch_t<AK, BK, 128, 64, EPI, 2>(a, s);
+      if (a.N <= 64 || dense_pair) return launch_t<AK, BK, 128, 64, EPI, 2>(a, s);
       return launch_t<AK, BK, 128, 128, EPI, 2>(a, s);
     }
-    if (a.N > 64 && (wgrad_tile() == 64 || (wgrad_tile() == 0 && dense_pair))) return launch_t<AK, BK, 128, 64, EPI>(a, s, 2);
+    if (a.N > 64 && dense_pair) return launch_t<AK, BK, 128, 64, EPI>(a, s, 2);
   }
   if (a.N <= 64) {
     if constexpr (ALLOW256) {
@@ -1527,7 +1326,7 @@ void launch_shape(IgemmArgs& a, hipStream_t s, int fam = -1) {
   } else {
     const long tiles128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
     if constexpr (ALLOW256) {
-      if (tile_policy() >= 1 && tiles128 < 512) return launch_t<AK, BK, 128, 64, EPI>(a, s);
+      if (tiles128 < 512) return launch_t<AK, BK, 128, 64, EPI>(a, s);
     }
     launch_t<AK, BK, 128, 128, EPI>(a, s);
   }

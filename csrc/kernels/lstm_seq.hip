@@ -23,25 +23,16 @@
 //
 // Inter-workgroup hand-off of h_t / dg_t: every handed-off byte is written ONCE per launch (hbuf
 // and dg keep one slot per time step) with 16-byte write-through (sc1) buffer stores and read
-// ONLY with sc1 buffer loads (cdna_hip_programming.md §6 Guideline 16).  Two protocols:
-//
-//   PROTO_DATA (TFX_LSTM_PROTO=1): the data is its own flag.  A memset node fills the slots with 0xFFFF
-//     (a bf16 NaN bit pattern the producers never store: a computed NaN is canonicalised to
-//     0x7FC0) before the launch; a consumer wave re-loads the fragments it still lacks until none
-//     holds the sentinel -- no drain, no counter, no barrier between producer and consumer
-//     (MI355X_MICROARCH.md price list: handoff-1to1 ~0.8-1.0 us vs handoff-flag 1.7-1.9x that).
-//     Measured SLOWER here (char-LSTM 2x512: 2.13 vs 1.79 ms/step, profiles/r02_lstm): each
-//     consumer must re-read 16-64 KB of fragments per attempt, and the sentinel memsets add
-//     ~65 MB of writes per step.
-//   PROTO_COUNTER (default): every storing wave drains vmcnt, a workgroup barrier, ONE
-//     lane adds 1 to the row block's counter (agent-scope atomic); a consumer lane polls the
-//     counter relaxed, a workgroup barrier, then the sc1 loads (Valid forms table row 1;
-//     TFX_LSTM_ACQUIRE=1 adds an agent acquire anyway).
+// ONLY with sc1 buffer loads (cdna_hip_programming.md §6 Guideline 16).  Protocol: every storing
+// wave drains vmcnt, a workgroup barrier, ONE lane adds 1 to the row block's counter (agent-scope
+// atomic); a consumer lane polls the counter relaxed, a workgroup barrier, then the sc1 loads
+// (MI355X_MICROARCH.md "Valid forms" table row 1).  (Rejected alternatives, measured slower and
+// removed: data-as-flag sentinel slots, 2.13 vs 1.79 ms/step; per-producer flag words --
+// profiles/r02_lstm.)
 //
 // A row block depends only on its own 16 rows.  Every spin is bounded: on expiry the status word
-// is set and the whole grid drains (no hang); the caller can read the status.
-#include <cstdlib>
-
+// is set and the whole grid drains (no hang).  The host reads the status word asynchronously
+// (ops/rnn.py: a pinned copy checked at the next log / sync point) and raises.
 #include "tfx_common.h"
 #include "tfx_kernels.h"
 
@@ -51,8 +42,6 @@ namespace {
 constexpr int LS_LDS = 96 * 1024;      // > 80 KB: one workgroup per CU (160 KB LDS)
 constexpr int LS_STRIDE = 32;          // u32 words per counter (own 128-B line)
 constexpr unsigned LS_SPIN_LIMIT = 1u << 20;
-enum { PROTO_COUNTER = 0, PROTO_DATA = 1, PROTO_FLAGS = 2 };
-constexpr uint16_t LS_SENTINEL = 0xFFFF;
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
@@ -73,43 +62,6 @@ __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int off, u32x4v
 
 __device__ __forceinline__ float ls_sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
-// bf16 for a handed-off slot: never the sentinel pattern (NaN -> canonical quiet NaN)
-__device__ __forceinline__ uint16_t ls_bf16(float f) {
-  const uint16_t b = f32_to_bf16(f);
-  return b == LS_SENTINEL ? (uint16_t)0x7FC0 : b;
-}
-
-__device__ __forceinline__ bool ls_ready(bf16x8_t v) {
-  const u32x4v w = __builtin_bit_cast(u32x4v, v);
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) ok = ok && (w[i] & 0xFFFFu) != 0xFFFFu && (w[i] >> 16) != 0xFFFFu;
-  return ok;
-}
-
-// PROTO_DATA consumer, one wave: load N fragments (byte offsets off0 + 64 kk) and re-load the ones
-// still holding the sentinel until the whole wave has real data.  false = bound hit (status set).
-template <int N>
-__device__ __forceinline__ bool ls_poll_load(__amdgpu_buffer_rsrc_t r, int off0, bf16x8_t (&a)[N], gu32* status) {
-  static_assert(N <= 32, "pending mask");
-  unsigned pend = N == 32 ? 0xFFFFFFFFu : ((1u << N) - 1u);
-  for (unsigned spins = 0;; ++spins) {
-#pragma unroll
-    for (int kk = 0; kk < N; ++kk)
-      if (pend & (1u << kk)) a[kk] = ld_sc1(r, off0 + kk * 64);
-#pragma unroll
-    for (int kk = 0; kk < N; ++kk)
-      if ((pend & (1u << kk)) && ls_ready(a[kk])) pend &= ~(1u << kk);
-    if (__all(pend == 0)) return true;
-    if (spins >= LS_SPIN_LIMIT) {
-      if ((threadIdx.x & 63) == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");  // the re-loads are real loads
-  }
-}
-
 // One lane: wait until *ctr >= target.  false = gave up (status word set).
 __device__ __forceinline__ bool ls_wait(gu32* ctr, unsigned target, gu32* status) {
   for (unsigned spins = 0;; ++spins) {
@@ -124,56 +76,13 @@ __device__ __forceinline__ bool ls_wait(gu32* ctr, unsigned target, gu32* status
 }
 
 // Block-wide: lane 0 waits; everyone learns the outcome after the barrier.
-template <bool ACQ>
 __device__ __forceinline__ bool ls_block_wait(gu32* ctr, unsigned target, gu32* status, int* flag) {
   if (threadIdx.x == 0) {
     const bool ok = ls_wait(ctr, target, status);
-    if constexpr (ACQ) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
     *flag = ok ? 1 : 0;
   }
   __syncthreads();
   return *flag != 0;
-}
-
-// PROTO_FLAGS: one flag word per producing workgroup (own 128-B line), holding the last step it
-// published.  Wave 0 of the consumer polls all of its row block's flags at once (lane l <-> flag
-// l), so no two producers ever meet on one atomic.
-template <bool ACQ>
-__device__ __forceinline__ bool ls_block_wait_flags(gu32* rbase, int nub, unsigned target, gu32* status,
-                                                    int* flag) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    bool ok = true;
-    for (unsigned spins = 0;; ++spins) {
-      const unsigned v =
-          lane < nub ? __hip_atomic_load(rbase + lane * LS_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
-      if (__all(v >= target)) break;
-      if (spins >= LS_SPIN_LIMIT) {
-        if (lane == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (lane == 0) {
-      if constexpr (ACQ) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      *flag = ok ? 1 : 0;
-    }
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-__device__ __forceinline__ void ls_publish_flag(gu32* mine, unsigned v) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(mine, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Publish: every storing wave drains, barrier, one lane bumps the counter.
@@ -184,7 +93,7 @@ __device__ __forceinline__ void ls_publish(gu32* ctr) {
 }
 
 // ------------------------------------------------------------------ forward
-template <int NK, int PROTO, bool ACQ>
+template <int NK>
 __global__ void __launch_bounds__(256, 1)
     lstm_seq_fwd_kernel(const float* __restrict__ gx, const uint16_t* __restrict__ whh, int T, int B,
                         uint16_t* hbuf, float* __restrict__ cbuf, float* __restrict__ act, float* __restrict__ hT,
@@ -221,18 +130,10 @@ __global__ void __launch_bounds__(256, 1)
     const float z0 = g[0], z1 = g[H], z2 = g[2 * H], z3 = g[3 * H];  // hoisted projection, pre-launch data
     const __amdgpu_buffer_rsrc_t hr = ls_rsrc(hbuf + t * BH + (int64_t)r0 * H, 16 * H * 2);
     bf16x8_t a[NKW];
-    if constexpr (PROTO == PROTO_DATA) {
-      if (!ls_poll_load<NKW>(hr, aoff, a, status)) flag[1] = 1;
-    } else {
-      if constexpr (PROTO == PROTO_FLAGS) {
-        if (t > 0 && !ls_block_wait_flags<ACQ>(ctr, nub, (unsigned)t, status, flag)) return;
-      } else {
-        if (t > 0 && !ls_block_wait<ACQ>(ctr, (unsigned)(t * nub), status, flag)) return;
-      }
+    if (t > 0 && !ls_block_wait(ctr, (unsigned)(t * nub), status, flag)) return;
 #pragma unroll
-      for (int kk = 0; kk < NKW; ++kk) a[kk] = ld_sc1(hr, aoff + kk * 64);
-      __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
-    }
+    for (int kk = 0; kk < NKW; ++kk) a[kk] = ld_sc1(hr, aoff + kk * 64);
+    __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
     f32x4_t acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -244,7 +145,6 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4_t*>(red + ((wave * 4 + q) * 64 + lane) * 4) = acc[q];
     __syncthreads();
-    if (PROTO == PROTO_DATA && flag[1]) return;  // a wave's wait expired: the whole grid drains
     float z[4] = {z0, z1, z2, z3};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -260,7 +160,7 @@ __global__ void __launch_bounds__(256, 1)
     ap[3 * H] = og;
     cbuf[(t + 1) * BH + cidx] = c;
     if (t == T - 1) hT[cidx] = h;
-    hs[cr * 16 + cu] = ls_bf16(h);
+    hs[cr * 16 + cu] = f32_to_bf16(h);
     __syncthreads();
     if (tid < 32) {
       const int row = tid >> 1, half = tid & 1;
@@ -268,15 +168,14 @@ __global__ void __launch_bounds__(256, 1)
       const __amdgpu_buffer_rsrc_t hw = ls_rsrc(hbuf + (t + 1) * BH + (int64_t)r0 * H, 16 * H * 2);
       st_sc1(hw, (row * H + u0 + half * 8) * 2, v);
     }
-    if constexpr (PROTO == PROTO_COUNTER) ls_publish(ctr);
-    if constexpr (PROTO == PROTO_FLAGS) ls_publish_flag(ctr + blockIdx.x * LS_STRIDE, (unsigned)(t + 1));
+    ls_publish(ctr);
   }
 }
 
 // ------------------------------------------------------------------ backward
 // dH (bf16, optional): gradient of every h_t from outside the recurrence; dhT / dc_in (f32,
 // optional): gradients of h_T / c_T; dbias (optional): += sum over t and rows of dgates (f32).
-template <int NK, int PROTO, bool ACQ>
+template <int NK>
 __global__ void __launch_bounds__(256, 1)
     lstm_seq_bwd_kernel(const float* __restrict__ act, const float* __restrict__ cbuf,
                         const uint16_t* __restrict__ dH, const float* __restrict__ dhT,
@@ -322,18 +221,10 @@ __global__ void __launch_bounds__(256, 1)
     if (s > 0) {
       const __amdgpu_buffer_rsrc_t gr = ls_rsrc(dg + (t + 1) * 4 * BH + (int64_t)r0 * 4 * H, 16 * 4 * H * 2);
       bf16x8_t a[NK];
-      if constexpr (PROTO == PROTO_DATA) {
-        if (!ls_poll_load<NK>(gr, aoff, a, status)) flag[1] = 1;
-      } else {
-        if constexpr (PROTO == PROTO_FLAGS) {
-          if (!ls_block_wait_flags<ACQ>(ctr, nub, (unsigned)s, status, flag)) return;
-        } else {
-          if (!ls_block_wait<ACQ>(ctr, (unsigned)(s * nub), status, flag)) return;
-        }
+      if (!ls_block_wait(ctr, (unsigned)(s * nub), status, flag)) return;
 #pragma unroll
-        for (int kk = 0; kk < NK; ++kk) a[kk] = ld_sc1(gr, aoff + kk * 64);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      for (int kk = 0; kk < NK; ++kk) a[kk] = ld_sc1(gr, aoff + kk * 64);
+      __builtin_amdgcn_sched_barrier(0);
       f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NK; kk += 2) {
@@ -342,7 +233,6 @@ __global__ void __launch_bounds__(256, 1)
       }
       *reinterpret_cast<f32x4_t*>(red + (wave * 64 + lane) * 4) = acc0 + acc1;
       __syncthreads();
-      if (PROTO == PROTO_DATA && flag[1]) return;
 #pragma unroll
       for (int w2 = 0; w2 < 4; ++w2) dhv += red[(w2 * 64 + rl) * 4 + ri];
     }
@@ -357,10 +247,10 @@ __global__ void __launch_bounds__(256, 1)
     dc *= fg;
     cn = cp;
     uint16_t* dp = ds + cr * 64 + cu;
-    dp[0] = ls_bf16(d0);
-    dp[16] = ls_bf16(d1);
-    dp[32] = ls_bf16(d2);
-    dp[48] = ls_bf16(d3);
+    dp[0] = f32_to_bf16(d0);
+    dp[16] = f32_to_bf16(d1);
+    dp[32] = f32_to_bf16(d2);
+    dp[48] = f32_to_bf16(d3);
     __syncthreads();
     if (tid < 128) {
       const int row = tid >> 3, q = (tid >> 1) & 3, half = tid & 1;
@@ -368,8 +258,7 @@ __global__ void __launch_bounds__(256, 1)
       const __amdgpu_buffer_rsrc_t gw = ls_rsrc(dg + t * 4 * BH + (int64_t)r0 * 4 * H, 16 * 4 * H * 2);
       st_sc1(gw, (row * 4 * H + q * H + u0 + half * 8) * 2, v);
     }
-    if constexpr (PROTO == PROTO_COUNTER) ls_publish(ctr);
-    if constexpr (PROTO == PROTO_FLAGS) ls_publish_flag(ctr + blockIdx.x * LS_STRIDE, (unsigned)(s + 1));
+    ls_publish(ctr);
   }
   if (dc_out) dc_out[cidx] = dc;
   if (dbias) {
@@ -396,62 +285,23 @@ void ls_prepare(K k) {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LS_LDS);
 }
 
-int ls_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-// kernel selection: protocol (TFX_LSTM_PROTO: 0 counter (default), 1 data-as-flag, 2 per-producer
-// flags) x acquire (TFX_LSTM_ACQUIRE)
-int ls_proto() {
-  const int p = ls_env("TFX_LSTM_PROTO", PROTO_COUNTER);
-  return (p == PROTO_DATA || p == PROTO_FLAGS) ? p : PROTO_COUNTER;
-}
-
 template <int NK>
 void fwd_launch(dim3 grid, const float* gx, const uint16_t* whh, int T, int B, uint16_t* hbuf, float* cbuf,
                 float* act, float* hT, unsigned* sync, hipStream_t s) {
-  static const int proto = ls_proto();
-  static const bool acq = ls_env("TFX_LSTM_ACQUIRE", 0) != 0;
-  auto k = proto == PROTO_DATA ? lstm_seq_fwd_kernel<NK, PROTO_DATA, false>
-         : proto == PROTO_FLAGS ? (acq ? lstm_seq_fwd_kernel<NK, PROTO_FLAGS, true>
-                                       : lstm_seq_fwd_kernel<NK, PROTO_FLAGS, false>)
-                                : (acq ? lstm_seq_fwd_kernel<NK, PROTO_COUNTER, true>
-                                       : lstm_seq_fwd_kernel<NK, PROTO_COUNTER, false>);
-  static bool once = (ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_DATA, false>),
-                      ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_FLAGS, true>),
-                      ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_FLAGS, false>),
-                      ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_COUNTER, true>),
-                      ls_prepare(lstm_seq_fwd_kernel<NK, PROTO_COUNTER, false>), true);
+  static bool once = (ls_prepare(lstm_seq_fwd_kernel<NK>), true);
   (void)once;
-  const int64_t BH = (int64_t)B * H_of<NK>();
   (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B, H_of<NK>()) * 4, s);
-  if (proto == PROTO_DATA) (void)hipMemsetAsync(hbuf + BH, 0xFF, (size_t)T * BH * 2, s);
-  k<<<grid, 256, LS_LDS, s>>>(gx, whh, T, B, hbuf, cbuf, act, hT, sync);
+  lstm_seq_fwd_kernel<NK><<<grid, 256, LS_LDS, s>>>(gx, whh, T, B, hbuf, cbuf, act, hT, sync);
 }
 
 template <int NK>
 void bwd_launch(dim3 grid, const float* act, const float* cbuf, const uint16_t* dH, const float* dhT,
                 const float* dc_in, const uint16_t* whh, int T, int B, uint16_t* dg, float* dc_out, float* dbias,
                 unsigned* sync, hipStream_t s) {
-  static const int proto = ls_proto();
-  static const bool acq = ls_env("TFX_LSTM_ACQUIRE", 0) != 0;
-  auto k = proto == PROTO_DATA ? lstm_seq_bwd_kernel<NK, PROTO_DATA, false>
-         : proto == PROTO_FLAGS ? (acq ? lstm_seq_bwd_kernel<NK, PROTO_FLAGS, true>
-                                       : lstm_seq_bwd_kernel<NK, PROTO_FLAGS, false>)
-                                : (acq ? lstm_seq_bwd_kernel<NK, PROTO_COUNTER, true>
-                                       : lstm_seq_bwd_kernel<NK, PROTO_COUNTER, false>);
-  static bool once = (ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_DATA, false>),
-                      ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_FLAGS, true>),
-                      ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_FLAGS, false>),
-                      ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_COUNTER, true>),
-                      ls_prepare(lstm_seq_bwd_kernel<NK, PROTO_COUNTER, false>), true);
+  static bool once = (ls_prepare(lstm_seq_bwd_kernel<NK>), true);
   (void)once;
-  const int64_t BH = (int64_t)B * H_of<NK>();
   (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B, H_of<NK>()) * 4, s);
-  // slot t = 0..T-2 are consumed in-launch (slot T-1 is produced first and read at step 1)
-  if (proto == PROTO_DATA) (void)hipMemsetAsync(dg, 0xFF, (size_t)T * 4 * BH * 2, s);
-  k<<<grid, 256, LS_LDS, s>>>(act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync);
+  lstm_seq_bwd_kernel<NK><<<grid, 256, LS_LDS, s>>>(act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync);
 }
 
 }  // namespace

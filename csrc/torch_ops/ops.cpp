@@ -96,14 +96,6 @@ Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t d
   return conv_fwd_impl(x, w, stride, pad, dil, slots.data_ptr<float>());
 }
 
-bool dgrad_classes_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("TFX_DGRAD_CLASSES");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  return on;
-}
-
 // dX = dgrad(dy) (+ addend: the gradient of x's other consumer, summed in the epilogue; the
 // result is written in place into addend's storage when given)
 // addend_mask: 1-bit ReLU mask of the addend (uint8 per 8 channels): dX = dgrad + addend * mask,
@@ -205,7 +197,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
     tfx::igemm_launch(a, mode, cur_stream());
     return dx;
   }
-  if (stride == 2 && dil == 1 && dgrad_classes_enabled()) {
+  if (stride == 2 && dil == 1) {
     // Stride-2 data gradient by output-parity class: pixel (h, w) only receives taps with
     // r = h + pad (mod 2), s = w + pad (mod 2), so each of the 4 classes is a dense stride-1
     // implicit GEMM over its own taps -- a quarter of the MACs of the zero-filled single GEMM.
@@ -241,32 +233,16 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> xshape, int64_t stri
   return dx;
 }
 
-// ---- fused BN epilogues.  ws = the BN layer's workspace: [NSLOT][2][C] f32 slots followed by
-// BN_CNT u32 column-tile counters (all zero between uses; the kernels restore that).
-unsigned* bn_counters(const Tensor& ws, int64_t C) {
+// ---- fused BN epilogues.  ws = the BN layer's workspace: [NSLOT][2][C] f32 slots (all zero
+// between uses; the finalize / slot-reduce kernels that consume them restore that).
+void check_bn_ws(const Tensor& ws, int64_t C) {
   CHECK_F32(ws); CHECK_CONTIG(ws);
-  TORCH_CHECK(ws.numel() >= tfx::NSLOT * 2 * C + tfx::BN_CNT, "BN workspace too small for the fused epilogue");
-  TORCH_CHECK(C <= 64 * tfx::BN_CNT, "fused BN epilogue: too many column tiles");
-  return reinterpret_cast<unsigned*>(ws.data_ptr<float>() + tfx::NSLOT * 2 * C);
+  TORCH_CHECK(ws.numel() >= tfx::NSLOT * 2 * C, "BN workspace too small for the fused epilogue");
 }
 
-// The in-kernel last-arriver reduce needs each column tile's slot columns to be whole 128-B lines
-// (igemm.hip bn_tile_reduce): C % 32 == 0 and a 128-B aligned workspace.  Otherwise the epilogue
-// only accumulates and a separate finalize / slot-reduce kernel follows.  OFF by default
-// (TFX_BN_LAST_ARRIVER=1 enables it): the counter round trip + the serial tail of the last block
-// cost more than the 5 us kernel they save -- ResNet-50 convs fwd 2.544 -> 2.651 ms, bwd 3.034 ->
-// 3.104 ms per step (profiles/r01_v9/epi_bench_la*.log).
-int bn_final_ok(const Tensor& ws, int64_t C) {
-  static const bool on = [] {
-    const char* e = getenv("TFX_BN_LAST_ARRIVER");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  return (on && C % 32 == 0 && (reinterpret_cast<uintptr_t>(ws.data_ptr()) & 127) == 0) ? 1 : 0;
-}
-
-// conv forward whose epilogue produces the following BN's batch statistics AND, in the last block
-// of each column tile, finalizes them: returns (y, save = [mean | invstd | scale | shift]) and
-// updates the running statistics -- the BN then only applies (bn_apply_train).
+// conv forward whose epilogue produces the following BN's batch statistics, then the finalize:
+// returns (y, save = [mean | invstd | scale | shift]) and updates the running statistics -- the BN
+// then only applies (bn_apply_train).
 std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor ws,
                                        optional<Tensor> gamma, optional<Tensor> beta, optional<Tensor> run_mean,
                                        optional<Tensor> run_var, double momentum, double eps) {
@@ -279,68 +255,12 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
   a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
   a.out_mode = tfx::OUT_BF16;
+  check_bn_ws(ws, g.Ko);
   a.stats = ws.data_ptr<float>();
-  a.bn_cnt = bn_counters(ws, g.Ko);
-  a.bn_final = bn_final_ok(ws, g.Ko);
-  a.bn_gamma = fp(gamma); a.bn_beta = fp(beta); a.bn_rmean = fpm(run_mean); a.bn_rvar = fpm(run_var);
-  a.bn_save = save.data_ptr<float>();
-  a.bn_eps = (float)eps; a.bn_momentum = (float)momentum;
   tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
-  if (!a.bn_final)
-    tfx::bn_finalize(a.stats, a.M, g.Ko, a.bn_gamma, a.bn_beta, a.bn_eps, a.bn_momentum, a.bn_rmean, a.bn_rvar,
-                     a.bn_save, cur_stream());
+  tfx::bn_finalize(a.stats, a.M, g.Ko, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
+                   fpm(run_var), save.data_ptr<float>(), cur_stream());
   return {y, save};
-}
-
-// conv_fwd_bn with two deferral hooks: `defer` = do NOT finalize this conv's BN here (the returned save
-// is filled later: a finalize folded into another launch's tail, or bn_finalize_into); and the
-// fin_* arguments = finalize ANOTHER, earlier-deferred BN in the tail blocks of this launch.
-std::tuple<Tensor, Tensor> conv_fwd_bn2(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor ws,
-                                        optional<Tensor> gamma, optional<Tensor> beta, optional<Tensor> run_mean,
-                                        optional<Tensor> run_var, double momentum, double eps, bool defer,
-                                        optional<Tensor> fin_slots, int64_t fin_C, int64_t fin_M,
-                                        optional<Tensor> fin_gamma, optional<Tensor> fin_beta,
-                                        optional<Tensor> fin_rmean, optional<Tensor> fin_rvar, double fin_momentum,
-                                        double fin_eps, optional<Tensor> fin_save) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
-  auto g = geom(x.sizes().vec(), w.sizes().vec(), stride, pad, dil);
-  auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
-  auto save = at::empty({4 * g.Ko}, x.options().dtype(at::kFloat));
-  auto a = conv_args(g, stride, pad, dil);
-  a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
-  a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
-  a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
-  a.out_mode = tfx::OUT_BF16;
-  a.stats = ws.data_ptr<float>();
-  a.bn_cnt = bn_counters(ws, g.Ko);
-  a.bn_final = 0;
-  a.bn_gamma = fp(gamma); a.bn_beta = fp(beta); a.bn_rmean = fpm(run_mean); a.bn_rvar = fpm(run_var);
-  a.bn_save = save.data_ptr<float>();
-  a.bn_eps = (float)eps; a.bn_momentum = (float)momentum;
-  if (fin_slots.has_value() && fin_slots->defined()) {
-    CHECK_DEV(*fin_slots); CHECK_F32(*fin_slots);
-    TORCH_CHECK(fin_C > 0 && fin_slots->numel() >= tfx::NSLOT * 2 * fin_C && fin_save.has_value() &&
-                    fin_save->defined() && fin_save->numel() == 4 * fin_C && fin_M > 0,
-                "conv_fwd_bn2: deferred finalize arguments");
-    a.fin_slots = fin_slots->data_ptr<float>(); a.fin_C = (int)fin_C; a.fin_M = fin_M;
-    a.fin_gamma = fp(fin_gamma); a.fin_beta = fp(fin_beta); a.fin_rmean = fpm(fin_rmean); a.fin_rvar = fpm(fin_rvar);
-    a.fin_save = fin_save->data_ptr<float>();
-    a.fin_eps = (float)fin_eps; a.fin_momentum = (float)fin_momentum;
-  }
-  tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
-  if (!defer)
-    tfx::bn_finalize(a.stats, a.M, g.Ko, a.bn_gamma, a.bn_beta, a.bn_eps, a.bn_momentum, a.bn_rmean, a.bn_rvar,
-                     a.bn_save, cur_stream());
-  return {y, save};
-}
-
-// the finalize of a deferred BN on its own (no later forward launch took it): slots -> save + running stats
-void bn_finalize_into(Tensor slots, int64_t C, int64_t M, optional<Tensor> gamma, optional<Tensor> beta,
-                      optional<Tensor> run_mean, optional<Tensor> run_var, double momentum, double eps, Tensor save) {
-  CHECK_DEV(slots); CHECK_F32(slots); CHECK_F32(save);
-  TORCH_CHECK(slots.numel() >= tfx::NSLOT * 2 * C && save.numel() == 4 * C, "bn_finalize_into: sizes");
-  tfx::bn_finalize(slots.data_ptr<float>(), M, (int)C, fp(gamma), fp(beta), (float)eps, (float)momentum,
-                   fpm(run_mean), fpm(run_var), save.data_ptr<float>(), cur_stream());
 }
 
 // stride-1 conv data gradient whose epilogue also reduces the backward of the BN that produced
@@ -355,8 +275,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
                                          optional<Tensor> addend_mask, bool reduce, bool addend_s2,
                                          optional<Tensor> wflip) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(w); CHECK_CONTIG(w);
-  TORCH_CHECK(stride == 1 || (stride == 2 && dil == 1 && dgrad_classes_enabled()),
-              "conv_dgrad_bn: stride-1 convs, or stride 2 by output-parity class");
+  TORCH_CHECK(stride == 1, "conv_dgrad_bn: stride-1 convs");
   auto g = geom(xshape, w.sizes().vec(), stride, pad, dil);
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.P && dy.size(2) == g.Q && dy.size(3) == g.Ko, "dy shape");
   CHECK_BF16(bn_x); CHECK_CONTIG(bn_x); CHECK_F32(bn_save);
@@ -371,40 +290,13 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
               "stride-2 compact addend: no mask");
   const uint8_t* amask = addend_s2 ? nullptr : addend_mask_ptr(addend, addend_mask);
   auto dx = (acc && !amask && !addend_s2) ? *addend : at::empty({g.N, g.H, g.W, g.C}, dy.options());
-  // reduce = false: the partials stay in the slots for bn_bwd_slots (no red, no slot reduce)
+  // reduce = false: the partials stay in the slots for a later launch to reduce (conv_wgrad_sr2 tail
+  // blocks, or bn_slots_reduce)
   auto red = reduce ? at::empty({2 * g.C}, dy.options().dtype(at::kFloat)) : Tensor();
   const uint8_t* bmask = nullptr;
   if (bn_mask.has_value() && bn_mask->defined()) {
     TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == bn_x.numel(), "bn_mask size");
     bmask = bn_mask->data_ptr<uint8_t>();
-  }
-  if (stride == 2) {
-    // the four output-parity classes (conv_dgrad's stride-2 path), each with the BN-backward
-    // epilogue: every pixel of dx is written by exactly one class, so their per-column partials
-    // add up in the slots to the full reduction; one slot reduce after the last class
-    TORCH_CHECK(!acc && !amask && !addend_s2, "conv_dgrad_bn stride 2: no addend");
-    for (int cph = 0; cph < 2; ++cph)
-      for (int cpw = 0; cpw < 2; ++cpw)
-        TORCH_CHECK((g.R - (cph + pad) % 2 + 1) / 2 > 0 && (g.S - (cpw + pad) % 2 + 1) / 2 > 0 &&
-                        (g.H - cph + 1) / 2 > 0 && (g.W - cpw + 1) / 2 > 0,
-                    "conv_dgrad_bn stride 2: every parity class must have taps and pixels");
-    bn_counters(ws, g.C);  // workspace size check
-    for (int cph = 0; cph < 2; ++cph) {
-      for (int cpw = 0; cpw < 2; ++cpw) {
-        tfx::IgemmArgs a;
-        cls_setup(a, g, dy, w, pad, cph, cpw);
-        a.Cp = dx.data_ptr();
-        a.out_mode = tfx::OUT_BF16;
-        a.bnb_x = bf(bn_x); a.bnb_save = bn_save.data_ptr<float>(); a.bnb_mask = bmask;
-        a.bnb_relu = relu ? 1 : 0;
-        a.bnb_slots = ws.data_ptr<float>();
-        a.bn_final = 0;
-        tfx::igemm_launch(a, tfx::MODE_DGRAD_CLS, cur_stream());
-      }
-    }
-    if (reduce)
-      tfx::bn_slot_reduce(ws.data_ptr<float>(), g.C, red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), cur_stream());
-    return {dx, red};
   }
   tfx::IgemmArgs a;
   const int mode = dgrad_setup(a, g, dy, w, wflip, stride, pad, dil);
@@ -416,14 +308,10 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, std::vector<int64_
   a.bnb_x = bf(bn_x); a.bnb_save = bn_save.data_ptr<float>();
   a.bnb_mask = bmask;
   a.bnb_relu = relu ? 1 : 0;
+  check_bn_ws(ws, g.C);
   a.bnb_slots = ws.data_ptr<float>();
-  a.bn_cnt = bn_counters(ws, g.C);
-  a.bn_final = reduce ? bn_final_ok(ws, g.C) : 0;
-  a.bnb_red = reduce ? red.data_ptr<float>() : nullptr;
-  a.bnb_dgamma = reduce ? fpm(dgamma) : nullptr;
-  a.bnb_dbeta = reduce ? fpm(dbeta) : nullptr;
   tfx::igemm_launch(a, mode, cur_stream());
-  if (reduce && !a.bn_final) tfx::bn_slot_reduce(a.bnb_slots, g.C, a.bnb_red, a.bnb_dgamma, a.bnb_dbeta, cur_stream());
+  if (reduce) tfx::bn_slot_reduce(a.bnb_slots, g.C, red.data_ptr<float>(), fpm(dgamma), fpm(dbeta), cur_stream());
   return {dx, red};
 }
 
@@ -794,70 +682,6 @@ std::tuple<Tensor, Tensor> bn_bwd_apply(Tensor g, Tensor x, optional<Tensor> res
   return {dx, dres};
 }
 
-// ---- two-slot-set BN (batchnorm.hip "slot-consuming passes"): slots_f = the layer's forward
-// statistics slots S_f, slots_b = its backward slots S_b, each [NSLOT][2][C] f32.  The forward
-// apply reduces S_f itself and zeroes S_b; the backward apply reduces S_b itself and zeroes S_f.
-// have_stats = false: a standalone statistics pass fills S_f first.
-std::tuple<Tensor, Tensor, Tensor> bn_fwd_slots(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
-                                                optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
-                                                double eps, optional<Tensor> res, bool relu, Tensor slots_f,
-                                                Tensor slots_b, bool have_stats) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(slots_f); CHECK_F32(slots_b);
-  const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(slots_f.numel() >= tfx::NSLOT * 2 * C && slots_b.numel() >= tfx::NSLOT * 2 * C, "stat slots");
-  TORCH_CHECK(tfx::bn_slots_ok((int)C), "bn_fwd_slots: C must be 64, 128, 256 or a multiple of 256");
-  auto save = at::empty({4 * C}, x.options().dtype(at::kFloat));
-  auto y = at::empty_like(x);
-  const uint16_t* r = nullptr;
-  if (res.has_value() && res->defined()) {
-    CHECK_BF16(*res); CHECK_CONTIG(*res);
-    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
-    r = bf(*res);
-  }
-  auto s = cur_stream();
-  if (!have_stats) tfx::bn_stats(bf(x), M, C, slots_f.data_ptr<float>(), s);
-  Tensor mask;
-  if (r && relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
-  tfx::bn_apply_slots(bf(x), r, slots_f.data_ptr<float>(), slots_b.data_ptr<float>(), M, C, fp(gamma), fp(beta),
-                      (float)eps, (float)momentum, fpm(run_mean), fpm(run_var), save.data_ptr<float>(), relu, bfm(y),
-                      mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, s);
-  return {y, save, mask};
-}
-
-// have_partials = true: a conv dgrad epilogue (conv_dgrad_bn, reduce=false) already accumulated
-// [sum g' | sum g' xhat] into S_b; else the vector reduce pass does.  Residual + ReLU layers need
-// the forward's mask.  Returns (dx, dres) as bn_bwd_apply.
-std::tuple<Tensor, Tensor> bn_bwd_slots(Tensor g, Tensor x, bool has_res, Tensor save, bool relu, optional<Tensor> mask,
-                                        Tensor slots_b, Tensor slots_f, optional<Tensor> dgamma,
-                                        optional<Tensor> dbeta, bool have_partials, bool want_dres) {
-  CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(save);
-  CHECK_F32(slots_b); CHECK_F32(slots_f);
-  const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(g.sizes() == x.sizes(), "bn_bwd_slots grad shape");
-  TORCH_CHECK(save.numel() == 4 * C, "save size");
-  TORCH_CHECK(slots_f.numel() >= tfx::NSLOT * 2 * C && slots_b.numel() >= tfx::NSLOT * 2 * C, "stat slots");
-  TORCH_CHECK(tfx::bn_slots_ok((int)C), "bn_bwd_slots: C must be 64, 128, 256 or a multiple of 256");
-  const uint8_t* mk = nullptr;
-  if (mask.has_value() && mask->defined()) {
-    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() * 8 == x.numel(), "relu mask size");
-    mk = mask->data_ptr<uint8_t>();
-  }
-  TORCH_CHECK(!(has_res && relu) || mk, "bn_bwd_slots: residual + ReLU needs the forward mask");
-  auto dx = at::empty_like(x);
-  Tensor dres;
-  if (has_res && want_dres) dres = at::empty_like(x);
-  auto s = cur_stream();
-  if (!have_partials) {
-    TORCH_CHECK(C <= 2048, "bn_bwd_slots: standalone reduce needs C <= 2048");
-    tfx::bn_bwd_reduce(bf(g), bf(x), mk, has_res, save.data_ptr<float>(), M, C, relu, slots_b.data_ptr<float>(), s);
-  }
-  tfx::bn_bwd_apply_slots(bf(g), bf(x), mk, has_res, save.data_ptr<float>(), slots_b.data_ptr<float>(),
-                          slots_f.data_ptr<float>(), M, C, relu, fpm(dgamma), fpm(dbeta), bfm(dx),
-                          dres.defined() ? bfm(dres) : nullptr, s);
-  return {dx, dres};
-}
-
-bool bn_slots_supported(int64_t C) { return tfx::bn_slots_ok((int)C); }
 int64_t bn_nslot() { return tfx::NSLOT; }
 
 // ------------------------------------------------------------------ loss / metrics / pooling
@@ -1563,15 +1387,10 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);
-  m.def("conv_fwd_bn2", &conv_fwd_bn2);
-  m.def("bn_finalize_into", &bn_finalize_into);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
         "Tensor bn_x, Tensor bn_save, Tensor? bn_mask, bool relu, Tensor ws, Tensor? dgamma, Tensor? dbeta, "
         "Tensor? addend_mask=None, bool reduce=True, bool addend_s2=False, Tensor? wflip=None) -> (Tensor, Tensor)",
         &conv_dgrad_bn);
-  m.def("bn_fwd_slots", &bn_fwd_slots);
-  m.def("bn_bwd_slots", &bn_bwd_slots);
-  m.def("bn_slots_supported", &bn_slots_supported);
   m.def("bn_nslot", &bn_nslot);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd(Tensor g, Tensor x, Tensor? res, Tensor save, bool relu, Tensor slots, Tensor? dgamma, "

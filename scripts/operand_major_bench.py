@@ -45,10 +45,10 @@ def main():
         t_mn = graph_us(lambda: torch.ops.tfx.gemm(dy, w, False, False, None, False, False))
         t_km = graph_us(lambda: torch.ops.tfx.gemm(dy, wt, False, True, None, False, False))
         xb = torch.randn(B, H, W, C, device="cuda").bfloat16()
-        sf = torch.zeros(ns * 2 * C + 64, device="cuda")
+        sf = torch.zeros(ns * 2 * C, device="cuda")
         sb = torch.zeros_like(sf)
         gam, bet = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
-        _, save, _ = torch.ops.tfx.bn_fwd_slots(xb, gam, bet, None, None, 0.1, 1e-5, None, True, sf, sb, False)
+        _, save, _ = torch.ops.tfx.bn_fwd_train(xb, gam, bet, None, None, 0.1, 1e-5, None, True, sf, False)
         w4 = w.reshape(Ko, 1, 1, C)
         dy4 = dy.reshape(B, H, W, Ko)
         t_dg = graph_us(lambda: torch.ops.tfx.conv_dgrad_bn(dy4, w4, [B, H, W, C], 1, 0, 1, None, xb, save, None,

@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from tensorflow_examples_amd.ops import _native, tuning  # noqa: E402
 from conv_bench import resnet50_convs  # noqa: E402
 
-NSLOT, BN_CNT = 64, 64
+NSLOT = 64
 # (tile, ks, gls, want): tile 1 = 128x128, 2 = 128x64, 3 = 256x64
 BF16_CANDS = [(t, 0, g, 0) for t in (1, 2, 3) for g in (0, 2, 3)] + [(t, 2, g, 0) for t in (1, 2) for g in (0, 2)]
 ATOMIC_CANDS = [(t, k, g, w) for t in (1, 2) for k in (1, 2) for g in (0, 3) for w in (256, 512)]
@@ -89,7 +89,7 @@ def main():
         gy = torch.randn_like(y)
         dw = torch.zeros(K, R, R, C, device=dev)
         slots = torch.zeros(NSLOT * 2 * K, device=dev)
-        ws = torch.zeros(NSLOT * 2 * C + BN_CNT, device=dev)
+        ws = torch.zeros(NSLOT * 2 * C, device=dev)
         save = torch.cat([torch.zeros(C), torch.ones(C), torch.ones(C), torch.zeros(C)]).to(dev)
         dgam, dbet = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
         passes = {

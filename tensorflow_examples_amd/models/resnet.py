@@ -12,7 +12,6 @@ the 16-byte vector-load granularity; its weights for channels 3..7 stay exactly 
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -32,16 +31,13 @@ STAGES = {
 IN_CH_PAD = 8
 _MEAN = (0.4914, 0.4822, 0.4465)  # CIFAR-10 per-channel statistics
 _STD = (0.2470, 0.2435, 0.2616)
-_SINK = os.environ.get("TFX_NO_GRADSINK", "0") != "1"  # A/B switch for the fused residual-gradient sum
-# A/B switch for the conv<->BN epilogue fusions: BN finalize in the producing conv's epilogue, BN
-# backward reduction in the consuming conv's data-gradient epilogue (igemm.hip EPI_STATS / EPI_BNB)
-_FUSE_BN = os.environ.get("TFX_FUSE_BN", "1") != "0"
-# A/B switch: identity blocks hand conv1 the residual BN's (gradient, ReLU mask) instead of the
-# masked gradient tensor (one full-size write less per block; igemm.hip masked addend)
-_MASKED_RES = os.environ.get("TFX_MASKED_RES", "1") != "0"
-# A/B switch: a 1x1 stride-2 projection parks its input gradient compact (even pixels only) and
-# conv1's data-gradient epilogue adds it there -- no zero-filled full-size gradient (ops/nn.py)
-_S2_ADDEND = os.environ.get("TFX_S2_ADDEND", "1") != "0"
+# GPU training fusions (each measured as an interleaved A/B when introduced, README ledger):
+# the residual-gradient sum in conv1's data-gradient epilogue (GradSink); the conv<->BN epilogue
+# fusions (BN statistics in the producing conv's epilogue, BN backward reduction in the consuming
+# conv's data-gradient epilogue: igemm.hip EPI_STATS / EPI_BNB); identity blocks hand conv1 the
+# residual BN's (gradient, ReLU mask) instead of the masked gradient tensor; a 1x1 stride-2
+# projection parks its input gradient compact (even pixels only) for conv1's epilogue to add.
+_SINK = _FUSE_BN = _MASKED_RES = _S2_ADDEND = True
 
 
 class _BN:
@@ -69,9 +65,6 @@ class _BN:
         fused = training and x.device.type == "cuda"
         if fused and _FUSE_BN:
             self.ws.finalize_args = (self.gamma.master, self.beta.master, self.mean, self.var, 0.1, 1e-5)
-            # a BN whose output is never written (read only by the tail BN) can finalize late: in the
-            # tail blocks of the next conv's forward launch (ops/nn.py _PENDING_FIN)
-            self.ws.defer_finalize = bool(defer_output)
             y = conv(x, self.ws, sink, fuse_input_bn_backward and _FUSE_BN)
             return self(y, training, relu=relu, residual=residual, stats_ready=True, residual_sink=residual_sink,
                         ws_obj=True, residual_is_bn=residual_is_bn, defer_output=defer_output)

@@ -14,7 +14,6 @@ launch a bucket's all-reduce as soon as its last gradient lands.
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional
 
 import torch
@@ -22,56 +21,6 @@ import torch.nn.functional as F
 
 from . import _native
 from ..variables import Variable
-
-
-# ---------------------------------------------------------------- side-stream weight gradients
-# A conv's weight gradient is off the backward critical path: nothing but the optimizer (and the
-# DP all-reduce of its bucket) reads it.  Running it on a second stream lets it overlap the data-
-# gradient / BN-backward chain of the next layers -- most of those kernels leave CUs idle (small
-# grids, memory latency).  The end of the backward pass (an autograd engine callback, so every
-# caller of .backward() gets it) makes the current stream wait for the side stream; the DP
-# all-reduce orders each bucket after both streams (parallel/allreduce.py).  Opt-in
-# (TFX_WGRAD_STREAM=1): the kernels do overlap (rocprofv3 traces: ~4.5 ms of overlapped kernel time
-# per step), but a replayed HIP graph with the branches ran 8.72-8.77 vs 8.37-8.39 ms/step, and
-# eager launches with it 8.26-8.86 ms (host-noise bound) -- profiles/r02_side.
-_WGRAD_STREAM = os.environ.get("TFX_WGRAD_STREAM", "0") == "1"
-_side = {}
-_side_pending = {"active": False}
-
-
-def wgrad_side_stream(device) -> Optional[torch.cuda.Stream]:
-    """The persistent side stream of `device` when side-stream weight gradients are on, else None."""
-    if not _WGRAD_STREAM or device.type != "cuda":
-        return None
-    s = _side.get(device.index)
-    if s is None:
-        s = _side[device.index] = torch.cuda.Stream(device=device)
-    return s
-
-
-def _join_side_streams() -> None:
-    _side_pending["active"] = False
-    for s in _side.values():
-        torch.cuda.current_stream(s.device).wait_stream(s)
-
-
-def compute_stream_of_backward(device) -> Optional[torch.cuda.Stream]:
-    """The stream the current backward pass runs its main chain on (recorded at the first side-
-    stream launch; None when no side-stream work is pending)."""
-    return _side_pending.get("main") if _side_pending["active"] else None
-
-
-def _enter_side(device) -> Optional[torch.cuda.Stream]:
-    ss = wgrad_side_stream(device)
-    if ss is None:
-        return None
-    cur = torch.cuda.current_stream(device)
-    ss.wait_stream(cur)
-    _side_pending["main"] = cur
-    if not _side_pending["active"]:
-        _side_pending["active"] = True
-        torch.autograd.Variable._execution_engine.queue_callback(_join_side_streams)
-    return ss
 
 
 def _grad_ready(*vs: Optional[Variable]) -> None:
@@ -108,37 +57,28 @@ def _conv_ref(x, w, stride=1, pad=0, dil=1):
     return y.permute(0, 2, 3, 1).contiguous()
 
 
-# Largest BN input (bytes) whose backward reduction runs in the consumer conv's dgrad epilogue.
-# With the residual gradient materialised, the 128 MB block inputs of ResNet-50 stage 1 were slower
-# fused (204 -> 229 us, scripts/epi_bench.py, profiles/r01_v9) and the cap was 64 MB; since the
-# identity blocks pass (gradient, mask bits) instead, fusing them too is faster end to end
-# (9.46 -> 9.43 ms/step, TFX_BNB_MAX_MB A/B), so the default cap covers every ResNet-50 layer.
-_BNB_MAX_BYTES = int(os.environ.get("TFX_BNB_MAX_MB", "256")) << 20
+# Largest BN input (bytes) whose backward reduction runs in the consumer conv's dgrad epilogue:
+# every ResNet-50 layer (since the identity blocks pass (gradient, mask bits) instead of a
+# materialised residual gradient, fusing the 128 MB stage-1 inputs too is faster end to end:
+# 9.46 -> 9.43 ms/step, profiles/r01_v9).
+_BNB_MAX_BYTES = 256 << 20
 
-
-# A/B switch: stride-1 3x3 data gradients as the forward conv of dY with flipped, transposed
-# filters (igemm_dgrad_flip.hip), all layers' copies refreshed by one launch per step
-_DGRAD_FLIP = os.environ.get("TFX_DGRAD_FLIP", "1") != "0"
-
-
-# A/B switch: the BN-backward slot reduction of a fused data gradient runs as tail blocks of the same
-# conv's weight-gradient launch (conv_wgrad_sr) instead of its own bn_slot_reduce launch
-_SR_FUSE = os.environ.get("TFX_SR_FUSE", "1") != "0"
-# ... and also the reductions of the stride-2 conv2's input BN and of the projection-shortcut BN
-# (deferred to the next weight-gradient launch's tail; TFX_SR_FUSE2=0 keeps their own launches)
-_SR_FUSE2 = _SR_FUSE and os.environ.get("TFX_SR_FUSE2", "1") != "0"
-# test hook: False leaves every deferred reduction to its own BN's backward (the fallback path)
+# The BN-backward slot reduction of a fused data gradient runs as tail blocks of the same conv's
+# weight-gradient launch (conv_wgrad_sr) instead of its own bn_slot_reduce launch; so do the
+# reductions of a stride-2 conv2's input BN and of the projection-shortcut BN (deferred to the next
+# weight-gradient launch's tail).  (Measured: profiles/r02_srfuse.  Rejected and removed: the same
+# reduction in the stride-2 parity-class data gradients' epilogues, a wash -- profiles/r02_s2bnb.)
+# test hooks: _SR_TAKE_PENDING = False leaves every deferred reduction to its own BN's backward
+# (the fallback path); _SR_DEFER = False never defers them (each BN reduces its own)
 _SR_TAKE_PENDING = True
-# opt-in (TFX_S2_BNB=1): fuse the BN-backward reduction into stride-2 (parity-class) data gradients
-# too.  Measured a wash in the step (8.152 vs 8.139 ms/step, profiles/r02_s2bnb): the four class
-# GEMMs' epilogue cost matches the reduce kernel it removes.  (The C++ side runs stride-2 data
-# gradients per class unless TFX_DGRAD_CLASSES=0.)
-_S2_BNB = os.environ.get("TFX_S2_BNB", "0") == "1" and os.environ.get("TFX_DGRAD_CLASSES", "1") != "0"
+_SR_DEFER = True
 
 
 def _flip_ok(w, stride, pad, dil):
+    """Stride-1 3x3 data gradients run as the forward conv of dY with flipped, transposed filters
+    (igemm_dgrad_flip.hip); every layer's copy is refreshed by one launch per step."""
     sh = w.shape
-    return _DGRAD_FLIP and stride == 1 and pad == 1 and dil == 1 and len(sh) == 4 and sh[1] == 3 and sh[2] == 3 \
+    return stride == 1 and pad == 1 and dil == 1 and len(sh) == 4 and sh[1] == 3 and sh[2] == 3 \
         and getattr(w.store, "shadow", None) is not None and w.store.flip_index(w) is not None
 
 
@@ -161,35 +101,7 @@ class _Conv2d(torch.autograd.Function):
                 w.store.flip_stale = True  # the weights may have changed since the last refresh
             if isinstance(stats_into, BNWorkspace):
                 ws = stats_into
-                if ws.two_phase(x.device):
-                    # epilogue statistics into the layer's forward slots S_f; the BN's apply pass
-                    # reduces them itself (bn_fwd_slots): no finalize launch
-                    sf = ws.fwd(x.device)
-                    if ws.fwd_dirty:  # an earlier training forward's backward never ran
-                        sf.zero_()
-                        ws.fwd_dirty = False
-                    y = torch.ops.tfx.conv_fwd_stats(x.contiguous(), w.value, stride, pad, dil, sf)
-                    ws.stats_ready = True
-                    return y
-                if _FIN_DEFER:
-                    # this conv's BN finalize may be deferred (ws.defer_finalize: a shortcut BN read only
-                    # by the tail BN), and a previously deferred one rides in this launch's tail blocks
-                    defer = bool(getattr(ws, "defer_finalize", False))
-                    fin = _PENDING_FIN.pop(0) if (_PENDING_FIN and _PENDING_FIN[0]["slots"].device == x.device) \
-                        else None
-                    fa = fin["args"] if fin is not None else (None,) * 6
-                    y, save = torch.ops.tfx.conv_fwd_bn2(
-                        x.contiguous(), w.value, stride, pad, dil, ws.get(x.device), *ws.finalize_args, defer,
-                        fin["slots"] if fin is not None else None, fin["C"] if fin is not None else 0,
-                        fin["M"] if fin is not None else 0, fa[0], fa[1], fa[2], fa[3],
-                        fa[4] if fin is not None else 0.1, fa[5] if fin is not None else 1e-5,
-                        fin["save"] if fin is not None else None)
-                    ws.pending_save = save
-                    if defer:
-                        _PENDING_FIN.append({"slots": ws.get(x.device), "C": y.shape[-1], "M": y.numel() // y.shape[-1],
-                                             "args": ws.finalize_args, "save": save})
-                    return y
-                # epilogue statistics + last-arriver finalize: the BN only applies
+                # epilogue statistics, then the finalize: the BN only applies
                 y, ws.pending_save = torch.ops.tfx.conv_fwd_bn(x.contiguous(), w.value, stride, pad, dil,
                                                                ws.get(x.device), *ws.finalize_args)
                 return y
@@ -211,27 +123,12 @@ class _Conv2d(torch.autograd.Function):
             sr_bnb = None
             if need_dx:
                 bnb = ctx.bnb
-                # stride 2: the data gradient runs per output-parity class, each class launch with
-                # the same BN-backward epilogue (no sink there: a stride-2 conv2 is its input's sole
-                # consumer)
-                s2_ok = stride == 2 and dil == 1 and sink is None and _S2_BNB
-                if bnb is not None and (stride == 1 or s2_ok) and (sink is None or sink.mode == "consume") \
+                if bnb is not None and stride == 1 and (sink is None or sink.mode == "consume") \
                         and x.numel() * x.element_size() <= _BNB_MAX_BYTES:
                     # dx is the complete gradient of the BN output x: the epilogue also reduces
                     # that BN's backward (sum g', sum g' xhat, dgamma, dbeta) -- see BNBackwardFusion
                     add, amask, s2 = _unpack_sink(sink.take()) if sink is not None else (None, None, False)
-                    if bnb.wsobj is not None:
-                        # partials stay in the layer's backward slots S_b: the BN's backward apply
-                        # reduces them itself (bn_bwd_slots), no slot-reduce launch
-                        sb = bnb.wsobj.bwd(x.device)
-                        if bnb.wsobj.bwd_dirty:
-                            sb.zero_()
-                            bnb.wsobj.bwd_dirty = False
-                        dx, _ = torch.ops.tfx.conv_dgrad_bn(
-                            gy, w.value, list(x.shape), stride, pad, dil, add, bnb.x, bnb.save, bnb.mask, bnb.relu,
-                            sb, None, None, amask, False, s2, _wflip(w, stride, pad, dil))
-                        bnb.red = BNBackwardFusion.IN_SLOTS
-                    elif _SR_FUSE and w.trainable and wgrad_side_stream(gy.device) is None:
+                    if w.trainable:
                         # partials stay in the slots; the weight-gradient launch below reduces them in
                         # tail blocks of its grid (conv_wgrad_sr): no bn_slot_reduce launch
                         dx, _ = torch.ops.tfx.conv_dgrad_bn(
@@ -261,24 +158,15 @@ class _Conv2d(torch.autograd.Function):
                     if sink is not None:  # mode "produce": park it for the last consumer
                         sink.put(dx)
                         dx = None
-                    elif bnb is not None and stride == 2 and _SR_FUSE2 and w.trainable and bnb.mask is None \
-                            and not bnb.deferred and bnb.wsobj is None and bnb.red is None \
-                            and wgrad_side_stream(gy.device) is None:
+                    elif bnb is not None and stride == 2 and _SR_DEFER and w.trainable and bnb.mask is None \
+                            and not bnb.deferred and bnb.red is None:
                         # dx is the complete output gradient of the BN that produced x: its backward
                         # partials go into the BN's slots now, their reduction rides in the tail of the
                         # weight-gradient launch below (no bn_bwd reduce + slot-reduce pair later)
                         torch.ops.tfx.bn_bwd_reduce_into(dx, bnb.x, bnb.save, bnb.relu, None, bnb.ws)
                         sr_bnb = bnb
             if w.trainable:
-                ss = _enter_side(gy.device)
-                if ss is not None:
-                    with torch.cuda.stream(ss):
-                        torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
-                        # the bucket hook (DP) runs with the side stream current: see allreduce.py
-                        _grad_ready(w)
-                    gy.record_stream(ss)
-                    x.record_stream(ss)
-                elif sr_bnb is not None or (_SR_TAKE_PENDING and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device):
+                if sr_bnb is not None or (_SR_TAKE_PENDING and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device):
                     take = _SR_TAKE_PENDING and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device
                     t2 = _PENDING_SR.pop(0) if take else None
                     t1 = sr_bnb
@@ -306,8 +194,8 @@ def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int
 
     ``bn_stats_into`` = the following BN layer's workspace: a raw slot tensor (the epilogue
     produces the per-channel sum / sum-of-squares of ``y``; the BN finalizes) or a
-    :class:`BNWorkspace` with ``finalize_args`` set (the epilogue's last-arriving blocks also
-    finalize; the BN only applies).  ``fuse_input_bn_backward``: the caller guarantees this conv's
+    :class:`BNWorkspace` with ``finalize_args`` set (the finalize runs right after the conv; the BN
+    only applies).  ``fuse_input_bn_backward``: the caller guarantees this conv's
     data gradient is the COMPLETE gradient of ``x`` (sole consumer, or the GradSink consumer); if
     ``x`` came from :func:`batch_norm` its backward reduction then runs in the dgrad epilogue.
     Ignored on CPU."""
@@ -371,78 +259,40 @@ class GradSink:
 
 
 class BNWorkspace:
-    """Per-BN-layer persistent f32 workspace.  Two slot sets, each [NSLOT][2][C] statistics slots
-    followed by BN_CNT column-tile arrival counters: S_f (forward statistics, filled by the producing
-    conv's epilogue) and S_b (backward partials, filled by the consuming conv's data-gradient
-    epilogue).  With channel counts the slab kernels take (``two_phase``), the BN's own passes
-    reduce the slots (bn_fwd_slots / bn_bwd_slots: no finalize or slot-reduce launch) and each
-    direction zeroes the OTHER direction's slots, so they are zero again before their next producer
-    runs (csrc/kernels/batchnorm.hip "slot-consuming passes").  ``fwd_dirty`` / ``bwd_dirty`` track
-    a direction whose slots were consumed but not yet zeroed -- a training forward with no backward,
-    or two backwards -- and the next producer then clears them explicitly.
-
-    Otherwise (``finalize_args`` set, older single-slot path) the producing conv may finalize the BN
-    in its epilogue and leave [mean | invstd | scale | shift] in ``pending_save``."""
+    """Per-BN-layer persistent f32 workspace: [NSLOT][2][C] statistics slots, zero between uses.
+    The producing conv's epilogue adds the forward statistics into them and the finalize that
+    follows re-zeroes them; in backward the consuming conv's data-gradient epilogue adds the BN
+    backward partials and the slot reduction (a weight-gradient launch's tail blocks, or
+    bn_slots_reduce) re-zeroes them.  With ``finalize_args`` set the producing conv finalizes the
+    statistics and leaves [mean | invstd | scale | shift] in ``pending_save``."""
     NSLOT = 64  # = tfx::NSLOT (csrc/include/tfx_kernels.h), checked on first GPU use
-    BN_CNT = 64
 
     def __init__(self, channels: int):
         self.c = channels
         self.buf = None
         self.finalize_args = None
         self.pending_save = None
-        self.stats_ready = False
-        self.fwd_dirty = False
-        self.bwd_dirty = False
-
-    def _half(self) -> int:
-        return self.NSLOT * 2 * self.c + self.BN_CNT
 
     def get(self, device) -> torch.Tensor:
         if self.buf is None or self.buf.device != device:
             if device.type == "cuda" and _native.use_native_device(device):
                 assert int(torch.ops.tfx.bn_nslot()) == self.NSLOT, "BNWorkspace.NSLOT != tfx::NSLOT"
-            self.buf = torch.zeros(2 * self._half(), dtype=torch.float32, device=device)
-            self.fwd_dirty = self.bwd_dirty = False
+            self.buf = torch.zeros(self.NSLOT * 2 * self.c, dtype=torch.float32, device=device)
         return self.buf
-
-    def fwd(self, device) -> torch.Tensor:
-        return self.get(device)[: self._half()]
-
-    def bwd(self, device) -> torch.Tensor:
-        return self.get(device)[self._half():]
-
-    def two_phase(self, device) -> bool:
-        return device.type == "cuda" and _native.use_native_device(device) and _slots_ok(self.c)
-
-
-_SLOTS_OK = {}
-
-
-def _slots_ok(c: int) -> bool:
-    if c not in _SLOTS_OK:
-        # opt-in (TFX_BN_SLOTS=1): inside the HIP-graph-replayed step the slot-reducing passes ran
-        # slower than finalize / slot-reduce kernel + lean apply (8.73 vs 8.60 ms/step; a graph
-        # replays the tiny kernels back to back, while every slab block pays the slot prologue):
-        # profiles/r02_bnslots
-        _SLOTS_OK[c] = bool(torch.ops.tfx.bn_slots_supported(c)) and os.environ.get("TFX_BN_SLOTS", "0") == "1"
-    return _SLOTS_OK[c]
 
 
 class BNBackwardFusion:
     """What a consumer conv's data-gradient epilogue needs to reduce a BN's backward (attached to
     the BN output as ``_tfx_bnb``): the BN input, its [mean|invstd|scale|shift], the residual
     layer's ReLU mask bits, the slot workspace and the parameter-gradient views.  The conv fills
-    ``red`` ([sum g' | sum g' xhat]), or -- two-slot-set workspaces (``wsobj``) -- leaves the
-    partials in the layer's backward slots and sets ``red = IN_SLOTS``; the BN backward then runs
-    only its apply pass."""
-    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "wsobj", "in_mask", "deferred",
+    ``red`` ([sum g' | sum g' xhat]) (or a later weight-gradient launch does, from the slots); the BN
+    backward then runs only its apply pass."""
+    __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "in_mask", "deferred",
                  "sr_pending")
-    IN_SLOTS = "slots"
 
-    def __init__(self, x, save, mask, relu, ws, dgamma, dbeta, wsobj=None):
+    def __init__(self, x, save, mask, relu, ws, dgamma, dbeta):
         self.x, self.save, self.mask, self.relu, self.ws = x, save, mask, relu, ws
-        self.dgamma, self.dbeta, self.red, self.wsobj = dgamma, dbeta, None, wsobj
+        self.dgamma, self.dbeta, self.red = dgamma, dbeta, None
         # set by a residual consumer (bn_bwd_apply_sec): the incoming gradient arrives unmasked,
         # the true gradient is g * in_mask (the consumer's ReLU mask bits)
         self.in_mask = None
@@ -477,27 +327,14 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
     return y.to(x.dtype)
 
 
-# A/B switch for batch_norm(fuse_residual_bn_backward=True)
-_FUSE_RES_BN = os.environ.get("TFX_FUSE_RES_BN", "1") != "0"
-# ... and the shortcut BN's output is never written (the tail normalizes its input on the fly)
-_DEFER_RES_BN = os.environ.get("TFX_DEFER_RES_BN", "1") != "0"
-# ... and with the tail's ReLU, pass gy + mask bits instead of writing gy * mask
-_FUSE_RES_BN_MASK = os.environ.get("TFX_FUSE_RES_BN_MASK", "1") != "0"
-
-
 # BN layers whose backward partials wait in their slot workspace for the next weight-gradient
 # launch to reduce them in its tail blocks (conv_wgrad_sr2) -- or for their own backward to reduce
 # them (bn_slots_reduce) if no such launch came first
 _PENDING_SR: List["BNBackwardFusion"] = []
 
 
-# deferred forward finalizes (a projection-shortcut BN whose output is consumed only by the block's
-# tail BN): the next conv forward launch runs them in its tail blocks (conv_fwd_bn2)
-_PENDING_FIN: List[dict] = []
-# A/B switch for the deferred finalize
-_FIN_DEFER = os.environ.get("TFX_FIN_DEFER", "0") == "1"
-# single-launch mean loss for small batches (TFX_XENT_MEAN=0: per-row kernel + mean + scale launches)
-_XENT_MEAN = os.environ.get("TFX_XENT_MEAN", "1") == "1"
+# single-launch mean loss for small batches (else: per-row kernel + mean + scale launches)
+_XENT_MEAN_MAX = 1024
 
 
 def reset_pending_slot_reductions() -> None:
@@ -505,18 +342,6 @@ def reset_pending_slot_reductions() -> None:
     for b in _PENDING_SR:
         b.sr_pending = False
     _PENDING_SR.clear()
-    _PENDING_FIN.clear()
-
-
-def _resolve_pending_fin(save: torch.Tensor) -> None:
-    """Make sure the deferred finalize that fills ``save`` has been issued (else issue it now)."""
-    for i, r in enumerate(_PENDING_FIN):
-        if r["save"] is save:
-            _PENDING_FIN.pop(i)
-            ga = r["args"]
-            torch.ops.tfx.bn_finalize_into(r["slots"], r["C"], r["M"], ga[0], ga[1], ga[2], ga[3], ga[4], ga[5],
-                                           r["save"])
-            return
 
 
 def _resolve_pending(b: "BNBackwardFusion") -> None:
@@ -551,7 +376,7 @@ def _res_bn_sec_ok(ctx, gy, mask, relu, masked):
     rb = ctx.res_bnb
     if rb is None or not ctx.has_res or masked or ctx.res_sink is not None or rb.red is not None:
         return False
-    if rb.relu or rb.mask is not None or rb.ws is None or rb.wsobj is not None:
+    if rb.relu or rb.mask is not None or rb.ws is None:
         return False
     if relu and mask is None:
         return False
@@ -562,6 +387,8 @@ class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
                 training, ws, stats_ready, res_sink, wsobj, bnb_out, res_bnb, defer):
+        # res_bnb: (BNBackwardFusion of the residual, fuse its backward here); defer: the output is
+        # only ever this layer's consumer's residual -- never written (see batch_norm)
         ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
         ctx.res_sink = res_sink
         res_bnb, res_sec = res_bnb if res_bnb is not None else (None, False)
@@ -574,40 +401,23 @@ class _BatchNorm(torch.autograd.Function):
         if ctx.native:
             x = x.contiguous()
             if ws is None:
-                ws = torch.zeros(BNWorkspace.NSLOT * 2 * x.shape[-1] + BNWorkspace.BN_CNT, dtype=torch.float32,
+                ws = torch.zeros(BNWorkspace.NSLOT * 2 * x.shape[-1], dtype=torch.float32,
                                  device=x.device)
                 stats_ready = False
             ctx.ws = ws
-            ctx.wsobj = None
             mask = None
-            two_phase = training and wsobj is not None and wsobj.two_phase(x.device)
-            pending = training and wsobj is not None and not two_phase and wsobj.pending_save is not None
+            pending = training and wsobj is not None and wsobj.pending_save is not None
             # residual = a BN output that was never written: normalize its input on the fly here
             # (bn_apply_res_bn), or materialize it for the other paths (autograd still routes its
             # gradient to that BN: the lazy tensor stays this Function's input)
             res_lazy = res is not None and res_bnb is not None and res_bnb.deferred
-            if res_lazy:
-                _resolve_pending_fin(res_bnb.save)  # no conv launch took its deferred finalize
             fuse_res = res_lazy and pending and relu
             if res_lazy and not fuse_res:
                 res = torch.ops.tfx.bn_apply_train(res_bnb.x, None, res_bnb.save, False)[0]
             defer_out = defer and pending and res is None and bnb_out is not None and _vec_ok(x.shape[-1])
-            if two_phase:
-                sf, sb = wsobj.fwd(x.device), wsobj.bwd(x.device)
-                have = bool(stats_ready) and wsobj.stats_ready
-                if not have and wsobj.fwd_dirty:
-                    sf.zero_()
-                wsobj.stats_ready = False
-                y, save, mask = torch.ops.tfx.bn_fwd_slots(x, g_t, b_t, rm, rv, momentum, eps, res, relu, sf, sb,
-                                                           have)
-                # S_f consumed (zeroed by this layer's backward apply); S_b zeroed by this pass
-                wsobj.fwd_dirty, wsobj.bwd_dirty = True, False
-                ctx.wsobj = wsobj
-            elif pending:
+            if pending:
                 # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
                 save, wsobj.pending_save = wsobj.pending_save, None
-                if not defer_out:
-                    _resolve_pending_fin(save)  # this BN applies now: its deferred finalize must have run
                 if fuse_res:
                     y, mask = torch.ops.tfx.bn_apply_res_bn(x, res_bnb.x, save, res_bnb.save, relu)
                 elif defer_out:
@@ -628,7 +438,7 @@ class _BatchNorm(torch.autograd.Function):
                     and x.shape[-1] % 8 == 0:
                 train_p = gamma is not None and gamma.trainable
                 ctx.bnb = BNBackwardFusion(x, save, mask, relu, ws, gamma.grad if train_p else None,
-                                           beta.grad if train_p else None, ctx.wsobj)
+                                           beta.grad if train_p else None)
                 ctx.bnb.deferred = defer_out
                 bnb_out.append(ctx.bnb)
             return y
@@ -653,29 +463,16 @@ class _BatchNorm(torch.autograd.Function):
             # tensor write less per identity block
             masked = ctx.has_res and ctx.res_sink is not None and mask is not None and \
                 getattr(ctx.res_sink, "accept_masked", False) and relu
-            if ctx.wsobj is not None:
-                wsobj = ctx.wsobj
-                sf, sb = wsobj.fwd(x.device), wsobj.bwd(x.device)
-                have = ctx.bnb is not None and ctx.bnb.red is BNBackwardFusion.IN_SLOTS
-                if ctx.bnb is not None:
-                    ctx.bnb.red = None
-                if not have and wsobj.bwd_dirty:
-                    sb.zero_()
-                dx, dres = torch.ops.tfx.bn_bwd_slots(gy, x, ctx.has_res, save, relu, mask, sb, sf,
-                                                      gamma.grad if train_p else None,
-                                                      beta.grad if train_p else None, have, not masked)
-                # S_b consumed (zeroed by the next forward); S_f zeroed by this pass
-                wsobj.fwd_dirty, wsobj.bwd_dirty = False, True
-            elif ctx.bnb is not None and ctx.bnb.red is not None and _res_bn_sec_ok(ctx, gy, mask, relu, masked):
+            if ctx.bnb is not None and ctx.bnb.red is not None and _res_bn_sec_ok(ctx, gy, mask, relu, masked):
                 # ... and the residual's own BN backward is reduced in the same pass
                 rb = ctx.res_bnb
                 p_t = rb.dgamma is not None
                 # with a ReLU the residual gradient is gy * mask: hand the residual BN gy itself and
                 # the mask bits instead of writing the masked copy
-                pass_mask = relu and _FUSE_RES_BN_MASK
-                # _SR_FUSE: the residual BN's slot reduction is deferred to the tail of the next weight-
-                # gradient launch (this block's conv3, which autograd runs before the residual BN)
-                defer = _SR_FUSE2 and wgrad_side_stream(gy.device) is None
+                pass_mask = relu
+                # the residual BN's slot reduction is deferred to the tail of the next weight-gradient
+                # launch (this block's conv3, which autograd runs before the residual BN)
+                defer = _SR_DEFER
                 dx, dres, red2 = torch.ops.tfx.bn_bwd_apply_sec(gy, x, save, ctx.bnb.red, relu, mask, rb.x, rb.save,
                                                                  rb.ws, rb.dgamma if p_t else None,
                                                                  rb.dbeta if p_t else None, not pass_mask, not defer)
@@ -756,10 +553,10 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
     rb = getattr(residual, "_tfx_bnb", None) if residual is not None else None
     res_bnb = None
     if rb is not None and (rb.deferred or fuse_residual_bn_backward):
-        res_bnb = (rb, bool(fuse_residual_bn_backward and _FUSE_RES_BN))
+        res_bnb = (rb, bool(fuse_residual_bn_backward))
     y = _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
                          workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out, res_bnb,
-                         bool(defer_output and _DEFER_RES_BN))
+                         bool(defer_output))
     if bnb_out:
         y._tfx_bnb = bnb_out[0]
     return y
@@ -948,7 +745,7 @@ class _SoftmaxXent(torch.autograd.Function):
             idx = labels.contiguous() if labels.dtype == torch.long else None
             dense = labels.float().contiguous() if labels.dtype != torch.long else None
             ctx.dtype = logits.dtype
-            if _XENT_MEAN and B * ((C + 63) // 64) <= 1024:
+            if B * ((C + 63) // 64) <= _XENT_MEAN_MAX:
                 # one launch: the mean loss and dz (already in the logits' dtype when the caller
                 # promises a unit seed gradient, so backward launches nothing)
                 loss, dz = torch.ops.tfx.softmax_xent_mean(logits.contiguous(), idx, dense, naive,

@@ -24,14 +24,12 @@ north-star RCCL path of BASELINE.json (configs 3 and 5).
 """
 from __future__ import annotations
 
-import contextlib
 import os
 from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
-from ..ops.nn import compute_stream_of_backward, wgrad_side_stream
 from ..variables import ALIGN, Variable, VariableStore
 
 
@@ -87,7 +85,6 @@ class GradAllReduce:
                 groups.append(last)
         for g in groups:
             self._close(g)
-        self._launch_stream = None
         self._pending: List[int] = []
         self._launched: List[bool] = []
         self._works = []
@@ -146,35 +143,17 @@ class GradAllReduce:
             raise RuntimeError("HIP graph capture of the DP step needs the nccl (RCCL) backend, not %s"
                                % dist.get_backend(self.group))
         op = dist.ReduceOp.SUM if self.premul is None else dist._make_nccl_premul_sum(float(self.premul))
-        # a bucket's gradients come from the compute stream AND the side stream of the weight
-        # gradients (ops/nn.py): issue the collective from a launch stream that waits on both, so it
-        # is ordered after every producer without stalling either
-        side = wgrad_side_stream(view.device) if view.is_cuda else None
-        ctx = contextlib.nullcontext()
-        if side is not None:
-            if self._launch_stream is None:
-                self._launch_stream = torch.cuda.Stream(device=view.device)
-            ls = self._launch_stream
-            ls.wait_stream(torch.cuda.current_stream(view.device))
-            ls.wait_stream(side)
-            main = compute_stream_of_backward(view.device)
-            if main is not None:
-                ls.wait_stream(main)
-            ctx = torch.cuda.stream(ls)
-        with ctx:
-            if self.compress:
-                tmp = view.to(torch.bfloat16)
-                work = dist.all_reduce(tmp, op=op, group=self.group, async_op=True)
-                self._works.append((work, view, tmp))
-            else:
-                self._works.append((dist.all_reduce(view, op=op, group=self.group, async_op=True), None, None))
+        # issued from the compute stream right after the bucket's last gradient kernel: RCCL runs it
+        # on its own stream, ordered after that kernel, beside the rest of backward
+        if self.compress:
+            tmp = view.to(torch.bfloat16)
+            work = dist.all_reduce(tmp, op=op, group=self.group, async_op=True)
+            self._works.append((work, view, tmp))
+        else:
+            self._works.append((dist.all_reduce(view, op=op, group=self.group, async_op=True), None, None))
 
     def finish(self) -> None:
         """Launch buckets not yet started (in order) and make the current stream wait for all."""
-        if torch.cuda.is_available() and self.store.grad.is_cuda:
-            side = wgrad_side_stream(self.store.grad.device)
-            if side is not None:  # the weight gradients of the last layers may still be running
-                torch.cuda.current_stream(self.store.grad.device).wait_stream(side)
         for b in range(len(self.buckets)):
             if not self._launched[b]:
                 self._launch(b)

@@ -13,7 +13,6 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from .ops import _native
 from .ops.nn import reset_pending_slot_reductions
 from .optim import Optimizer
 from .parallel.allreduce import GradAllReduce
@@ -101,12 +100,6 @@ class ClassifierTrainer:
             # Reset it so the eager fallback reduces every bucket exactly once.
             self.graph, self._static = None, None
             if self.dp is not None:
-                # a side stream forked into the failed capture and never joined stays capturing (and
-                # then blocks every synchronous call of this thread): end it, drop the stream
-                ls = getattr(self.dp, "_launch_stream", None)
-                if ls is not None and _native.use_native_device(ls.device):
-                    torch.ops.tfx.end_stream_capture(ls.cuda_stream)
-                self.dp._launch_stream = None
                 self.dp.reset()
             raise
         self.graph = g

@@ -121,7 +121,7 @@ def test_resnet50_batch256_first_step_vs_fp32_reference(gpu):
 def test_deferred_slot_reductions_fallback_and_off_agree(gpu):
     """ResNet-50 first-step gradients with the BN-backward slot reductions (i) taken by the next
     weight-gradient launch's tail (default), (ii) deferred but resolved by each BN's own backward
-    (no wgrad takes them: the fallback path), (iii) never deferred (TFX_SR_FUSE2 off): the same
+    (no wgrad takes them: the fallback path), (iii) never deferred (_SR_DEFER off): the same
     gradients up to the f32-atomic noise floor measured between two default runs."""
     from tensorflow_examples_amd import ops
     from tensorflow_examples_amd.ops import nn as nnops
@@ -139,16 +139,16 @@ def test_deferred_slot_reductions_fallback_and_off_agree(gpu):
         assert not nnops._PENDING_SR, "a deferred reduction was never resolved"
         return st.grad.clone(), st
 
-    saved = (nnops._SR_TAKE_PENDING, nnops._SR_FUSE2)
+    saved = (nnops._SR_TAKE_PENDING, nnops._SR_DEFER)
     try:
         g0, st = run()
         g1, _ = run()
         nnops._SR_TAKE_PENDING = False
         g2, _ = run()
-        nnops._SR_TAKE_PENDING, nnops._SR_FUSE2 = True, False
+        nnops._SR_TAKE_PENDING, nnops._SR_DEFER = True, False
         g3, _ = run()
     finally:
-        nnops._SR_TAKE_PENDING, nnops._SR_FUSE2 = saved
+        nnops._SR_TAKE_PENDING, nnops._SR_DEFER = saved
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
@@ -156,42 +156,3 @@ def test_deferred_slot_reductions_fallback_and_off_agree(gpu):
         for gx, tag in ((g2, "fallback"), (g3, "off")):
             e = (gx[sl] - g0[sl]).norm().item() / n
             assert e <= max(4 * noise, 1e-3), (tag, v.name, e, noise)
-
-
-def test_deferred_shortcut_finalize_matches_immediate(gpu):
-    """The projection-shortcut BN's forward finalize deferred into the tail blocks of the next conv
-    launch (conv_fwd_bn2 fin_*), or resolved late by its consumer (bn_finalize_into), gives the same
-    loss, running statistics and gradients as the immediate finalize."""
-    from tensorflow_examples_amd import ops
-    from tensorflow_examples_amd.ops import nn as nnops
-
-    g = torch.Generator().manual_seed(6)
-    img = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, generator=g)
-    lab = torch.randint(0, 10, (32,), generator=g).to(gpu)
-    xin = to_model_input(img.to(gpu))
-
-    def run():
-        st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=4)
-        st.zero_grad()
-        loss = ops.softmax_cross_entropy(m(xin, training=True), lab)
-        loss.backward()
-        torch.cuda.synchronize()
-        assert not nnops._PENDING_FIN, "a deferred finalize was never issued"
-        return float(loss), st.grad.clone(), {k: t.clone() for k, t in st.state.items()}
-
-    saved = nnops._FIN_DEFER
-    try:
-        nnops._FIN_DEFER = False
-        l0, g0, s0 = run()
-        la, ga, sa = run()  # noise floor: the epilogue's f32-atomic statistics sum in any order
-        nnops._FIN_DEFER = True
-        l1, g1, s1 = run()
-    finally:
-        nnops._FIN_DEFER = saved
-    assert abs(l1 - l0) <= 4 * abs(la - l0) + 2e-3 * abs(l0), (l0, la, l1)
-    for k in s0:
-        noise = (sa[k] - s0[k]).abs().max().item()
-        assert (s1[k] - s0[k]).abs().max().item() <= 4 * noise + 1e-4 * s0[k].abs().max().item() + 1e-6, k
-    eg = ((g1 - g0).norm() / g0.norm()).item()
-    en = ((ga - g0).norm() / g0.norm()).item()
-    assert eg <= 4 * en + 1e-3, (eg, en)
