@@ -11,9 +11,16 @@ Launch modes (the process-per-task model of R/distributed/distributed.py:7-14,37
 * ``python bench.py --gpus N`` with no RANK in the environment: this process is only a launcher --
   it never touches the GPU, spawns N fresh ranks of itself (parallel/launch.py ``spawn_local``,
   rendezvous on 127.0.0.1), relays rank 0's JSON line and exits non-zero if any rank fails;
-* under ``torch.distributed.run`` (or our launcher) every rank runs the step; each checks that the
-  process group spans exactly ``--gpus`` ranks (size + an all-reduce of ones) before timing, and
-  ``n_gpus`` in the JSON is that verified world size.
+* under ``torch.distributed.run`` each rank process is a supervisor that never touches the GPU and
+  runs the real rank as a child (parallel/launch.py ``supervise_rank``);
+* either way the job cannot end without a result line inside ``--launch-timeout`` (default 480 s,
+  below the driver's 600 s lease): attempt 1 (HIP-graph-replayed DP step) gets half of it; if any
+  rank fails or hangs, every rank is killed and the job reruns ONCE as fresh processes with
+  ``TFX_DP_GRAPH=0`` (eager RCCL collectives) on a new rendezvous.  The JSON says which attempt
+  produced it (``config.attempt``, ``config.hip_graph``).  ``TFX_BENCH_HANG=<rank>:<attempt>`` makes
+  that rank hang before its first step (test hook);
+* every rank checks that the process group spans exactly ``--gpus`` ranks (size + an all-reduce of
+  ones) before timing; ``n_gpus`` / ``config.rccl_ranks`` in the JSON are that verified size.
 
 Timing: W untimed warmup steps; barrier + synchronize; K timed steps; barrier + synchronize; the
 MAX elapsed over ranks is reported.  Rank 0 prints ONE JSON line.
@@ -63,8 +70,10 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--backend", default=None, help="process-group backend (default nccl = RCCL, gloo on cpu)")
-    ap.add_argument("--launch-timeout", type=float, default=1800.0,
-                    help="launcher mode: seconds before the whole job is killed")
+    ap.add_argument("--launch-timeout", type=float, default=480.0,
+                    help="N>1: seconds by which the job must have produced its result line (both attempts)")
+    ap.add_argument("--attempt-timeout", type=float, default=None,
+                    help="N>1: seconds for attempt 1 before the eager fallback (default: half of --launch-timeout)")
     return ap.parse_args(argv)
 
 
@@ -94,8 +103,9 @@ def run(a):
     dev = init_distributed(backend=a.backend, device=a.device)
     world = dist.get_world_size() if dist.is_initialized() else 1
     forced = dist.is_initialized() and world == 1  # TFX_DP_FORCE_COLLECTIVE rehearsal of the RCCL path
+    ranks = 1
     if "RANK" in os.environ or a.gpus > 1:
-        verify_world(a.gpus if not forced else 1, dev)
+        ranks = verify_world(a.gpus if not forced else 1, dev)
     rank = dist.get_rank() if dist.is_initialized() else 0
     # host-side control collectives (capture agreement, timing barriers, elapsed-time MAX) run on a
     # gloo group: the RCCL communicator then carries only the gradient all-reduces, and no eager RCCL
@@ -184,6 +194,10 @@ def run(a):
             topt.step()
             return loss.detach()
 
+    hang = os.environ.get("TFX_BENCH_HANG", "")
+    if hang and hang == "%d:%s" % (rank, os.environ.get("TFX_BENCH_ATTEMPT", "1")):
+        print("rank %d: TFX_BENCH_HANG -- hanging before the first step" % rank, file=sys.stderr, flush=True)
+        time.sleep(1e6)
     for i in range(a.warmup):
         loss = step(i)
     sync()
@@ -231,6 +245,9 @@ def run(a):
                 "parallelism": "dp%d" % world,
                 "device": a.device,
                 "backend": dist.get_backend() if dist.is_initialized() else None,
+                "rccl_ranks": ranks if (dist.is_initialized() and dist.get_backend() == "nccl") else None,
+                "verified_ranks": ranks,
+                "attempt": int(os.environ.get("TFX_BENCH_ATTEMPT", "1")),
                 "impl": a.impl,
                 "optimizer": "momentum-SGD 0.9, wd 5e-4 (fused flat-buffer kernel)" if a.impl == "native" else "torch.optim.SGD foreach",
                 "allreduce_bucket_mb": a.bucket_mb,
@@ -247,13 +264,20 @@ def run(a):
         dist.destroy_process_group()
 
 
+FALLBACK_ENV = {"TFX_DP_GRAPH": "0"}  # attempt 2: eager RCCL collectives instead of graph replay
+
+
 def main(argv=None):
     a = parse(argv)
-    from tensorflow_examples_amd.parallel.launch import under_launcher, spawn_local
+    from tensorflow_examples_amd.parallel.launch import (can_supervise, launch_with_fallback, supervise_rank,
+                                                         under_launcher)
+    args = [os.path.abspath(__file__), *list(sys.argv[1:] if argv is None else argv)]
     if a.gpus > 1 and not under_launcher():
         # launcher mode: this process never initialises the GPU; the ranks are fresh processes
-        args = list(sys.argv[1:] if argv is None else argv)
-        return spawn_local(a.gpus, [os.path.abspath(__file__), *args], timeout_s=a.launch_timeout)
+        return launch_with_fallback(a.gpus, args, a.launch_timeout, FALLBACK_ENV, a.attempt_timeout)
+    if a.gpus > 1 and can_supervise():
+        # one torch.distributed.run rank: supervise the real rank as a child (never touch the GPU here)
+        return supervise_rank(args, a.launch_timeout, FALLBACK_ENV, a.attempt_timeout)
     run(a)
     return 0
 

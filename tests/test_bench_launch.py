@@ -10,6 +10,7 @@ import os
 import subprocess
 import sys
 import textwrap
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -65,3 +66,67 @@ def test_verify_world_rejects_wrong_size(tmp_path):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert p.returncode != 0
     assert "expected 2" in p.stderr
+
+
+def _one_json(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+_BENCH_SMALL = ["--gpus", "2", "--device", "cpu", "--depth", "18", "--batch", "4", "--steps", "2", "--warmup", "1",
+                "--nbatches", "2", "--launch-timeout", "240", "--attempt-timeout", "45"]
+
+
+def test_bench_hang_falls_back_in_launcher_mode():
+    """Rank 1 hangs before its first step (TFX_BENCH_HANG, attempt 1 only): the launcher kills the job
+    at the attempt deadline and reruns fresh ranks with the eager fallback -- exactly one JSON line,
+    from attempt 2, spanning both ranks, well inside the overall deadline."""
+    env = dict(_env(), TFX_BENCH_HANG="1:1")
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *_BENCH_SMALL], capture_output=True,
+                       text=True, timeout=400, env=env, cwd=ROOT)
+    took = time.monotonic() - t0
+    assert p.returncode == 0, p.stderr[-4000:]
+    rec = _one_json(p.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["verified_ranks"] == 2
+    assert rec["config"]["attempt"] == 2 and rec["config"]["hip_graph"] is False
+    assert "attempt 1 failed" in p.stderr
+    assert took < 240, took
+
+
+def test_bench_hang_falls_back_under_torchrun():
+    """The driver's form of the scaling run: ``python -m torch.distributed.run ... bench.py --gpus 2``.
+    Each torchrun rank supervises its real rank as a child; rank 1's child hangs in attempt 1, the
+    supervisors agree on the failure through the agent store and rerun on a fresh rendezvous: one JSON
+    line, from attempt 2, with n_gpus == 2."""
+    env = dict(_env(), TFX_BENCH_HANG="1:1")
+    t0 = time.monotonic()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), *_BENCH_SMALL]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    took = time.monotonic() - t0
+    assert p.returncode == 0, p.stderr[-4000:]
+    rec = _one_json(p.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["attempt"] == 2
+    assert "attempt 2" in p.stderr
+    assert took < 240, took
+
+
+def test_bench_under_torchrun_no_fault_runs_once():
+    """Without a fault the supervised job runs attempt 1 only and prints its one JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), *_BENCH_SMALL]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=_env(), cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-4000:]
+    rec = _one_json(p.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["attempt"] == 1
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port

@@ -463,43 +463,6 @@ def test_linear_small_bwd(gpu, B, I, O):
     assert _rel(db - 1, g.float().sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("shape", [(256, 32, 32, 128, 128, 3), (256, 16, 16, 256, 256, 3), (256, 8, 8, 512, 512, 3),
-                                   (8, 9, 7, 64, 32, 3)])
-@pytest.mark.parametrize("variant", ["relu", "plain"])
-def test_conv_dgrad_bn_stride2_classes(gpu, shape, variant):
-    """Stride-2 data gradient run as 4 output-parity-class GEMMs, each with the BN-backward epilogue
-    (the stride-2 conv2 of ResNet-50's transition blocks): dx and the reduction vs the unfused
-    conv_dgrad -> bn_bwd, the workspace restored to zero, dgamma / dbeta accumulated."""
-    N, H, W, C, Ko, R = shape
-    st, pad = 2, 1
-    torch.manual_seed(16)
-    xb = _bf(torch.randn(N, H, W, C, device=gpu) * 1.5 + 0.3)
-    relu = variant == "relu"
-    gamma = torch.rand(C, device=gpu) + 0.5
-    beta = torch.randn(C, device=gpu)
-    ws = torch.zeros(64 * 2 * C + 64, device=gpu)
-    y, save, _ = torch.ops.tfx.bn_fwd_train(xb, gamma, beta, None, None, 0.1, 1e-5, None, relu, ws, False)
-    w = _bf(torch.randn(Ko, R, R, C, device=gpu) * 0.1)
-    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
-    dy = _bf(torch.randn(N, P, Q, Ko, device=gpu))
-    ref_dx = torch.ops.tfx.conv_dgrad(dy, w, list(y.shape), st, pad, 1, None)
-    ref_f = torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
-                                       stride=st, padding=pad).permute(0, 2, 3, 1)
-    assert _rel(ref_dx, ref_f) < 1e-2
-    wsr = torch.zeros(64 * 2 * C, device=gpu)
-    dgr, dbr = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
-    ref_bx, _, ref_red = torch.ops.tfx.bn_bwd(ref_dx, xb, None, save, relu, wsr, dgr, dbr, None)
-    dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
-    dx, red = torch.ops.tfx.conv_dgrad_bn(dy, w, list(y.shape), st, pad, 1, None, xb, save, None, relu, ws, dg, db)
-    torch.cuda.synchronize()
-    assert ws.abs().max().item() == 0.0, "workspace not restored to zero"
-    assert _rel(dx, ref_dx) < 1e-3
-    assert _rel(red, ref_red) < 1e-3
-    assert _rel(dg, dgr) < 1e-3 and _rel(db, dbr) < 1e-3
-    bx, _ = torch.ops.tfx.bn_bwd_apply(dx, xb, None, save, red, relu, None)
-    assert _rel(bx, ref_bx) < 1e-2
-
-
 @pytest.mark.parametrize("shape", [(256, 32, 32, 64, 64, 1, 1), (256, 32, 32, 64, 64, 3, 1),
                                    (256, 16, 16, 128, 128, 3, 1), (256, 8, 8, 1024, 256, 1, 1),
                                    (256, 4, 4, 512, 2048, 1, 1), (256, 16, 16, 256, 256, 3, 2), (4, 5, 5, 24, 40, 3, 1)])
