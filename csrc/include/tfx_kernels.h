@@ -106,6 +106,33 @@ struct IgemmArgs {
 };
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s);
 
+// ---------------------------------------------------------------- fused pointwise-conv backward (pw_bwd.hip)
+// Backward of a bottleneck's expanding 1x1 conv (CN -> CW = 4 CN) fused with the block-tail BN's
+// backward apply: dy3 = A (g * mask) + B y3 + D formed on load, dA2 = dy3 . W3 (+ BN2 backward
+// partials into slots2 when y2 != null), dW3 partials into slab[grid][CW * CN] (pw_slab_reduce).
+struct PwExpandArgs {
+  const uint16_t* g = nullptr;      // [M][CW] output gradient of the block
+  const uint16_t* y3 = nullptr;     // [M][CW] tail BN input (conv3 output)
+  const uint8_t* mask3 = nullptr;   // [M][CW / 8] tail ReLU mask bits
+  const float* save3 = nullptr;     // [4][CW] mean | invstd | scale | shift
+  const float* red3 = nullptr;      // [2][CW] sum g' | sum g' xhat
+  const uint16_t* a2 = nullptr;     // [M][CN] conv3 input
+  const uint16_t* w = nullptr;      // [CW][CN] conv3 weight
+  uint16_t* dA2 = nullptr;          // [M][CN] out
+  const uint16_t* y2 = nullptr;     // [M][CN] BN2 input (null: no BN2 partials)
+  const float* save2 = nullptr;     // [4][CN]
+  int relu2 = 0;
+  float* slots2 = nullptr;          // [NSLOT][2][CN]
+  float* slab = nullptr;            // [grid][CW * CN] f32
+  int M = 0, CN = 0;
+};
+bool pw_bwd_expand_ok(int CN, int64_t M);
+int pw_bwd_expand_grid(int CN, int64_t M);
+void pw_bwd_expand(const PwExpandArgs& args, int nblocks, hipStream_t s);
+// dw[CW][CN] += sum of nslab slabs; + optional BN slot reduction (bn_slot_reduce's math) in tail blocks
+void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_slots, int sr_C, float* sr_red,
+                    float* sr_dgamma, float* sr_dbeta, hipStream_t s);
+
 // ---------------------------------------------------------------- f32 GEMM (MFMA f32, exact)
 // C[M][N] = act(alpha * op(A) op(B) + bias) (+ C if accumulate); op = transpose flags
 // allow_split: split K over blocks with f32-atomic partials when the output has few tiles (act 0)
@@ -213,11 +240,13 @@ void lstm_cell_bwd(const float* act, const float* c, const float* c_prev, const 
 // persistent whole-sequence recurrence (lstm_seq.hip): one launch per layer and direction
 int lstm_seq_sync_words(int B, int H);
 bool lstm_seq_supported(int B, int H, int num_cus);
+// status: a sticky health word (set to 1 when a bounded hand-off wait expires; never cleared by the
+// launch) -- null = the sync buffer's own status word; spin_limit 0 = the default bound (tests force 1)
 void lstm_seq_fwd(const float* gx, const uint16_t* whh, int T, int B, int H, uint16_t* hbuf, float* cbuf, float* act,
-                  float* hT, unsigned* sync, hipStream_t s);
+                  float* hT, unsigned* sync, unsigned* status, unsigned spin_limit, hipStream_t s);
 void lstm_seq_bwd(const float* act, const float* cbuf, const uint16_t* dH, const float* dhT, const float* dc_in,
                   const uint16_t* whh, int T, int B, int H, uint16_t* dg, float* dc_out, float* dbias, unsigned* sync,
-                  hipStream_t s);
+                  unsigned* status, unsigned spin_limit, hipStream_t s);
 
 // ---------------------------------------------------------------- input pipeline
 // uint8 NHWC [npix][cin] (cin <= 4) -> bf16 NHWC [npix][cout] (cout 4 or 8): (x/255 - mean)/std, zero pad

@@ -63,11 +63,11 @@ __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int off, u32x4v
 __device__ __forceinline__ float ls_sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // One lane: wait until *ctr >= target.  false = gave up (status word set).
-__device__ __forceinline__ bool ls_wait(gu32* ctr, unsigned target, gu32* status) {
+__device__ __forceinline__ bool ls_wait(gu32* ctr, unsigned target, gu32* status, unsigned limit) {
   for (unsigned spins = 0;; ++spins) {
     const unsigned v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v >= target) return true;
-    if (spins >= LS_SPIN_LIMIT) {
+    if (spins >= limit) {
       __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
@@ -76,9 +76,10 @@ __device__ __forceinline__ bool ls_wait(gu32* ctr, unsigned target, gu32* status
 }
 
 // Block-wide: lane 0 waits; everyone learns the outcome after the barrier.
-__device__ __forceinline__ bool ls_block_wait(gu32* ctr, unsigned target, gu32* status, int* flag) {
+__device__ __forceinline__ bool ls_block_wait(gu32* ctr, unsigned target, gu32* status, int* flag,
+                                              unsigned limit) {
   if (threadIdx.x == 0) {
-    const bool ok = ls_wait(ctr, target, status);
+    const bool ok = ls_wait(ctr, target, status, limit);
     *flag = ok ? 1 : 0;
   }
   __syncthreads();
@@ -97,7 +98,7 @@ template <int NK>
 __global__ void __launch_bounds__(256, 1)
     lstm_seq_fwd_kernel(const float* __restrict__ gx, const uint16_t* __restrict__ whh, int T, int B,
                         uint16_t* hbuf, float* __restrict__ cbuf, float* __restrict__ act, float* __restrict__ hT,
-                        unsigned* sync) {
+                        unsigned* sync, unsigned* status_word, unsigned limit) {
   constexpr int H = NK * 32, NKW = NK / 4, KQ = H / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);                    // [wave][gate][lane][4]  16 KB
@@ -106,7 +107,7 @@ __global__ void __launch_bounds__(256, 1)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int nub = gridDim.x, u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
   gu32* ctr = (gu32*)(sync + blockIdx.y * nub * LS_STRIDE);  // row block's counter / flag lines
-  gu32* status = (gu32*)(sync + gridDim.y * nub * LS_STRIDE);
+  gu32* status = (gu32*)status_word;  // sticky health word: set on a bounded wait's expiry
   if (tid == 0) flag[1] = 0;
 
   // W_hh rows (gate q, unit u0 + lane%16), this wave's K quarter: B operand, resident all sequence
@@ -130,7 +131,7 @@ __global__ void __launch_bounds__(256, 1)
     const float z0 = g[0], z1 = g[H], z2 = g[2 * H], z3 = g[3 * H];  // hoisted projection, pre-launch data
     const __amdgpu_buffer_rsrc_t hr = ls_rsrc(hbuf + t * BH + (int64_t)r0 * H, 16 * H * 2);
     bf16x8_t a[NKW];
-    if (t > 0 && !ls_block_wait(ctr, (unsigned)(t * nub), status, flag)) return;
+    if (t > 0 && !ls_block_wait(ctr, (unsigned)(t * nub), status, flag, limit)) return;
 #pragma unroll
     for (int kk = 0; kk < NKW; ++kk) a[kk] = ld_sc1(hr, aoff + kk * 64);
     __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA waits
@@ -180,7 +181,8 @@ __global__ void __launch_bounds__(256, 1)
     lstm_seq_bwd_kernel(const float* __restrict__ act, const float* __restrict__ cbuf,
                         const uint16_t* __restrict__ dH, const float* __restrict__ dhT,
                         const float* __restrict__ dc_in, const uint16_t* __restrict__ whh, int T, int B, uint16_t* dg,
-                        float* __restrict__ dc_out, float* __restrict__ dbias, unsigned* sync) {
+                        float* __restrict__ dc_out, float* __restrict__ dbias, unsigned* sync, unsigned* status_word,
+                        unsigned limit) {
   constexpr int H = NK * 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);                    // [wave][lane][4]  4 KB
@@ -189,7 +191,7 @@ __global__ void __launch_bounds__(256, 1)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int nub = gridDim.x, u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
   gu32* ctr = (gu32*)(sync + blockIdx.y * nub * LS_STRIDE);
-  gu32* status = (gu32*)(sync + gridDim.y * nub * LS_STRIDE);
+  gu32* status = (gu32*)status_word;  // sticky health word: set on a bounded wait's expiry
   if (tid == 0) flag[1] = 0;
 
   // W_hh^T slice: B operand k = gate column q*H + kk*32 + (lane/16)*8 + e, n = unit u0 + lane%16
@@ -221,7 +223,7 @@ __global__ void __launch_bounds__(256, 1)
     if (s > 0) {
       const __amdgpu_buffer_rsrc_t gr = ls_rsrc(dg + (t + 1) * 4 * BH + (int64_t)r0 * 4 * H, 16 * 4 * H * 2);
       bf16x8_t a[NK];
-      if (!ls_block_wait(ctr, (unsigned)(s * nub), status, flag)) return;
+      if (!ls_block_wait(ctr, (unsigned)(s * nub), status, flag, limit)) return;
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) a[kk] = ld_sc1(gr, aoff + kk * 64);
       __builtin_amdgcn_sched_barrier(0);
@@ -287,21 +289,22 @@ void ls_prepare(K k) {
 
 template <int NK>
 void fwd_launch(dim3 grid, const float* gx, const uint16_t* whh, int T, int B, uint16_t* hbuf, float* cbuf,
-                float* act, float* hT, unsigned* sync, hipStream_t s) {
+                float* act, float* hT, unsigned* sync, unsigned* status, unsigned limit, hipStream_t s) {
   static bool once = (ls_prepare(lstm_seq_fwd_kernel<NK>), true);
   (void)once;
   (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B, H_of<NK>()) * 4, s);
-  lstm_seq_fwd_kernel<NK><<<grid, 256, LS_LDS, s>>>(gx, whh, T, B, hbuf, cbuf, act, hT, sync);
+  lstm_seq_fwd_kernel<NK><<<grid, 256, LS_LDS, s>>>(gx, whh, T, B, hbuf, cbuf, act, hT, sync, status, limit);
 }
 
 template <int NK>
 void bwd_launch(dim3 grid, const float* act, const float* cbuf, const uint16_t* dH, const float* dhT,
                 const float* dc_in, const uint16_t* whh, int T, int B, uint16_t* dg, float* dc_out, float* dbias,
-                unsigned* sync, hipStream_t s) {
+                unsigned* sync, unsigned* status, unsigned limit, hipStream_t s) {
   static bool once = (ls_prepare(lstm_seq_bwd_kernel<NK>), true);
   (void)once;
   (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B, H_of<NK>()) * 4, s);
-  lstm_seq_bwd_kernel<NK><<<grid, 256, LS_LDS, s>>>(act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync);
+  lstm_seq_bwd_kernel<NK><<<grid, 256, LS_LDS, s>>>(act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync,
+                                                    status, limit);
 }
 
 }  // namespace
@@ -315,25 +318,29 @@ bool lstm_seq_supported(int B, int H, int num_cus) {
 }
 
 void lstm_seq_fwd(const float* gx, const uint16_t* whh, int T, int B, int H, uint16_t* hbuf, float* cbuf, float* act,
-                  float* hT, unsigned* sync, hipStream_t s) {
+                  float* hT, unsigned* sync, unsigned* status, unsigned spin_limit, hipStream_t s) {
   const dim3 grid(H / 16, B / 16);
+  if (status == nullptr) status = sync + (B / 16) * (H / 16) * LS_STRIDE;
+  const unsigned lim = spin_limit ? spin_limit : LS_SPIN_LIMIT;
   switch (H) {
-    case 128: fwd_launch<4>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
-    case 256: fwd_launch<8>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
-    case 512: fwd_launch<16>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
-    default: fwd_launch<32>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, s); break;
+    case 128: fwd_launch<4>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, status, lim, s); break;
+    case 256: fwd_launch<8>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, status, lim, s); break;
+    case 512: fwd_launch<16>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, status, lim, s); break;
+    default: fwd_launch<32>(grid, gx, whh, T, B, hbuf, cbuf, act, hT, sync, status, lim, s); break;
   }
 }
 
 void lstm_seq_bwd(const float* act, const float* cbuf, const uint16_t* dH, const float* dhT, const float* dc_in,
                   const uint16_t* whh, int T, int B, int H, uint16_t* dg, float* dc_out, float* dbias, unsigned* sync,
-                  hipStream_t s) {
+                  unsigned* status, unsigned spin_limit, hipStream_t s) {
   const dim3 grid(H / 16, B / 16);
+  if (status == nullptr) status = sync + (B / 16) * (H / 16) * LS_STRIDE;
+  const unsigned lim = spin_limit ? spin_limit : LS_SPIN_LIMIT;
   switch (H) {
-    case 128: bwd_launch<4>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, s); break;
-    case 256: bwd_launch<8>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, s); break;
-    case 512: bwd_launch<16>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, s); break;
-    default: bwd_launch<32>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, s); break;
+    case 128: bwd_launch<4>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, status, lim, s); break;
+    case 256: bwd_launch<8>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, status, lim, s); break;
+    case 512: bwd_launch<16>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, status, lim, s); break;
+    default: bwd_launch<32>(grid, act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync, status, lim, s); break;
   }
 }
 

@@ -1,0 +1,430 @@
+// Fused backward of a ResNet bottleneck's EXPANDING 1x1 conv (conv3: narrow width CN -> wide CW = 4 CN)
+// together with the block-tail BN's backward apply, for gfx950.
+//
+// The layer-wise backward of an identity block's tail is three passes over wide (CW-channel) tensors:
+//   bn_bwd_apply   dy3 = A (g * relu_mask) + B y3 + D          reads g, y3, mask   writes dy3
+//   conv3 dgrad    dA2 = dy3 . W3        (+ BN2-backward partials of dA2 in the epilogue)   reads dy3
+//   conv3 wgrad    dW3 += dy3^T . a2                                                         reads dy3
+// Here ONE persistent launch reads g, y3 and the mask bits once, forms dy3 (bf16, as the apply pass
+// would have written it) straight into LDS, and runs BOTH GEMMs from that tile: per 32-row m-tile
+//   dgrad  acc_d[32 x CN]  += T[32 x CW] . W3[CW x CN]      (W3 resident in LDS for the whole launch)
+//   wgrad  acc_w[CW x CN]  += T^T[CW x 32] . A2[32 x CN]    (accumulated in registers over every
+//                                                            m-tile of the block)
+// so dy3 never exists in HBM: two wide passes and a launch fewer per block (ResNet-50/CIFAR stage 1:
+// 134 MB each).  The dgrad epilogue stores dA2 and accumulates the BN2 backward partials (sum g',
+// sum g' xhat with g' = bf16(dA2) * [y2 scale + shift > 0]) -- igemm.hip's EPI_BNB math.  Each block
+// leaves its wgrad accumulator in a per-block f32 slab (plain coalesced stores, no f32 atomics:
+// MI355X_MICROARCH.md "Global float atomics" runs those at ~1.3 TB/s); pw_slab_reduce then sums the
+// slabs into dW3 and, in tail blocks of the same launch, reduces BN2's slots.
+//
+// Pipeline: 512 threads (8 waves), one block per CU, register staging ring of two m-tiles: at step i
+// tile i's staged registers are transformed into LDS slot i%2, then tile i+2 is issued into the same
+// registers -- two m-tiles (~90 KB) in flight per CU while tile i computes.  One barrier per step
+// (two LDS slots: a slot is rewritten two steps after it was read, behind the barrier between).
+// Reference: the unfused chain of R/distributed/distributed.py:96-102 that SURVEY §2.7 says the
+// framework fuses; north-star ResNet-50 (BASELINE.json configs 3).
+#include "tfx_common.h"
+#include "tfx_kernels.h"
+
+#include <utility>
+
+namespace tfx {
+namespace {
+
+constexpr int PW_NT = 512;   // threads per block
+constexpr int PW_BM = 32;    // rows (pixels) per m-tile
+
+typedef short pw_s4 __attribute__((ext_vector_type(4)));
+typedef short pw_s8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) pw_s4 pw_lds_s4;
+typedef __attribute__((address_space(3))) char pw_lds_char;
+typedef __attribute__((address_space(3))) bf16x8_t pw_lds_bf16x8;
+typedef unsigned int pw_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int pw_u32x2 __attribute__((ext_vector_type(2)));
+
+// K-major image of 64-channel rows (128 B): 16-B chunk c of row r at r*128 + ((c ^ (r&7)) << 4)
+__device__ __forceinline__ int pw_kmaj(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+// MN-major image of COLS-element rows (as igemm_impl.h mn_off): XOR swizzle per row length
+template <int COLS>
+__device__ __forceinline__ int pw_mn(int r, int c) {
+  int swz;
+  if constexpr (COLS >= 128) swz = ((r & 3) << 2) | ((r >> 2) & 3);
+  else swz = (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1;
+  return r * (COLS * 2) + ((c ^ swz) << 4);
+}
+
+// A fragment (16 rows x 32 k) of a K-major image: lane holds row rb + (l&15), k = 8(l>>4) + j
+__device__ __forceinline__ bf16x8_t pw_frag_kmaj(const char* img, int off, int rb, int kc, int lane) {
+  return *(const pw_lds_bf16x8*)((pw_lds_char*)img + off + pw_kmaj(rb + (lane & 15), kc + (lane >> 4)));
+}
+// Transposed fragment of a row-major image: lane holds X[col = cb + (l&15)][k = 8(l>>4) + j], where the
+// image rows are k and its columns the fragment's M (or N) index; OFF(r, c16) = byte offset of 16-B
+// chunk c16 of row r (ds_read_b64_tr_b16, cdna_hip_programming.md T10)
+template <typename OFF>
+__device__ __forceinline__ bf16x8_t pw_frag_tr(const char* img, int off, int cb, int lane, OFF offf) {
+  const int g = lane >> 4, ii = lane & 15, q = ii >> 2, p = ii & 3;
+  const int chunk = (cb >> 3) + (p >> 1);
+  pw_s4 v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int kr = 8 * g + 4 * h + q;
+    v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((pw_lds_s4*)((pw_lds_char*)img + off + offf(kr, chunk) + (p & 1) * 8));
+  }
+  pw_s8 r = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pw_rsrc(const void* p, int64_t bytes) {
+  const int n = bytes > 0x7fffffff ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, n, 0x00020000);
+}
+
+template <int... I, typename F>
+__device__ __forceinline__ void pw_sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void pw_sfor(F&& f) {
+  pw_sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---------------------------------------------------------------------------------- F3 (expand)
+// CN = narrow width (conv3 input channels), CW = 4 CN (conv3 output channels).
+template <int CN>
+struct PwExpandCfg {
+  static constexpr int CW = 4 * CN;
+  static constexpr int NCH = CW / 64;                  // 64-channel chunks of the wide tile
+  static constexpr int TPR = CW / 8;                   // threads per wide row (16-B chunks)
+  static constexpr int LPT = PW_BM * TPR / PW_NT;      // wide-tensor 16-B loads per thread per tile
+  static constexpr int RSTEP = PW_NT / TPR;            // rows between a thread's loads
+  static constexpr int NTPR = CN / 8;                  // threads per narrow row
+  static constexpr int NLD = PW_BM * NTPR;             // threads that load one narrow chunk
+  static constexpr int T_BYTES = NCH * PW_BM * 128;    // dy3 tile (K-major, 64-channel chunks)
+  static constexpr int A2_BYTES = PW_BM * CN * 2;      // a2 tile (row-major, MN image)
+  static constexpr int SLOT = T_BYTES + A2_BYTES;
+  static constexpr int W_BYTES = CW * CN * 2;          // W3 image, resident
+  static constexpr int WCOLS = CN / 2;                 // wgrad: columns per wave (2 column groups)
+  static constexpr int WTN = WCOLS / 16;               // wgrad: 16-col tiles per wave per chunk
+  static constexpr int DCOLS = CN / 4;                 // dgrad: columns per wave (2 x 4 waves)
+  static constexpr int DTN = DCOLS / 16;
+  static_assert(LPT >= 1 && PW_BM * TPR % PW_NT == 0, "wide tile mapping");
+  static_assert(NLD <= PW_NT, "narrow tile mapping");
+  static_assert(2 * SLOT + W_BYTES <= 160 * 1024, "LDS budget");
+};
+
+template <int CN>
+__global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a) {
+  using C = PwExpandCfg<CN>;
+  constexpr int CW = C::CW, NCH = C::NCH, LPT = C::LPT, TPR = C::TPR;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::SLOT + C::W_BYTES];
+  char* wimg = smem + 2 * C::SLOT;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int ntiles = a.M / PW_BM;
+
+  // ---- per-thread wide-channel group (fixed for the whole launch) and its BN3 backward coefficients
+  const int chc = t % TPR, c0 = 8 * chc, r0 = t / TPR;
+  float A[8], B[8], D[8];
+  {
+    const float inv_m = 1.f / (float)a.M;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float mu = a.save3[c], is = a.save3[CW + c], sc = a.save3[2 * CW + c];
+      const float kg = a.red3[c] * inv_m, kx = a.red3[CW + c] * inv_m * is;
+      A[k] = sc;
+      B[k] = -sc * kx;
+      D[k] = sc * (kx * mu - kg);
+    }
+  }
+  // ---- W3 [CW][CN] -> MN image (rows = k = wide channel), resident
+  for (int q = t; q < CW * CN / 8; q += PW_NT) {
+    const int k = q / (CN / 8), cc = q % (CN / 8);
+    *reinterpret_cast<pw_u32x4*>(wimg + pw_mn<CN>(k, cc)) =
+        *reinterpret_cast<const pw_u32x4*>(a.w + (int64_t)k * CN + 8 * cc);
+  }
+
+  const __amdgpu_buffer_rsrc_t rg = pw_rsrc(a.g, (int64_t)a.M * CW * 2), ry = pw_rsrc(a.y3, (int64_t)a.M * CW * 2);
+  const __amdgpu_buffer_rsrc_t rm = pw_rsrc(a.mask3, (int64_t)a.M * CW / 8);
+  const __amdgpu_buffer_rsrc_t ra = pw_rsrc(a.a2, (int64_t)a.M * CN * 2);
+  const __amdgpu_buffer_rsrc_t rx2 = pw_rsrc(a.y2, a.y2 ? (int64_t)a.M * CN * 2 : 0);
+
+  // dgrad wave tile: rows 16 (wv & 1), columns DCOLS (wv >> 1); SWAP orientation -> lane holds row
+  // (lane & 15), columns dcb + (lane >> 4) * 4 + r of each 16-col tile
+  const int drb = 16 * (wv & 1), dcb = C::DCOLS * (wv >> 1);
+  // BN2 backward partials of this lane's 4 * DTN columns (accumulated over the whole launch)
+  float bs[C::DTN][4], bq[C::DTN][4], mu2[C::DTN][4], is2[C::DTN][4], sc2[C::DTN][4], sh2[C::DTN][4];
+#pragma unroll
+  for (int j = 0; j < C::DTN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = dcb + 16 * j + (lane >> 4) * 4 + r;
+      bs[j][r] = bq[j][r] = 0.f;
+      mu2[j][r] = a.y2 ? a.save2[c] : 0.f;
+      is2[j][r] = a.y2 ? a.save2[CN + c] : 0.f;
+      sc2[j][r] = a.y2 ? a.save2[2 * CN + c] : 0.f;
+      sh2[j][r] = a.y2 ? a.save2[3 * CN + c] : 0.f;
+    }
+  // wgrad wave tile: chunk rows 16 (wv & 3) of every chunk, columns WCOLS (wv >> 2)
+  const int wrb = 16 * (wv & 3), wcb = C::WCOLS * (wv >> 2);
+  f32x4_t accw[NCH][C::WTN];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int n = 0; n < C::WTN; ++n) accw[j][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // ---- register staging ring (two tiles)
+  struct Stage {
+    pw_u32x4 g[LPT], y[LPT];
+    uint32_t m[LPT];
+    pw_u32x4 a2;
+    pw_u32x2 x2[C::DTN];
+  };
+  Stage st0, st1;
+  const int tile0 = blockIdx.x, tstep = gridDim.x;
+  auto issue = [&](Stage& s, int tile) {
+    const bool ok = tile < ntiles;
+    const int row0 = tile * PW_BM;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int row = row0 + r0 + C::RSTEP * i;
+      const uint32_t off = ok ? (uint32_t)(row * CW + c0) * 2u : 0x80000000u;
+      s.g[i] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
+      s.y[i] = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
+      s.m[i] = __builtin_amdgcn_raw_buffer_load_b8(rm, ok ? (uint32_t)(row * TPR + chc) : 0x80000000u, 0, 0);
+    }
+    {
+      const int row = row0 + t / C::NTPR, cc = t % C::NTPR;
+      const bool aok = ok && t < C::NLD;
+      s.a2 = __builtin_amdgcn_raw_buffer_load_b128(ra, aok ? (uint32_t)(row * CN + 8 * cc) * 2u : 0x80000000u, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < C::DTN; ++j) {
+      const int row = row0 + drb + (lane & 15), col = dcb + 16 * j + (lane >> 4) * 4;
+      s.x2[j] = __builtin_amdgcn_raw_buffer_load_b64(rx2, ok ? (uint32_t)(row * CN + col) * 2u : 0x80000000u, 0, 0);
+    }
+  };
+  // transform tile (registers) -> LDS slot; the epilogue's y2 values move to `x2` (the staging
+  // registers are re-issued before the tile computes)
+  pw_u32x2 x2[C::DTN];
+  auto stage = [&](const Stage& s, char* slot) {
+#pragma unroll
+    for (int j = 0; j < C::DTN; ++j) x2[j] = s.x2[j];
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      float gf[8], yf[8], o[8];
+      unpack8(__builtin_bit_cast(U4, s.g[i]), gf);
+      unpack8(__builtin_bit_cast(U4, s.y[i]), yf);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gg = ((s.m[i] >> k) & 1u) ? gf[k] : 0.f;
+        o[k] = fmaf(A[k], gg, fmaf(B[k], yf[k], D[k]));
+      }
+      const int row = r0 + C::RSTEP * i;
+      *reinterpret_cast<U4*>(slot + (chc >> 3) * (PW_BM * 128) + pw_kmaj(row, chc & 7)) = pack8(o);
+    }
+    if (t < C::NLD) {
+      const int row = t / C::NTPR, cc = t % C::NTPR;
+      *reinterpret_cast<pw_u32x4*>(slot + C::T_BYTES + pw_mn<CN>(row, cc)) = s.a2;
+    }
+  };
+  auto compute = [&](const char* slot, int tile) {
+    // dgrad: acc_d[32 x CN] = T[32 x CW] . W3
+    f32x4_t accd[C::DTN];
+#pragma unroll
+    for (int j = 0; j < C::DTN; ++j) accd[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < CW / 32; ++kc) {  // 32-deep k-steps over the wide channels
+      const bf16x8_t fa = pw_frag_kmaj(slot, (kc >> 1) * (PW_BM * 128), drb, 4 * (kc & 1), lane);
+#pragma unroll
+      for (int j = 0; j < C::DTN; ++j) {
+        const bf16x8_t fb = pw_frag_tr(wimg, 32 * kc * CN * 2, dcb + 16 * j, lane,
+                                       [](int r, int c) { return pw_mn<CN>(r, c); });
+        accd[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, accd[j], 0, 0, 0);  // SWAP
+      }
+    }
+    // wgrad: acc_w[CW x CN] += T^T . A2 (k = the tile's 32 rows)
+    bf16x8_t fb2[C::WTN];
+#pragma unroll
+    for (int n = 0; n < C::WTN; ++n)
+      fb2[n] = pw_frag_tr(slot + C::T_BYTES, 0, wcb + 16 * n, lane, [](int r, int c) { return pw_mn<CN>(r, c); });
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const bf16x8_t fa = pw_frag_tr(slot + j * (PW_BM * 128), 0, wrb, lane, [](int r, int c) { return pw_kmaj(r, c); });
+#pragma unroll
+      for (int n = 0; n < C::WTN; ++n) accw[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb2[n], accw[j][n], 0, 0, 0);
+    }
+    // dgrad epilogue: dA2 (bf16, 8-byte stores) + BN2 backward partials
+    const int row = tile * PW_BM + drb + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < C::DTN; ++j) {
+      const int col = dcb + 16 * j + (lane >> 4) * 4;
+      const uint32_t lo = pack_bf16x2(accd[j][0], accd[j][1]), hi = pack_bf16x2(accd[j][2], accd[j][3]);
+      *reinterpret_cast<pw_u32x2*>(a.dA2 + (int64_t)row * CN + col) = (pw_u32x2){lo, hi};
+      if (a.y2) {
+        const float gv[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                             __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+        const float xv[4] = {__uint_as_float(x2[j][0] << 16), __uint_as_float(x2[j][0] & 0xffff0000u),
+                             __uint_as_float(x2[j][1] << 16), __uint_as_float(x2[j][1] & 0xffff0000u)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gp = (!a.relu2 || fmaf(xv[r], sc2[j][r], sh2[j][r]) > 0.f) ? gv[r] : 0.f;
+          bs[j][r] += gp;
+          bq[j][r] = fmaf(gp, (xv[r] - mu2[j][r]) * is2[j][r], bq[j][r]);
+        }
+      }
+    }
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  // ---- main loop over this block's m-tiles (tile0, tile0 + tstep, ...): staged two ahead
+  issue(st0, tile0);
+  issue(st1, tile0 + tstep);
+  __syncthreads();  // W3 image written
+  for (int tile = tile0; tile < ntiles; tile += 2 * tstep) {
+    stage(st0, smem);
+    issue(st0, tile + 2 * tstep);
+    sync();
+    compute(smem, tile);
+    const int t1 = tile + tstep;
+    if (t1 >= ntiles) break;
+    stage(st1, smem + C::SLOT);
+    issue(st1, t1 + 2 * tstep);
+    sync();
+    compute(smem + C::SLOT, t1);
+  }
+
+  // ---- wgrad accumulators -> this block's slab, in register order (coalesced 16-B stores)
+  float* slab = a.slab + (size_t)blockIdx.x * (CW * CN);
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int n = 0; n < C::WTN; ++n)
+      *reinterpret_cast<f32x4_t*>(slab + ((size_t)(j * C::WTN + n) * PW_NT + t) * 4) = accw[j][n];
+  // ---- BN2 partials: sum the 16 rows of each DPP row (same columns), one atomic per column
+  if (a.y2) {
+    float* slots = a.slots2 + (size_t)(blockIdx.x % NSLOT) * 2 * CN;
+#pragma unroll
+    for (int j = 0; j < C::DTN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = row16_sum(bs[j][r]), q = row16_sum(bq[j][r]);
+        if ((lane & 15) == 0) {
+          const int c = dcb + 16 * j + (lane >> 4) * 4 + r;
+          atomicAdd(slots + c, s);
+          atomicAdd(slots + CN + c, q);
+        }
+      }
+  }
+}
+
+// Slab element e = ((j * WTN + n) * NT + t) * 4 + r  ->  dW3 (row = wide channel, col = narrow):
+// lane = t & 63, wave = t >> 6; row = 64 j + 16 (wave & 3) + (lane >> 4) * 4 + r,
+// col = WCOLS (wave >> 2) + 16 n + (lane & 15)   (the !SWAP accumulator layout)
+template <int CN>
+__device__ __forceinline__ int pw_slab_to_dw(int e) {
+  using C = PwExpandCfg<CN>;
+  const int r = e & 3, t = (e >> 2) % PW_NT, jn = (e >> 2) / PW_NT;
+  const int j = jn / C::WTN, n = jn % C::WTN;
+  const int lane = t & 63, wv = t >> 6;
+  const int row = 64 * j + 16 * (wv & 3) + (lane >> 4) * 4 + r;
+  const int col = C::WCOLS * (wv >> 2) + 16 * n + (lane & 15);
+  return row * CN + col;
+}
+
+// dW3 += sum over the nslab slabs; grid.x = elements / 256 column groups x PW_RG slab groups (f32
+// atomics of the partial sums: nslab / PW_RG-fold fewer than per-block atomics).  Blocks past that
+// grid reduce a BN layer's backward slots (bn_slot_reduce's math), 16 channels each.
+constexpr int PW_RG = 8;
+template <int CN>
+__global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __restrict__ slab, int nslab,
+                                                             float* __restrict__ dw, float* __restrict__ sr_slots,
+                                                             int sr_C, float* __restrict__ sr_red,
+                                                             float* __restrict__ sr_dgamma,
+                                                             float* __restrict__ sr_dbeta) {
+  constexpr int E = 4 * CN * CN;
+  const int ngemm = (E / 256) * PW_RG;
+  if ((int)blockIdx.x >= ngemm) {
+    // BN slot reduction: 16 channels per block, 16 slot-lanes x NSLOT/16 slots each
+    const int sb = blockIdx.x - ngemm;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4, c = sb * 16 + tx;
+    __shared__ float red2[512];
+    float s = 0.f, q = 0.f;
+    if (c < sr_C) {
+      float vs[NSLOT / 16], vq[NSLOT / 16];
+#pragma unroll
+      for (int i = 0; i < NSLOT / 16; ++i) {
+        const float* p = sr_slots + (size_t)(ty + 16 * i) * 2 * sr_C;
+        vs[i] = p[c];
+        vq[i] = p[sr_C + c];
+      }
+#pragma unroll
+      for (int i = 0; i < NSLOT / 16; ++i) {
+        s += vs[i];
+        q += vq[i];
+        float* p = sr_slots + (size_t)(ty + 16 * i) * 2 * sr_C;
+        p[c] = 0.f;
+        p[sr_C + c] = 0.f;
+      }
+    }
+    red2[threadIdx.x] = s;
+    red2[256 + threadIdx.x] = q;
+    __syncthreads();
+    if (ty == 0 && c < sr_C) {
+#pragma unroll
+      for (int k = 1; k < 16; ++k) {
+        s += red2[threadIdx.x + 16 * k];
+        q += red2[256 + threadIdx.x + 16 * k];
+      }
+      sr_red[c] = s;
+      sr_red[sr_C + c] = q;
+      if (sr_dbeta) sr_dbeta[c] += s;
+      if (sr_dgamma) sr_dgamma[c] += q;
+    }
+    return;
+  }
+  const int e = (blockIdx.x % (E / 256)) * 256 + threadIdx.x, grp = blockIdx.x / (E / 256);
+  float acc = 0.f;
+  int b = grp;
+  for (; b + 3 * PW_RG < nslab; b += 4 * PW_RG) {
+    const float v0 = slab[(size_t)b * E + e], v1 = slab[(size_t)(b + PW_RG) * E + e];
+    const float v2 = slab[(size_t)(b + 2 * PW_RG) * E + e], v3 = slab[(size_t)(b + 3 * PW_RG) * E + e];
+    acc += (v0 + v1) + (v2 + v3);
+  }
+  for (; b < nslab; b += PW_RG) acc += slab[(size_t)b * E + e];
+  atomicAdd(dw + pw_slab_to_dw<CN>(e), acc);
+}
+
+}  // namespace
+
+bool pw_bwd_expand_ok(int CN, int64_t M) { return (CN == 64) && M % PW_BM == 0 && M > 0 && M < (1 << 24); }
+
+int pw_bwd_expand_grid(int CN, int64_t M) {
+  (void)CN;
+  const int64_t tiles = M / PW_BM;
+  return (int)std::min<int64_t>(256, tiles);
+}
+
+void pw_bwd_expand(const PwExpandArgs& args, int nblocks, hipStream_t s) {
+  switch (args.CN) {
+    case 64: pw_bwd_expand_kernel<64><<<nblocks, PW_NT, 0, s>>>(args); break;
+    default: abort();
+  }
+}
+
+void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_slots, int sr_C, float* sr_red,
+                    float* sr_dgamma, float* sr_dbeta, hipStream_t s) {
+  const int E = 4 * CN * CN;
+  const int grid = (E / 256) * PW_RG + (sr_slots ? (sr_C + 15) / 16 : 0);
+  switch (CN) {
+    case 64:
+      pw_slab_reduce_kernel<64><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red, sr_dgamma,
+                                                     sr_dbeta);
+      break;
+    default: abort();
+  }
+}
+
+}  // namespace tfx

@@ -420,6 +420,50 @@ Tensor bn_slots_reduce(Tensor slots, int64_t C, optional<Tensor> dgamma, optiona
   return red;
 }
 
+// ------------------------------------------------------------------ fused pointwise-conv backward
+// Backward of an expanding 1x1 conv (a ResNet bottleneck's conv3, w = [CW][1][1][CN], CW = 4 CN)
+// fused with the tail BN's backward apply (pw_bwd.hip): g = the block's output gradient, y3 / mask3 /
+// save3 / red3 = the tail BN's input, ReLU mask bits, [mean|invstd|scale|shift] and reduction
+// [sum g'|sum g' xhat]; a2 = the conv's input.  dw += the weight gradient.  With y2 (the BN2 input that
+// produced a2), its save2 / relu2 and slots2: the BN2 backward partials of dA2 are reduced too and
+// returned as red2 = [sum g'|sum g' xhat] (dgamma2 / dbeta2 +=).  Returns (dA2, red2).
+std::tuple<Tensor, Tensor> pw_bwd_expand(Tensor g, Tensor y3, Tensor mask3, Tensor save3, Tensor red3, Tensor a2,
+                                         Tensor w, Tensor dw, optional<Tensor> y2, optional<Tensor> save2, bool relu2,
+                                         optional<Tensor> slots2, optional<Tensor> dgamma2, optional<Tensor> dbeta2) {
+  CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(y3); CHECK_CONTIG(y3); CHECK_BF16(a2); CHECK_CONTIG(a2);
+  CHECK_BF16(w); CHECK_CONTIG(w); CHECK_F32(dw); CHECK_CONTIG(dw); CHECK_F32(save3); CHECK_F32(red3);
+  const int64_t CW = w.size(0), CN = w.size(-1), M = a2.numel() / CN;
+  TORCH_CHECK(w.numel() == CW * CN && CW == 4 * CN && dw.numel() == CW * CN, "pw_bwd_expand: weight shape");
+  TORCH_CHECK(a2.size(-1) == CN && g.numel() == M * CW && y3.numel() == M * CW && g.size(-1) == CW, "pw_bwd_expand: shapes");
+  TORCH_CHECK(mask3.scalar_type() == at::kByte && mask3.numel() * 8 == M * CW && mask3.is_contiguous(), "mask3");
+  TORCH_CHECK(save3.numel() == 4 * CW && red3.numel() == 2 * CW, "save3 / red3");
+  TORCH_CHECK(tfx::pw_bwd_expand_ok((int)CN, M), "pw_bwd_expand: unsupported width / rows");
+  auto dA2 = at::empty_like(a2);
+  tfx::PwExpandArgs a;
+  a.g = bf(g); a.y3 = bf(y3); a.mask3 = mask3.data_ptr<uint8_t>(); a.save3 = save3.data_ptr<float>();
+  a.red3 = red3.data_ptr<float>(); a.a2 = bf(a2); a.w = bf(w); a.dA2 = bfm(dA2); a.M = (int)M; a.CN = (int)CN;
+  Tensor red2 = at::empty({0}, g.options().dtype(at::kFloat));
+  const bool bnb = y2.has_value() && y2->defined();
+  if (bnb) {
+    CHECK_BF16(*y2); CHECK_CONTIG(*y2);
+    TORCH_CHECK(y2->numel() == M * CN && save2.has_value() && save2->numel() == 4 * CN && slots2.has_value(),
+                "pw_bwd_expand: BN2 arguments");
+    check_bn_ws(*slots2, CN);
+    a.y2 = bf(*y2); a.save2 = save2->data_ptr<float>(); a.relu2 = relu2 ? 1 : 0; a.slots2 = slots2->data_ptr<float>();
+    red2 = at::empty({2 * CN}, g.options().dtype(at::kFloat));
+  }
+  const int nb = tfx::pw_bwd_expand_grid((int)CN, M);
+  auto slab = at::empty({(int64_t)nb * CW * CN}, g.options().dtype(at::kFloat));
+  a.slab = slab.data_ptr<float>();
+  tfx::pw_bwd_expand(a, nb, cur_stream());
+  tfx::pw_slab_reduce(a.slab, nb, (int)CN, dw.data_ptr<float>(), bnb ? a.slots2 : nullptr, (int)CN,
+                      bnb ? red2.data_ptr<float>() : nullptr, bnb ? fpm(dgamma2) : nullptr,
+                      bnb ? fpm(dbeta2) : nullptr, cur_stream());
+  return {dA2, red2};
+}
+
+bool pw_bwd_expand_supported(int64_t CN, int64_t M) { return tfx::pw_bwd_expand_ok((int)CN, M); }
+
 // ------------------------------------------------------------------ dense bf16 GEMM
 // out = op(a) @ op(b) (+bias)(relu); a: [M,K] (or [K,M] if trans_a); b: [K,N] (or [N,K] if trans_b)
 void gemm_setup(tfx::IgemmArgs& g, const Tensor& a, const Tensor& b, bool ta, bool tb) {
@@ -1136,8 +1180,11 @@ void lstm_cell_bwd(Tensor act, Tensor c, optional<Tensor> c_prev, optional<Tenso
 
 // Whole-sequence persistent LSTM (lstm_seq.hip).  gx [T,B,4H] f32 (input projection + bias),
 // whh [4H,H] bf16; hbuf [T+1,B,H] bf16 and cbuf [T+1,B,H] f32 with h0 / c0 in slot 0; act [T,B,4H]
-// f32 and hT [B,H] f32 are written.  Returns the launch's status word (int32 [1]; nonzero = a
-// hand-off wait exceeded its bound and the results are invalid).
+// f32 and hT [B,H] f32 are written.  status (optional): a persistent int32 [1] health word the
+// launch sets to 1 if a hand-off wait exceeds its bound (results invalid); it is never cleared by a
+// launch, so the host checks it at its own sync points (ops/rnn.py check_lstm_health).  Without it
+// the launch's own status word is set instead.  Returns the launch's own word.  spin_limit 0 =
+// the default bound.
 bool lstm_seq_supported(int64_t B, int64_t H) {
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
@@ -1145,7 +1192,14 @@ bool lstm_seq_supported(int64_t B, int64_t H) {
   return tfx::lstm_seq_supported((int)B, (int)H, cus);
 }
 
-Tensor lstm_seq_fwd(Tensor gx, Tensor whh, Tensor hbuf, Tensor cbuf, Tensor act, Tensor hT) {
+unsigned* lstm_status_ptr(const optional<Tensor>& status) {
+  if (!(status.has_value() && status->defined())) return nullptr;
+  TORCH_CHECK(status->is_cuda() && status->scalar_type() == at::kInt && status->numel() >= 1, "lstm status word");
+  return reinterpret_cast<unsigned*>(status->data_ptr());
+}
+
+Tensor lstm_seq_fwd(Tensor gx, Tensor whh, Tensor hbuf, Tensor cbuf, Tensor act, Tensor hT, optional<Tensor> status,
+                    int64_t spin_limit) {
   CHECK_DEV(gx); CHECK_F32(gx); CHECK_CONTIG(gx); CHECK_BF16(whh); CHECK_CONTIG(whh);
   CHECK_BF16(hbuf); CHECK_CONTIG(hbuf); CHECK_F32(cbuf); CHECK_CONTIG(cbuf); CHECK_F32(act); CHECK_CONTIG(act);
   CHECK_F32(hT); CHECK_CONTIG(hT);
@@ -1157,10 +1211,11 @@ Tensor lstm_seq_fwd(Tensor gx, Tensor whh, Tensor hbuf, Tensor cbuf, Tensor act,
   TORCH_CHECK(T * B * 4 * H * 4 < (int64_t(1) << 31), "lstm_seq: tensors must be < 2 GiB");
   for (const Tensor* t : {&gx, &whh, &hbuf}) check_aligned16(*t, "lstm_seq operand");
   Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B, (int)H)}, gx.options().dtype(at::kInt));
+  unsigned* st = lstm_status_ptr(status);
   tfx::lstm_seq_fwd(gx.data_ptr<float>(), bf(whh), (int)T, (int)B, (int)H, bfm(hbuf), cbuf.data_ptr<float>(),
-                    act.data_ptr<float>(), hT.data_ptr<float>(), reinterpret_cast<unsigned*>(sync.data_ptr()),
-                    cur_stream());
-  return sync.narrow(0, sync.numel() - 32, 1);
+                    act.data_ptr<float>(), hT.data_ptr<float>(), reinterpret_cast<unsigned*>(sync.data_ptr()), st,
+                    (unsigned)spin_limit, cur_stream());
+  return sync.narrow(0, sync.numel() - 32, 1);  // this launch's own word (stays 0 when `status` is given)
 }
 
 // act, cbuf from the forward; dH [T,B,H] bf16 (optional) = gradient of every h_t from outside the
@@ -1168,7 +1223,8 @@ Tensor lstm_seq_fwd(Tensor gx, Tensor whh, Tensor hbuf, Tensor cbuf, Tensor act,
 // (gate pre-activation gradients), optionally dc_out [B,H] (gradient of c_0) and accumulates the
 // bias gradient into dbias [4H] f32 (optional).
 Tensor lstm_seq_bwd(Tensor act, Tensor cbuf, optional<Tensor> dH, optional<Tensor> dhT, optional<Tensor> dc_in,
-                    Tensor whh, Tensor dg, optional<Tensor> dc_out, optional<Tensor> dbias) {
+                    Tensor whh, Tensor dg, optional<Tensor> dc_out, optional<Tensor> dbias, optional<Tensor> status,
+                    int64_t spin_limit) {
   CHECK_DEV(act); CHECK_F32(act); CHECK_CONTIG(act); CHECK_F32(cbuf); CHECK_CONTIG(cbuf);
   CHECK_BF16(whh); CHECK_CONTIG(whh); CHECK_BF16(dg); CHECK_CONTIG(dg);
   TORCH_CHECK(cbuf.dim() == 3, "cbuf must be [T+1,B,H]");
@@ -1189,10 +1245,11 @@ Tensor lstm_seq_bwd(Tensor act, Tensor cbuf, optional<Tensor> dH, optional<Tenso
                              "dbias shape");
   check_aligned16(dg, "dg");
   Tensor sync = at::empty({tfx::lstm_seq_sync_words((int)B, (int)H)}, act.options().dtype(at::kInt));
+  unsigned* st = lstm_status_ptr(status);
   tfx::lstm_seq_bwd(act.data_ptr<float>(), cbuf.data_ptr<float>(), dh16, fp(dhT), fp(dc_in), bf(whh), (int)T,
-                    (int)B, (int)H, bfm(dg), fpm(dc_out), fpm(dbias), reinterpret_cast<unsigned*>(sync.data_ptr()),
-                    cur_stream());
-  return sync.narrow(0, sync.numel() - 32, 1);
+                    (int)B, (int)H, bfm(dg), fpm(dc_out), fpm(dbias), reinterpret_cast<unsigned*>(sync.data_ptr()), st,
+                    (unsigned)spin_limit, cur_stream());
+  return sync.narrow(0, sync.numel() - 32, 1);  // this launch's own word (stays 0 when `status` is given)
 }
 
 // ------------------------------------------------------------------ measured igemm launch configurations
@@ -1359,8 +1416,10 @@ TORCH_LIBRARY(tfx, m) {
   m.def("igemm_tune_force", &igemm_tune_force);
   m.def("igemm_tune_trace", &igemm_tune_trace);
   m.def("igemm_tune_traced", &igemm_tune_traced);
-  m.def("lstm_seq_fwd", &lstm_seq_fwd);
-  m.def("lstm_seq_bwd", &lstm_seq_bwd);
+  m.def("lstm_seq_fwd(Tensor gx, Tensor whh, Tensor hbuf, Tensor cbuf, Tensor act, Tensor hT, "
+        "Tensor? status=None, int spin_limit=0) -> Tensor", &lstm_seq_fwd);
+  m.def("lstm_seq_bwd(Tensor act, Tensor cbuf, Tensor? dH, Tensor? dhT, Tensor? dc_in, Tensor whh, Tensor dg, "
+        "Tensor? dc_out, Tensor? dbias, Tensor? status=None, int spin_limit=0) -> Tensor", &lstm_seq_bwd);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("conv_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
@@ -1392,6 +1451,8 @@ TORCH_LIBRARY(tfx, m) {
         "Tensor? addend_mask=None, bool reduce=True, bool addend_s2=False, Tensor? wflip=None) -> (Tensor, Tensor)",
         &conv_dgrad_bn);
   m.def("bn_nslot", &bn_nslot);
+  m.def("pw_bwd_expand", &pw_bwd_expand);
+  m.def("pw_bwd_expand_supported", &pw_bwd_expand_supported);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd(Tensor g, Tensor x, Tensor? res, Tensor save, bool relu, Tensor slots, Tensor? dgamma, "
         "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);

@@ -86,6 +86,7 @@ def main(_):
             if step % 50 == 0:
                 costs += float(loss)
                 iters += 1
+                trainer.check()  # a timed-out persistent-LSTM hand-off raises here, not silently trains on
                 if rank == 0:
                     print("epoch %d step %d perplexity %.3f  %.0f tokens/sec" %
                           (ep + 1, step, math.exp(costs / iters), tokens / (time.time() - t0)), flush=True)
@@ -95,6 +96,7 @@ def main(_):
             break
     if dev.type == "cuda":
         torch.cuda.synchronize()
+        trainer.check()
     dt = time.time() - t0
     # validation perplexity (rank 0's model; all ranks hold identical weights)
     from tensorflow_examples_amd import ops

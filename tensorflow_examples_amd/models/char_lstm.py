@@ -96,6 +96,11 @@ class LMTrainer:
         self.opt.apply_gradients(grad_scale=scale, sumsq=sumsq, max_norm=self.max_norm / scale)
         return loss.detach(), new_state
 
+    def check(self) -> None:
+        """Raise if a persistent LSTM launch timed out a hand-off since the last check (reads the
+        device health word: call it where the host synchronises anyway, e.g. when logging)."""
+        ops.check_lstm_health(self.store.master.device if self.store.master.is_cuda else None)
+
 
 def build_char_lstm(device="cuda", vocab_size=65, embed=128, hidden=512, layers=2, dtype=torch.bfloat16,
                     seed=0) -> Tuple[VariableStore, CharLSTM]:

@@ -50,24 +50,25 @@ class _BN:
         self.ws = BNWorkspace(c)
 
     def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None, ws_obj=False,
-                 residual_is_bn=False, defer_output=False):
+                 residual_is_bn=False, defer_output=False, lazy_backward=False):
         ws = (self.ws if ws_obj else self.ws.get(x.device)) if x.device.type == "cuda" else None
         return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
                               eps=1e-5, residual=residual, relu=relu, workspace=ws, stats_ready=stats_ready,
                               residual_grad_sink=residual_sink, fuse_residual_bn_backward=residual_is_bn,
-                              defer_output=defer_output)
+                              defer_output=defer_output, lazy_backward=lazy_backward)
 
     def after_conv(self, conv, x, training, relu=False, residual=None, sink=None, residual_sink=None,
                    fuse_input_bn_backward=False, residual_is_bn=False, defer_output=False):
         """conv -> BN with the BN statistics produced (and, with _FUSE_BN, finalized) by the conv's
         epilogue (GPU, training).  ``fuse_input_bn_backward``: the conv's data gradient is the
-        complete gradient of ``x`` -- reduce x's producing BN's backward in its epilogue."""
+        complete gradient of ``x`` -- reduce x's producing BN's backward in its epilogue.  The BN's
+        input gradient may reach ``conv`` unmaterialised (ops.nn.LazyBNGrad): it is its only producer."""
         fused = training and x.device.type == "cuda"
         if fused and _FUSE_BN:
             self.ws.finalize_args = (self.gamma.master, self.beta.master, self.mean, self.var, 0.1, 1e-5)
             y = conv(x, self.ws, sink, fuse_input_bn_backward and _FUSE_BN)
             return self(y, training, relu=relu, residual=residual, stats_ready=True, residual_sink=residual_sink,
-                        ws_obj=True, residual_is_bn=residual_is_bn, defer_output=defer_output)
+                        ws_obj=True, residual_is_bn=residual_is_bn, defer_output=defer_output, lazy_backward=True)
         y = conv(x, self.ws.get(x.device) if fused else None, sink)
         return self(y, training, relu=relu, residual=residual, stats_ready=fused, residual_sink=residual_sink,
                     residual_is_bn=residual_is_bn)

@@ -2,11 +2,11 @@
 from . import _native
 from .nn import (BNWorkspace, GradSink, accuracy, avg_pool2d, batch_norm, conv2d, dense, global_avg_pool, linear,
                  max_pool2d, scale_shift, softmax_cross_entropy, sum_squared_error)
-from .rnn import lstm_layer
+from .rnn import LSTMHandoffError, check_lstm_health, lstm_layer
 from .sparse import (embedding_lookup, gather_rows, log_uniform_logq, log_uniform_sample, nce_loss,
                      sampled_loss_grads, sampled_softmax_loss, scatter_add_rows)
 
 __all__ = ["_native", "BNWorkspace", "GradSink", "accuracy", "avg_pool2d", "batch_norm", "conv2d", "dense",
-           "global_avg_pool", "linear", "max_pool2d", "scale_shift", "softmax_cross_entropy", "sum_squared_error", "lstm_layer", "embedding_lookup",
+           "global_avg_pool", "linear", "max_pool2d", "scale_shift", "softmax_cross_entropy", "sum_squared_error", "lstm_layer", "check_lstm_health", "LSTMHandoffError", "embedding_lookup",
            "gather_rows", "log_uniform_logq", "log_uniform_sample", "nce_loss", "sampled_loss_grads",
            "sampled_softmax_loss", "scatter_add_rows"]

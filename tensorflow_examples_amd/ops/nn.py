@@ -90,6 +90,38 @@ def _wflip(w, stride, pad, dil):
     return w.store.flipped3x3(w)
 
 
+# test hook: False keeps every tail BN backward materialised (the layer-wise path)
+_LAZY_BN_BWD = True
+PW_EXPAND_CALLS = [0]  # fused expanding-1x1 backward launches (tests)
+
+
+class LazyBNGrad:
+    """The input gradient of a residual + ReLU batch norm (a ResNet bottleneck's tail), NOT
+    materialised: dy = A (g * mask) + B x + D per channel, with g the BN's output gradient, x its
+    input, mask the forward's ReLU mask bits and (A, B, D) folded from ``save`` and ``red``.  The BN's
+    backward returns a zero-stride placeholder carrying this (``_tfx_lazy_bnbwd``); its producer conv
+    (the expanding 1x1 conv3) then forms dy on load inside its fused backward (pw_bwd.hip) -- or
+    calls :meth:`materialize` (bn_bwd_apply, the layer-wise path) when it cannot."""
+    __slots__ = ("g", "x", "save", "red", "relu", "mask")
+
+    def __init__(self, g, x, save, red, relu, mask):
+        self.g, self.x, self.save, self.red, self.relu, self.mask = g, x, save, red, relu, mask
+
+    def materialize(self) -> torch.Tensor:
+        return torch.ops.tfx.bn_bwd_apply(self.g, self.x, None, self.save, self.red, self.relu, self.mask, False)[0]
+
+
+def _pw_expand_ok(x, w, stride, pad, dil, lazy, sink) -> bool:
+    """Can this conv's backward run as the fused expanding-1x1 kernel (pw_bwd.hip) on ``lazy``?"""
+    sh = w.shape
+    if not (stride == 1 and pad == 0 and dil == 1 and sink is None and w.trainable and len(sh) == 4
+            and sh[1] == 1 and sh[2] == 1 and sh[0] == 4 * sh[3] and x.is_contiguous()):
+        return False
+    if lazy.mask is None or lazy.g.shape[-1] != sh[0] or x.shape[-1] != sh[3]:
+        return False
+    return bool(torch.ops.tfx.pw_bwd_expand_supported(sh[3], x.numel() // sh[3]))
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into, sink, bnb):
@@ -117,6 +149,25 @@ class _Conv2d(torch.autograd.Function):
         stride, pad, dil = ctx.cfg
         need_dx = ctx.needs_input_grad[0]
         if ctx.native:
+            lazy = getattr(gy, "_tfx_lazy_bnbwd", None)
+            if lazy is not None:
+                if need_dx and _pw_expand_ok(x, w, stride, pad, dil, lazy, ctx.sink):
+                    # the tail BN's backward apply + this conv's data AND weight gradient in one
+                    # launch; dy never written (pw_bwd.hip).  The BN2 backward partials of dx ride along.
+                    bnb = ctx.bnb
+                    use_bnb = bnb is not None and bnb.mask is None and not bnb.deferred and bnb.red is None \
+                        and x.numel() * x.element_size() <= _BNB_MAX_BYTES
+                    dx, red2 = torch.ops.tfx.pw_bwd_expand(
+                        lazy.g.contiguous(), lazy.x, lazy.mask, lazy.save, lazy.red, x, w.value, w.grad,
+                        bnb.x if use_bnb else None, bnb.save if use_bnb else None, bool(use_bnb and bnb.relu),
+                        bnb.ws if use_bnb else None, bnb.dgamma if use_bnb else None,
+                        bnb.dbeta if use_bnb else None)
+                    if use_bnb:
+                        bnb.red = red2
+                    PW_EXPAND_CALLS[0] += 1
+                    _grad_ready(w)
+                    return dx, None, None, None, None, None, None, None, None
+                gy = lazy.materialize()
             gy = gy.contiguous()
             sink = ctx.sink
             dx = None
@@ -386,9 +437,11 @@ def _res_bn_sec_ok(ctx, gy, mask, relu, masked):
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
-                training, ws, stats_ready, res_sink, wsobj, bnb_out, res_bnb, defer):
+                training, ws, stats_ready, res_sink, wsobj, bnb_out, res_bnb, defer, lazy_bwd):
         # res_bnb: (BNBackwardFusion of the residual, fuse its backward here); defer: the output is
-        # only ever this layer's consumer's residual -- never written (see batch_norm)
+        # only ever this layer's consumer's residual -- never written (see batch_norm); lazy_bwd: the
+        # input gradient may be returned unmaterialised (LazyBNGrad) -- the producer is a conv
+        ctx.lazy_bwd = bool(lazy_bwd)
         ctx.gamma, ctx.beta, ctx.cfg = gamma, beta, (rm, rv, momentum, eps, relu, training)
         ctx.res_sink = res_sink
         res_bnb, res_sec = res_bnb if res_bnb is not None else (None, False)
@@ -489,6 +542,14 @@ class _BatchNorm(torch.autograd.Function):
                 assert not relu and not ctx.has_res
                 dx, dres = torch.ops.tfx.bn_bwd_apply(gy, x, None, save, ctx.bnb.red, True, ctx.bnb.in_mask, False)
                 ctx.bnb.red = ctx.bnb.in_mask = None
+            elif ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and _LAZY_BN_BWD and masked \
+                    and res is None and relu and mask is not None:
+                # residual + ReLU tail whose residual gradient is parked as (gy, mask): dx stays lazy --
+                # the producing conv forms it on load (LazyBNGrad)
+                dx = _zero_scalar(x.dtype, x.device).expand(x.shape)
+                dx._tfx_lazy_bnbwd = LazyBNGrad(gy, x, save, ctx.bnb.red, relu, mask)
+                dres = None
+                ctx.bnb.red = None
             elif ctx.bnb is not None and ctx.bnb.red is not None:
                 # the consumer conv's dgrad epilogue reduced this backward (and dgamma / dbeta)
                 dx, dres = torch.ops.tfx.bn_bwd_apply(gy, x, res, save, ctx.bnb.red, relu, mask, not masked)
@@ -503,7 +564,7 @@ class _BatchNorm(torch.autograd.Function):
                 ctx.res_sink.put((gy, mask) if masked else dres)
                 dres = None
             return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None, \
-                None, None, None, None, None
+                None, None, None, None, None, None
         x, res = ctx.saved_tensors
         with torch.enable_grad():
             xs = x.detach().requires_grad_(True)
@@ -518,14 +579,14 @@ class _BatchNorm(torch.autograd.Function):
             gamma.grad.add_(grads[0])
             beta.grad.add_(grads[1])
             _grad_ready(gamma, beta)
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
                momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False,
                workspace=None, stats_ready: bool = False,
                residual_grad_sink: Optional[GradSink] = None, fuse_residual_bn_backward: bool = False,
-               defer_output: bool = False):
+               defer_output: bool = False, lazy_backward: bool = False):
     """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
     ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass).
 
@@ -541,7 +602,10 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
     ``defer_output``: the caller promises the output is used ONLY as the ``residual`` of one
     later batch_norm (with ``fuse_residual_bn_backward``).  On the fused GPU path the output is then
     never written (a zero-stride placeholder that keeps the autograd edge); the consumer
-    normalizes this BN's input on the fly."""
+    normalizes this BN's input on the fly.
+
+    ``lazy_backward``: the caller promises ``x`` is the output of :func:`conv2d` (used nowhere else),
+    so the input gradient may reach it unmaterialised (:class:`LazyBNGrad`)."""
     anchor = gamma.store.anchor if gamma is not None else None
     wsobj = workspace if isinstance(workspace, BNWorkspace) else None
     if wsobj is not None:
@@ -556,7 +620,7 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
         res_bnb = (rb, bool(fuse_residual_bn_backward))
     y = _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
                          workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out, res_bnb,
-                         bool(defer_output))
+                         bool(defer_output), bool(lazy_backward))
     if bnb_out:
         y._tfx_bnb = bnb_out[0]
     return y

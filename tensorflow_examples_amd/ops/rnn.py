@@ -23,6 +23,13 @@ write-through stores and per-row-block counters -- so the 2T dependent launches 
 become one.  ``TFX_LSTM_PERSISTENT=0`` selects the per-step kernels above.
 Gate order: i, f, g, o (f gets ``forget_bias`` added in the pointwise kernel through ``b``).
 The whole step is HIP-graph capturable (no host syncs), which removes the per-step launch cost.
+
+Failure reporting of the persistent kernels: their inter-workgroup waits are bounded (a workgroup
+that is not resident -- CUs taken by another stream or process, e.g. RCCL kernels under DP -- would
+otherwise hang the grid).  On expiry a launch sets a per-device STICKY health word and drains; its
+results are invalid.  The training step never synchronises on it: :func:`check_lstm_health` reads
+it at the caller's own sync points (the examples' log cadence, LMTrainer.check) and raises
+:class:`LSTMHandoffError`, so a timed-out hand-off cannot silently train on wrong gradients.
 """
 from __future__ import annotations
 
@@ -54,6 +61,36 @@ def _lstm_ref(x, w_ih, w_hh, b, h0, c0):
 
 
 _SEQ_OK: Dict[Tuple[int, int, int], bool] = {}
+_HEALTH: Dict[int, torch.Tensor] = {}
+# test hook: a spin bound for the persistent kernels' hand-off waits (None = the kernel default)
+_SPIN_LIMIT: Optional[int] = None
+
+
+class LSTMHandoffError(RuntimeError):
+    """A persistent LSTM launch gave up on an inter-workgroup hand-off: its outputs are invalid."""
+
+
+def _health(dev: torch.device) -> torch.Tensor:
+    h = _HEALTH.get(dev.index or 0)
+    if h is None:
+        assert not torch.cuda.is_current_stream_capturing(), "allocate the LSTM health word before capture"
+        h = _HEALTH[dev.index or 0] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return h
+
+
+def check_lstm_health(device=None, reset: bool = True) -> None:
+    """Raise :class:`LSTMHandoffError` if any persistent LSTM launch on ``device`` (default: all)
+    timed out a hand-off since the last check.  Reads the device health word: call it where the host
+    synchronises anyway (a logged loss), not inside the step."""
+    devs = [torch.device(device).index or 0] if device is not None else list(_HEALTH)
+    for d in devs:
+        h = _HEALTH.get(d)
+        if h is not None and int(h.item()) != 0:
+            if reset:
+                h.zero_()
+            raise LSTMHandoffError("persistent LSTM recurrence on cuda:%d: an inter-workgroup hand-off exceeded "
+                                   "its wait bound (not every workgroup resident?); the step's results are "
+                                   "invalid -- rerun with TFX_LSTM_PERSISTENT=0" % d)
 
 
 def _persistent(B: int, H: int, dev: torch.device) -> bool:
@@ -66,8 +103,8 @@ def _persistent(B: int, H: int, dev: torch.device) -> bool:
 
 
 class _LSTMLayer(torch.autograd.Function):
-    # status words of the last persistent launches (nonzero = a hand-off wait hit its bound);
-    # read by the GPU tests, never synchronised on in the training step
+    # per-launch status words of the last persistent launches (they stay 0: a timed-out wait sets the
+    # device's sticky health word instead, which check_lstm_health reads at the caller's sync points)
     last_status: Dict[str, torch.Tensor] = {}
 
     @staticmethod
@@ -93,7 +130,8 @@ class _LSTMLayer(torch.autograd.Function):
         gx = gx.view(T, B, 4 * H)
         ctx.persistent = _persistent(B, H, dev)
         if ctx.persistent:
-            _LSTMLayer.last_status["fwd"] = torch.ops.tfx.lstm_seq_fwd(gx, w_hh.value, hbuf, cbuf, act, hT)
+            _LSTMLayer.last_status["fwd"] = torch.ops.tfx.lstm_seq_fwd(gx, w_hh.value, hbuf, cbuf, act, hT,
+                                                                       _health(dev), int(_SPIN_LIMIT or 0))
         else:
             for t in range(T):
                 torch.ops.tfx.gemm_into(hbuf[t], w_hh.value, False, True, gx[t], True)
@@ -135,7 +173,8 @@ class _LSTMLayer(torch.autograd.Function):
             dhT = g_hT.float().contiguous() if g_hT is not None else None
             dc_in = g_cT.float().contiguous() if g_cT is not None else None
             _LSTMLayer.last_status["bwd"] = torch.ops.tfx.lstm_seq_bwd(
-                act, cbuf, dH16, dhT, dc_in, w_hh.value, dg, None, b.grad if b.trainable else None)
+                act, cbuf, dH16, dhT, dc_in, w_hh.value, dg, None, b.grad if b.trainable else None,
+                _health(xf.device), int(_SPIN_LIMIT or 0))
             bias_done = True
         else:
             dH = gout.float().contiguous().clone() if gout is not None else \
@@ -178,4 +217,4 @@ def lstm_layer(x: torch.Tensor, w_ih: Variable, w_hh: Variable, b: Variable,
     return out, (hT.detach(), cT.detach())
 
 
-__all__ = ["lstm_layer"]
+__all__ = ["lstm_layer", "check_lstm_health", "LSTMHandoffError"]

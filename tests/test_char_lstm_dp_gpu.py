@@ -1,0 +1,125 @@
+"""char-LSTM (BASELINE.json config 5) on the GPU: data-parallel training with 2 ranks on one GPU
+against a single-process full-batch step, and the persistent recurrence kernels' failure reporting.
+
+RCCL refuses two ranks on one device, so the DP test uses gloo (GPU tensors) to exercise the same
+GradAllReduce hooks / bucket launches as the RCCL path (as tests/test_dp_gpu.py does for ResNet)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"])
+from tensorflow_examples_amd.data.text import ptb_batches, synthetic_char_ids
+from tensorflow_examples_amd.models.char_lstm import LMTrainer, build_char_lstm
+from tensorflow_examples_amd.ops import rnn as rnn_ops
+from tensorflow_examples_amd.optim import GradientDescentOptimizer
+from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed
+dev = init_distributed(backend="gloo", device="cuda")
+rank, world = dist.get_rank(), dist.get_world_size()
+B, T, H, V = 16, 20, 256, 65
+ids = synthetic_char_ids(20000, V, seed=0)
+x, y = next(iter(ptb_batches(ids, B * world, T)))          # one global [T, B*world] window
+x, y = torch.as_tensor(x, device=dev), torch.as_tensor(y, device=dev)
+assert rnn_ops._persistent(B, H, dev), "the persistent recurrence kernels must be the path under test"
+
+def build(seed):
+    st, m = build_char_lstm(dev, vocab_size=V, embed=64, hidden=H, layers=2, dtype=torch.bfloat16, seed=seed)
+    return st, m
+
+store, model = build(rank)                                 # different init per rank ...
+broadcast_variables(store)                                 # ... made identical by the broadcast
+w0 = store.master.clone()
+dp = GradAllReduce(store, bucket_bytes=1 << 20)
+tr = LMTrainer(model, GradientDescentOptimizer(store, 1.0), dp, max_grad_norm=0.25)
+loss, _ = tr.step(x[:, rank * B:(rank + 1) * B].contiguous(), y[:, rank * B:(rank + 1) * B].contiguous(), None)
+torch.cuda.synchronize()
+tr.check()
+d_dp = store.master - w0
+w = store.master.clone()
+dist.broadcast(w, 0)
+diff = (w - store.master).abs().max().item()
+
+def reference():
+    rs, rm = build(0)
+    assert torch.equal(rs.master, w0)
+    rt = LMTrainer(rm, GradientDescentOptimizer(rs, 1.0), None, max_grad_norm=0.25)
+    rt.step(x, y, None)                                    # the full 2B-row batch in one process
+    torch.cuda.synchronize()
+    return rs.master - w0
+
+d_ref = reference()
+rel = ((d_dp - d_ref).norm() / d_ref.norm()).item()
+print(f"RANK{rank} diff={diff} rel={rel:.3e} loss={float(loss):.4f}", flush=True)
+assert diff == 0.0, diff
+assert rel < 2e-2, rel
+dist.destroy_process_group()
+"""
+
+
+def test_char_lstm_dp_two_ranks_one_gpu(gpu, tmp_path):
+    """One DP step (2 ranks x 16 rows, bucketed all-reduce, global-norm clip on the summed gradient)
+    moves the weights exactly like one single-process step on the full 32-row batch."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    script = tmp_path / "w.py"
+    script.write_text(WORKER)
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, ROOT=ROOT, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=300)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    print("\n".join(outs))
+    assert all(p.returncode == 0 for p in procs), outs
+    assert all("diff=0.0" in o and "rel=" in o for o in outs)
+
+
+def test_persistent_lstm_spin_expiry_raises(gpu):
+    """A forced hand-off timeout (spin bound 1) must surface as LSTMHandoffError at the next health
+    check instead of training on silently wrong gradients; the sticky word resets after reporting."""
+    from tensorflow_examples_amd.ops import rnn as rnn_ops
+    from tensorflow_examples_amd.variables import Uniform, VariableStore
+
+    T, B, In, H = 50, 64, 128, 512
+    store = VariableStore(device=gpu, compute_dtype=torch.bfloat16, seed=1)
+    w_ih = store.variable([4 * H, In], Uniform(-0.1, 0.1), name="w_ih")
+    w_hh = store.variable([4 * H, H], Uniform(-0.1, 0.1), name="w_hh")
+    b = store.variable([4 * H], Uniform(-0.1, 0.1), name="b")
+    store.finalize()
+    assert rnn_ops._persistent(B, H, gpu)
+    x = torch.randn(T, B, In, device=gpu).to(torch.bfloat16).requires_grad_(True)
+
+    def step():
+        out, _ = rnn_ops.lstm_layer(x, w_ih, w_hh, b)
+        out.float().sum().backward()
+        torch.cuda.synchronize()
+
+    rnn_ops.check_lstm_health(gpu)  # clean start
+    saved = rnn_ops._SPIN_LIMIT
+    try:
+        rnn_ops._SPIN_LIMIT = 1
+        step()
+    finally:
+        rnn_ops._SPIN_LIMIT = saved
+    with pytest.raises(rnn_ops.LSTMHandoffError):
+        rnn_ops.check_lstm_health(gpu)
+    step()  # the default bound: healthy again
+    rnn_ops.check_lstm_health(gpu)

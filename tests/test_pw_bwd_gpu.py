@@ -1,0 +1,108 @@
+"""Fused backward of the bottleneck's expanding 1x1 conv with the tail BN's backward applied on load
+(csrc/kernels/pw_bwd.hip): numerics vs an fp32 PyTorch reference of the same chain, and the whole
+ResNet-50 first step with the fused path on vs the layer-wise path."""
+import pytest
+import torch
+
+from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("shape", [(256, 32, 32, 64), (4, 8, 8, 64), (3, 4, 8, 64)])
+@pytest.mark.parametrize("bn2", [True, False])
+def test_pw_bwd_expand_matches_reference(gpu, shape, bn2):
+    N, H, W, CN = shape
+    CW = 4 * CN
+    M = N * H * W
+    torch.manual_seed(7)
+    # tail BN: y3 (its input), statistics and the backward reduction of a random output gradient
+    y3 = _bf(torch.randn(N, H, W, CW, device=gpu) * 1.3 + 0.2)
+    g = _bf(torch.randn(N, H, W, CW, device=gpu))
+    res = _bf(torch.randn(N, H, W, CW, device=gpu))
+    gam3, bet3 = torch.rand(CW, device=gpu) + 0.5, torch.randn(CW, device=gpu) * 0.3
+    ws3 = torch.zeros(64 * 2 * CW, device=gpu)
+    _, save3, mask3 = torch.ops.tfx.bn_fwd_train(y3, gam3, bet3, None, None, 0.1, 1e-5, res, True, ws3, False)
+    _, _, red3 = torch.ops.tfx.bn_bwd(g, y3, None, save3, True, ws3, None, None, mask3, False)
+    # conv3: a2 -> y3 ; BN2 produced a2 from y2
+    a2 = _bf(torch.relu(torch.randn(N, H, W, CN, device=gpu)))
+    w = _bf(torch.randn(CW, 1, 1, CN, device=gpu) * 0.1)
+    y2 = _bf(torch.randn(N, H, W, CN, device=gpu) * 1.1 - 0.1)
+    gam2, bet2 = torch.rand(CN, device=gpu) + 0.5, torch.randn(CN, device=gpu) * 0.3
+    ws2 = torch.zeros(64 * 2 * CN, device=gpu)
+    _, save2, _ = torch.ops.tfx.bn_fwd_train(y2, gam2, bet2, None, None, 0.1, 1e-5, None, True, ws2, False)
+    assert ws2.abs().max().item() == 0.0
+
+    # reference: the layer-wise chain, in fp32 from the same bf16 dy3 the apply pass writes
+    dy3 = torch.ops.tfx.bn_bwd_apply(g, y3, None, save3, red3, True, mask3, False)[0]
+    dyf = dy3.float().reshape(M, CW)
+    wf = w.float().reshape(CW, CN)
+    dA2_ref = dyf @ wf
+    dW_ref = dyf.t() @ a2.float().reshape(M, CN)
+
+    dw = torch.zeros(CW, 1, 1, CN, device=gpu)
+    dg2, db2 = torch.zeros(CN, device=gpu), torch.zeros(CN, device=gpu)
+    dA2, red2 = torch.ops.tfx.pw_bwd_expand(g, y3, mask3, save3, red3, a2, w, dw, y2 if bn2 else None,
+                                            save2 if bn2 else None, True, ws2 if bn2 else None,
+                                            dg2 if bn2 else None, db2 if bn2 else None)
+    torch.cuda.synchronize()
+    assert dA2.shape == a2.shape and dA2.dtype == torch.bfloat16
+    assert _rel(dA2.reshape(M, CN), dA2_ref) < 8e-3
+    assert _rel(dw.reshape(CW, CN), dW_ref) < 1e-4
+    if bn2:
+        assert ws2.abs().max().item() == 0.0, "BN2 slots not restored to zero"
+        # BN2 backward partials of the kernel's own bf16 dA2 (relu mask recomputed from y2)
+        mu, istd, sc, sh = save2.reshape(4, CN)
+        x2 = y2.float().reshape(M, CN)
+        gp = dA2.float().reshape(M, CN) * ((x2 * sc + sh) > 0).float()
+        ref_s, ref_q = gp.sum(0), (gp * (x2 - mu) * istd).sum(0)
+        assert _rel(red2[:CN], ref_s) < 1e-4 and _rel(red2[CN:], ref_q) < 1e-4
+        assert _rel(db2, ref_s) < 1e-4 and _rel(dg2, ref_q) < 1e-4
+    else:
+        assert red2.numel() == 0
+
+
+def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
+    """ResNet-50 first-step gradients with the identity blocks' tail BN backward fused into conv3's
+    backward (default) vs materialised by bn_bwd_apply (layer-wise): equal up to the f32-atomic noise
+    floor measured between two fused runs."""
+    from tensorflow_examples_amd import ops
+    from tensorflow_examples_amd.ops import nn as nnops
+
+    g = torch.Generator().manual_seed(5)
+    img = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 10, (32,), generator=g).to(gpu)
+    xin = to_model_input(img.to(gpu))
+
+    def run():
+        st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=3)
+        st.zero_grad()
+        ops.softmax_cross_entropy(m(xin, training=True), lab).backward()
+        torch.cuda.synchronize()
+        return st.grad.clone(), st
+
+    saved = nnops._LAZY_BN_BWD
+    try:
+        n0 = nnops.PW_EXPAND_CALLS[0]
+        g0, st = run()
+        assert nnops.PW_EXPAND_CALLS[0] - n0 == 2, "stage-1 identity blocks 2 and 3 run fused"
+        g1, _ = run()
+        nnops._LAZY_BN_BWD = False
+        g2, _ = run()
+    finally:
+        nnops._LAZY_BN_BWD = saved
+    for v in st.trainable():
+        sl = slice(v.offset, v.offset + v.numel)
+        n = g0[sl].norm().item() + 1e-12
+        noise = (g1[sl] - g0[sl]).norm().item() / n
+        e = (g2[sl] - g0[sl]).norm().item() / n
+        assert e <= max(4 * noise, 2e-3), (v.name, e, noise)
