@@ -124,14 +124,28 @@ struct PwExpandArgs {
   int relu2 = 0;
   float* slots2 = nullptr;          // [NSLOT][2][CN]
   float* slab = nullptr;            // [grid][CW * CN] f32
+  // projection-block tail (optional): the shortcut BN's input ysc [M][CW]; partial sums g' * ysc go
+  // to the second halves of slots_sc [NSLOT][2][CW] (pw_slab_reduce centres and scales them)
+  const uint16_t* ysc = nullptr;
+  float* slots_sc = nullptr;
   int M = 0, CN = 0;
+};
+// the shortcut BN's reduction in pw_slab_reduce's tail (C = 0: none): red = [red3's sum g' | sum q]
+struct PwSecReduce {
+  float* slots = nullptr;
+  const float* red3 = nullptr;
+  const float* save = nullptr;  // the shortcut BN's [mu | istd | ...]
+  float* red = nullptr;
+  float* dgamma = nullptr;
+  float* dbeta = nullptr;
+  int C = 0;
 };
 bool pw_bwd_expand_ok(int CN, int64_t M);
 int pw_bwd_expand_grid(int CN, int64_t M);
 void pw_bwd_expand(const PwExpandArgs& args, int nblocks, hipStream_t s);
 // dw[CW][CN] += sum of nslab slabs; + optional BN slot reduction (bn_slot_reduce's math) in tail blocks
 void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_slots, int sr_C, float* sr_red,
-                    float* sr_dgamma, float* sr_dbeta, hipStream_t s);
+                    float* sr_dgamma, float* sr_dbeta, const PwSecReduce& sec, hipStream_t s);
 
 // ---------------------------------------------------------------- f32 GEMM (MFMA f32, exact)
 // C[M][N] = act(alpha * op(A) op(B) + bias) (+ C if accumulate); op = transpose flags

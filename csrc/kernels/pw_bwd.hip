@@ -112,11 +112,14 @@ struct PwExpandCfg {
   static_assert(2 * SLOT + W_BYTES <= 160 * 1024, "LDS budget");
 };
 
-template <int CN>
+// SEC (a projection block's tail): the residual was the shortcut BN's output, used only there, so its
+// output gradient is the same g' = g * mask -- accumulate that BN's sum g' * ysc per channel while g'
+// is in registers (pw_slab_reduce turns it into sum g' * xhat_sc); its sum g' equals red3's.
+template <int CN, bool SEC>
 __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a) {
   using C = PwExpandCfg<CN>;
   constexpr int CW = C::CW, NCH = C::NCH, LPT = C::LPT, TPR = C::TPR;
-  __shared__ __attribute__((aligned(16))) char smem[2 * C::SLOT + C::W_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::SLOT + C::W_BYTES + (SEC ? 8 * 4 * PW_NT : 0)];
   char* wimg = smem + 2 * C::SLOT;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int ntiles = a.M / PW_BM;
@@ -147,6 +150,26 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
   const __amdgpu_buffer_rsrc_t rm = pw_rsrc(a.mask3, (int64_t)a.M * CW / 8);
   const __amdgpu_buffer_rsrc_t ra = pw_rsrc(a.a2, (int64_t)a.M * CN * 2);
   const __amdgpu_buffer_rsrc_t rx2 = pw_rsrc(a.y2, a.y2 ? (int64_t)a.M * CN * 2 : 0);
+  const __amdgpu_buffer_rsrc_t rsc = pw_rsrc(a.ysc, SEC ? (int64_t)a.M * CW * 2 : 0);
+  // SEC: sum g' * ysc per channel of this thread, accumulated in a private LDS column qcol[k][PW_NT]
+  // (registers are full); the tail turns it into sum g' * xhat_sc = is_sc * (S - mu_sc * sum g') with
+  // red3's sum g'.  ysc is staged ONE tile ahead in a single register buffer (the ring is two deep).
+  float* qcol = reinterpret_cast<float*>(smem + 2 * C::SLOT + C::W_BYTES);
+  if constexpr (SEC) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) qcol[k * PW_NT + t] = 0.f;
+  }
+  pw_u32x4 ysb[SEC ? LPT : 1];
+  auto issue_ys = [&](int tile) {
+    if constexpr (SEC) {
+      const bool ok = tile < ntiles;
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        const int row = tile * PW_BM + r0 + C::RSTEP * i;
+        ysb[i] = __builtin_amdgcn_raw_buffer_load_b128(rsc, ok ? (uint32_t)(row * CW + c0) * 2u : 0x80000000u, 0, 0);
+      }
+    }
+  };
 
   // dgrad wave tile: rows 16 (wv & 1), columns DCOLS (wv >> 1); SWAP orientation -> lane holds row
   // (lane & 15), columns dcb + (lane >> 4) * 4 + r of each 16-col tile
@@ -206,21 +229,34 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
   // transform tile (registers) -> LDS slot; the epilogue's y2 values move to `x2` (the staging
   // registers are re-issued before the tile computes)
   pw_u32x2 x2[C::DTN];
-  auto stage = [&](const Stage& s, char* slot) {
+  auto stage = [&](const Stage& s, char* slot, int next_tile) {
 #pragma unroll
     for (int j = 0; j < C::DTN; ++j) x2[j] = s.x2[j];
+    float q[SEC ? 8 : 1];
+    if constexpr (SEC) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) q[k] = qcol[k * PW_NT + t];
+    }
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       float gf[8], yf[8], o[8];
       unpack8(__builtin_bit_cast(U4, s.g[i]), gf);
       unpack8(__builtin_bit_cast(U4, s.y[i]), yf);
+      float sf[SEC ? 8 : 1];
+      if constexpr (SEC) unpack8(__builtin_bit_cast(U4, ysb[i]), sf);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float gg = ((s.m[i] >> k) & 1u) ? gf[k] : 0.f;
         o[k] = fmaf(A[k], gg, fmaf(B[k], yf[k], D[k]));
+        if constexpr (SEC) q[k] = fmaf(gg, sf[k], q[k]);
       }
       const int row = r0 + C::RSTEP * i;
       *reinterpret_cast<U4*>(slot + (chc >> 3) * (PW_BM * 128) + pw_kmaj(row, chc & 7)) = pack8(o);
+    }
+    if constexpr (SEC) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qcol[k * PW_NT + t] = q[k];
+      issue_ys(next_tile);
     }
     if (t < C::NLD) {
       const int row = t / C::NTPR, cc = t % C::NTPR;
@@ -282,15 +318,16 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
   // ---- main loop over this block's m-tiles (tile0, tile0 + tstep, ...): staged two ahead
   issue(st0, tile0);
   issue(st1, tile0 + tstep);
+  issue_ys(tile0);
   __syncthreads();  // W3 image written
   for (int tile = tile0; tile < ntiles; tile += 2 * tstep) {
-    stage(st0, smem);
+    stage(st0, smem, tile + tstep);
     issue(st0, tile + 2 * tstep);
     sync();
     compute(smem, tile);
     const int t1 = tile + tstep;
     if (t1 >= ntiles) break;
-    stage(st1, smem + C::SLOT);
+    stage(st1, smem + C::SLOT, t1 + tstep);
     issue(st1, t1 + 2 * tstep);
     sync();
     compute(smem + C::SLOT, t1);
@@ -303,6 +340,21 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
 #pragma unroll
     for (int n = 0; n < C::WTN; ++n)
       *reinterpret_cast<f32x4_t*>(slab + ((size_t)(j * C::WTN + n) * PW_NT + t) * 4) = accw[j][n];
+  // ---- SEC partials: threads t, t + TPR, ... share channel group chc -> sum their LDS columns,
+  // one atomic per channel
+  if constexpr (SEC) {
+    __syncthreads();
+    const float* red = qcol;
+    if (t < TPR) {
+      float* slots = a.slots_sc + (size_t)(blockIdx.x % NSLOT) * 2 * CW;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float q = 0.f;
+        for (int r = 0; r < PW_NT / TPR; ++r) q += red[k * PW_NT + r * TPR + t];
+        atomicAdd(slots + CW + c0 + k, q);
+      }
+    }
+  }
   // ---- BN2 partials: sum the 16 rows of each DPP row (same columns), one atomic per column
   if (a.y2) {
     float* slots = a.slots2 + (size_t)(blockIdx.x % NSLOT) * 2 * CN;
@@ -338,14 +390,47 @@ __device__ __forceinline__ int pw_slab_to_dw(int e) {
 // atomics of the partial sums: nslab / PW_RG-fold fewer than per-block atomics).  Blocks past that
 // grid reduce a BN layer's backward slots (bn_slot_reduce's math), 16 channels each.
 constexpr int PW_RG = 8;
+// SEC tail (sec_C > 0): the shortcut BN's reduction -- red_sc = [red3's sum g' | sum of the q slots]
+// (its slots' first halves are never written), dbeta_sc / dgamma_sc +=, q slots re-zeroed.
 template <int CN>
 __global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __restrict__ slab, int nslab,
                                                              float* __restrict__ dw, float* __restrict__ sr_slots,
                                                              int sr_C, float* __restrict__ sr_red,
                                                              float* __restrict__ sr_dgamma,
-                                                             float* __restrict__ sr_dbeta) {
+                                                             float* __restrict__ sr_dbeta, PwSecReduce sec) {
   constexpr int E = 4 * CN * CN;
   const int ngemm = (E / 256) * PW_RG;
+  const int nsr = sr_C ? (sr_C + 15) / 16 : 0;
+  if ((int)blockIdx.x >= ngemm + nsr) {
+    // SEC: 16 channels per block, 16 slot-lanes x NSLOT/16 slots each (q halves only)
+    const int sb = blockIdx.x - ngemm - nsr, C = sec.C;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4, c = sb * 16 + tx;
+    __shared__ float redq[256];
+    float q = 0.f;
+    if (c < C) {
+      float vq[NSLOT / 16];
+#pragma unroll
+      for (int i = 0; i < NSLOT / 16; ++i) vq[i] = sec.slots[(size_t)(ty + 16 * i) * 2 * C + C + c];
+#pragma unroll
+      for (int i = 0; i < NSLOT / 16; ++i) {
+        q += vq[i];
+        sec.slots[(size_t)(ty + 16 * i) * 2 * C + C + c] = 0.f;
+      }
+    }
+    redq[threadIdx.x] = q;
+    __syncthreads();
+    if (ty == 0 && c < C) {
+#pragma unroll
+      for (int k = 1; k < 16; ++k) q += redq[threadIdx.x + 16 * k];
+      const float sg = sec.red3[c];
+      q = sec.save[C + c] * (q - sec.save[c] * sg);
+      sec.red[c] = sg;
+      sec.red[C + c] = q;
+      if (sec.dbeta) sec.dbeta[c] += sg;
+      if (sec.dgamma) sec.dgamma[c] += q;
+    }
+    return;
+  }
   if ((int)blockIdx.x >= ngemm) {
     // BN slot reduction: 16 channels per block, 16 slot-lanes x NSLOT/16 slots each
     const int sb = blockIdx.x - ngemm;
@@ -409,19 +494,23 @@ int pw_bwd_expand_grid(int CN, int64_t M) {
 
 void pw_bwd_expand(const PwExpandArgs& args, int nblocks, hipStream_t s) {
   switch (args.CN) {
-    case 64: pw_bwd_expand_kernel<64><<<nblocks, PW_NT, 0, s>>>(args); break;
+    case 64:
+      if (args.ysc) pw_bwd_expand_kernel<64, true><<<nblocks, PW_NT, 0, s>>>(args);
+      else pw_bwd_expand_kernel<64, false><<<nblocks, PW_NT, 0, s>>>(args);
+      break;
     default: abort();
   }
 }
 
 void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_slots, int sr_C, float* sr_red,
-                    float* sr_dgamma, float* sr_dbeta, hipStream_t s) {
+                    float* sr_dgamma, float* sr_dbeta, const PwSecReduce& sec, hipStream_t s) {
   const int E = 4 * CN * CN;
-  const int grid = (E / 256) * PW_RG + (sr_slots ? (sr_C + 15) / 16 : 0);
+  const int nsr = sr_slots ? (sr_C + 15) / 16 : 0;
+  const int grid = (E / 256) * PW_RG + nsr + (sec.C ? (sec.C + 15) / 16 : 0);
   switch (CN) {
     case 64:
       pw_slab_reduce_kernel<64><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red, sr_dgamma,
-                                                     sr_dbeta);
+                                                     sr_dbeta, sec);
       break;
     default: abort();
   }

@@ -426,10 +426,16 @@ Tensor bn_slots_reduce(Tensor slots, int64_t C, optional<Tensor> dgamma, optiona
 // save3 / red3 = the tail BN's input, ReLU mask bits, [mean|invstd|scale|shift] and reduction
 // [sum g'|sum g' xhat]; a2 = the conv's input.  dw += the weight gradient.  With y2 (the BN2 input that
 // produced a2), its save2 / relu2 and slots2: the BN2 backward partials of dA2 are reduced too and
-// returned as red2 = [sum g'|sum g' xhat] (dgamma2 / dbeta2 +=).  Returns (dA2, red2).
-std::tuple<Tensor, Tensor> pw_bwd_expand(Tensor g, Tensor y3, Tensor mask3, Tensor save3, Tensor red3, Tensor a2,
-                                         Tensor w, Tensor dw, optional<Tensor> y2, optional<Tensor> save2, bool relu2,
-                                         optional<Tensor> slots2, optional<Tensor> dgamma2, optional<Tensor> dbeta2) {
+// returned as red2 = [sum g'|sum g' xhat] (dgamma2 / dbeta2 +=).  With ysc (a projection block: the
+// residual was the shortcut BN's output, input ysc, stats save_sc, slots slots_sc) that BN's backward
+// reduction rides along too: red_sc (dgamma_sc / dbeta_sc +=).  Returns (dA2, red2, red_sc).
+std::tuple<Tensor, Tensor, Tensor> pw_bwd_expand(Tensor g, Tensor y3, Tensor mask3, Tensor save3, Tensor red3,
+                                                 Tensor a2, Tensor w, Tensor dw, optional<Tensor> y2,
+                                                 optional<Tensor> save2, bool relu2, optional<Tensor> slots2,
+                                                 optional<Tensor> dgamma2, optional<Tensor> dbeta2,
+                                                 optional<Tensor> ysc, optional<Tensor> save_sc,
+                                                 optional<Tensor> slots_sc, optional<Tensor> dgamma_sc,
+                                                 optional<Tensor> dbeta_sc) {
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(y3); CHECK_CONTIG(y3); CHECK_BF16(a2); CHECK_CONTIG(a2);
   CHECK_BF16(w); CHECK_CONTIG(w); CHECK_F32(dw); CHECK_CONTIG(dw); CHECK_F32(save3); CHECK_F32(red3);
   const int64_t CW = w.size(0), CN = w.size(-1), M = a2.numel() / CN;
@@ -452,14 +458,26 @@ std::tuple<Tensor, Tensor> pw_bwd_expand(Tensor g, Tensor y3, Tensor mask3, Tens
     a.y2 = bf(*y2); a.save2 = save2->data_ptr<float>(); a.relu2 = relu2 ? 1 : 0; a.slots2 = slots2->data_ptr<float>();
     red2 = at::empty({2 * CN}, g.options().dtype(at::kFloat));
   }
+  Tensor red_sc = at::empty({0}, g.options().dtype(at::kFloat));
+  tfx::PwSecReduce sec;
+  if (ysc.has_value() && ysc->defined()) {
+    CHECK_BF16(*ysc); CHECK_CONTIG(*ysc);
+    TORCH_CHECK(ysc->numel() == M * CW && save_sc.has_value() && save_sc->numel() == 4 * CW && slots_sc.has_value(),
+                "pw_bwd_expand: shortcut BN arguments");
+    check_bn_ws(*slots_sc, CW);
+    a.ysc = bf(*ysc); a.slots_sc = slots_sc->data_ptr<float>();
+    red_sc = at::empty({2 * CW}, g.options().dtype(at::kFloat));
+    sec.slots = a.slots_sc; sec.red3 = a.red3; sec.save = save_sc->data_ptr<float>(); sec.red = red_sc.data_ptr<float>();
+    sec.dgamma = fpm(dgamma_sc); sec.dbeta = fpm(dbeta_sc); sec.C = (int)CW;
+  }
   const int nb = tfx::pw_bwd_expand_grid((int)CN, M);
   auto slab = at::empty({(int64_t)nb * CW * CN}, g.options().dtype(at::kFloat));
   a.slab = slab.data_ptr<float>();
   tfx::pw_bwd_expand(a, nb, cur_stream());
   tfx::pw_slab_reduce(a.slab, nb, (int)CN, dw.data_ptr<float>(), bnb ? a.slots2 : nullptr, (int)CN,
                       bnb ? red2.data_ptr<float>() : nullptr, bnb ? fpm(dgamma2) : nullptr,
-                      bnb ? fpm(dbeta2) : nullptr, cur_stream());
-  return {dA2, red2};
+                      bnb ? fpm(dbeta2) : nullptr, sec, cur_stream());
+  return {dA2, red2, red_sc};
 }
 
 bool pw_bwd_expand_supported(int64_t CN, int64_t M) { return tfx::pw_bwd_expand_ok((int)CN, M); }

@@ -183,18 +183,26 @@ class XgmiPSClient:
         self.store.refresh_shadow()
         return -1  # the step value arrives with the next push
 
+    def push_async(self, lr: float, zero_grad: bool = True) -> torch.Tensor:
+        """Apply SGD into the peer arenas and bump global_step behind the WHOLE update: every ps
+        task's runs are issued first and the step task's counter is bumped by the last launch of all
+        (stream order puts it after every earlier SGD kernel's peer writes) -- TF orders
+        AssignAdd(global_step) after all ApplyGradientDescent ops (R/distributed/distributed.py:108).
+        No host sync: returns the device tensor the new step value lands in (``step_out``)."""
+        launches = [(t, lo, hi) for t in range(self.num_ps) for lo, hi in self.runs[t]]
+        step_hdr = self.headers[self.step_task][:1]
+        if not launches:
+            _ops().ps_peer_sgd(self.params[self.step_task][:0], self.store.grad[:0], float(lr), step_hdr,
+                               self.step_out, zero_grad)
+        for n, (t, lo, hi) in enumerate(launches):
+            last = n == len(launches) - 1
+            _ops().ps_peer_sgd(self.params[t][lo:hi], self.store.grad[lo:hi], float(lr), step_hdr if last else None,
+                               self.step_out, zero_grad)
+        return self.step_out
+
     def push(self, lr: float, zero_grad: bool = True) -> int:
-        """Apply SGD into the peer arenas; bump global_step (after the update). Returns the new
-        step.  ``zero_grad``: the local gradient buffer is cleared by the same kernel."""
-        for t in range(self.num_ps):
-            rs = self.runs[t]
-            for i, (lo, hi) in enumerate(rs):
-                last = t == self.step_task and i == len(rs) - 1
-                _ops().ps_peer_sgd(self.params[t][lo:hi], self.store.grad[lo:hi], float(lr),
-                                   self.headers[t][:1] if last else None, self.step_out, zero_grad)
-            if t == self.step_task and not rs:
-                _ops().ps_peer_sgd(self.params[t][:0], self.store.grad[:0], float(lr), self.headers[t][:1],
-                                   self.step_out, zero_grad)
+        """:meth:`push_async` + wait: returns the new global step."""
+        self.push_async(lr, zero_grad)
         self._step_host.copy_(self.step_out, non_blocking=True)
         torch.cuda.current_stream(self.store.device).synchronize()
         return int(self._step_host[0])

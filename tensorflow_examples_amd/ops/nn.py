@@ -101,14 +101,30 @@ class LazyBNGrad:
     input, mask the forward's ReLU mask bits and (A, B, D) folded from ``save`` and ``red``.  The BN's
     backward returns a zero-stride placeholder carrying this (``_tfx_lazy_bnbwd``); its producer conv
     (the expanding 1x1 conv3) then forms dy on load inside its fused backward (pw_bwd.hip) -- or
-    calls :meth:`materialize` (bn_bwd_apply, the layer-wise path) when it cannot."""
-    __slots__ = ("g", "x", "save", "red", "relu", "mask")
+    calls :meth:`materialize` (bn_bwd_apply, the layer-wise path) when it cannot.
 
-    def __init__(self, g, x, save, red, relu, mask):
+    ``sec`` (a projection block's tail): the residual was the shortcut BN's output, whose gradient is
+    the same g * mask; that BN's backward reduction is still owed (``sec.red`` is None until the fused
+    kernel or :meth:`materialize` fills it -- whichever of conv3 / the shortcut BN runs first)."""
+    __slots__ = ("g", "x", "save", "red", "relu", "mask", "sec", "dy")
+
+    def __init__(self, g, x, save, red, relu, mask, sec=None):
         self.g, self.x, self.save, self.red, self.relu, self.mask = g, x, save, red, relu, mask
+        self.sec, self.dy = sec, None
 
     def materialize(self) -> torch.Tensor:
-        return torch.ops.tfx.bn_bwd_apply(self.g, self.x, None, self.save, self.red, self.relu, self.mask, False)[0]
+        if self.dy is None:
+            rb = self.sec
+            if rb is None:
+                self.dy = torch.ops.tfx.bn_bwd_apply(self.g, self.x, None, self.save, self.red, self.relu, self.mask,
+                                                     False)[0]
+            else:
+                p_t = rb.dgamma is not None
+                self.dy, _, rb.red = torch.ops.tfx.bn_bwd_apply_sec(
+                    self.g, self.x, self.save, self.red, self.relu, self.mask, rb.x, rb.save, rb.ws,
+                    rb.dgamma if p_t else None, rb.dbeta if p_t else None, False, True)
+                rb.sec_lazy = None
+        return self.dy
 
 
 def _pw_expand_ok(x, w, stride, pad, dil, lazy, sink) -> bool:
@@ -118,6 +134,8 @@ def _pw_expand_ok(x, w, stride, pad, dil, lazy, sink) -> bool:
             and sh[1] == 1 and sh[2] == 1 and sh[0] == 4 * sh[3] and x.is_contiguous()):
         return False
     if lazy.mask is None or lazy.g.shape[-1] != sh[0] or x.shape[-1] != sh[3]:
+        return False
+    if lazy.dy is not None:  # already materialised (the shortcut BN's backward ran first)
         return False
     return bool(torch.ops.tfx.pw_bwd_expand_supported(sh[3], x.numel() // sh[3]))
 
@@ -157,13 +175,18 @@ class _Conv2d(torch.autograd.Function):
                     bnb = ctx.bnb
                     use_bnb = bnb is not None and bnb.mask is None and not bnb.deferred and bnb.red is None \
                         and x.numel() * x.element_size() <= _BNB_MAX_BYTES
-                    dx, red2 = torch.ops.tfx.pw_bwd_expand(
+                    # projection block: the shortcut BN's backward reduction too (F3-SEC)
+                    rb = lazy.sec if lazy.dy is None else None
+                    dx, red2, red_sc = torch.ops.tfx.pw_bwd_expand(
                         lazy.g.contiguous(), lazy.x, lazy.mask, lazy.save, lazy.red, x, w.value, w.grad,
                         bnb.x if use_bnb else None, bnb.save if use_bnb else None, bool(use_bnb and bnb.relu),
                         bnb.ws if use_bnb else None, bnb.dgamma if use_bnb else None,
-                        bnb.dbeta if use_bnb else None)
+                        bnb.dbeta if use_bnb else None, rb.x if rb else None, rb.save if rb else None,
+                        rb.ws if rb else None, rb.dgamma if rb else None, rb.dbeta if rb else None)
                     if use_bnb:
                         bnb.red = red2
+                    if rb is not None:
+                        rb.red, rb.sec_lazy = red_sc, None
                     PW_EXPAND_CALLS[0] += 1
                     _grad_ready(w)
                     return dx, None, None, None, None, None, None, None, None
@@ -339,7 +362,7 @@ class BNBackwardFusion:
     ``red`` ([sum g' | sum g' xhat]) (or a later weight-gradient launch does, from the slots); the BN
     backward then runs only its apply pass."""
     __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "in_mask", "deferred",
-                 "sr_pending")
+                 "sr_pending", "sec_lazy")
 
     def __init__(self, x, save, mask, relu, ws, dgamma, dbeta):
         self.x, self.save, self.mask, self.relu, self.ws = x, save, mask, relu, ws
@@ -352,6 +375,8 @@ class BNBackwardFusion:
         self.deferred = False
         # backward partials sit in ``ws`` waiting for a later launch to reduce them (_PENDING_SR)
         self.sr_pending = False
+        # a projection tail's LazyBNGrad that still owes this (shortcut) BN's reduction
+        self.sec_lazy = None
 
 
 # ====================================================================== batch norm (+res, +relu)
@@ -508,6 +533,8 @@ class _BatchNorm(torch.autograd.Function):
             if not training:
                 raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
             if ctx.bnb is not None:
+                if ctx.bnb.sec_lazy is not None:  # the tail's conv3 has not run yet: reduce here
+                    ctx.bnb.sec_lazy.materialize()
                 _resolve_pending(ctx.bnb)  # no weight-gradient launch took its deferred reduction
             train_p = gamma is not None and gamma.trainable
             gy = gy.contiguous()
@@ -516,7 +543,20 @@ class _BatchNorm(torch.autograd.Function):
             # tensor write less per identity block
             masked = ctx.has_res and ctx.res_sink is not None and mask is not None and \
                 getattr(ctx.res_sink, "accept_masked", False) and relu
-            if ctx.bnb is not None and ctx.bnb.red is not None and _res_bn_sec_ok(ctx, gy, mask, relu, masked):
+            if ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and _LAZY_BN_BWD and relu \
+                    and mask is not None and res is None and _res_bn_sec_ok(ctx, gy, mask, relu, masked) \
+                    and x.shape[-1] % 4 == 0 \
+                    and torch.ops.tfx.pw_bwd_expand_supported(x.shape[-1] // 4, x.numel() // x.shape[-1]):
+                # projection tail: dx stays lazy and the shortcut BN's reduction is owed by it -- conv3's
+                # fused backward forms both (pw_bwd.hip); the shortcut BN gets gy unmasked + the mask bits
+                rb = ctx.res_bnb
+                dx = _zero_scalar(x.dtype, x.device).expand(x.shape)
+                lz = LazyBNGrad(gy, x, save, ctx.bnb.red, relu, mask, sec=rb)
+                dx._tfx_lazy_bnbwd = lz
+                rb.sec_lazy = lz
+                rb.in_mask, dres = mask, gy
+                ctx.bnb.red = None
+            elif ctx.bnb is not None and ctx.bnb.red is not None and _res_bn_sec_ok(ctx, gy, mask, relu, masked):
                 # ... and the residual's own BN backward is reduced in the same pass
                 rb = ctx.res_bnb
                 p_t = rb.dgamma is not None

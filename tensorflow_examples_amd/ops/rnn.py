@@ -94,7 +94,7 @@ def check_lstm_health(device=None, reset: bool = True) -> None:
 
 
 def _persistent(B: int, H: int, dev: torch.device) -> bool:
-    if os.environ.get("TFX_LSTM_PERSISTENT", "1") == "0":
+    if os.environ.get("TFX_LSTM_PERSISTENT", "1") == "0" or not _native.use_native_device(dev):
         return False
     key = (B, H, dev.index or 0)
     if key not in _SEQ_OK:

@@ -33,34 +33,39 @@ def test_mlp_grads_match_cpu(gpu):
     assert torch.allclose(sg.grad.cpu(), sc.grad, atol=1e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("transport", ["tcp", "xgmi"])
-def test_distributed_script_on_gpu(tmp_path, transport):
+@pytest.mark.parametrize("transport,num_ps", [("tcp", 1), ("xgmi", 1), ("xgmi", 2)])
+def test_distributed_script_on_gpu(tmp_path, transport, num_ps):
     """ps + 2 workers on the GPU (the reference's 3-process recipe, R/distributed/distributed.py:7-14).
     xgmi: the ps arena is mapped into both workers; every push lands and bumps global_step exactly once,
-    so the last progress line printed by the later worker shows the total worker step count."""
+    so the last progress line printed by the later worker shows the total worker step count.  With
+    two ps tasks the variables are placed round-robin (global_step, W2, b2 on ps0; W1, b1 on ps1) and
+    the step bump is issued behind BOTH tasks' SGD runs (cluster/xgmi.py push_async)."""
     import re
     import socket
-    s = [socket.socket() for _ in range(3)]
+    s = [socket.socket() for _ in range(2 + num_ps)]
     for x in s:
         x.bind(("127.0.0.1", 0))
-    ps, w1, w2 = [x.getsockname()[1] for x in s]
+    ports = [x.getsockname()[1] for x in s]
     for x in s:
         x.close()
+    pss, (w1, w2) = ports[:num_ps], ports[num_ps:]
     script = os.path.join(ROOT, "distributed", "distributed.py")
     epochs, batches = 2, 200
-    args = [f"--ps_hosts=127.0.0.1:{ps}", f"--worker_hosts=127.0.0.1:{w1},127.0.0.1:{w2}", "--device=cuda",
-            f"--logs_path={tmp_path}", "--recovery_wait_secs=0.2", f"--training_epochs={epochs}",
+    args = ["--ps_hosts=" + ",".join(f"127.0.0.1:{q}" for q in pss), f"--worker_hosts=127.0.0.1:{w1},127.0.0.1:{w2}",
+            "--device=cuda", f"--logs_path={tmp_path}", "--recovery_wait_secs=0.2", f"--training_epochs={epochs}",
             f"--max_batches_per_epoch={batches}", "--ps_exit_after_workers", f"--transport={transport}",
             "--xgmi_arena_mb=4"]
-    p = subprocess.Popen([sys.executable, script, *args, "--job_name=ps", "--task_index=0"])
+    p = [subprocess.Popen([sys.executable, script, *args, "--job_name=ps", f"--task_index={k}"])
+         for k in range(num_ps)]
     w = [subprocess.Popen([sys.executable, script, *args, "--job_name=worker", f"--task_index={i}"],
                           stdout=subprocess.PIPE, text=True) for i in (0, 1)]
     try:
         outs = [x.communicate(timeout=300)[0] for x in w]
         assert all(x.returncode == 0 for x in w), outs
-        assert p.wait(timeout=60) == 0
+        for q in p:
+            assert q.wait(timeout=60) == 0
     finally:
-        for x in [p] + w:
+        for x in p + w:
             if x.poll() is None:
                 x.kill()
     finals = []

@@ -19,8 +19,8 @@ def _bf(t):
 
 
 @pytest.mark.parametrize("shape", [(256, 32, 32, 64), (4, 8, 8, 64), (3, 4, 8, 64)])
-@pytest.mark.parametrize("bn2", [True, False])
-def test_pw_bwd_expand_matches_reference(gpu, shape, bn2):
+@pytest.mark.parametrize("bn2,sec", [(True, False), (False, False), (True, True)])
+def test_pw_bwd_expand_matches_reference(gpu, shape, bn2, sec):
     N, H, W, CN = shape
     CW = 4 * CN
     M = N * H * W
@@ -49,12 +49,31 @@ def test_pw_bwd_expand_matches_reference(gpu, shape, bn2):
     dA2_ref = dyf @ wf
     dW_ref = dyf.t() @ a2.float().reshape(M, CN)
 
+    # projection block: the residual was a shortcut BN's output (input ysc), whose backward
+    # reduction rides along (F3-SEC)
+    ysc = _bf(torch.randn(N, H, W, CW, device=gpu) * 0.9 + 0.4)
+    gsc, bsc = torch.rand(CW, device=gpu) + 0.5, torch.randn(CW, device=gpu) * 0.3
+    wssc = torch.zeros(64 * 2 * CW, device=gpu)
+    _, savesc, _ = torch.ops.tfx.bn_fwd_train(ysc, gsc, bsc, None, None, 0.1, 1e-5, None, False, wssc, False)
+    dgsc, dbsc = torch.full((CW,), 0.5, device=gpu), torch.full((CW,), -0.25, device=gpu)
+
     dw = torch.zeros(CW, 1, 1, CN, device=gpu)
     dg2, db2 = torch.zeros(CN, device=gpu), torch.zeros(CN, device=gpu)
-    dA2, red2 = torch.ops.tfx.pw_bwd_expand(g, y3, mask3, save3, red3, a2, w, dw, y2 if bn2 else None,
-                                            save2 if bn2 else None, True, ws2 if bn2 else None,
-                                            dg2 if bn2 else None, db2 if bn2 else None)
+    dA2, red2, redsc = torch.ops.tfx.pw_bwd_expand(
+        g, y3, mask3, save3, red3, a2, w, dw, y2 if bn2 else None, save2 if bn2 else None, True,
+        ws2 if bn2 else None, dg2 if bn2 else None, db2 if bn2 else None, ysc if sec else None,
+        savesc if sec else None, wssc if sec else None, dgsc if sec else None, dbsc if sec else None)
     torch.cuda.synchronize()
+    if sec:
+        assert wssc.abs().max().item() == 0.0, "shortcut BN slots not restored to zero"
+        bits = (mask3.reshape(M, CW // 8, 1).int() >> torch.arange(8, device=gpu, dtype=torch.int32)) & 1
+        gp = g.float().reshape(M, CW) * bits.reshape(M, CW).float()
+        xh = (ysc.float().reshape(M, CW) - savesc[:CW]) * savesc[CW:2 * CW]
+        ref_s, ref_q = gp.sum(0), (gp * xh).sum(0)
+        assert _rel(redsc[:CW], ref_s) < 1e-4 and _rel(redsc[CW:], ref_q) < 2e-4
+        assert _rel(dbsc + 0.25, ref_s) < 1e-4 and _rel(dgsc - 0.5, ref_q) < 2e-4
+    else:
+        assert redsc.numel() == 0
     assert dA2.shape == a2.shape and dA2.dtype == torch.bfloat16
     assert _rel(dA2.reshape(M, CN), dA2_ref) < 8e-3
     assert _rel(dw.reshape(CW, CN), dW_ref) < 1e-4
@@ -90,19 +109,25 @@ def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
         torch.cuda.synchronize()
         return st.grad.clone(), st
 
-    saved = nnops._LAZY_BN_BWD
+    saved, saved_ok = nnops._LAZY_BN_BWD, nnops._pw_expand_ok
     try:
         n0 = nnops.PW_EXPAND_CALLS[0]
         g0, st = run()
-        assert nnops.PW_EXPAND_CALLS[0] - n0 == 2, "stage-1 identity blocks 2 and 3 run fused"
+        assert nnops.PW_EXPAND_CALLS[0] - n0 == 3, "stage-1 blocks run fused (projection block 1 with F3-SEC)"
         g1, _ = run()
+        # lazy gradients, but every conv3 declines the fused kernel: LazyBNGrad.materialize (the
+        # projection tail's reduces the shortcut BN there, or in the shortcut BN's backward if first)
+        nnops._pw_expand_ok = lambda *a: False
+        g3, _ = run()
+        nnops._pw_expand_ok = saved_ok
         nnops._LAZY_BN_BWD = False
         g2, _ = run()
     finally:
-        nnops._LAZY_BN_BWD = saved
+        nnops._LAZY_BN_BWD, nnops._pw_expand_ok = saved, saved_ok
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
         noise = (g1[sl] - g0[sl]).norm().item() / n
-        e = (g2[sl] - g0[sl]).norm().item() / n
-        assert e <= max(4 * noise, 2e-3), (v.name, e, noise)
+        for gx in (g2, g3):
+            e = (gx[sl] - g0[sl]).norm().item() / n
+            assert e <= max(4 * noise, 2e-3), (v.name, e, noise)
