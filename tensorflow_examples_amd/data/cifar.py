@@ -57,7 +57,8 @@ def load_cifar10(data_dir: Optional[str], synthetic_train: int = 50000, syntheti
 def augment_offsets(n: int, device, generator: Optional[torch.Generator] = None, pad: int = 4) -> torch.Tensor:
     """Per-image crop origin in the padded image and flip bit: int32 [n, 3] = (ox, oy, flip)."""
     r = torch.randint(0, 2 * pad + 1, (n, 3), device=device, generator=generator, dtype=torch.int32)
-    r[:, 2] %= 2
+    # the flip bit is its own fair coin (randint(0, 2 pad + 1) % 2 would favour 0: 5 of 9)
+    r[:, 2] = torch.randint(0, 2, (n,), device=device, generator=generator, dtype=torch.int32)
     return r
 
 

@@ -178,12 +178,19 @@ class CyclicFeeder:
 
 
 class DevicePrefetcher:
-    """Iterate host batches as device tensors, ``depth`` batches ahead (tf.data prefetch_to_device)."""
+    """Iterate host batches as device tensors, ``depth`` batches ahead (tf.data prefetch_to_device).
 
-    def __init__(self, source: Iterable, device, depth: int = 2):
+    Lifetime: on a GPU the yielded tensors ARE the ring's device slot.  Work enqueued on the current
+    stream before the iterator advances may read them; the slot is released at the next step and
+    overwritten ``depth`` + 1 batches later, so a batch kept beyond its step (e.g. for evaluation at
+    the end of an epoch) must be copied -- ``copy=True`` yields a private clone of every batch
+    (one device-to-device copy per tensor, made on the current stream)."""
+
+    def __init__(self, source: Iterable, device, depth: int = 2, copy: bool = False):
         self.source = source
         self.ring = PinnedRing(device, depth)
         self.depth = max(1, depth)
+        self.copy = bool(copy)
 
     def __iter__(self) -> Iterator:
         it = iter(self.source)
@@ -199,6 +206,8 @@ class DevicePrefetcher:
         while q:
             k = q.pop(0)
             out = self.ring.acquire(k)
+            if self.copy:
+                out = tuple(t.clone() for t in out)
             try:
                 b = next(it)
                 single = not isinstance(b, (tuple, list))

@@ -29,7 +29,9 @@ def _shapes(B=256):
     return out
 
 
-SHAPES = _shapes()
+# batch 256 (bench.py's default) and 128 (a second per-GPU batch: a non-256 ``--batch`` must not
+# reach a tile / ring pick that no test ran)
+SHAPES = _shapes(256) + _shapes(128)
 
 
 def _bf(t):

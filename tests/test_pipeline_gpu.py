@@ -150,3 +150,12 @@ def test_fused_augment_normalize_matches_two_step(gpu):
     assert torch.equal(fused, ref)
     cpu = augment_model_input(img.cpu(), dtype=torch.float32, offsets=off.cpu())  # the CPU reference path
     assert (cpu - fused.float().cpu()).abs().max().item() < 2e-2
+
+
+def test_prefetcher_copy_keeps_batches(gpu):
+    """copy=True: batches held past their step keep their values (the ring slots are overwritten)."""
+    batches = _host_batches(8)
+    kept = [x for x, _ in DevicePrefetcher(batches, gpu, depth=2, copy=True)]
+    torch.cuda.synchronize()
+    for i, x in enumerate(kept):
+        assert float(x.mean()) == float(i)
