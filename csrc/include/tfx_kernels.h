@@ -130,6 +130,24 @@ struct PwExpandArgs {
   float* slots_sc = nullptr;
   int M = 0, CN = 0;
 };
+// Fused block tail + next squeezing 1x1 conv forward (pw_fwd.hip): out = relu(y3 sc3 + sh3 + res')
+// (res' = res, or res * sc_r + sh_r when save_r is set: a never-written shortcut BN output), out and its
+// mask bits stored, y1 = out . W1^T stored with BN1's statistics added into slots1 [NSLOT][2][CO].
+struct PwSqueezeArgs {
+  const uint16_t* y3 = nullptr;    // [M][CI] tail BN input
+  const float* save3 = nullptr;    // [4][CI]
+  const uint16_t* res = nullptr;   // [M][CI] residual (or the shortcut BN's input)
+  const float* save_r = nullptr;   // [4][CI] shortcut BN (null: plain residual)
+  const uint16_t* w = nullptr;     // [CO][CI]
+  uint16_t* out = nullptr;         // [M][CI]
+  uint8_t* mask = nullptr;         // [M][CI / 8]
+  uint16_t* y1 = nullptr;          // [M][CO]
+  float* slots1 = nullptr;         // [NSLOT][2][CO]
+  int M = 0, CI = 0, CO = 0;
+};
+bool pw_fwd_squeeze_ok(int CI, int CO, int64_t M);
+int pw_fwd_squeeze_grid(int64_t M);
+void pw_fwd_squeeze(const PwSqueezeArgs& args, int nblocks, hipStream_t s);
 // the shortcut BN's reduction in pw_slab_reduce's tail (C = 0: none): red = [red3's sum g' | sum q]
 struct PwSecReduce {
   float* slots = nullptr;

@@ -263,6 +263,58 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   return {y, save};
 }
 
+// Block tail + the next block's conv1 (1x1, CI -> CO) forward in one launch (pw_fwd.hip): writes the
+// tail's output `out` and ReLU mask bits into the given buffers (allocated by the tail BN, which
+// deferred its apply), then finalizes BN1 from the epilogue statistics as conv_fwd_bn does.
+// res_save set: the residual is a never-written shortcut BN output (res = its input).  Returns (y1, save1).
+std::tuple<Tensor, Tensor> pw_fwd_squeeze(Tensor y3, Tensor save3, Tensor res, optional<Tensor> res_save, Tensor w,
+                                          Tensor out, Tensor mask, Tensor ws, optional<Tensor> gamma,
+                                          optional<Tensor> beta, optional<Tensor> run_mean,
+                                          optional<Tensor> run_var, double momentum, double eps) {
+  CHECK_DEV(y3); CHECK_BF16(y3); CHECK_CONTIG(y3); CHECK_BF16(res); CHECK_CONTIG(res); CHECK_BF16(w);
+  CHECK_CONTIG(w); CHECK_BF16(out); CHECK_CONTIG(out); CHECK_F32(save3);
+  const int64_t CI = y3.size(-1), CO = w.size(0), M = y3.numel() / CI;
+  TORCH_CHECK(w.numel() == CO * CI && res.numel() == M * CI && out.numel() == M * CI && save3.numel() == 4 * CI,
+              "pw_fwd_squeeze: shapes");
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.is_contiguous() && mask.numel() * 8 == M * CI, "pw_fwd_squeeze: mask");
+  TORCH_CHECK(tfx::pw_fwd_squeeze_ok((int)CI, (int)CO, M), "pw_fwd_squeeze: unsupported widths / rows");
+  check_bn_ws(ws, CO);
+  std::vector<int64_t> ysh = y3.sizes().vec();
+  ysh.back() = CO;
+  auto y1 = at::empty(ysh, y3.options());
+  auto save = at::empty({4 * CO}, y3.options().dtype(at::kFloat));
+  tfx::PwSqueezeArgs a;
+  a.y3 = bf(y3); a.save3 = save3.data_ptr<float>(); a.res = bf(res); a.w = bf(w); a.out = bfm(out);
+  a.mask = mask.data_ptr<uint8_t>(); a.y1 = bfm(y1); a.slots1 = ws.data_ptr<float>();
+  a.M = (int)M; a.CI = (int)CI; a.CO = (int)CO;
+  if (res_save.has_value() && res_save->defined()) {
+    CHECK_F32(*res_save);
+    TORCH_CHECK(res_save->numel() == 4 * CI, "pw_fwd_squeeze: res_save");
+    a.save_r = res_save->data_ptr<float>();
+  }
+  tfx::pw_fwd_squeeze(a, tfx::pw_fwd_squeeze_grid(M), cur_stream());
+  tfx::bn_finalize(a.slots1, M, (int)CO, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
+                   fpm(run_var), save.data_ptr<float>(), cur_stream());
+  return {y1, save};
+}
+
+bool pw_fwd_squeeze_supported(int64_t CI, int64_t CO, int64_t M) { return tfx::pw_fwd_squeeze_ok((int)CI, (int)CO, M); }
+
+// tail apply into caller-provided buffers (the fallback of a deferred tail whose consumer could
+// not fuse it): out = relu(x sc + sh + res'), mask bits
+void bn_apply_into(Tensor x, Tensor res, Tensor save, optional<Tensor> res_save, Tensor out, Tensor mask) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(res); CHECK_CONTIG(res); CHECK_BF16(out); CHECK_CONTIG(out);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(res.numel() == x.numel() && out.numel() == x.numel() && mask.numel() * 8 == x.numel() && C % 8 == 0,
+              "bn_apply_into: shapes");
+  if (res_save.has_value() && res_save->defined())
+    tfx::bn_apply_res_bn(bf(x), bf(res), save.data_ptr<float>(), res_save->data_ptr<float>(), M, (int)C, true,
+                         bfm(out), mask.data_ptr<uint8_t>(), cur_stream());
+  else
+    tfx::bn_apply(bf(x), bf(res), save.data_ptr<float>(), M, (int)C, true, bfm(out), mask.data_ptr<uint8_t>(),
+                  cur_stream());
+}
+
 // stride-1 conv data gradient whose epilogue also reduces the backward of the BN that produced
 // the conv's input (the gradient written here is that BN's complete output gradient): returns
 // (dx, red = [sum g' | sum g' xhat]) with dgamma / dbeta accumulated -- the BN then only applies
@@ -1471,6 +1523,9 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_nslot", &bn_nslot);
   m.def("pw_bwd_expand", &pw_bwd_expand);
   m.def("pw_bwd_expand_supported", &pw_bwd_expand_supported);
+  m.def("pw_fwd_squeeze", &pw_fwd_squeeze);
+  m.def("pw_fwd_squeeze_supported", &pw_fwd_squeeze_supported);
+  m.def("bn_apply_into", &bn_apply_into);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd(Tensor g, Tensor x, Tensor? res, Tensor save, bool relu, Tensor slots, Tensor? dgamma, "
         "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);

@@ -50,25 +50,28 @@ class _BN:
         self.ws = BNWorkspace(c)
 
     def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None, ws_obj=False,
-                 residual_is_bn=False, defer_output=False, lazy_backward=False):
+                 residual_is_bn=False, defer_output=False, lazy_backward=False, defer_apply=False):
         ws = (self.ws if ws_obj else self.ws.get(x.device)) if x.device.type == "cuda" else None
         return ops.batch_norm(x, self.gamma, self.beta, self.mean, self.var, training=training, momentum=0.1,
                               eps=1e-5, residual=residual, relu=relu, workspace=ws, stats_ready=stats_ready,
                               residual_grad_sink=residual_sink, fuse_residual_bn_backward=residual_is_bn,
-                              defer_output=defer_output, lazy_backward=lazy_backward)
+                              defer_output=defer_output, lazy_backward=lazy_backward, defer_apply=defer_apply)
 
     def after_conv(self, conv, x, training, relu=False, residual=None, sink=None, residual_sink=None,
-                   fuse_input_bn_backward=False, residual_is_bn=False, defer_output=False):
+                   fuse_input_bn_backward=False, residual_is_bn=False, defer_output=False, defer_apply=False):
         """conv -> BN with the BN statistics produced (and, with _FUSE_BN, finalized) by the conv's
         epilogue (GPU, training).  ``fuse_input_bn_backward``: the conv's data gradient is the
         complete gradient of ``x`` -- reduce x's producing BN's backward in its epilogue.  The BN's
-        input gradient may reach ``conv`` unmaterialised (ops.nn.LazyBNGrad): it is its only producer."""
+        input gradient may reach ``conv`` unmaterialised (ops.nn.LazyBNGrad): it is its only producer.
+        ``defer_apply``: the output's first reader is the next bottleneck's conv1, which applies this
+        (tail) BN while loading it (ops.nn.TailPending)."""
         fused = training and x.device.type == "cuda"
         if fused and _FUSE_BN:
             self.ws.finalize_args = (self.gamma.master, self.beta.master, self.mean, self.var, 0.1, 1e-5)
             y = conv(x, self.ws, sink, fuse_input_bn_backward and _FUSE_BN)
             return self(y, training, relu=relu, residual=residual, stats_ready=True, residual_sink=residual_sink,
-                        ws_obj=True, residual_is_bn=residual_is_bn, defer_output=defer_output, lazy_backward=True)
+                        ws_obj=True, residual_is_bn=residual_is_bn, defer_output=defer_output, lazy_backward=True,
+                        defer_apply=defer_apply)
         y = conv(x, self.ws.get(x.device) if fused else None, sink)
         return self(y, training, relu=relu, residual=residual, stats_ready=fused, residual_sink=residual_sink,
                     residual_is_bn=residual_is_bn)
@@ -101,7 +104,9 @@ class Bottleneck:
                 self.proj = _Conv(store, cin, cout, 1, stride, "shortcut")
                 self.bp = _BN(store, cout, "shortcut_bn")
 
-    def __call__(self, x, training):
+    def __call__(self, x, training, defer_tail=False):
+        # defer_tail: the output feeds the next bottleneck, whose conv1 runs first -- that conv applies
+        # this block's tail BN while loading its input (pw_fwd.hip)
         # x feeds conv1 and the shortcut: the shortcut's input-gradient is folded into conv1's
         # dgrad epilogue (GradSink) instead of an autograd add kernel
         prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
@@ -115,12 +120,12 @@ class Bottleneck:
         o3_fuse = True
         if self.proj is None:
             return self.b3.after_conv(self.c3, o, training, relu=True, residual=x, residual_sink=prod,
-                                      fuse_input_bn_backward=o3_fuse)
+                                      fuse_input_bn_backward=o3_fuse, defer_apply=defer_tail)
         # sc (the shortcut BN's output) is used only as the tail's residual: never written (the tail
         # normalizes the shortcut conv's output on the fly), and its BN backward rides along
         sc = self.bp.after_conv(self.proj, x, training, sink=prod, defer_output=True)
         return self.b3.after_conv(self.c3, o, training, relu=True, residual=sc, fuse_input_bn_backward=o3_fuse,
-                                  residual_is_bn=True)
+                                  residual_is_bn=True, defer_apply=defer_tail)
 
 
 class Basic:
@@ -179,8 +184,12 @@ class ResNetCifar:
 
     def __call__(self, x: torch.Tensor, training: bool = True) -> torch.Tensor:
         o = self.stem_bn.after_conv(self.stem, x, training, relu=True)
-        for blk in self.blocks:
-            o = blk(o, training)
+        for i, blk in enumerate(self.blocks):
+            if isinstance(blk, Bottleneck):
+                nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+                o = blk(o, training, defer_tail=isinstance(nxt, Bottleneck))
+            else:
+                o = blk(o, training)
         f = ops.global_avg_pool(o)
         return ops.linear(f, self.fc_w, self.fc_b)
 

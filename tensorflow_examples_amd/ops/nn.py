@@ -127,6 +127,46 @@ class LazyBNGrad:
         return self.dy
 
 
+# test hook: False keeps every block tail applied by its own pass (the layer-wise forward)
+_DEFER_TAIL = True
+PW_SQUEEZE_CALLS = [0]  # fused tail + conv1 forward launches (tests)
+
+
+class TailPending:
+    """A residual + ReLU batch norm's output whose apply pass was deferred to its consumer (the next
+    bottleneck's conv1): ``out`` (and the ReLU ``mask`` bits the backward saved) are allocated but
+    not yet written.  The consumer conv forms them while it loads its input (pw_fwd_squeeze, one
+    launch), or calls :meth:`materialize` (bn_apply_into).  Everything that reads ``out`` runs after
+    that conv in the block's forward order (the tail's residual use, the projection shortcut)."""
+    __slots__ = ("x", "save", "res", "res_save", "out", "mask", "done")
+
+    def __init__(self, x, save, res, res_save, out, mask):
+        self.x, self.save, self.res, self.res_save, self.out, self.mask = x, save, res, res_save, out, mask
+        self.done = False
+
+    def materialize(self) -> None:
+        if not self.done:
+            torch.ops.tfx.bn_apply_into(self.x, self.res, self.save, self.res_save, self.out, self.mask)
+            self.done = True
+
+
+def _settle(t):
+    """Write a deferred block-tail output before anything but its fused consumer reads it."""
+    tp = getattr(t, "_tfx_tail", None) if t is not None else None
+    if tp is not None and not tp.done:
+        tp.materialize()
+    return t
+
+
+def _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into) -> bool:
+    """Can this conv's forward run fused with the deferred tail ``tp`` of its input (pw_fwd.hip)?"""
+    sh = w.shape
+    if not (stride == 1 and pad == 0 and dil == 1 and isinstance(stats_into, BNWorkspace) and len(sh) == 4
+            and sh[1] == 1 and sh[2] == 1 and sh[3] == x.shape[-1] and x.is_contiguous()):
+        return False
+    return bool(torch.ops.tfx.pw_fwd_squeeze_supported(sh[3], sh[0], x.numel() // sh[3]))
+
+
 def _pw_expand_ok(x, w, stride, pad, dil, lazy, sink) -> bool:
     """Can this conv's backward run as the fused expanding-1x1 kernel (pw_bwd.hip) on ``lazy``?"""
     sh = w.shape
@@ -149,6 +189,18 @@ class _Conv2d(torch.autograd.Function):
         if ctx.native:
             if _flip_ok(w, stride, pad, dil):
                 w.store.flip_stale = True  # the weights may have changed since the last refresh
+            tp = getattr(x, "_tfx_tail", None)
+            if tp is not None and not tp.done:
+                if _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into):
+                    # the previous block's tail apply + this conv + its BN statistics in one launch:
+                    # x (and the tail's mask bits) are written here (pw_fwd.hip)
+                    ws = stats_into
+                    y, ws.pending_save = torch.ops.tfx.pw_fwd_squeeze(
+                        tp.x, tp.save, tp.res, tp.res_save, w.value, x, tp.mask, ws.get(x.device), *ws.finalize_args)
+                    tp.done = True
+                    PW_SQUEEZE_CALLS[0] += 1
+                    return y
+                tp.materialize()
             if isinstance(stats_into, BNWorkspace):
                 ws = stats_into
                 # epilogue statistics, then the finalize: the BN only applies
@@ -462,7 +514,7 @@ def _res_bn_sec_ok(ctx, gy, mask, relu, masked):
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, anchor, gamma: Optional[Variable], beta: Optional[Variable], rm, rv, momentum, eps, relu,
-                training, ws, stats_ready, res_sink, wsobj, bnb_out, res_bnb, defer, lazy_bwd):
+                training, ws, stats_ready, res_sink, wsobj, bnb_out, res_bnb, defer, lazy_bwd, defer_apply):
         # res_bnb: (BNBackwardFusion of the residual, fuse its backward here); defer: the output is
         # only ever this layer's consumer's residual -- never written (see batch_norm); lazy_bwd: the
         # input gradient may be returned unmaterialised (LazyBNGrad) -- the producer is a conv
@@ -488,15 +540,25 @@ class _BatchNorm(torch.autograd.Function):
             # residual = a BN output that was never written: normalize its input on the fly here
             # (bn_apply_res_bn), or materialize it for the other paths (autograd still routes its
             # gradient to that BN: the lazy tensor stays this Function's input)
+            _settle(res)
             res_lazy = res is not None and res_bnb is not None and res_bnb.deferred
             fuse_res = res_lazy and pending and relu
+            # residual + ReLU tail whose only first reader is the next block's conv1: leave the apply
+            # to that conv (TailPending) -- it forms out / mask while loading its input
+            defer_tail = defer_apply and _DEFER_TAIL and pending and relu and res is not None and \
+                x.shape[-1] % 8 == 0 and (fuse_res or not res_lazy)
             if res_lazy and not fuse_res:
                 res = torch.ops.tfx.bn_apply_train(res_bnb.x, None, res_bnb.save, False)[0]
             defer_out = defer and pending and res is None and bnb_out is not None and _vec_ok(x.shape[-1])
             if pending:
                 # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
                 save, wsobj.pending_save = wsobj.pending_save, None
-                if fuse_res:
+                if defer_tail:
+                    y = torch.empty_like(x)
+                    mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
+                    y._tfx_tail = TailPending(x, save, res_bnb.x if fuse_res else res.contiguous(),
+                                              res_bnb.save if fuse_res else None, y, mask)
+                elif fuse_res:
                     y, mask = torch.ops.tfx.bn_apply_res_bn(x, res_bnb.x, save, res_bnb.save, relu)
                 elif defer_out:
                     y = _zero_scalar(x.dtype, x.device).expand(x.shape)
@@ -604,7 +666,7 @@ class _BatchNorm(torch.autograd.Function):
                 ctx.res_sink.put((gy, mask) if masked else dres)
                 dres = None
             return dx, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None, None, \
-                None, None, None, None, None, None
+                None, None, None, None, None, None, None
         x, res = ctx.saved_tensors
         with torch.enable_grad():
             xs = x.detach().requires_grad_(True)
@@ -619,14 +681,15 @@ class _BatchNorm(torch.autograd.Function):
             gamma.grad.add_(grads[0])
             beta.grad.add_(grads[1])
             _grad_ready(gamma, beta)
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None, \
+            None
 
 
 def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_mean, running_var, training=True,
                momentum=0.1, eps=1e-5, residual: Optional[torch.Tensor] = None, relu=False,
                workspace=None, stats_ready: bool = False,
                residual_grad_sink: Optional[GradSink] = None, fuse_residual_bn_backward: bool = False,
-               defer_output: bool = False, lazy_backward: bool = False):
+               defer_output: bool = False, lazy_backward: bool = False, defer_apply: bool = False):
     """Channels-last batch norm over all leading dims, with optional fused residual add + ReLU:
     ``y = relu(bn(x) + residual)`` (the ResNet bottleneck tail in one pass).
 
@@ -645,7 +708,11 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
     normalizes this BN's input on the fly.
 
     ``lazy_backward``: the caller promises ``x`` is the output of :func:`conv2d` (used nowhere else),
-    so the input gradient may reach it unmaterialised (:class:`LazyBNGrad`)."""
+    so the input gradient may reach it unmaterialised (:class:`LazyBNGrad`).
+
+    ``defer_apply`` (a residual + ReLU tail): the caller promises the output's FIRST reader is a
+    1x1 :func:`conv2d` with a BN workspace (the next bottleneck's conv1); on the fused GPU path the
+    apply pass is left to that conv (:class:`TailPending`), which writes the output while loading it."""
     anchor = gamma.store.anchor if gamma is not None else None
     wsobj = workspace if isinstance(workspace, BNWorkspace) else None
     if wsobj is not None:
@@ -660,7 +727,7 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
         res_bnb = (rb, bool(fuse_residual_bn_backward))
     y = _BatchNorm.apply(x, residual, anchor, gamma, beta, running_mean, running_var, momentum, eps, relu, training,
                          workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out, res_bnb,
-                         bool(defer_output), bool(lazy_backward))
+                         bool(defer_output), bool(lazy_backward), bool(defer_apply))
     if bnb_out:
         y._tfx_bnb = bnb_out[0]
     return y
