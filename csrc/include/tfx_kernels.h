@@ -162,8 +162,31 @@ bool pw_bwd_expand_ok(int CN, int64_t M);
 int pw_bwd_expand_grid(int CN, int64_t M);
 void pw_bwd_expand(const PwExpandArgs& args, int nblocks, hipStream_t s);
 // dw[CW][CN] += sum of nslab slabs; + optional BN slot reduction (bn_slot_reduce's math) in tail blocks
+// map: 0 = pw_bwd_expand's slab (dW3), 1 = pw_bwd_squeeze's (dW1, CO = CN, CI = 4 CN)
 void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_slots, int sr_C, float* sr_red,
-                    float* sr_dgamma, float* sr_dbeta, const PwSecReduce& sec, hipStream_t s);
+                    float* sr_dgamma, float* sr_dbeta, const PwSecReduce& sec, hipStream_t s, int map = 0);
+// Fused backward of an identity bottleneck's squeezing 1x1 conv1 with BN1's backward apply
+// (pw_bwd.hip F1): dx = T1 . W1 + addend * amask, the previous tail BN's partials into pslots, the
+// weight gradient into per-block slabs (pw_slab_reduce map 1).
+struct PwSqueezeBwdArgs {
+  const uint16_t* g1 = nullptr;    // [M][CO] BN1 output gradient
+  const uint16_t* y1 = nullptr;    // [M][CO] BN1 input
+  const float* save1 = nullptr;    // [4][CO]
+  const float* red1 = nullptr;     // [2][CO] BN1 backward reduction
+  const uint16_t* x = nullptr;     // [M][CI] conv1 input
+  const uint16_t* w = nullptr;     // [CO][CI]
+  const uint16_t* addend = nullptr;  // [M][CI] residual branch gradient (unmasked)
+  const uint8_t* amask = nullptr;  // its ReLU mask bits
+  const uint16_t* px = nullptr;    // [M][CI] previous tail BN input
+  const float* psave = nullptr;    // [4][CI]
+  const uint8_t* pmask = nullptr;  // previous tail ReLU mask bits
+  float* pslots = nullptr;         // [NSLOT][2][CI]
+  uint16_t* dx = nullptr;          // [M][CI]
+  float* slab = nullptr;           // [grid][CO * CI]
+  int M = 0, CI = 0, CO = 0;
+};
+bool pw_bwd_squeeze_ok(int CI, int CO, int64_t M);
+void pw_bwd_squeeze(const PwSqueezeBwdArgs& args, int nblocks, hipStream_t s);
 
 // ---------------------------------------------------------------- f32 GEMM (MFMA f32, exact)
 // C[M][N] = act(alpha * op(A) op(B) + bias) (+ C if accumulate); op = transpose flags

@@ -312,6 +312,269 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
   }
 }
 
+// ---------------------------------------------------------------------------------- F1 (squeeze)
+// Backward of an identity bottleneck's SQUEEZING 1x1 conv1 (CI wide -> CO narrow) fused with BN1's
+// backward apply.  Layer-wise: bn_bwd_apply (dy1, narrow), conv1 dgrad (dx, wide: + the residual
+// branch's masked gradient + the previous tail BN's backward partials in its epilogue), conv1 wgrad.
+// Here per 32-row m-tile:
+//   T1 = A1 (g1 * relu1) + B1 y1 + D1        (relu1 from y1 sc1 + sh1 > 0; bf16, LDS only)
+//   dgrad  dx [32 x CI] = T1 . W1 + addend * amask     (W1 resident as an MN image: rows = co)
+//          epilogue: dx stored; previous tail BN partials (sum g', sum g' xhat), g' = bf16(dx) * pmask
+//   wgrad  dW1 [CO x CI] += T1^T . X                   (X = conv1's input tile, MN image)
+// dy1 never exists in HBM and dx's tensors are read once: the launch moves g1, y1, X, the addend and
+// its mask, the previous tail's input and mask, and writes dx (ResNet-50/CIFAR stage 1: ~610 MB).
+template <int CI, int CO>
+struct PwSqueezeBwdCfg {
+  static constexpr int NTPR = CO / 4;                  // threads per narrow row (8-B pieces)
+  static constexpr int T_BYTES = PW_BM * CO * 2;       // T1 tile, K-major 64-channel rows
+  static constexpr int X_BYTES = PW_BM * CI * 2;       // X tile, MN image
+  static constexpr int SLOT = T_BYTES + X_BYTES;
+  static constexpr int W_BYTES = CO * CI * 2;          // W1 MN image (rows = co), resident
+  static constexpr int XLD = PW_BM * CI / 8 / PW_NT;   // X 16-B pieces per thread per tile
+  static constexpr int DCOLS = CI / 4;                 // dgrad columns per wave (2 row x 4 col groups)
+  static constexpr int DTN = DCOLS / 16;
+  static constexpr int WROWS = CO / 2;                 // wgrad: co rows per wave (2 groups)
+  static constexpr int WTM = WROWS / 16;
+  static constexpr int WCOLS = CI / 4;                 // wgrad: ci columns per wave (4 groups)
+  static constexpr int WTN = WCOLS / 16;
+  static_assert(CO == 64, "T1 is one 64-channel K-major chunk");
+  static_assert(PW_BM * NTPR == PW_NT, "narrow tile mapping");
+  static_assert(XLD >= 1 && PW_BM * CI / 8 % PW_NT == 0, "wide tile mapping");
+  static_assert(2 * SLOT + W_BYTES <= 160 * 1024, "LDS budget");
+};
+
+template <int CI, int CO>
+__global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdArgs a) {
+  using C = PwSqueezeBwdCfg<CI, CO>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::SLOT + C::W_BYTES + 2 * CI * 4 + 5 * CO * 4];
+  char* wimg = smem + 2 * C::SLOT;
+  // previous tail BN's [invstd | -mean invstd] per wide channel, read by the dgrad epilogue
+  float* pcoef = reinterpret_cast<float*>(smem + 2 * C::SLOT + C::W_BYTES);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int ntiles = a.M / PW_BM;
+
+  // ---- narrow piece of this thread (fixed channels nc0 .. nc0 + 3); BN1 backward coefficients
+  // [A | B | D | scale | shift] per narrow channel in LDS (registers go to the accumulators)
+  const int nrow = t / C::NTPR, nc0 = 4 * (t % C::NTPR);
+  float* ncoef = pcoef + 2 * CI;
+  if (t < CO) {
+    const float inv_m = 1.f / (float)a.M;
+    const float mu = a.save1[t], is = a.save1[CO + t], sc = a.save1[2 * CO + t];
+    const float kg = a.red1[t] * inv_m, kx = a.red1[CO + t] * inv_m * is;
+    ncoef[t] = sc;
+    ncoef[CO + t] = -sc * kx;
+    ncoef[2 * CO + t] = sc * (kx * mu - kg);
+    ncoef[3 * CO + t] = sc;
+    ncoef[4 * CO + t] = a.save1[3 * CO + t];
+  }
+  for (int c = t; c < CI; c += PW_NT) {
+    const float is = a.psave[CI + c];
+    pcoef[c] = is;
+    pcoef[CI + c] = -a.psave[c] * is;
+  }
+  // ---- W1 [CO][CI] -> MN image (row = co), resident
+  for (int q = t; q < CO * CI / 8; q += PW_NT) {
+    const int co = q / (CI / 8), cc = q % (CI / 8);
+    *reinterpret_cast<pw_u32x4*>(wimg + pw_mn<CI>(co, cc)) = *reinterpret_cast<const pw_u32x4*>(a.w + (int64_t)co * CI + 8 * cc);
+  }
+  const int64_t wide = (int64_t)a.M * CI * 2, narrow = (int64_t)a.M * CO * 2;
+  const __amdgpu_buffer_rsrc_t rg = pw_rsrc(a.g1, narrow), ry = pw_rsrc(a.y1, narrow), rx = pw_rsrc(a.x, wide);
+  const __amdgpu_buffer_rsrc_t rad = pw_rsrc(a.addend, wide), ram = pw_rsrc(a.amask, (int64_t)a.M * CI / 8);
+  const __amdgpu_buffer_rsrc_t rpx = pw_rsrc(a.px, wide), rpm = pw_rsrc(a.pmask, (int64_t)a.M * CI / 8);
+  const __amdgpu_buffer_rsrc_t rdx = pw_rsrc(a.dx, wide);
+
+  // dgrad wave tile: rows 16 (wv & 1), columns DCOLS (wv >> 1); SWAP -> lane holds row (lane & 15),
+  // columns dcb + 16 j + (lane >> 4) * 4 + r
+  const int drb = 16 * (wv & 1), dcb = C::DCOLS * (wv >> 1);
+  const int hsel = 4 * ((lane >> 4) & 1);  // this lane's 4 columns within their mask byte
+  float bs[C::DTN][4], bq[C::DTN][4];  // previous tail BN partials, whole launch
+#pragma unroll
+  for (int j = 0; j < C::DTN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs[j][r] = bq[j][r] = 0.f;
+  // wgrad wave tile: co rows WROWS (wv & 1), ci columns WCOLS (wv >> 1); !SWAP
+  const int wrb = C::WROWS * (wv & 1), wcb = C::WCOLS * (wv >> 1);
+  f32x4_t accw[C::WTM][C::WTN];
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int n = 0; n < C::WTN; ++n) accw[i][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // ---- staging: narrow g1 / y1 + the X tile two tiles ahead; the dgrad epilogue operands (addend,
+  // its mask, the previous tail's input and mask) one tile ahead in a single register set
+  struct Stage {
+    pw_u32x2 g, y;
+    pw_u32x4 x[C::XLD];
+  };
+  Stage st0, st1;
+  pw_u32x2 ead[C::DTN], epx[C::DTN];
+  uint32_t emk[C::DTN];  // addend mask byte | previous mask byte << 8
+  const int tile0 = blockIdx.x, tstep = gridDim.x;
+  auto issue = [&](Stage& s, int tile) {
+    const bool ok = tile < ntiles;
+    const int row = tile * PW_BM + nrow;
+    const uint32_t no = ok ? (uint32_t)(row * CO + nc0) * 2u : 0x80000000u;
+    s.g = __builtin_amdgcn_raw_buffer_load_b64(rg, no, 0, 0);
+    s.y = __builtin_amdgcn_raw_buffer_load_b64(ry, no, 0, 0);
+#pragma unroll
+    for (int i = 0; i < C::XLD; ++i) {
+      const int q = t + PW_NT * i, xr = tile * PW_BM + q / (CI / 8), xc = q % (CI / 8);
+      s.x[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? (uint32_t)(xr * CI + 8 * xc) * 2u : 0x80000000u, 0, 0);
+    }
+  };
+  auto issue_ep = [&](int tile) {
+    const bool ok = tile < ntiles;
+    const int row = tile * PW_BM + drb + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < C::DTN; ++j) {
+      const int col = dcb + 16 * j + (lane >> 4) * 4;
+      const uint32_t o = ok ? (uint32_t)(row * CI + col) * 2u : 0x80000000u;
+      const uint32_t ob = ok ? (uint32_t)(row * CI + col) / 8u : 0x80000000u;
+      ead[j] = __builtin_amdgcn_raw_buffer_load_b64(rad, o, 0, 0);
+      epx[j] = __builtin_amdgcn_raw_buffer_load_b64(rpx, o, 0, 0);
+      emk[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(ram, ob, 0, 0) |
+               ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rpm, ob, 0, 0) << 8);
+    }
+  };
+  auto stage = [&](const Stage& s, char* slot) {
+    float gf[4], yf[4], o[4];
+    const float4 A4 = *reinterpret_cast<const float4*>(ncoef + nc0);
+    const float4 B4 = *reinterpret_cast<const float4*>(ncoef + CO + nc0);
+    const float4 D4 = *reinterpret_cast<const float4*>(ncoef + 2 * CO + nc0);
+    const float4 S4 = *reinterpret_cast<const float4*>(ncoef + 3 * CO + nc0);
+    const float4 H4 = *reinterpret_cast<const float4*>(ncoef + 4 * CO + nc0);
+    const float A[4] = {A4.x, A4.y, A4.z, A4.w}, B[4] = {B4.x, B4.y, B4.z, B4.w}, D[4] = {D4.x, D4.y, D4.z, D4.w};
+    const float sc[4] = {S4.x, S4.y, S4.z, S4.w}, sh[4] = {H4.x, H4.y, H4.z, H4.w};
+    gf[0] = __uint_as_float(s.g[0] << 16); gf[1] = __uint_as_float(s.g[0] & 0xffff0000u);
+    gf[2] = __uint_as_float(s.g[1] << 16); gf[3] = __uint_as_float(s.g[1] & 0xffff0000u);
+    yf[0] = __uint_as_float(s.y[0] << 16); yf[1] = __uint_as_float(s.y[0] & 0xffff0000u);
+    yf[2] = __uint_as_float(s.y[1] << 16); yf[3] = __uint_as_float(s.y[1] & 0xffff0000u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gg = fmaf(yf[k], sc[k], sh[k]) > 0.f ? gf[k] : 0.f;
+      o[k] = fmaf(A[k], gg, fmaf(B[k], yf[k], D[k]));
+    }
+    const int c16 = nc0 >> 3;  // 16-B chunk of the 128-B row, 8-B half (nc0 >> 2) & 1
+    *reinterpret_cast<pw_u32x2*>(slot + pw_kmaj(nrow, c16) + ((nc0 >> 2) & 1) * 8) =
+        (pw_u32x2){pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+#pragma unroll
+    for (int i = 0; i < C::XLD; ++i) {
+      const int q = t + PW_NT * i;
+      *reinterpret_cast<pw_u32x4*>(slot + C::T_BYTES + pw_mn<CI>(q / (CI / 8), q % (CI / 8))) = s.x[i];
+    }
+  };
+  auto compute = [&](const char* slot, int tile) {
+    // dgrad: acc_d[32 x CI] = T1[32 x CO] . W1
+    f32x4_t accd[C::DTN];
+#pragma unroll
+    for (int j = 0; j < C::DTN; ++j) accd[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < CO / 32; ++kc) {
+      const bf16x8_t fa = pw_frag_kmaj(slot, 0, drb, 4 * kc, lane);
+#pragma unroll
+      for (int j = 0; j < C::DTN; ++j) {
+        const bf16x8_t fb = pw_frag_tr(wimg, 32 * kc * CI * 2, dcb + 16 * j, lane,
+                                       [](int r, int c) { return pw_mn<CI>(r, c); });
+        accd[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, accd[j], 0, 0, 0);  // SWAP
+      }
+    }
+    // wgrad: acc_w[CO x CI] += T1^T . X (k = the tile's 32 rows)
+    bf16x8_t fx[C::WTN];
+#pragma unroll
+    for (int n = 0; n < C::WTN; ++n)
+      fx[n] = pw_frag_tr(slot + C::T_BYTES, 0, wcb + 16 * n, lane, [](int r, int c) { return pw_mn<CI>(r, c); });
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) {
+      const bf16x8_t ft = pw_frag_tr(slot, 0, wrb + 16 * i, lane, [](int r, int c) { return pw_kmaj(r, c); });
+#pragma unroll
+      for (int n = 0; n < C::WTN; ++n) accw[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft, fx[n], accw[i][n], 0, 0, 0);
+    }
+    // dgrad epilogue: + masked addend -> dx (bf16, 8-byte stores); previous tail BN partials
+    const int row = tile * PW_BM + drb + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < C::DTN; ++j) {
+      const int col = dcb + 16 * j + (lane >> 4) * 4;
+      const uint32_t ab = (emk[j] >> hsel) & 0xfu, pb = (emk[j] >> (8 + hsel)) & 0xfu;
+      const float ad[4] = {__uint_as_float(ead[j][0] << 16), __uint_as_float(ead[j][0] & 0xffff0000u),
+                           __uint_as_float(ead[j][1] << 16), __uint_as_float(ead[j][1] & 0xffff0000u)};
+      const float xv[4] = {__uint_as_float(epx[j][0] << 16), __uint_as_float(epx[j][0] & 0xffff0000u),
+                           __uint_as_float(epx[j][1] << 16), __uint_as_float(epx[j][1] & 0xffff0000u)};
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = accd[j][r] + (((ab >> r) & 1u) ? ad[r] : 0.f);
+      const uint32_t lo = pack_bf16x2(v[0], v[1]), hi = pack_bf16x2(v[2], v[3]);
+      __builtin_amdgcn_raw_buffer_store_b64((pw_u32x2){lo, hi}, rdx, (uint32_t)(row * CI + col) * 2u, 0, 0);
+      const float gv[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u), __uint_as_float(hi << 16),
+                           __uint_as_float(hi & 0xffff0000u)};
+      const float4 pi4 = *reinterpret_cast<const float4*>(pcoef + col);
+      const float4 pn4 = *reinterpret_cast<const float4*>(pcoef + CI + col);
+      const float pis[4] = {pi4.x, pi4.y, pi4.z, pi4.w}, pnm[4] = {pn4.x, pn4.y, pn4.z, pn4.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gp = ((pb >> r) & 1u) ? gv[r] : 0.f;
+        bs[j][r] += gp;
+        bq[j][r] = fmaf(gp, fmaf(xv[r], pis[r], pnm[r]), bq[j][r]);
+      }
+    }
+    issue_ep(tile + tstep);
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  issue(st0, tile0);
+  issue(st1, tile0 + tstep);
+  issue_ep(tile0);
+  __syncthreads();  // W1 image written
+  for (int tile = tile0; tile < ntiles; tile += 2 * tstep) {
+    stage(st0, smem);
+    issue(st0, tile + 2 * tstep);
+    sync();
+    compute(smem, tile);
+    const int t1 = tile + tstep;
+    if (t1 >= ntiles) break;
+    stage(st1, smem + C::SLOT);
+    issue(st1, t1 + 2 * tstep);
+    sync();
+    compute(smem + C::SLOT, t1);
+  }
+
+  // ---- wgrad accumulators -> this block's slab, in register order (coalesced 16-B stores)
+  float* slab = a.slab + (size_t)blockIdx.x * (CO * CI);
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int n = 0; n < C::WTN; ++n)
+      *reinterpret_cast<f32x4_t*>(slab + ((size_t)(i * C::WTN + n) * PW_NT + t) * 4) = accw[i][n];
+  // ---- previous tail BN partials: sum the 16 rows of each DPP row, one atomic pair per column
+  float* slots = a.pslots + (size_t)(blockIdx.x % NSLOT) * 2 * CI;
+#pragma unroll
+  for (int j = 0; j < C::DTN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float s = row16_sum(bs[j][r]), q = row16_sum(bq[j][r]);
+      if ((lane & 15) == 0) {
+        const int c = dcb + 16 * j + (lane >> 4) * 4 + r;
+        atomicAdd(slots + c, s);
+        atomicAdd(slots + CI + c, q);
+      }
+    }
+}
+
+// F1 slab element e = ((i * WTN + n) * NT + t) * 4 + r  ->  dW1 [co][ci]: lane = t & 63, wave = t >> 6;
+// co = WROWS (wave & 1) + 16 i + (lane >> 4) * 4 + r, ci = WCOLS (wave >> 1) + 16 n + (lane & 15)
+template <int CI, int CO>
+__device__ __forceinline__ int pw_slab_to_dw1(int e) {
+  using C = PwSqueezeBwdCfg<CI, CO>;
+  const int r = e & 3, t = (e >> 2) % PW_NT, in = (e >> 2) / PW_NT;
+  const int i = in / C::WTN, n = in % C::WTN;
+  const int lane = t & 63, wv = t >> 6;
+  const int co = C::WROWS * (wv & 1) + 16 * i + (lane >> 4) * 4 + r;
+  const int ci = C::WCOLS * (wv >> 1) + 16 * n + (lane & 15);
+  return co * CI + ci;
+}
+
 // Slab element e = ((j * WTN + n) * NT + t) * 4 + r  ->  dW3 (row = wide channel, col = narrow):
 // lane = t & 63, wave = t >> 6; row = 64 j + 16 (wave & 3) + (lane >> 4) * 4 + r,
 // col = WCOLS (wave >> 2) + 16 n + (lane & 15)   (the !SWAP accumulator layout)
@@ -332,7 +595,8 @@ __device__ __forceinline__ int pw_slab_to_dw(int e) {
 constexpr int PW_RG = 8;
 // SEC tail (sec_C > 0): the shortcut BN's reduction -- red_sc = [red3's sum g' | sum of the q slots]
 // (its slots' first halves are never written), dbeta_sc / dgamma_sc +=, q slots re-zeroed.
-template <int CN>
+// MAP: the slab's register-order layout -- 0 = F3's dW3 (CW x CN), 1 = F1's dW1 (CO = CN x CI = 4 CN)
+template <int CN, int MAP>
 __global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __restrict__ slab, int nslab,
                                                              float* __restrict__ dw, float* __restrict__ sr_slots,
                                                              int sr_C, float* __restrict__ sr_red,
@@ -419,7 +683,8 @@ __global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __rest
     acc += (v0 + v1) + (v2 + v3);
   }
   for (; b < nslab; b += PW_RG) acc += slab[(size_t)b * E + e];
-  atomicAdd(dw + pw_slab_to_dw<CN>(e), acc);
+  if constexpr (MAP == 0) atomicAdd(dw + pw_slab_to_dw<CN>(e), acc);
+  else atomicAdd(dw + pw_slab_to_dw1<4 * CN, CN>(e), acc);
 }
 
 }  // namespace
@@ -442,15 +707,28 @@ void pw_bwd_expand(const PwExpandArgs& args, int nblocks, hipStream_t s) {
   }
 }
 
+bool pw_bwd_squeeze_ok(int CI, int CO, int64_t M) {
+  return CI == 256 && CO == 64 && M % PW_BM == 0 && M > 0 && (int64_t)M * CI < (1ll << 30);
+}
+
+void pw_bwd_squeeze(const PwSqueezeBwdArgs& args, int nblocks, hipStream_t s) {
+  if (args.CI == 256 && args.CO == 64) pw_bwd_squeeze_kernel<256, 64><<<nblocks, PW_NT, 0, s>>>(args);
+  else abort();
+}
+
 void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_slots, int sr_C, float* sr_red,
-                    float* sr_dgamma, float* sr_dbeta, const PwSecReduce& sec, hipStream_t s) {
+                    float* sr_dgamma, float* sr_dbeta, const PwSecReduce& sec, hipStream_t s, int map) {
   const int E = 4 * CN * CN;
   const int nsr = sr_slots ? (sr_C + 15) / 16 : 0;
   const int grid = (E / 256) * PW_RG + nsr + (sec.C ? (sec.C + 15) / 16 : 0);
   switch (CN) {
     case 64:
-      pw_slab_reduce_kernel<64><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red, sr_dgamma,
-                                                     sr_dbeta, sec);
+      if (map == 0)
+        pw_slab_reduce_kernel<64, 0><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
+                                                          sr_dgamma, sr_dbeta, sec);
+      else
+        pw_slab_reduce_kernel<64, 1><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
+                                                          sr_dgamma, sr_dbeta, sec);
       break;
     default: abort();
   }

@@ -534,6 +534,46 @@ std::tuple<Tensor, Tensor, Tensor> pw_bwd_expand(Tensor g, Tensor y3, Tensor mas
 
 bool pw_bwd_expand_supported(int64_t CN, int64_t M) { return tfx::pw_bwd_expand_ok((int)CN, M); }
 
+// Backward of an identity bottleneck's squeezing 1x1 conv1 (w = [CO][1][1][CI]) fused with BN1's backward
+// apply (pw_bwd.hip F1): g1 / y1 / save1 / red1 = BN1's output gradient, input, stats and reduction;
+// x = conv1's input; addend / amask = the residual branch's parked gradient and ReLU mask bits;
+// px / psave / pmask / pslots = the previous tail BN (input, stats, mask bits, slot workspace) whose
+// backward partials the dx epilogue reduces.  dw += dW1.  Returns (dx, pred = [sum g'|sum g' xhat]) with
+// pdgamma / pdbeta +=.
+std::tuple<Tensor, Tensor> pw_bwd_squeeze(Tensor g1, Tensor y1, Tensor save1, Tensor red1, Tensor x, Tensor w,
+                                          Tensor dw, Tensor addend, Tensor amask, Tensor px, Tensor psave,
+                                          Tensor pmask, Tensor pslots, optional<Tensor> pdgamma,
+                                          optional<Tensor> pdbeta) {
+  CHECK_DEV(g1); CHECK_BF16(g1); CHECK_CONTIG(g1); CHECK_BF16(y1); CHECK_CONTIG(y1); CHECK_BF16(x); CHECK_CONTIG(x);
+  CHECK_BF16(w); CHECK_CONTIG(w); CHECK_F32(dw); CHECK_CONTIG(dw); CHECK_BF16(addend); CHECK_CONTIG(addend);
+  CHECK_BF16(px); CHECK_CONTIG(px); CHECK_F32(save1); CHECK_F32(red1); CHECK_F32(psave);
+  const int64_t CO = w.size(0), CI = w.size(-1), M = x.numel() / CI;
+  TORCH_CHECK(w.numel() == CO * CI && dw.numel() == CO * CI && x.size(-1) == CI, "pw_bwd_squeeze: weight shape");
+  TORCH_CHECK(g1.numel() == M * CO && y1.numel() == M * CO && addend.numel() == M * CI && px.numel() == M * CI,
+              "pw_bwd_squeeze: shapes");
+  TORCH_CHECK(save1.numel() == 4 * CO && red1.numel() == 2 * CO && psave.numel() == 4 * CI, "pw_bwd_squeeze: stats");
+  for (const Tensor* m : {&amask, &pmask})
+    TORCH_CHECK(m->scalar_type() == at::kByte && m->is_contiguous() && m->numel() * 8 == M * CI, "pw_bwd_squeeze: mask");
+  TORCH_CHECK(tfx::pw_bwd_squeeze_ok((int)CI, (int)CO, M), "pw_bwd_squeeze: unsupported widths / rows");
+  check_bn_ws(pslots, CI);
+  auto dx = at::empty_like(x);
+  auto pred = at::empty({2 * CI}, x.options().dtype(at::kFloat));
+  tfx::PwSqueezeBwdArgs a;
+  a.g1 = bf(g1); a.y1 = bf(y1); a.save1 = save1.data_ptr<float>(); a.red1 = red1.data_ptr<float>(); a.x = bf(x);
+  a.w = bf(w); a.addend = bf(addend); a.amask = amask.data_ptr<uint8_t>(); a.px = bf(px);
+  a.psave = psave.data_ptr<float>(); a.pmask = pmask.data_ptr<uint8_t>(); a.pslots = pslots.data_ptr<float>();
+  a.dx = bfm(dx); a.M = (int)M; a.CI = (int)CI; a.CO = (int)CO;
+  const int nb = tfx::pw_bwd_expand_grid((int)CO, M);
+  auto slab = at::empty({(int64_t)nb * CO * CI}, x.options().dtype(at::kFloat));
+  a.slab = slab.data_ptr<float>();
+  tfx::pw_bwd_squeeze(a, nb, cur_stream());
+  tfx::pw_slab_reduce(a.slab, nb, (int)CO, dw.data_ptr<float>(), a.pslots, (int)CI, pred.data_ptr<float>(),
+                      fpm(pdgamma), fpm(pdbeta), tfx::PwSecReduce{}, cur_stream(), 1);
+  return {dx, pred};
+}
+
+bool pw_bwd_squeeze_supported(int64_t CI, int64_t CO, int64_t M) { return tfx::pw_bwd_squeeze_ok((int)CI, (int)CO, M); }
+
 // ------------------------------------------------------------------ dense bf16 GEMM
 // out = op(a) @ op(b) (+bias)(relu); a: [M,K] (or [K,M] if trans_a); b: [K,N] (or [N,K] if trans_b)
 void gemm_setup(tfx::IgemmArgs& g, const Tensor& a, const Tensor& b, bool ta, bool tb) {
@@ -1524,6 +1564,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("pw_bwd_expand", &pw_bwd_expand);
   m.def("pw_bwd_expand_supported", &pw_bwd_expand_supported);
   m.def("pw_fwd_squeeze", &pw_fwd_squeeze);
+  m.def("pw_bwd_squeeze", &pw_bwd_squeeze);
+  m.def("pw_bwd_squeeze_supported", &pw_bwd_squeeze_supported);
   m.def("pw_fwd_squeeze_supported", &pw_fwd_squeeze_supported);
   m.def("bn_apply_into", &bn_apply_into);
   m.def("bn_fwd_eval", &bn_fwd_eval);

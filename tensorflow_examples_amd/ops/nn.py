@@ -180,6 +180,26 @@ def _pw_expand_ok(x, w, stride, pad, dil, lazy, sink) -> bool:
     return bool(torch.ops.tfx.pw_bwd_expand_supported(sh[3], x.numel() // sh[3]))
 
 
+PW_SQUEEZE_BWD_CALLS = [0]  # fused conv1 backward launches (tests)
+
+
+def _pw_squeeze_bwd_ok(x, w, stride, pad, dil, lazy, sink, bnb) -> bool:
+    """Can this conv's backward run as the fused squeezing-1x1 kernel (pw_bwd.hip F1) on ``lazy``
+    (a plain ReLU BN's unmaterialised input gradient), with the residual branch's masked gradient
+    parked in ``sink`` and the previous tail BN (``bnb``, with its ReLU mask bits) to reduce?"""
+    sh = w.shape
+    if not (stride == 1 and pad == 0 and dil == 1 and w.trainable and len(sh) == 4 and sh[1] == 1 and sh[2] == 1
+            and x.is_contiguous() and lazy.mask is None and lazy.sec is None and lazy.dy is None):
+        return False
+    if sink is None or sink.mode != "consume" or not isinstance(sink.buf, tuple) or isinstance(sink.buf[0], str):
+        return False
+    if bnb is None or bnb.mask is None or not bnb.relu or bnb.deferred or bnb.red is not None or bnb.sr_pending:
+        return False
+    if lazy.g.shape[-1] != sh[0] or x.shape[-1] != sh[3] or bnb.x.shape != x.shape:
+        return False
+    return bool(torch.ops.tfx.pw_bwd_squeeze_supported(sh[3], sh[0], x.numel() // sh[3]))
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into, sink, bnb):
@@ -221,6 +241,18 @@ class _Conv2d(torch.autograd.Function):
         if ctx.native:
             lazy = getattr(gy, "_tfx_lazy_bnbwd", None)
             if lazy is not None:
+                if need_dx and _pw_squeeze_bwd_ok(x, w, stride, pad, dil, lazy, ctx.sink, ctx.bnb):
+                    # BN1's backward apply + this conv's data AND weight gradient in one launch, the
+                    # residual branch's masked gradient added and the previous tail BN's backward
+                    # partials reduced in the dx epilogue (pw_bwd.hip F1)
+                    add, amask, _ = _unpack_sink(ctx.sink.take())
+                    bnb = ctx.bnb
+                    dx, bnb.red = torch.ops.tfx.pw_bwd_squeeze(
+                        lazy.g.contiguous(), lazy.x, lazy.save, lazy.red, x, w.value, w.grad, add.contiguous(), amask,
+                        bnb.x, bnb.save, bnb.mask, bnb.ws, bnb.dgamma, bnb.dbeta)
+                    PW_SQUEEZE_BWD_CALLS[0] += 1
+                    _grad_ready(w)
+                    return dx, None, None, None, None, None, None, None, None
                 if need_dx and _pw_expand_ok(x, w, stride, pad, dil, lazy, ctx.sink):
                     # the tail BN's backward apply + this conv's data AND weight gradient in one
                     # launch; dy never written (pw_bwd.hip).  The BN2 backward partials of dx ride along.
@@ -650,6 +682,14 @@ class _BatchNorm(torch.autograd.Function):
                 # the producing conv forms it on load (LazyBNGrad)
                 dx = _zero_scalar(x.dtype, x.device).expand(x.shape)
                 dx._tfx_lazy_bnbwd = LazyBNGrad(gy, x, save, ctx.bnb.red, relu, mask)
+                dres = None
+                ctx.bnb.red = None
+            elif ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and _LAZY_BN_BWD and relu \
+                    and not ctx.has_res and mask is None and ctx.bnb.in_mask is None:
+                # plain ReLU BN fed by a conv: dx stays lazy (LazyBNGrad, ReLU mask recomputed from x) --
+                # a squeezing 1x1 producer forms it on load (pw_bwd.hip F1), any other materialises it
+                dx = _zero_scalar(x.dtype, x.device).expand(x.shape)
+                dx._tfx_lazy_bnbwd = LazyBNGrad(gy, x, save, ctx.bnb.red, relu, None)
                 dres = None
                 ctx.bnb.red = None
             elif ctx.bnb is not None and ctx.bnb.red is not None:

@@ -90,6 +90,58 @@ def test_pw_bwd_expand_matches_reference(gpu, shape, bn2, sec):
         assert red2.numel() == 0
 
 
+def _mask_bits(mask, M, C, dev):
+    bits = (mask.reshape(M, C // 8, 1).int() >> torch.arange(8, device=dev, dtype=torch.int32)) & 1
+    return bits.reshape(M, C).float()
+
+
+@pytest.mark.parametrize("shape", [(256, 32, 32), (4, 8, 8), (3, 4, 8)])
+def test_pw_bwd_squeeze_matches_reference(gpu, shape):
+    """F1: BN1 backward apply + conv1 dgrad (+ masked residual addend, + previous tail BN partials)
+    + conv1 wgrad in one launch, vs the layer-wise apply and fp32 GEMMs."""
+    N, H, W = shape
+    CI, CO, M = 256, 64, N * H * W
+    torch.manual_seed(13)
+    # BN1 (plain ReLU): input y1, output gradient g1, its backward reduction
+    y1 = _bf(torch.randn(N, H, W, CO, device=gpu) * 1.1 + 0.2)
+    g1 = _bf(torch.randn(N, H, W, CO, device=gpu))
+    gam1, bet1 = torch.rand(CO, device=gpu) + 0.5, torch.randn(CO, device=gpu) * 0.3
+    ws1 = torch.zeros(64 * 2 * CO, device=gpu)
+    _, save1, _ = torch.ops.tfx.bn_fwd_train(y1, gam1, bet1, None, None, 0.1, 1e-5, None, True, ws1, False)
+    _, _, red1 = torch.ops.tfx.bn_bwd(g1, y1, None, save1, True, ws1, None, None, None, False)
+    dy1 = torch.ops.tfx.bn_bwd_apply(g1, y1, None, save1, red1, True, None, False)[0]
+    # conv1 input x, weight, the residual branch's gradient + mask, the previous tail BN
+    x = _bf(torch.relu(torch.randn(N, H, W, CI, device=gpu)))
+    w = _bf(torch.randn(CO, 1, 1, CI, device=gpu) * 0.1)
+    addend = _bf(torch.randn(N, H, W, CI, device=gpu))
+    r0 = _bf(torch.randn(N, H, W, CI, device=gpu))
+    wst = torch.zeros(64 * 2 * CI, device=gpu)
+    _, _, amask = torch.ops.tfx.bn_fwd_train(_bf(torch.randn(N, H, W, CI, device=gpu)), None, None, None, None, 0.1,
+                                             1e-5, r0, True, wst, False)
+    px = _bf(torch.randn(N, H, W, CI, device=gpu) * 1.3 - 0.1)
+    gp, bp = torch.rand(CI, device=gpu) + 0.5, torch.randn(CI, device=gpu) * 0.3
+    pws = torch.zeros(64 * 2 * CI, device=gpu)
+    _, psave, pmask = torch.ops.tfx.bn_fwd_train(px, gp, bp, None, None, 0.1, 1e-5, r0, True, pws, False)
+    assert pws.abs().max().item() == 0.0
+
+    dw = torch.zeros(CO, 1, 1, CI, device=gpu)
+    pdg, pdb = torch.full((CI,), 0.25, device=gpu), torch.full((CI,), -0.5, device=gpu)
+    dx, pred = torch.ops.tfx.pw_bwd_squeeze(g1, y1, save1, red1, x, w, dw, addend, amask, px, psave, pmask, pws,
+                                            pdg, pdb)
+    torch.cuda.synchronize()
+    am = _mask_bits(amask, M, CI, gpu)
+    dx_ref = dy1.float().reshape(M, CO) @ w.float().reshape(CO, CI) + addend.float().reshape(M, CI) * am
+    assert _rel(dx.reshape(M, CI), dx_ref) < 8e-3
+    dw_ref = dy1.float().reshape(M, CO).t() @ x.float().reshape(M, CI)
+    assert _rel(dw.reshape(CO, CI), dw_ref) < 1e-4
+    assert pws.abs().max().item() == 0.0, "previous tail BN slots not restored to zero"
+    g_ = dx.float().reshape(M, CI) * _mask_bits(pmask, M, CI, gpu)
+    xh = (px.float().reshape(M, CI) - psave[:CI]) * psave[CI:2 * CI]
+    ref_s, ref_q = g_.sum(0), (g_ * xh).sum(0)
+    assert _rel(pred[:CI], ref_s) < 1e-4 and _rel(pred[CI:], ref_q) < 2e-4
+    assert _rel(pdb + 0.5, ref_s) < 1e-4 and _rel(pdg - 0.25, ref_q) < 2e-4
+
+
 def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
     """ResNet-50 first-step gradients with the identity blocks' tail BN backward fused into conv3's
     backward (default) vs materialised by bn_bwd_apply (layer-wise): equal up to the f32-atomic noise
@@ -109,21 +161,23 @@ def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
         torch.cuda.synchronize()
         return st.grad.clone(), st
 
-    saved, saved_ok = nnops._LAZY_BN_BWD, nnops._pw_expand_ok
+    saved, saved_ok, saved_sq = nnops._LAZY_BN_BWD, nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok
     try:
-        n0 = nnops.PW_EXPAND_CALLS[0]
+        n0, n1 = nnops.PW_EXPAND_CALLS[0], nnops.PW_SQUEEZE_BWD_CALLS[0]
         g0, st = run()
         assert nnops.PW_EXPAND_CALLS[0] - n0 == 3, "stage-1 blocks run fused (projection block 1 with F3-SEC)"
+        assert nnops.PW_SQUEEZE_BWD_CALLS[0] - n1 == 2, "stage-1 identity blocks' conv1 backward runs fused (F1)"
         g1, _ = run()
-        # lazy gradients, but every conv3 declines the fused kernel: LazyBNGrad.materialize (the
+        # lazy gradients, but every conv declines the fused kernels: LazyBNGrad.materialize (the
         # projection tail's reduces the shortcut BN there, or in the shortcut BN's backward if first)
         nnops._pw_expand_ok = lambda *a: False
+        nnops._pw_squeeze_bwd_ok = lambda *a: False
         g3, _ = run()
-        nnops._pw_expand_ok = saved_ok
+        nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok = saved_ok, saved_sq
         nnops._LAZY_BN_BWD = False
         g2, _ = run()
     finally:
-        nnops._LAZY_BN_BWD, nnops._pw_expand_ok = saved, saved_ok
+        nnops._LAZY_BN_BWD, nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok = saved, saved_ok, saved_sq
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
