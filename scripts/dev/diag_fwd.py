@@ -6,6 +6,8 @@ from tensorflow_examples_amd.ops import nn as nnops
 from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
 
 dev = torch.device("cuda")
+from tensorflow_examples_amd.ops import _native
+assert _native.load()
 torch.manual_seed(11)
 N, H, W, CI, co = 256, 32, 32, 256, 64
 M = N * H * W

@@ -33,7 +33,9 @@ for s in $STEPS; do
         python3 "$R/bench.py" --steps 5 --warmup 2 > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/prof.log; exit $rc; }
       f=$(find gpurun_out/prof -name '*kernel_stats.csv' | head -1)
-      python scripts/kstats.py "$f" auto 60 > gpurun_out/kernel_summary.txt; head -25 gpurun_out/kernel_summary.txt ;;
+      python scripts/kstats.py "$f" auto 60 > gpurun_out/kernel_summary.txt; head -25 gpurun_out/kernel_summary.txt
+      kt=$(find gpurun_out/prof -name '*kernel_trace.csv' | head -1)
+      python scripts/step_trace.py "$kt" > gpurun_out/step_trace.txt; head -1 gpurun_out/step_trace.txt ;;
     pmc)
       i=0
       for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" \

@@ -98,7 +98,11 @@ def test_resnet50_deferred_tails_match_layerwise(gpu):
         l2, g2, _ = run()
     finally:
         nnops._DEFER_TAIL = saved
-    assert abs(l0 - l2) <= 1e-3 * max(1.0, abs(l2)), (l0, l2)
+    # the first-step loss of a random-init ResNet-50 moves ~0.4% between two runs of the SAME path
+    # (f32-atomic BN statistics, amplified through 50 layers; scripts/dev/diag_fwd.py): bound the
+    # fused-vs-layerwise gap by that spread, with a 1% floor -- the kernel test above pins the
+    # fused values bit-exactly
+    assert abs(l0 - l2) <= max(4 * abs(l0 - l1), 0.01 * abs(l2)), (l0, l1, l2)
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
