@@ -312,6 +312,21 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
   }
 }
 
+// zero the bf16 halves of 8 x bf16 whose bit in `bits` is clear (as igemm_impl.h mask_bf16x8)
+__device__ __forceinline__ U4 mask_bf16x8_pw(const U4& v, uint32_t bits) {
+  auto wmask = [&](int s) -> uint32_t {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)bits, s, 1) & 0xffffu;
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)bits, s + 1, 1) << 16;
+    return lo | hi;
+  };
+  U4 r;
+  r.x = v.x & wmask(0);
+  r.y = v.y & wmask(2);
+  r.z = v.z & wmask(4);
+  r.w = v.w & wmask(6);
+  return r;
+}
+
 // ---------------------------------------------------------------------------------- F1 (squeeze)
 // Backward of an identity bottleneck's SQUEEZING 1x1 conv1 (CI wide -> CO narrow) fused with BN1's
 // backward apply.  Layer-wise: bn_bwd_apply (dy1, narrow), conv1 dgrad (dx, wide: + the residual
@@ -326,11 +341,14 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
 template <int CI, int CO>
 struct PwSqueezeBwdCfg {
   static constexpr int NTPR = CO / 4;                  // threads per narrow row (8-B pieces)
+  static constexpr int TPR = CI / 8;                   // threads per wide row (16-B pieces)
+  static constexpr int RSTEP = PW_NT / TPR;            // rows between a thread's wide pieces
+  static constexpr int LPT = PW_BM * TPR / PW_NT;      // wide pieces per thread per tensor per tile
   static constexpr int T_BYTES = PW_BM * CO * 2;       // T1 tile, K-major 64-channel rows
   static constexpr int X_BYTES = PW_BM * CI * 2;       // X tile, MN image
   static constexpr int SLOT = T_BYTES + X_BYTES;
   static constexpr int W_BYTES = CO * CI * 2;          // W1 MN image (rows = co), resident
-  static constexpr int XLD = PW_BM * CI / 8 / PW_NT;   // X 16-B pieces per thread per tile
+  static constexpr int D_BYTES = PW_BM * CI * 4;       // dgrad accumulator tile (f32), epilogue hand-off
   static constexpr int DCOLS = CI / 4;                 // dgrad columns per wave (2 row x 4 col groups)
   static constexpr int DTN = DCOLS / 16;
   static constexpr int WROWS = CO / 2;                 // wgrad: co rows per wave (2 groups)
@@ -339,24 +357,33 @@ struct PwSqueezeBwdCfg {
   static constexpr int WTN = WCOLS / 16;
   static_assert(CO == 64, "T1 is one 64-channel K-major chunk");
   static_assert(PW_BM * NTPR == PW_NT, "narrow tile mapping");
-  static_assert(XLD >= 1 && PW_BM * CI / 8 % PW_NT == 0, "wide tile mapping");
-  static_assert(2 * SLOT + W_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(LPT >= 1 && PW_BM * TPR % PW_NT == 0, "wide tile mapping");
+  static_assert(2 * SLOT + W_BYTES + D_BYTES + (2 * CI + 5 * CO) * 4 <= 160 * 1024, "LDS budget");
 };
+
+// D tile (f32 [32][CI]): 16-B chunk q of row r at r * CI * 4 + ((q ^ (r & 7)) << 4)  (the SWAP writers put
+// 16 rows x 4 consecutive columns per instruction; the row-contiguous readers take 32 B of one row)
+template <int CI>
+__device__ __forceinline__ int pw_doff(int r, int q) { return r * CI * 4 + ((q ^ (r & 7)) << 4); }
 
 template <int CI, int CO>
 __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdArgs a) {
   using C = PwSqueezeBwdCfg<CI, CO>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * C::SLOT + C::W_BYTES + 2 * CI * 4 + 5 * CO * 4];
+  constexpr int LPT = C::LPT;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::SLOT + C::W_BYTES + C::D_BYTES + (2 * CI + 5 * CO) * 4];
   char* wimg = smem + 2 * C::SLOT;
-  // previous tail BN's [invstd | -mean invstd] per wide channel, read by the dgrad epilogue
-  float* pcoef = reinterpret_cast<float*>(smem + 2 * C::SLOT + C::W_BYTES);
+  char* dimg = wimg + C::W_BYTES;
+  // previous tail BN's [invstd | -mean invstd] per wide channel; BN1's [A | B | D | scale | shift]
+  float* pcoef = reinterpret_cast<float*>(dimg + C::D_BYTES);
+  float* ncoef = pcoef + 2 * CI;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int ntiles = a.M / PW_BM;
 
-  // ---- narrow piece of this thread (fixed channels nc0 .. nc0 + 3); BN1 backward coefficients
-  // [A | B | D | scale | shift] per narrow channel in LDS (registers go to the accumulators)
-  const int nrow = t / C::NTPR, nc0 = 4 * (t % C::NTPR);
-  float* ncoef = pcoef + 2 * CI;
+  for (int c = t; c < CI; c += PW_NT) {
+    const float is = a.psave[CI + c];
+    pcoef[c] = is;
+    pcoef[CI + c] = -a.psave[c] * is;
+  }
   if (t < CO) {
     const float inv_m = 1.f / (float)a.M;
     const float mu = a.save1[t], is = a.save1[CO + t], sc = a.save1[2 * CO + t];
@@ -366,11 +393,6 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
     ncoef[2 * CO + t] = sc * (kx * mu - kg);
     ncoef[3 * CO + t] = sc;
     ncoef[4 * CO + t] = a.save1[3 * CO + t];
-  }
-  for (int c = t; c < CI; c += PW_NT) {
-    const float is = a.psave[CI + c];
-    pcoef[c] = is;
-    pcoef[CI + c] = -a.psave[c] * is;
   }
   // ---- W1 [CO][CI] -> MN image (row = co), resident
   for (int q = t; q < CO * CI / 8; q += PW_NT) {
@@ -383,15 +405,16 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
   const __amdgpu_buffer_rsrc_t rpx = pw_rsrc(a.px, wide), rpm = pw_rsrc(a.pmask, (int64_t)a.M * CI / 8);
   const __amdgpu_buffer_rsrc_t rdx = pw_rsrc(a.dx, wide);
 
-  // dgrad wave tile: rows 16 (wv & 1), columns DCOLS (wv >> 1); SWAP -> lane holds row (lane & 15),
-  // columns dcb + 16 j + (lane >> 4) * 4 + r
+  // narrow piece (g1 / y1 -> T1): row t / NTPR, channels nc0 .. nc0 + 3
+  const int nrow = t / C::NTPR, nc0 = 4 * (t % C::NTPR);
+  // wide pieces (X, addend, previous tail input, masks; the dx epilogue): rows r0 + RSTEP i, channels
+  // 8 chc .. 8 chc + 7 -- fixed for the launch, so the previous tail BN's partials stay per thread
+  const int chc = t % C::TPR, r0 = t / C::TPR;
+  float bs[8], bq[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) bs[k] = bq[k] = 0.f;
+  // dgrad wave tile: rows 16 (wv & 1), columns DCOLS (wv >> 1); SWAP
   const int drb = 16 * (wv & 1), dcb = C::DCOLS * (wv >> 1);
-  const int hsel = 4 * ((lane >> 4) & 1);  // this lane's 4 columns within their mask byte
-  float bs[C::DTN][4], bq[C::DTN][4];  // previous tail BN partials, whole launch
-#pragma unroll
-  for (int j = 0; j < C::DTN; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bs[j][r] = bq[j][r] = 0.f;
   // wgrad wave tile: co rows WROWS (wv & 1), ci columns WCOLS (wv >> 1); !SWAP
   const int wrb = C::WROWS * (wv & 1), wcb = C::WCOLS * (wv >> 1);
   f32x4_t accw[C::WTM][C::WTN];
@@ -400,42 +423,35 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
 #pragma unroll
     for (int n = 0; n < C::WTN; ++n) accw[i][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  // ---- staging: narrow g1 / y1 + the X tile two tiles ahead; the dgrad epilogue operands (addend,
-  // its mask, the previous tail's input and mask) one tile ahead in a single register set
+  // ---- register staging ring (two tiles): every operand of a tile, coalesced 8 / 16-B pieces
   struct Stage {
     pw_u32x2 g, y;
-    pw_u32x4 x[C::XLD];
+    pw_u32x4 x[LPT], ad[LPT], px[LPT];
+    uint32_t mk[LPT];  // addend mask byte | previous tail mask byte << 8
   };
   Stage st0, st1;
-  pw_u32x2 ead[C::DTN], epx[C::DTN];
-  uint32_t emk[C::DTN];  // addend mask byte | previous mask byte << 8
   const int tile0 = blockIdx.x, tstep = gridDim.x;
   auto issue = [&](Stage& s, int tile) {
     const bool ok = tile < ntiles;
-    const int row = tile * PW_BM + nrow;
-    const uint32_t no = ok ? (uint32_t)(row * CO + nc0) * 2u : 0x80000000u;
+    const uint32_t no = ok ? (uint32_t)((tile * PW_BM + nrow) * CO + nc0) * 2u : 0x80000000u;
     s.g = __builtin_amdgcn_raw_buffer_load_b64(rg, no, 0, 0);
     s.y = __builtin_amdgcn_raw_buffer_load_b64(ry, no, 0, 0);
 #pragma unroll
-    for (int i = 0; i < C::XLD; ++i) {
-      const int q = t + PW_NT * i, xr = tile * PW_BM + q / (CI / 8), xc = q % (CI / 8);
-      s.x[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? (uint32_t)(xr * CI + 8 * xc) * 2u : 0x80000000u, 0, 0);
+    for (int i = 0; i < LPT; ++i) {
+      const int row = tile * PW_BM + r0 + C::RSTEP * i;
+      const uint32_t o = ok ? (uint32_t)(row * CI + 8 * chc) * 2u : 0x80000000u;
+      const uint32_t ob = ok ? (uint32_t)(row * C::TPR + chc) : 0x80000000u;
+      s.x[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, o, 0, 0);
+      s.ad[i] = __builtin_amdgcn_raw_buffer_load_b128(rad, o, 0, 0);
+      s.px[i] = __builtin_amdgcn_raw_buffer_load_b128(rpx, o, 0, 0);
+      s.mk[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(ram, ob, 0, 0) |
+                ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rpm, ob, 0, 0) << 8);
     }
   };
-  auto issue_ep = [&](int tile) {
-    const bool ok = tile < ntiles;
-    const int row = tile * PW_BM + drb + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < C::DTN; ++j) {
-      const int col = dcb + 16 * j + (lane >> 4) * 4;
-      const uint32_t o = ok ? (uint32_t)(row * CI + col) * 2u : 0x80000000u;
-      const uint32_t ob = ok ? (uint32_t)(row * CI + col) / 8u : 0x80000000u;
-      ead[j] = __builtin_amdgcn_raw_buffer_load_b64(rad, o, 0, 0);
-      epx[j] = __builtin_amdgcn_raw_buffer_load_b64(rpx, o, 0, 0);
-      emk[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(ram, ob, 0, 0) |
-               ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rpm, ob, 0, 0) << 8);
-    }
-  };
+  // epilogue operands of the tile being staged move to `ep` (the staging registers are re-issued
+  // before the tile's epilogue runs)
+  pw_u32x4 ead[LPT], epx[LPT];
+  uint32_t emk[LPT];
   auto stage = [&](const Stage& s, char* slot) {
     float gf[4], yf[4], o[4];
     const float4 A4 = *reinterpret_cast<const float4*>(ncoef + nc0);
@@ -454,29 +470,40 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
       const float gg = fmaf(yf[k], sc[k], sh[k]) > 0.f ? gf[k] : 0.f;
       o[k] = fmaf(A[k], gg, fmaf(B[k], yf[k], D[k]));
     }
-    const int c16 = nc0 >> 3;  // 16-B chunk of the 128-B row, 8-B half (nc0 >> 2) & 1
-    *reinterpret_cast<pw_u32x2*>(slot + pw_kmaj(nrow, c16) + ((nc0 >> 2) & 1) * 8) =
+    *reinterpret_cast<pw_u32x2*>(slot + pw_kmaj(nrow, nc0 >> 3) + ((nc0 >> 2) & 1) * 8) =
         (pw_u32x2){pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
 #pragma unroll
-    for (int i = 0; i < C::XLD; ++i) {
-      const int q = t + PW_NT * i;
-      *reinterpret_cast<pw_u32x4*>(slot + C::T_BYTES + pw_mn<CI>(q / (CI / 8), q % (CI / 8))) = s.x[i];
+    for (int i = 0; i < LPT; ++i) {
+      *reinterpret_cast<pw_u32x4*>(slot + C::T_BYTES + pw_mn<CI>(r0 + C::RSTEP * i, chc)) = s.x[i];
+      ead[i] = s.ad[i];
+      epx[i] = s.px[i];
+      emk[i] = s.mk[i];
     }
   };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
   auto compute = [&](const char* slot, int tile) {
-    // dgrad: acc_d[32 x CI] = T1[32 x CO] . W1
-    f32x4_t accd[C::DTN];
+    // dgrad: acc_d[32 x CI] = T1[32 x CO] . W1 -> D tile (f32, LDS)
+    {
+      f32x4_t accd[C::DTN];
 #pragma unroll
-    for (int j = 0; j < C::DTN; ++j) accd[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < C::DTN; ++j) accd[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kc = 0; kc < CO / 32; ++kc) {
-      const bf16x8_t fa = pw_frag_kmaj(slot, 0, drb, 4 * kc, lane);
+      for (int kc = 0; kc < CO / 32; ++kc) {
+        const bf16x8_t fa = pw_frag_kmaj(slot, 0, drb, 4 * kc, lane);
 #pragma unroll
-      for (int j = 0; j < C::DTN; ++j) {
-        const bf16x8_t fb = pw_frag_tr(wimg, 32 * kc * CI * 2, dcb + 16 * j, lane,
-                                       [](int r, int c) { return pw_mn<CI>(r, c); });
-        accd[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, accd[j], 0, 0, 0);  // SWAP
+        for (int j = 0; j < C::DTN; ++j) {
+          const bf16x8_t fb = pw_frag_tr(wimg, 32 * kc * CI * 2, dcb + 16 * j, lane,
+                                         [](int r, int c) { return pw_mn<CI>(r, c); });
+          accd[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, accd[j], 0, 0, 0);  // SWAP
+        }
       }
+      const int drow = drb + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < C::DTN; ++j)
+        *reinterpret_cast<f32x4_t*>(dimg + pw_doff<CI>(drow, (dcb + 16 * j) / 4 + (lane >> 4))) = accd[j];
     }
     // wgrad: acc_w[CO x CI] += T1^T . X (k = the tile's 32 rows)
     bf16x8_t fx[C::WTN];
@@ -489,48 +516,44 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
 #pragma unroll
       for (int n = 0; n < C::WTN; ++n) accw[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft, fx[n], accw[i][n], 0, 0, 0);
     }
-    // dgrad epilogue: + masked addend -> dx (bf16, 8-byte stores); previous tail BN partials
-    const int row = tile * PW_BM + drb + (lane & 15);
+    sync();  // D tile complete
+    // dx epilogue, row-contiguous: + masked addend -> bf16 16-B stores; previous tail BN partials
+    const float4 pi0 = *reinterpret_cast<const float4*>(pcoef + 8 * chc);
+    const float4 pi1 = *reinterpret_cast<const float4*>(pcoef + 8 * chc + 4);
+    const float4 pn0 = *reinterpret_cast<const float4*>(pcoef + CI + 8 * chc);
+    const float4 pn1 = *reinterpret_cast<const float4*>(pcoef + CI + 8 * chc + 4);
+    const float pis[8] = {pi0.x, pi0.y, pi0.z, pi0.w, pi1.x, pi1.y, pi1.z, pi1.w};
+    const float pnm[8] = {pn0.x, pn0.y, pn0.z, pn0.w, pn1.x, pn1.y, pn1.z, pn1.w};
 #pragma unroll
-    for (int j = 0; j < C::DTN; ++j) {
-      const int col = dcb + 16 * j + (lane >> 4) * 4;
-      const uint32_t ab = (emk[j] >> hsel) & 0xfu, pb = (emk[j] >> (8 + hsel)) & 0xfu;
-      const float ad[4] = {__uint_as_float(ead[j][0] << 16), __uint_as_float(ead[j][0] & 0xffff0000u),
-                           __uint_as_float(ead[j][1] << 16), __uint_as_float(ead[j][1] & 0xffff0000u)};
-      const float xv[4] = {__uint_as_float(epx[j][0] << 16), __uint_as_float(epx[j][0] & 0xffff0000u),
-                           __uint_as_float(epx[j][1] << 16), __uint_as_float(epx[j][1] & 0xffff0000u)};
-      float v[4];
+    for (int i = 0; i < LPT; ++i) {
+      const int lrow = r0 + C::RSTEP * i;
+      const f32x4_t v0 = *reinterpret_cast<const f32x4_t*>(dimg + pw_doff<CI>(lrow, 2 * chc));
+      const f32x4_t v1 = *reinterpret_cast<const f32x4_t*>(dimg + pw_doff<CI>(lrow, 2 * chc + 1));
+      float ad[8], xv[8], v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      unpack8(mask_bf16x8_pw(__builtin_bit_cast(U4, ead[i]), emk[i] & 0xffu), ad);
+      unpack8(__builtin_bit_cast(U4, epx[i]), xv);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = accd[j][r] + (((ab >> r) & 1u) ? ad[r] : 0.f);
-      const uint32_t lo = pack_bf16x2(v[0], v[1]), hi = pack_bf16x2(v[2], v[3]);
-      __builtin_amdgcn_raw_buffer_store_b64((pw_u32x2){lo, hi}, rdx, (uint32_t)(row * CI + col) * 2u, 0, 0);
-      const float gv[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u), __uint_as_float(hi << 16),
-                           __uint_as_float(hi & 0xffff0000u)};
-      const float4 pi4 = *reinterpret_cast<const float4*>(pcoef + col);
-      const float4 pn4 = *reinterpret_cast<const float4*>(pcoef + CI + col);
-      const float pis[4] = {pi4.x, pi4.y, pi4.z, pi4.w}, pnm[4] = {pn4.x, pn4.y, pn4.z, pn4.w};
+      for (int k = 0; k < 8; ++k) v[k] += ad[k];
+      const U4 packed = pack8(v);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pw_u32x4, packed), rdx,
+                                             (uint32_t)((tile * PW_BM + lrow) * CI + 8 * chc) * 2u, 0, 0);
+      float gv[8];
+      unpack8(mask_bf16x8_pw(packed, emk[i] >> 8), gv);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float gp = ((pb >> r) & 1u) ? gv[r] : 0.f;
-        bs[j][r] += gp;
-        bq[j][r] = fmaf(gp, fmaf(xv[r], pis[r], pnm[r]), bq[j][r]);
+      for (int k = 0; k < 8; ++k) {
+        bs[k] += gv[k];
+        bq[k] = fmaf(gv[k], fmaf(xv[k], pis[k], pnm[k]), bq[k]);
       }
     }
-    issue_ep(tile + tstep);
-  };
-  auto sync = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
   };
 
   issue(st0, tile0);
   issue(st1, tile0 + tstep);
-  issue_ep(tile0);
-  __syncthreads();  // W1 image written
+  __syncthreads();  // W1 image, coefficient tables written
   for (int tile = tile0; tile < ntiles; tile += 2 * tstep) {
     stage(st0, smem);
     issue(st0, tile + 2 * tstep);
-    sync();
+    sync();  // also: every thread is past the previous tile's D reads
     compute(smem, tile);
     const int t1 = tile + tstep;
     if (t1 >= ntiles) break;
@@ -547,19 +570,24 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
 #pragma unroll
     for (int n = 0; n < C::WTN; ++n)
       *reinterpret_cast<f32x4_t*>(slab + ((size_t)(i * C::WTN + n) * PW_NT + t) * 4) = accw[i][n];
-  // ---- previous tail BN partials: sum the 16 rows of each DPP row, one atomic pair per column
-  float* slots = a.pslots + (size_t)(blockIdx.x % NSLOT) * 2 * CI;
+  // ---- previous tail BN partials: threads t, t + TPR, ... share channels 8 chc .. 8 chc + 7 -> LDS
+  // (the D tile, free now) tree over the RSTEP row groups, one atomic pair per channel
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(dimg);  // [16][RSTEP][TPR]
 #pragma unroll
-  for (int j = 0; j < C::DTN; ++j)
+  for (int k = 0; k < 8; ++k) {
+    red[(k * C::RSTEP + r0) * C::TPR + chc] = bs[k];
+    red[((8 + k) * C::RSTEP + r0) * C::TPR + chc] = bq[k];
+  }
+  __syncthreads();
+  for (int e = t; e < 16 * C::TPR; e += PW_NT) {
+    const int kk = e / C::TPR, ch = e % C::TPR;
+    float v = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float s = row16_sum(bs[j][r]), q = row16_sum(bq[j][r]);
-      if ((lane & 15) == 0) {
-        const int c = dcb + 16 * j + (lane >> 4) * 4 + r;
-        atomicAdd(slots + c, s);
-        atomicAdd(slots + CI + c, q);
-      }
-    }
+    for (int r = 0; r < C::RSTEP; ++r) v += red[(kk * C::RSTEP + r) * C::TPR + ch];
+    const int c = 8 * ch + (kk & 7);
+    atomicAdd(a.pslots + (size_t)(blockIdx.x % NSLOT) * 2 * CI + (kk >> 3) * CI + c, v);
+  }
 }
 
 // F1 slab element e = ((i * WTN + n) * NT + t) * 4 + r  ->  dW1 [co][ci]: lane = t & 63, wave = t >> 6;
