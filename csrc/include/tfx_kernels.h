@@ -148,6 +148,18 @@ struct PwSqueezeArgs {
 bool pw_fwd_squeeze_ok(int CI, int CO, int64_t M);
 int pw_fwd_squeeze_grid(int64_t M);
 void pw_fwd_squeeze(const PwSqueezeArgs& args, int nblocks, hipStream_t s);
+// Stage-1 3x3 conv (64 -> 64, stride 1, pad 1, width 32) with its BN layers fused (conv3x3_fused.hip).
+// Forward: y = conv(relu(x sc_in + sh_in)) with BN statistics of y added into slots [NSLOT][2][64].
+struct Conv3Args {
+  const uint16_t* x = nullptr;      // [N][H][32][64] input BN's input (y1)
+  const float* save_in = nullptr;   // [4][64] input BN's [mean | invstd | scale | shift]
+  const uint16_t* w = nullptr;      // [64][3][3][64]
+  uint16_t* y = nullptr;            // [N][H][32][64]
+  float* slots = nullptr;           // [NSLOT][2][64] output BN statistics
+  int N = 0, H = 0;
+};
+bool conv3x3_fused_ok(int N, int H, int W, int C, int K);
+void conv3x3_fwd_fused(const Conv3Args& a, hipStream_t s);
 // the shortcut BN's reduction in pw_slab_reduce's tail (C = 0: none): red = [red3's sum g' | sum q]
 struct PwSecReduce {
   float* slots = nullptr;

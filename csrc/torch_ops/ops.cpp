@@ -300,19 +300,57 @@ std::tuple<Tensor, Tensor> pw_fwd_squeeze(Tensor y3, Tensor save3, Tensor res, o
 
 bool pw_fwd_squeeze_supported(int64_t CI, int64_t CO, int64_t M) { return tfx::pw_fwd_squeeze_ok((int)CI, (int)CO, M); }
 
-// tail apply into caller-provided buffers (the fallback of a deferred tail whose consumer could
-// not fuse it): out = relu(x sc + sh + res'), mask bits
-void bn_apply_into(Tensor x, Tensor res, Tensor save, optional<Tensor> res_save, Tensor out, Tensor mask) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(res); CHECK_CONTIG(res); CHECK_BF16(out); CHECK_CONTIG(out);
+// BN apply into caller-provided buffers (the fallback of a deferred apply whose consumer could not
+// fuse it): out = relu(x sc + sh + res'), res' = res, res * rsc + rsh (res_save) or none; mask bits
+// (residual + ReLU layers only)
+void bn_apply_into(Tensor x, optional<Tensor> res, Tensor save, optional<Tensor> res_save, Tensor out,
+                   optional<Tensor> mask) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(out); CHECK_CONTIG(out);
   const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(res.numel() == x.numel() && out.numel() == x.numel() && mask.numel() * 8 == x.numel() && C % 8 == 0,
-              "bn_apply_into: shapes");
-  if (res_save.has_value() && res_save->defined())
-    tfx::bn_apply_res_bn(bf(x), bf(res), save.data_ptr<float>(), res_save->data_ptr<float>(), M, (int)C, true,
-                         bfm(out), mask.data_ptr<uint8_t>(), cur_stream());
+  TORCH_CHECK(out.numel() == x.numel() && C % 8 == 0, "bn_apply_into: shapes");
+  const bool has_res = res.has_value() && res->defined();
+  uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->numel() * 8 == x.numel(), "bn_apply_into: mask");
+    mk = mask->data_ptr<uint8_t>();
+  }
+  if (has_res) {
+    CHECK_BF16(*res); CHECK_CONTIG(*res);
+    TORCH_CHECK(res->numel() == x.numel(), "bn_apply_into: residual");
+  }
+  if (has_res && res_save.has_value() && res_save->defined())
+    tfx::bn_apply_res_bn(bf(x), bf(*res), save.data_ptr<float>(), res_save->data_ptr<float>(), M, (int)C, true,
+                         bfm(out), mk, cur_stream());
   else
-    tfx::bn_apply(bf(x), bf(res), save.data_ptr<float>(), M, (int)C, true, bfm(out), mask.data_ptr<uint8_t>(),
+    tfx::bn_apply(bf(x), has_res ? bf(*res) : nullptr, save.data_ptr<float>(), M, (int)C, true, bfm(out), mk,
                   cur_stream());
+}
+
+// Stage-1 3x3 conv (64 -> 64, stride 1, pad 1, width 32) applying its input BN + ReLU on load
+// (conv3x3_fused.hip): x = the input BN's input, save_in its stats; the output BN's statistics land in
+// ws and are finalized as conv_fwd_bn does.  Returns (y, save).
+std::tuple<Tensor, Tensor> conv3x3_fwd_fused(Tensor x, Tensor save_in, Tensor w, Tensor ws, optional<Tensor> gamma,
+                                             optional<Tensor> beta, optional<Tensor> run_mean,
+                                             optional<Tensor> run_var, double momentum, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_F32(save_in);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(1) == 3 && w.size(2) == 3, "conv3x3_fwd_fused: shapes");
+  const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3), K = (int)w.size(0);
+  TORCH_CHECK(w.size(3) == C && save_in.numel() == 4 * C, "conv3x3_fwd_fused: shapes");
+  TORCH_CHECK(tfx::conv3x3_fused_ok(N, H, W, C, K), "conv3x3_fwd_fused: unsupported geometry");
+  check_bn_ws(ws, K);
+  auto y = at::empty({N, H, W, K}, x.options());
+  auto save = at::empty({4 * K}, x.options().dtype(at::kFloat));
+  tfx::Conv3Args a;
+  a.x = bf(x); a.save_in = save_in.data_ptr<float>(); a.w = bf(w); a.y = bfm(y); a.slots = ws.data_ptr<float>();
+  a.N = N; a.H = H;
+  tfx::conv3x3_fwd_fused(a, cur_stream());
+  tfx::bn_finalize(a.slots, (int64_t)N * H * W, K, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
+                   fpm(run_var), save.data_ptr<float>(), cur_stream());
+  return {y, save};
+}
+
+bool conv3x3_fused_supported(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K) {
+  return tfx::conv3x3_fused_ok((int)N, (int)H, (int)W, (int)C, (int)K);
 }
 
 // stride-1 conv data gradient whose epilogue also reduces the backward of the BN that produced
@@ -1568,6 +1606,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("pw_bwd_squeeze_supported", &pw_bwd_squeeze_supported);
   m.def("pw_fwd_squeeze_supported", &pw_fwd_squeeze_supported);
   m.def("bn_apply_into", &bn_apply_into);
+  m.def("conv3x3_fwd_fused", &conv3x3_fwd_fused);
+  m.def("conv3x3_fused_supported", &conv3x3_fused_supported);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd(Tensor g, Tensor x, Tensor? res, Tensor save, bool relu, Tensor slots, Tensor? dgamma, "
         "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);

@@ -115,7 +115,9 @@ class Bottleneck:
         if prod is not None and _S2_ADDEND:
             prod.accept_s2 = True  # ... and a 1x1 stride-2 projection's compact gradient
         # conv1 is x's last consumer in backward only when the GradSink carries the other branch
-        o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons, fuse_input_bn_backward=cons is not None)
+        # BN1's apply is left to conv2 (a stage-1 3x3 conv applies it on load: conv3x3_fused.hip)
+        o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons, fuse_input_bn_backward=cons is not None,
+                               defer_apply=True)
         o = self.b2.after_conv(self.c2, o, training, relu=True, fuse_input_bn_backward=True)
         o3_fuse = True
         if self.proj is None:

@@ -127,17 +127,20 @@ class LazyBNGrad:
         return self.dy
 
 
-# test hook: False keeps every block tail applied by its own pass (the layer-wise forward)
+# test hooks: False keeps every block tail / plain BN applied by its own pass (the layer-wise forward)
 _DEFER_TAIL = True
+_DEFER_BN_IN = True
 PW_SQUEEZE_CALLS = [0]  # fused tail + conv1 forward launches (tests)
 
 
 class TailPending:
-    """A residual + ReLU batch norm's output whose apply pass was deferred to its consumer (the next
-    bottleneck's conv1): ``out`` (and the ReLU ``mask`` bits the backward saved) are allocated but
-    not yet written.  The consumer conv forms them while it loads its input (pw_fwd_squeeze, one
-    launch), or calls :meth:`materialize` (bn_apply_into).  Everything that reads ``out`` runs after
-    that conv in the block's forward order (the tail's residual use, the projection shortcut)."""
+    """A ReLU batch norm's output whose apply pass was deferred to its consumer conv: ``out`` (and,
+    for a residual tail, the ReLU ``mask`` bits the backward saved) are allocated but not yet written.
+    A residual tail's consumer (the next bottleneck's conv1) forms them while it loads its input
+    (pw_fwd_squeeze, one launch, ``done``); a plain BN's consumer (the stage-1 3x3 conv2) applies it
+    on load WITHOUT writing it (conv3x3_fwd_fused) -- whatever reads ``out`` later (that conv's
+    weight gradient) calls :meth:`materialize` (bn_apply_into), as does any consumer that cannot fuse.
+    Everything that reads ``out`` runs after that conv in the block's forward order."""
     __slots__ = ("x", "save", "res", "res_save", "out", "mask", "done")
 
     def __init__(self, x, save, res, res_save, out, mask):
@@ -156,6 +159,19 @@ def _settle(t):
     if tp is not None and not tp.done:
         tp.materialize()
     return t
+
+
+CONV3_FWD_CALLS = [0]  # fused stage-1 3x3 forward launches (tests)
+
+
+def _conv3_fused_ok(x, w, stride, pad, dil, stats_into) -> bool:
+    """Stage-1 3x3 conv (64 -> 64, stride 1, pad 1, width 32) with a BN workspace: conv3x3_fused.hip."""
+    sh = w.shape
+    if not (stride == 1 and pad == 1 and dil == 1 and isinstance(stats_into, BNWorkspace) and x.dim() == 4
+            and len(sh) == 4 and sh[1] == 3 and sh[2] == 3 and sh[3] == x.shape[-1] and x.is_contiguous()):
+        return False
+    n, h, wd, c = x.shape
+    return bool(torch.ops.tfx.conv3x3_fused_supported(n, h, wd, c, sh[0]))
 
 
 def _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into) -> bool:
@@ -211,6 +227,15 @@ class _Conv2d(torch.autograd.Function):
                 w.store.flip_stale = True  # the weights may have changed since the last refresh
             tp = getattr(x, "_tfx_tail", None)
             if tp is not None and not tp.done:
+                if tp.res is None and _conv3_fused_ok(x, w, stride, pad, dil, stats_into):
+                    # BN + ReLU of the input applied on load, 3x3 conv from a halo tile, the output
+                    # BN's statistics (conv3x3_fused.hip); x stays unwritten until something reads it
+                    ws = stats_into
+                    y, ws.pending_save = torch.ops.tfx.conv3x3_fwd_fused(tp.x, tp.save, w.value, ws.get(x.device),
+                                                                         *ws.finalize_args)
+                    ctx.pending_in = tp
+                    CONV3_FWD_CALLS[0] += 1
+                    return y
                 if _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into):
                     # the previous block's tail apply + this conv + its BN statistics in one launch:
                     # x (and the tail's mask bits) are written here (pw_fwd.hip)
@@ -235,6 +260,9 @@ class _Conv2d(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, *unused):
         (x,) = ctx.saved_tensors
+        tp = getattr(ctx, "pending_in", None)
+        if tp is not None:
+            tp.materialize()  # the forward applied the input BN on load only
         w = ctx.w
         stride, pad, dil = ctx.cfg
         need_dx = ctx.needs_input_grad[0]
@@ -579,13 +607,18 @@ class _BatchNorm(torch.autograd.Function):
             # to that conv (TailPending) -- it forms out / mask while loading its input
             defer_tail = defer_apply and _DEFER_TAIL and pending and relu and res is not None and \
                 x.shape[-1] % 8 == 0 and (fuse_res or not res_lazy)
+            # plain ReLU BN whose only reader is a 3x3 conv that applies it on load
+            defer_plain = defer_apply and _DEFER_BN_IN and pending and relu and res is None and x.shape[-1] % 8 == 0
             if res_lazy and not fuse_res:
                 res = torch.ops.tfx.bn_apply_train(res_bnb.x, None, res_bnb.save, False)[0]
             defer_out = defer and pending and res is None and bnb_out is not None and _vec_ok(x.shape[-1])
             if pending:
                 # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
                 save, wsobj.pending_save = wsobj.pending_save, None
-                if defer_tail:
+                if defer_plain:
+                    y = torch.empty_like(x)
+                    y._tfx_tail = TailPending(x, save, None, None, y, None)
+                elif defer_tail:
                     y = torch.empty_like(x)
                     mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
                     y._tfx_tail = TailPending(x, save, res_bnb.x if fuse_res else res.contiguous(),

@@ -1,0 +1,90 @@
+"""Stage-1 3x3 conv with its input BN applied on load (csrc/kernels/conv3x3_fused.hip): the kernel
+against the layer-wise pair (bn_apply + conv_fwd_bn) and an fp32 PyTorch conv, and the ResNet-50 first
+step with the deferred BN1 apply on vs off."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("shape", [(256, 32, 32), (2, 32, 32), (3, 8, 32)])
+def test_conv3x3_fwd_fused_matches_layerwise(gpu, shape):
+    N, H, W = shape
+    C = K = 64
+    torch.manual_seed(17)
+    y1 = _bf(torch.randn(N, H, W, C, device=gpu) * 1.3 + 0.2)
+    g1, b1 = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.3
+    ws1 = torch.zeros(64 * 2 * C, device=gpu)
+    _, save1, _ = torch.ops.tfx.bn_fwd_train(y1, g1, b1, None, None, 0.1, 1e-5, None, False, ws1, False)
+    w = _bf(torch.randn(K, 3, 3, C, device=gpu) * (1.0 / math.sqrt(9 * C)))
+    g2, b2 = torch.rand(K, device=gpu) + 0.5, torch.randn(K, device=gpu) * 0.2
+
+    a1, _ = torch.ops.tfx.bn_apply_train(y1, None, save1, True)
+    wsa = torch.zeros(64 * 2 * K, device=gpu)
+    rma, rva = torch.zeros(K, device=gpu), torch.ones(K, device=gpu)
+    y_ref, save_ref = torch.ops.tfx.conv_fwd_bn(a1, w, 1, 1, 1, wsa, g2, b2, rma, rva, 0.1, 1e-5)
+
+    ws = torch.zeros(64 * 2 * K, device=gpu)
+    rm, rv = torch.zeros(K, device=gpu), torch.ones(K, device=gpu)
+    y, save = torch.ops.tfx.conv3x3_fwd_fused(y1, save1, w, ws, g2, b2, rm, rv, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    ref = F.conv2d(a1.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 8e-3
+    assert _rel(y, y_ref) < 8e-3
+    assert ws.abs().max().item() == 0.0, "output BN slots not restored to zero"
+    yf = y.float().reshape(-1, K)
+    assert torch.allclose(save[:K], yf.mean(0), rtol=1e-3, atol=1e-3)
+    assert torch.allclose(save[K:2 * K], torch.rsqrt(yf.var(0, unbiased=False) + 1e-5), rtol=2e-3, atol=1e-3)
+    assert torch.allclose(save, save_ref, rtol=5e-3, atol=5e-3)
+    assert torch.allclose(rm, rma, rtol=1e-3, atol=1e-4) and torch.allclose(rv, rva, rtol=1e-3, atol=1e-4)
+
+
+def test_resnet50_deferred_bn1_matches_layerwise(gpu):
+    """ResNet-50 first step: stage-1 BN1 applied inside conv2 (conv3x3_fwd_fused) vs its own pass."""
+    from tensorflow_examples_amd import ops
+    from tensorflow_examples_amd.ops import nn as nnops
+
+    g = torch.Generator().manual_seed(21)
+    img = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 10, (32,), generator=g).to(gpu)
+    xin = to_model_input(img.to(gpu))
+
+    def run():
+        st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=6)
+        st.zero_grad()
+        loss = ops.softmax_cross_entropy(m(xin, training=True), lab)
+        loss.backward()
+        torch.cuda.synchronize()
+        return float(loss), st.grad.clone(), st
+
+    saved = nnops._DEFER_BN_IN
+    try:
+        n0 = nnops.CONV3_FWD_CALLS[0]
+        l0, g0, st = run()
+        assert nnops.CONV3_FWD_CALLS[0] - n0 == 3, "the three stage-1 conv2 run fused"
+        l1, g1, _ = run()
+        nnops._DEFER_BN_IN = False
+        l2, g2, _ = run()
+    finally:
+        nnops._DEFER_BN_IN = saved
+    assert abs(l0 - l2) <= max(4 * abs(l0 - l1), 0.01 * abs(l2)), (l0, l1, l2)
+    for v in st.trainable():
+        sl = slice(v.offset, v.offset + v.numel)
+        n = g0[sl].norm().item() + 1e-12
+        noise = (g1[sl] - g0[sl]).norm().item() / n
+        e = (g2[sl] - g0[sl]).norm().item() / n
+        assert e <= max(4 * noise, 2e-3), (v.name, e, noise)
