@@ -160,6 +160,23 @@ struct Conv3Args {
 };
 bool conv3x3_fused_ok(int N, int H, int W, int C, int K);
 void conv3x3_fwd_fused(const Conv3Args& a, hipStream_t s);
+// Backward: dy2 = BN2's backward apply (g2, y2, save2, red2) formed on load; dx = dgrad(dy2) with BN1's
+// backward partials (y1, save1; ReLU mask recomputed) into slots1; dW into per-block slabs [grid][64 * 576].
+struct Conv3BwdArgs {
+  const uint16_t* g2 = nullptr;
+  const uint16_t* y2 = nullptr;
+  const float* save2 = nullptr;
+  const float* red2 = nullptr;
+  const uint16_t* y1 = nullptr;
+  const float* save1 = nullptr;
+  const uint16_t* w = nullptr;
+  uint16_t* dx = nullptr;
+  float* slots1 = nullptr;
+  float* slab = nullptr;
+  int N = 0, H = 0;
+};
+int conv3x3_bwd_fused_grid(int N, int H);
+void conv3x3_bwd_fused(const Conv3BwdArgs& a, int nblocks, hipStream_t s);
 // the shortcut BN's reduction in pw_slab_reduce's tail (C = 0: none): red = [red3's sum g' | sum q]
 struct PwSecReduce {
   float* slots = nullptr;

@@ -170,6 +170,268 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
     }
 }
 
+// ---------------------------------------------------------------------------------------- backward
+// Layer-wise: bn_bwd_apply (dy2 = A2 (g2 relu2) + B2 y2 + D2, written), the data gradient (a flipped-tap
+// implicit GEMM over dy2, + BN1's backward partials in its epilogue) and the weight gradient (an
+// implicit GEMM over dy2 and a materialised a1 = relu(y1 sc1 + sh1)).  Here per 128-pixel tile the
+// block loads the g2 / y2 / y1 halos once and forms, in LDS, the dy2 halo (the data gradient's A
+// operand, shifted per tap; its interior is the weight gradient's A^T) and the a1 halo (the weight
+// gradient's B, shifted per tap); the raw y1 interior serves BN1's partials.  dA1 is stored; BN1's
+// partials go to its slots; the weight gradient accumulates in registers over the block's tiles
+// (64 x 576, 72 per thread) and leaves through a per-block slab (pw_bwd.hip pw_slab_reduce, map 2).
+// LDS: weights (MN images per tap, 72 KB) + dy2 halo + a1 halo + y1 interior + coefficient tables
+// (141 KB): the halos are single-buffered, the next tile's raw halos wait in registers.
+constexpr int C3_YBYTES = C3_BM * 128;  // raw y1 interior, K-major rows
+
+__global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[9 * C3_WTAP + 2 * C3_HBYTES + C3_YBYTES + 9 * C3_C * 4];
+  __shared__ float bnacc[2 * C3_C];  // BN1 backward partials of the block (sum g', sum g' xhat)
+  char* wimg = smem;
+  char* timg = wimg + 9 * C3_WTAP;   // dy2 halo
+  char* aimg = timg + C3_HBYTES;     // a1 halo
+  char* yimg = aimg + C3_HBYTES;     // raw y1, tile interior
+  float* coef = reinterpret_cast<float*>(yimg + C3_YBYTES);
+  // coef: [A2 | B2 | D2 | sc2 | sh2 | sc1 | sh1 | is1 | -mu1 is1] x 64
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int tiles_img = a.H / C3_TR, ntiles = a.N * tiles_img;
+
+  if (t < 2 * C3_C) bnacc[t] = 0.f;
+  if (t < C3_C) {
+    const float inv_m = 1.f / ((float)a.N * a.H * C3_IW);
+    const float mu = a.save2[t], is = a.save2[C3_C + t], sc = a.save2[2 * C3_C + t];
+    const float kg = a.red2[t] * inv_m, kx = a.red2[C3_C + t] * inv_m * is;
+    coef[t] = sc;
+    coef[C3_C + t] = -sc * kx;
+    coef[2 * C3_C + t] = sc * (kx * mu - kg);
+    coef[3 * C3_C + t] = sc;
+    coef[4 * C3_C + t] = a.save2[3 * C3_C + t];
+    const float is1 = a.save1[C3_C + t];
+    coef[5 * C3_C + t] = a.save1[2 * C3_C + t];
+    coef[6 * C3_C + t] = a.save1[3 * C3_C + t];
+    coef[7 * C3_C + t] = is1;
+    coef[8 * C3_C + t] = -a.save1[t] * is1;
+  }
+  // ---- W [K][3][3][C] -> per-tap MN images (row = output channel co, columns = ci), resident
+  for (int q = t; q < 9 * C3_C * 8; q += PW_NT) {
+    const int co = q / 72, rem = q % 72, tap = rem / 8, ch = rem % 8;
+    *reinterpret_cast<pw_u32x4*>(wimg + tap * C3_WTAP + pw_mn<64>(co, ch)) =
+        *reinterpret_cast<const pw_u32x4*>(a.w + (int64_t)co * 576 + tap * 64 + ch * 8);
+  }
+  const int64_t bytes = (int64_t)a.N * a.H * C3_IW * C3_C * 2;
+  const __amdgpu_buffer_rsrc_t rg = pw_rsrc(a.g2, bytes), ry2 = pw_rsrc(a.y2, bytes), ry1 = pw_rsrc(a.y1, bytes);
+  const __amdgpu_buffer_rsrc_t rdx = pw_rsrc(a.dx, bytes);
+
+  // halo pieces of this thread: chunk t % 8 (fixed), halo pixels t / 8 + 64 i
+  const int hch = t & 7;
+  struct Stage {
+    pw_u32x4 g[C3_PPT], y2[C3_PPT], y1[C3_PPT];
+  };
+  Stage st;
+  auto issue = [&](int tile) {
+    const bool ok = tile < ntiles;
+    const int n = tile / tiles_img, y0 = (tile % tiles_img) * C3_TR;
+#pragma unroll
+    for (int i = 0; i < C3_PPT; ++i) {
+      const int hp = (t >> 3) + 64 * i, hy = hp / C3_HW, hx = hp % C3_HW;
+      const int iy = y0 + hy - 1, ix = hx - 1;
+      const bool in = ok && hp < C3_HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)C3_IW;
+      const uint32_t off = in ? (uint32_t)(((n * a.H + iy) * C3_IW + ix) * C3_C + 8 * hch) * 2u : 0x80000000u;
+      st.g[i] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
+      st.y2[i] = __builtin_amdgcn_raw_buffer_load_b128(ry2, off, 0, 0);
+      st.y1[i] = __builtin_amdgcn_raw_buffer_load_b128(ry1, off, 0, 0);
+    }
+  };
+  // dy2 halo (BN2 backward apply), a1 halo (BN1 + ReLU), raw y1 interior; padding stays zero
+  auto stage = [&](int tile) {
+    const int y0 = (tile % tiles_img) * C3_TR;
+    // two passes (dy2, then a1 + raw y1) keep only one coefficient set live
+    {
+      float cA[8], cB[8], cD[8], s2[8], h2[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = 8 * hch + k;
+        cA[k] = coef[c]; cB[k] = coef[C3_C + c]; cD[k] = coef[2 * C3_C + c];
+        s2[k] = coef[3 * C3_C + c]; h2[k] = coef[4 * C3_C + c];
+      }
+#pragma unroll
+      for (int i = 0; i < C3_PPT; ++i) {
+        const int hp = (t >> 3) + 64 * i, hy = hp / C3_HW, hx = hp % C3_HW;
+        if (hp < C3_HP) {
+          const bool in = (unsigned)(y0 + hy - 1) < (unsigned)a.H && (unsigned)(hx - 1) < (unsigned)C3_IW;
+          float g[8], y2[8];
+          unpack8(__builtin_bit_cast(U4, st.g[i]), g);
+          unpack8(__builtin_bit_cast(U4, st.y2[i]), y2);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float gg = fmaf(y2[k], s2[k], h2[k]) > 0.f ? g[k] : 0.f;
+            g[k] = in ? fmaf(cA[k], gg, fmaf(cB[k], y2[k], cD[k])) : 0.f;
+          }
+          *reinterpret_cast<U4*>(timg + pw_kmaj(hp, hch)) = pack8(g);
+        }
+      }
+    }
+    {
+      float s1[8], h1[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] = coef[5 * C3_C + 8 * hch + k];
+        h1[k] = coef[6 * C3_C + 8 * hch + k];
+      }
+#pragma unroll
+      for (int i = 0; i < C3_PPT; ++i) {
+        const int hp = (t >> 3) + 64 * i, hy = hp / C3_HW, hx = hp % C3_HW;
+        if (hp < C3_HP) {
+          const bool in = (unsigned)(y0 + hy - 1) < (unsigned)a.H && (unsigned)(hx - 1) < (unsigned)C3_IW;
+          float y1[8];
+          unpack8(__builtin_bit_cast(U4, st.y1[i]), y1);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) y1[k] = in ? fmaxf(fmaf(y1[k], s1[k], h1[k]), 0.f) : 0.f;
+          *reinterpret_cast<U4*>(aimg + pw_kmaj(hp, hch)) = pack8(y1);
+          if (hy >= 1 && hy <= C3_TR && hx >= 1 && hx <= C3_IW)
+            *reinterpret_cast<pw_u32x4*>(yimg + pw_kmaj((hy - 1) * C3_IW + hx - 1, hch)) = st.y1[i];
+        }
+      }
+    }
+  };
+
+  // dgrad wave tile: output row wr = wv & 3 (2 m-tiles of 16 pixels), 32 input channels (wv >> 2); SWAP
+  const int wr = wv & 3, dcb = 32 * (wv >> 2);
+  // wgrad wave tile: output channels 32 (wv & 1: 2 m-tiles), (tap, 16-ci) column tiles 9 (wv >> 1) * 9 + nn
+  const int wco = 32 * (wv & 1), wng = 9 * (wv >> 1);
+  f32x4_t accw[2][9];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 9; ++nn) accw[m][nn] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int tile) {
+    // ---- data gradient: dA1[px][ci] = sum over taps of dy2(px + (1 - ky, 1 - kx)) . W[:, tap, ci]
+    {
+      f32x4_t acc[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int tap = 3 * ky + kx;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          bf16x8_t fa[2], fb[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int hp = (wr + 2 - ky) * C3_HW + 16 * i + (lane & 15) + 2 - kx;
+            fa[i] = *(const pw_lds_bf16x8*)((pw_lds_char*)timg + pw_kmaj(hp, 4 * kk + (lane >> 4)));
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            fb[j] = pw_frag_tr(wimg, tap * C3_WTAP + 32 * kk * 128, dcb + 16 * j, lane,
+                               [](int r, int c) { return pw_mn<64>(r, c); });
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        }
+      }
+      // epilogue: dA1 (bf16, 8-byte stores) + BN1 backward partials (ReLU mask from y1 sc1 + sh1 > 0)
+      const int n = tile / tiles_img, y0 = (tile % tiles_img) * C3_TR;
+      float bs[2][4], bq[2][4];  // this tile's BN1 partials of the lane's 8 columns
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bs[j][r] = bq[j][r] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int lpx = wr * C3_IW + 16 * i + (lane & 15);
+        const int pix = (n * a.H + y0 + wr) * C3_IW + 16 * i + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = dcb + 16 * j + (lane >> 4) * 4;
+          const uint32_t lo = pack_bf16x2(acc[i][j][0], acc[i][j][1]), hi = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+          __builtin_amdgcn_raw_buffer_store_b64((pw_u32x2){lo, hi}, rdx, (uint32_t)(pix * C3_C + col) * 2u, 0, 0);
+          const pw_u32x2 yv = *reinterpret_cast<const pw_u32x2*>(yimg + pw_kmaj(lpx, col >> 3) + ((col >> 2) & 1) * 8);
+          const float y1[4] = {__uint_as_float(yv[0] << 16), __uint_as_float(yv[0] & 0xffff0000u),
+                               __uint_as_float(yv[1] << 16), __uint_as_float(yv[1] & 0xffff0000u)};
+          const float gv[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u), __uint_as_float(hi << 16),
+                               __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = col + r;
+            const float gp = fmaf(y1[r], coef[5 * C3_C + c], coef[6 * C3_C + c]) > 0.f ? gv[r] : 0.f;
+            bs[j][r] += gp;
+            bq[j][r] = fmaf(gp, fmaf(y1[r], coef[7 * C3_C + c], coef[8 * C3_C + c]), bq[j][r]);
+          }
+        }
+      }
+      // the 16 rows of each DPP row share columns: reduce, one LDS float atomic per column and wave
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sv = row16_sum(bs[j][r]), qv = row16_sum(bq[j][r]);
+          if ((lane & 15) == 0) {
+            const int c = dcb + 16 * j + (lane >> 4) * 4 + r;
+            atomicAdd(&bnacc[c], sv);
+            atomicAdd(&bnacc[C3_C + c], qv);
+          }
+        }
+    }
+    // ---- weight gradient: dW[co][tap][ci] += sum over the tile's pixels of dy2[px][co] a1[px + tap - 1][ci]
+#pragma unroll 1
+    for (int r = 0; r < C3_TR; ++r) {  // k-step = one output row (32 pixels)
+      const int hp0 = (r + 1) * C3_HW + 1;
+      bf16x8_t fa[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        fa[m] = pw_frag_tr(timg, 0, wco + 16 * m, lane, [hp0](int kr, int c) { return pw_kmaj(hp0 + kr, c); });
+#pragma unroll
+      for (int nn = 0; nn < 9; ++nn) {
+        const int idx = wng + nn, tap = idx >> 2, cit = idx & 3, ky = tap / 3, kx = tap % 3;
+        const int hb0 = (r + ky) * C3_HW + kx;
+        const bf16x8_t fb = pw_frag_tr(aimg, 0, 16 * cit, lane, [hb0](int kr, int c) { return pw_kmaj(hb0 + kr, c); });
+#pragma unroll
+        for (int m = 0; m < 2; ++m) accw[m][nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb, accw[m][nn], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // bound the fragment reads hoisted ahead
+      }
+    }
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  const int tile0 = blockIdx.x, tstep = gridDim.x;
+  issue(tile0);
+  __syncthreads();  // weight images, coefficient tables written
+  if (tile0 < ntiles) {
+    stage(tile0);
+    issue(tile0 + tstep);
+    sync();
+  }
+  for (int tile = tile0; tile < ntiles; tile += tstep) {
+    compute(tile);
+    const int nt = tile + tstep;
+    if (nt >= ntiles) break;
+    sync();  // every wave is done with this tile's halos
+    stage(nt);
+    issue(nt + tstep);
+    sync();
+  }
+
+  // ---- weight-gradient accumulators -> this block's slab, register order (coalesced 16-B stores)
+  float* slab = a.slab + (size_t)blockIdx.x * (C3_C * 576);
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 9; ++nn)
+      *reinterpret_cast<f32x4_t*>(slab + ((size_t)(m * 9 + nn) * PW_NT + t) * 4) = accw[m][nn];
+  // ---- BN1 partials of the block -> its slot (one global atomic per value)
+  __syncthreads();
+  if (t < 2 * C3_C) atomicAdd(a.slots1 + (size_t)(blockIdx.x % NSLOT) * 2 * C3_C + t, bnacc[t]);
+}
+
 }  // namespace
 
 bool conv3x3_fused_ok(int N, int H, int W, int C, int K) {
@@ -179,6 +441,12 @@ bool conv3x3_fused_ok(int N, int H, int W, int C, int K) {
 void conv3x3_fwd_fused(const Conv3Args& a, hipStream_t s) {
   const int ntiles = a.N * (a.H / C3_TR);
   conv3x3_fwd_fused_kernel<<<std::min(256, ntiles), PW_NT, 0, s>>>(a);
+}
+
+int conv3x3_bwd_fused_grid(int N, int H) { return std::min(256, N * (H / C3_TR)); }
+
+void conv3x3_bwd_fused(const Conv3BwdArgs& a, int nblocks, hipStream_t s) {
+  conv3x3_bwd_fused_kernel<<<nblocks, PW_NT, 0, s>>>(a);
 }
 
 }  // namespace tfx

@@ -623,14 +623,26 @@ __device__ __forceinline__ int pw_slab_to_dw(int e) {
 constexpr int PW_RG = 8;
 // SEC tail (sec_C > 0): the shortcut BN's reduction -- red_sc = [red3's sum g' | sum of the q slots]
 // (its slots' first halves are never written), dbeta_sc / dgamma_sc +=, q slots re-zeroed.
-// MAP: the slab's register-order layout -- 0 = F3's dW3 (CW x CN), 1 = F1's dW1 (CO = CN x CI = 4 CN)
+// conv3x3_fused.hip backward slab element e = ((m * 9 + nn) * NT + t) * 4 + r  ->  dW [co][tap][ci]:
+// lane = t & 63, wave = t >> 6; co = 32 (wave & 1) + 16 m + (lane >> 4) * 4 + r; column tile
+// idx = 9 (wave >> 1) + nn: tap = idx / 4, ci = 16 (idx % 4) + (lane & 15)
+__device__ __forceinline__ int pw_slab_to_dw_c3(int e) {
+  const int r = e & 3, t = (e >> 2) % PW_NT, mn = (e >> 2) / PW_NT;
+  const int m = mn / 9, nn = mn % 9, lane = t & 63, wv = t >> 6;
+  const int co = 32 * (wv & 1) + 16 * m + (lane >> 4) * 4 + r;
+  const int idx = 9 * (wv >> 1) + nn;
+  return co * 576 + (idx >> 2) * 64 + 16 * (idx & 3) + (lane & 15);
+}
+
+// MAP: the slab's register-order layout -- 0 = F3's dW3 (CW x CN), 1 = F1's dW1 (CO = CN x CI = 4 CN),
+// 2 = the stage-1 3x3 conv's dW (64 x 9 x 64)
 template <int CN, int MAP>
 __global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __restrict__ slab, int nslab,
                                                              float* __restrict__ dw, float* __restrict__ sr_slots,
                                                              int sr_C, float* __restrict__ sr_red,
                                                              float* __restrict__ sr_dgamma,
                                                              float* __restrict__ sr_dbeta, PwSecReduce sec) {
-  constexpr int E = 4 * CN * CN;
+  constexpr int E = MAP == 2 ? 64 * 576 : 4 * CN * CN;
   const int ngemm = (E / 256) * PW_RG;
   const int nsr = sr_C ? (sr_C + 15) / 16 : 0;
   if ((int)blockIdx.x >= ngemm + nsr) {
@@ -712,7 +724,8 @@ __global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __rest
   }
   for (; b < nslab; b += PW_RG) acc += slab[(size_t)b * E + e];
   if constexpr (MAP == 0) atomicAdd(dw + pw_slab_to_dw<CN>(e), acc);
-  else atomicAdd(dw + pw_slab_to_dw1<4 * CN, CN>(e), acc);
+  else if constexpr (MAP == 1) atomicAdd(dw + pw_slab_to_dw1<4 * CN, CN>(e), acc);
+  else atomicAdd(dw + pw_slab_to_dw_c3(e), acc);
 }
 
 }  // namespace
@@ -746,7 +759,7 @@ void pw_bwd_squeeze(const PwSqueezeBwdArgs& args, int nblocks, hipStream_t s) {
 
 void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_slots, int sr_C, float* sr_red,
                     float* sr_dgamma, float* sr_dbeta, const PwSecReduce& sec, hipStream_t s, int map) {
-  const int E = 4 * CN * CN;
+  const int E = map == 2 ? 64 * 576 : 4 * CN * CN;
   const int nsr = sr_slots ? (sr_C + 15) / 16 : 0;
   const int grid = (E / 256) * PW_RG + nsr + (sec.C ? (sec.C + 15) / 16 : 0);
   switch (CN) {
@@ -754,8 +767,11 @@ void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_s
       if (map == 0)
         pw_slab_reduce_kernel<64, 0><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
                                                           sr_dgamma, sr_dbeta, sec);
-      else
+      else if (map == 1)
         pw_slab_reduce_kernel<64, 1><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
+                                                          sr_dgamma, sr_dbeta, sec);
+      else
+        pw_slab_reduce_kernel<64, 2><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
                                                           sr_dgamma, sr_dbeta, sec);
       break;
     default: abort();

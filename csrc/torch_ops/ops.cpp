@@ -349,6 +349,35 @@ std::tuple<Tensor, Tensor> conv3x3_fwd_fused(Tensor x, Tensor save_in, Tensor w,
   return {y, save};
 }
 
+// Backward of the stage-1 3x3 conv with both BN layers fused (conv3x3_fused.hip): g2 / y2 / save2 / red2
+// = the output BN's gradient, input, stats and backward reduction (its apply formed on load); y1 / save1
+// = the input BN's input and stats (its ReLU output formed on load for the weight gradient).  dw += dW;
+// returns (dx = the input BN's output gradient, red1 = its backward reduction) with dgamma1 / dbeta1 +=.
+std::tuple<Tensor, Tensor> conv3x3_bwd_fused(Tensor g2, Tensor y2, Tensor save2, Tensor red2, Tensor y1, Tensor save1,
+                                             Tensor w, Tensor dw, Tensor slots1, optional<Tensor> dgamma1,
+                                             optional<Tensor> dbeta1) {
+  CHECK_DEV(g2); CHECK_BF16(g2); CHECK_CONTIG(g2); CHECK_BF16(y2); CHECK_CONTIG(y2); CHECK_BF16(y1); CHECK_CONTIG(y1);
+  CHECK_BF16(w); CHECK_CONTIG(w); CHECK_F32(dw); CHECK_CONTIG(dw); CHECK_F32(save2); CHECK_F32(red2); CHECK_F32(save1);
+  TORCH_CHECK(y1.dim() == 4 && g2.sizes() == y1.sizes() && y2.sizes() == y1.sizes(), "conv3x3_bwd_fused: shapes");
+  const int N = (int)y1.size(0), H = (int)y1.size(1), W = (int)y1.size(2), C = (int)y1.size(3), K = (int)w.size(0);
+  TORCH_CHECK(tfx::conv3x3_fused_ok(N, H, W, C, K) && w.numel() == (int64_t)K * 9 * C && dw.numel() == w.numel(),
+              "conv3x3_bwd_fused: unsupported geometry");
+  TORCH_CHECK(save2.numel() == 4 * K && red2.numel() == 2 * K && save1.numel() == 4 * C, "conv3x3_bwd_fused: stats");
+  check_bn_ws(slots1, C);
+  auto dx = at::empty_like(y1);
+  auto red1 = at::empty({2 * C}, y1.options().dtype(at::kFloat));
+  const int nb = tfx::conv3x3_bwd_fused_grid(N, H);
+  auto slab = at::empty({(int64_t)nb * K * 9 * C}, y1.options().dtype(at::kFloat));
+  tfx::Conv3BwdArgs a;
+  a.g2 = bf(g2); a.y2 = bf(y2); a.save2 = save2.data_ptr<float>(); a.red2 = red2.data_ptr<float>(); a.y1 = bf(y1);
+  a.save1 = save1.data_ptr<float>(); a.w = bf(w); a.dx = bfm(dx); a.slots1 = slots1.data_ptr<float>();
+  a.slab = slab.data_ptr<float>(); a.N = N; a.H = H;
+  tfx::conv3x3_bwd_fused(a, nb, cur_stream());
+  tfx::pw_slab_reduce(a.slab, nb, 64, dw.data_ptr<float>(), a.slots1, C, red1.data_ptr<float>(), fpm(dgamma1),
+                      fpm(dbeta1), tfx::PwSecReduce{}, cur_stream(), 2);
+  return {dx, red1};
+}
+
 bool conv3x3_fused_supported(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K) {
   return tfx::conv3x3_fused_ok((int)N, (int)H, (int)W, (int)C, (int)K);
 }
@@ -1608,6 +1637,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_apply_into", &bn_apply_into);
   m.def("conv3x3_fwd_fused", &conv3x3_fwd_fused);
   m.def("conv3x3_fused_supported", &conv3x3_fused_supported);
+  m.def("conv3x3_bwd_fused", &conv3x3_bwd_fused);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd(Tensor g, Tensor x, Tensor? res, Tensor save, bool relu, Tensor slots, Tensor? dgamma, "
         "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);

@@ -130,6 +130,7 @@ class LazyBNGrad:
 # test hooks: False keeps every block tail / plain BN applied by its own pass (the layer-wise forward)
 _DEFER_TAIL = True
 _DEFER_BN_IN = True
+_FUSE_CONV3_BWD = True  # False: the stage-1 3x3 conv's backward runs layer-wise (forward still fused)
 PW_SQUEEZE_CALLS = [0]  # fused tail + conv1 forward launches (tests)
 
 
@@ -162,6 +163,19 @@ def _settle(t):
 
 
 CONV3_FWD_CALLS = [0]  # fused stage-1 3x3 forward launches (tests)
+CONV3_BWD_CALLS = [0]  # ... and backward launches
+
+
+def _conv3_bwd_fused_ok(w, lazy, bnb, tp) -> bool:
+    """The stage-1 3x3 conv's fused backward (conv3x3_fused.hip) applies: its output gradient is a plain
+    ReLU BN's lazy input gradient, its input the deferred output of the plain ReLU BN ``bnb`` (the
+    forward ran conv3x3_fwd_fused), whose backward partials nobody reduced yet."""
+    if not _FUSE_CONV3_BWD or lazy.mask is not None or lazy.sec is not None or lazy.dy is not None \
+            or not w.trainable:
+        return False
+    if bnb is None or bnb.mask is not None or not bnb.relu or bnb.deferred or bnb.red is not None or bnb.sr_pending:
+        return False
+    return bnb.x is tp.x and lazy.g.shape == tp.x.shape
 
 
 def _conv3_fused_ok(x, w, stride, pad, dil, stats_into) -> bool:
@@ -260,14 +274,24 @@ class _Conv2d(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, *unused):
         (x,) = ctx.saved_tensors
-        tp = getattr(ctx, "pending_in", None)
-        if tp is not None:
-            tp.materialize()  # the forward applied the input BN on load only
         w = ctx.w
         stride, pad, dil = ctx.cfg
         need_dx = ctx.needs_input_grad[0]
+        tp = getattr(ctx, "pending_in", None)
+        lazy = getattr(gy, "_tfx_lazy_bnbwd", None) if ctx.native else None
+        if tp is not None and not tp.done and lazy is not None and need_dx and _conv3_bwd_fused_ok(w, lazy, ctx.bnb, tp):
+            # the stage-1 3x3 conv's whole backward: the output BN's backward apply and the input BN's ReLU
+            # output formed on load, data + weight gradient, the input BN's backward partials
+            # (conv3x3_fused.hip) -- neither dy nor x is ever written
+            bnb = ctx.bnb
+            dx, bnb.red = torch.ops.tfx.conv3x3_bwd_fused(lazy.g.contiguous(), lazy.x, lazy.save, lazy.red, tp.x,
+                                                          tp.save, w.value, w.grad, bnb.ws, bnb.dgamma, bnb.dbeta)
+            CONV3_BWD_CALLS[0] += 1
+            _grad_ready(w)
+            return dx, None, None, None, None, None, None, None, None
+        if tp is not None:
+            tp.materialize()  # the forward applied the input BN on load only
         if ctx.native:
-            lazy = getattr(gy, "_tfx_lazy_bnbwd", None)
             if lazy is not None:
                 if need_dx and _pw_squeeze_bwd_ok(x, w, stride, pad, dil, lazy, ctx.sink, ctx.bnb):
                     # BN1's backward apply + this conv's data AND weight gradient in one launch, the

@@ -53,6 +53,46 @@ def test_conv3x3_fwd_fused_matches_layerwise(gpu, shape):
     assert torch.allclose(rm, rma, rtol=1e-3, atol=1e-4) and torch.allclose(rv, rva, rtol=1e-3, atol=1e-4)
 
 
+@pytest.mark.parametrize("shape", [(256, 32, 32), (2, 32, 32), (3, 8, 32)])
+def test_conv3x3_bwd_fused_matches_reference(gpu, shape):
+    """Backward: BN2's apply + BN1's ReLU output on load, data and weight gradient, BN1's partials --
+    vs the layer-wise apply kernels and fp32 PyTorch conv gradients."""
+    N, H, W = shape
+    C = K = 64
+    torch.manual_seed(19)
+    y1 = _bf(torch.randn(N, H, W, C, device=gpu) * 1.2 + 0.1)
+    y2 = _bf(torch.randn(N, H, W, K, device=gpu) * 0.9 + 0.2)
+    g2 = _bf(torch.randn(N, H, W, K, device=gpu))
+    ws1, ws2 = torch.zeros(64 * 2 * C, device=gpu), torch.zeros(64 * 2 * K, device=gpu)
+    _, save1, _ = torch.ops.tfx.bn_fwd_train(y1, torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.3,
+                                             None, None, 0.1, 1e-5, None, False, ws1, False)
+    _, save2, _ = torch.ops.tfx.bn_fwd_train(y2, torch.rand(K, device=gpu) + 0.5, torch.randn(K, device=gpu) * 0.3,
+                                             None, None, 0.1, 1e-5, None, False, ws2, False)
+    _, _, red2 = torch.ops.tfx.bn_bwd(g2, y2, None, save2, True, ws2, None, None, None, False)
+    w = _bf(torch.randn(K, 3, 3, C, device=gpu) * (1.0 / math.sqrt(9 * C)))
+    dy2 = torch.ops.tfx.bn_bwd_apply(g2, y2, None, save2, red2, True, None, False)[0]
+    a1 = torch.ops.tfx.bn_apply_train(y1, None, save1, True)[0]
+
+    dw = torch.zeros(K, 3, 3, C, device=gpu)
+    dg1, db1 = torch.full((C,), 0.5, device=gpu), torch.full((C,), -1.0, device=gpu)
+    dx, red1 = torch.ops.tfx.conv3x3_bwd_fused(g2, y2, save2, red2, y1, save1, w, dw, ws1, dg1, db1)
+    torch.cuda.synchronize()
+    xr = a1.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(dy2.float().permute(0, 3, 1, 2))
+    assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 8e-3
+    assert _rel(dw, wr.grad.permute(0, 2, 3, 1)) < 2e-3
+    assert ws1.abs().max().item() == 0.0, "BN1 slots not restored to zero"
+    M = N * H * W
+    y1f = y1.float().reshape(M, C)
+    relu1 = ((y1f * save1[2 * C:3 * C] + save1[3 * C:]) > 0).float()
+    gp = dx.float().reshape(M, C) * relu1
+    xh = (y1f - save1[:C]) * save1[C:2 * C]
+    ref_s, ref_q = gp.sum(0), (gp * xh).sum(0)
+    assert _rel(red1[:C], ref_s) < 1e-4 and _rel(red1[C:], ref_q) < 2e-4
+    assert _rel(db1 + 1.0, ref_s) < 1e-4 and _rel(dg1 - 0.5, ref_q) < 2e-4
+
+
 def test_resnet50_deferred_bn1_matches_layerwise(gpu):
     """ResNet-50 first step: stage-1 BN1 applied inside conv2 (conv3x3_fwd_fused) vs its own pass."""
     from tensorflow_examples_amd import ops
@@ -73,9 +113,10 @@ def test_resnet50_deferred_bn1_matches_layerwise(gpu):
 
     saved = nnops._DEFER_BN_IN
     try:
-        n0 = nnops.CONV3_FWD_CALLS[0]
+        n0, n1 = nnops.CONV3_FWD_CALLS[0], nnops.CONV3_BWD_CALLS[0]
         l0, g0, st = run()
         assert nnops.CONV3_FWD_CALLS[0] - n0 == 3, "the three stage-1 conv2 run fused"
+        assert nnops.CONV3_BWD_CALLS[0] - n1 == 3, "... forward and backward"
         l1, g1, _ = run()
         nnops._DEFER_BN_IN = False
         l2, g2, _ = run()
