@@ -57,9 +57,11 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
     const int n = tile / tiles_img, y0 = (tile % tiles_img) * C3_TR;
 #pragma unroll
     for (int i = 0; i < C3_PPT; ++i) {
-      const int hp = (t >> 3) + 64 * i, hy = hp / C3_HW, hx = hp % C3_HW;
+      // pieces past the halo re-load its last pixel (identical duplicate writes): no branch in the
+      // load path, so hipcc keeps the counted waits instead of draining vmcnt at a join
+      const int hp = min((t >> 3) + 64 * i, C3_HP - 1), hy = hp / C3_HW, hx = hp % C3_HW;
       const int iy = y0 + hy - 1, ix = hx - 1;
-      const bool in = ok && hp < C3_HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)C3_IW;
+      const bool in = ok & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)C3_IW);
       const uint32_t off = in ? (uint32_t)(((n * a.H + iy) * C3_IW + ix) * C3_C + 8 * hch) * 2u : 0x80000000u;
       s.v[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
     }
@@ -69,16 +71,13 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
     const int y0 = (tile % tiles_img) * C3_TR;
 #pragma unroll
     for (int i = 0; i < C3_PPT; ++i) {
-      const int hp = (t >> 3) + 64 * i, hy = hp / C3_HW, hx = hp % C3_HW;
-      if (hp < C3_HP) {
-        const int iy = y0 + hy - 1, ix = hx - 1;
-        const bool in = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)C3_IW;
-        float f[8];
-        unpack8(__builtin_bit_cast(U4, s.v[i]), f);
+      const int hp = min((t >> 3) + 64 * i, C3_HP - 1), hy = hp / C3_HW, hx = hp % C3_HW;
+      const bool in = ((unsigned)(y0 + hy - 1) < (unsigned)a.H) & ((unsigned)(hx - 1) < (unsigned)C3_IW);
+      float f[8];
+      unpack8(__builtin_bit_cast(U4, s.v[i]), f);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) f[k] = in ? fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f) : 0.f;
-        *reinterpret_cast<U4*>(img + pw_kmaj(hp, hch)) = pack8(f);
-      }
+      for (int k = 0; k < 8; ++k) f[k] = in ? fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f) : 0.f;
+      *reinterpret_cast<U4*>(img + pw_kmaj(hp, hch)) = pack8(f);
     }
   };
   // wave tile: output row r = wv & 3 of the tile (32 pixels = 2 m-tiles), 32 output channels (wv >> 2)
@@ -184,13 +183,13 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
 constexpr int C3_YBYTES = C3_BM * 128;  // raw y1 interior, K-major rows
 
 __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[9 * C3_WTAP + 2 * C3_HBYTES + C3_YBYTES + 9 * C3_C * 4];
+  __shared__ __attribute__((aligned(16))) char smem[9 * C3_WTAP + 2 * C3_HBYTES + C3_YBYTES + 16 + 9 * C3_C * 4];
   __shared__ float bnacc[2 * C3_C];  // BN1 backward partials of the block (sum g', sum g' xhat)
   char* wimg = smem;
   char* timg = wimg + 9 * C3_WTAP;   // dy2 halo
   char* aimg = timg + C3_HBYTES;     // a1 halo
   char* yimg = aimg + C3_HBYTES;     // raw y1, tile interior
-  float* coef = reinterpret_cast<float*>(yimg + C3_YBYTES);
+  float* coef = reinterpret_cast<float*>(yimg + C3_YBYTES + 16);  // (+ the 16-B trash slot)
   // coef: [A2 | B2 | D2 | sc2 | sh2 | sc1 | sh1 | is1 | -mu1 is1] x 64
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int tiles_img = a.H / C3_TR, ntiles = a.N * tiles_img;
@@ -232,9 +231,11 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
     const int n = tile / tiles_img, y0 = (tile % tiles_img) * C3_TR;
 #pragma unroll
     for (int i = 0; i < C3_PPT; ++i) {
-      const int hp = (t >> 3) + 64 * i, hy = hp / C3_HW, hx = hp % C3_HW;
+      // pieces past the halo re-load its last pixel (identical duplicate writes): no branch in the
+      // load path, so hipcc keeps the counted waits instead of draining vmcnt at a join
+      const int hp = min((t >> 3) + 64 * i, C3_HP - 1), hy = hp / C3_HW, hx = hp % C3_HW;
       const int iy = y0 + hy - 1, ix = hx - 1;
-      const bool in = ok && hp < C3_HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)C3_IW;
+      const bool in = ok & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)C3_IW);
       const uint32_t off = in ? (uint32_t)(((n * a.H + iy) * C3_IW + ix) * C3_C + 8 * hch) * 2u : 0x80000000u;
       st.g[i] = __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0);
       st.y2[i] = __builtin_amdgcn_raw_buffer_load_b128(ry2, off, 0, 0);
@@ -255,19 +256,18 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
       }
 #pragma unroll
       for (int i = 0; i < C3_PPT; ++i) {
-        const int hp = (t >> 3) + 64 * i, hy = hp / C3_HW, hx = hp % C3_HW;
-        if (hp < C3_HP) {
-          const bool in = (unsigned)(y0 + hy - 1) < (unsigned)a.H && (unsigned)(hx - 1) < (unsigned)C3_IW;
-          float g[8], y2[8];
-          unpack8(__builtin_bit_cast(U4, st.g[i]), g);
-          unpack8(__builtin_bit_cast(U4, st.y2[i]), y2);
+        const int hp = min((t >> 3) + 64 * i, C3_HP - 1), hy = hp / C3_HW, hx = hp % C3_HW;
+        const bool in = ((unsigned)(y0 + hy - 1) < (unsigned)a.H) & ((unsigned)(hx - 1) < (unsigned)C3_IW);
+        float g[8], y2[8];
+        unpack8(__builtin_bit_cast(U4, st.g[i]), g);
+        unpack8(__builtin_bit_cast(U4, st.y2[i]), y2);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const float gg = fmaf(y2[k], s2[k], h2[k]) > 0.f ? g[k] : 0.f;
-            g[k] = in ? fmaf(cA[k], gg, fmaf(cB[k], y2[k], cD[k])) : 0.f;
-          }
-          *reinterpret_cast<U4*>(timg + pw_kmaj(hp, hch)) = pack8(g);
+        for (int k = 0; k < 8; ++k) {
+          const float gg = fmaf(y2[k], s2[k], h2[k]) > 0.f ? g[k] : 0.f;
+          g[k] = in ? fmaf(cA[k], gg, fmaf(cB[k], y2[k], cD[k])) : 0.f;
         }
+        *reinterpret_cast<U4*>(timg + pw_kmaj(hp, hch)) = pack8(g);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     {
@@ -279,17 +279,17 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
       }
 #pragma unroll
       for (int i = 0; i < C3_PPT; ++i) {
-        const int hp = (t >> 3) + 64 * i, hy = hp / C3_HW, hx = hp % C3_HW;
-        if (hp < C3_HP) {
-          const bool in = (unsigned)(y0 + hy - 1) < (unsigned)a.H && (unsigned)(hx - 1) < (unsigned)C3_IW;
-          float y1[8];
-          unpack8(__builtin_bit_cast(U4, st.y1[i]), y1);
+        const int hp = min((t >> 3) + 64 * i, C3_HP - 1), hy = hp / C3_HW, hx = hp % C3_HW;
+        const bool in = ((unsigned)(y0 + hy - 1) < (unsigned)a.H) & ((unsigned)(hx - 1) < (unsigned)C3_IW);
+        float y1[8];
+        unpack8(__builtin_bit_cast(U4, st.y1[i]), y1);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) y1[k] = in ? fmaxf(fmaf(y1[k], s1[k], h1[k]), 0.f) : 0.f;
-          *reinterpret_cast<U4*>(aimg + pw_kmaj(hp, hch)) = pack8(y1);
-          if (hy >= 1 && hy <= C3_TR && hx >= 1 && hx <= C3_IW)
-            *reinterpret_cast<pw_u32x4*>(yimg + pw_kmaj((hy - 1) * C3_IW + hx - 1, hch)) = st.y1[i];
-        }
+        for (int k = 0; k < 8; ++k) y1[k] = in ? fmaxf(fmaf(y1[k], s1[k], h1[k]), 0.f) : 0.f;
+        *reinterpret_cast<U4*>(aimg + pw_kmaj(hp, hch)) = pack8(y1);
+        // raw y1 of the tile interior; border pixels go to a trash slot past the image (no branch)
+        const bool inner = ((unsigned)(hy - 1) < (unsigned)C3_TR) & ((unsigned)(hx - 1) < (unsigned)C3_IW);
+        *reinterpret_cast<pw_u32x4*>(yimg + (inner ? pw_kmaj((hy - 1) * C3_IW + hx - 1, hch) : C3_YBYTES)) = st.y1[i];
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   };
