@@ -72,6 +72,110 @@ class AsyncPSWorker:
         return hits / len(images)
 
 
+class GraphedPSLoop:
+    """The asynchronous xGMI worker step as ONE HIP graph (``--transport=xgmi``, async replicas).
+
+    Per replay, all on the device: the feed -- the batch gathered from the training set resident
+    on the GPU at a device-side cursor (the ``feed_dict`` of R/distributed/distributed.py:150
+    without a host hop) -- the PULL of every variable out of the ps arenas (xGMI reads), forward,
+    the reference's naive cross-entropy and accuracy, backward, the peer SGD into the ps arenas
+    and the global-step bump behind it (R/distributed/distributed.py:107-108), and one row
+    (cost, accuracy, global step) of a device-side history ring.  The host only enqueues replays;
+    it reads the history back at the log cadence (``read``), where the per-step summaries are
+    written.  ``dataset`` keeps TF1's ``next_batch`` order (the same RNG draws): the arrangement is
+    permuted on the device at each epoch boundary, between replays.
+    Requires ``num_examples % batch_size == 0`` (no batch straddles an epoch)."""
+
+    EAGER_STEPS = 2  # run eagerly before the capture (allocator / autograd warm-up)
+
+    def __init__(self, worker: AsyncPSWorker, dataset, batch_size: int, ring: int = 128):
+        self.w, self.ds, self.B = worker, dataset, int(batch_size)
+        self.dev = worker.device
+        self.N = int(dataset.num_examples)
+        if self.N % self.B:
+            raise ValueError("GraphedPSLoop needs num_examples % batch_size == 0")
+        self.X = torch.as_tensor(np.ascontiguousarray(dataset.images, dtype=np.float32)).to(self.dev)
+        self.Y = torch.as_tensor(np.ascontiguousarray(dataset.labels, dtype=np.float32)).to(self.dev)
+        self.ar = torch.arange(self.B, device=self.dev)
+        self.cursor = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.ring = int(ring)
+        self.hist = torch.zeros(self.ring, 3, dtype=torch.float64, device=self.dev)
+        self.k = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.hist_host = torch.zeros(self.ring, 3, dtype=torch.float64, pin_memory=True)
+        self.start = 0          # host mirror of the cursor (TF1 DataSet._index_in_epoch)
+        self.pending = 0        # replays since the last read
+        self.steps = 0
+        self.graph = None
+
+    # ---- feed order: TF1 DataSet.next_batch (R/.../input_data.py), index-only
+    def _advance(self) -> None:
+        ds = self.ds
+        if ds._epochs_completed == 0 and self.start == 0 and ds._index_in_epoch == 0:
+            self._permute()
+        if self.start + self.B > self.N:
+            ds._epochs_completed += 1
+            self._permute()
+            self.start = 0
+            self.cursor.zero_()
+        self.start += self.B
+        ds._index_in_epoch = self.start
+
+    def _permute(self) -> None:
+        perm = np.arange(self.N)
+        self.ds._rng.shuffle(perm)
+        p = torch.as_tensor(perm, device=self.dev)
+        self.X.copy_(self.X.index_select(0, p))
+        self.Y.copy_(self.Y.index_select(0, p))
+
+    def _body(self) -> None:
+        w = self.w
+        idx = self.cursor + self.ar
+        x, y = self.X.index_select(0, idx), self.Y.index_select(0, idx)
+        self.cursor.add_(self.B)
+        w.client.pull()
+        logits = w.model.logits(x)
+        loss = ops.softmax_cross_entropy(logits, y, naive=w.naive)
+        acc = ops.accuracy(logits.detach(), y)
+        loss.backward()
+        step = w.client.push_async(w.lr, zero_grad=True)
+        row = torch.stack([loss.detach().double().reshape(()), acc.double().reshape(()),
+                           (step.double() - 1).reshape(())])
+        self.hist.index_copy_(0, self.k, row[None])
+        self.k.add_(1)
+
+    def step(self) -> None:
+        """Enqueue one training step (no host sync)."""
+        if self.pending >= self.ring:
+            raise RuntimeError("GraphedPSLoop: read() the history at least every %d steps" % self.ring)
+        self._advance()
+        if self.graph is None and self.steps >= self.EAGER_STEPS:
+            s = torch.cuda.Stream(self.dev)
+            s.wait_stream(torch.cuda.current_stream(self.dev))
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(self.graph, stream=s):
+                    self._body()
+            torch.cuda.current_stream(self.dev).wait_stream(s)
+            # the capture recorded the work without running it: replay it for this step
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.w.store.zero_grad()
+            self._body()
+        self.w._grad_clean = True
+        self.pending += 1
+        self.steps += 1
+
+    def read(self):
+        """(cost, accuracy, global step before the update) of every step since the last read."""
+        n = self.pending
+        self.hist_host[:n].copy_(self.hist[:n], non_blocking=True)
+        torch.cuda.current_stream(self.dev).synchronize()
+        self.k.zero_()
+        self.pending = 0
+        return [(float(c), float(a), int(st)) for c, a, st in self.hist_host[:n].tolist()]
+
+
 class SyncReplicasPSWorker(AsyncPSWorker):
     """Synchronous replicas over the parameter server (``--sync_replicas``).
 

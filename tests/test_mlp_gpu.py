@@ -79,6 +79,47 @@ def test_distributed_script_on_gpu(tmp_path, transport, num_ps):
     assert max(finals) == 2 * epochs * batches, finals
 
 
+def test_xgmi_graph_loop_matches_eager(tmp_path):
+    """One ps + one worker over xGMI: the graphed step (device-resident feed in TF1 next_batch order,
+    pull/fwd/bwd/peer-SGD/step-bump in one HIP graph, cost read back at the log cadence) prints the
+    same progress lines as the eager per-step loop (parallel/ps_worker.py GraphedPSLoop)."""
+    import re
+    import socket
+
+    def run(graph):
+        s = [socket.socket() for _ in range(2)]
+        for x in s:
+            x.bind(("127.0.0.1", 0))
+        ps, wk = [x.getsockname()[1] for x in s]
+        for x in s:
+            x.close()
+        script = os.path.join(ROOT, "distributed", "distributed.py")
+        args = [f"--ps_hosts=127.0.0.1:{ps}", f"--worker_hosts=127.0.0.1:{wk}", "--device=cuda",
+                f"--logs_path={tmp_path / str(graph)}", "--training_epochs=2", "--max_batches_per_epoch=300",
+                "--ps_exit_after_workers", "--transport=xgmi", "--xgmi_arena_mb=4", f"--graph={graph}"]
+        p = subprocess.Popen([sys.executable, script, *args, "--job_name=ps", "--task_index=0"])
+        w = subprocess.Popen([sys.executable, script, *args, "--job_name=worker", "--task_index=0"],
+                             stdout=subprocess.PIPE, text=True)
+        try:
+            out = w.communicate(timeout=300)[0]
+            assert w.returncode == 0, out
+            assert p.wait(timeout=60) == 0
+        finally:
+            for x in (p, w):
+                if x.poll() is None:
+                    x.kill()
+        steps = [int(m.group(1)) for m in re.finditer(r"Step so far: (\d+),", out)]
+        costs = [float(m.group(1)) for m in re.finditer(r"Cost now: ([0-9.]+),", out)]
+        acc = float(re.search(r"Acc: ([0-9.]+)", out).group(1))
+        return steps, costs, acc
+
+    s_e, c_e, a_e = run(False)
+    s_g, c_g, a_g = run(True)
+    assert s_e == s_g and s_g[-1] == 600, (s_e, s_g)
+    assert len(c_e) == len(c_g) and all(abs(x - y) <= 2e-4 for x, y in zip(c_e, c_g)), (c_e, c_g)
+    assert abs(a_e - a_g) <= 0.01, (a_e, a_g)
+
+
 def test_simple_script_on_gpu():
     """simple.py on the HIP kernels (affine / SSE / fused SGD) reaches the reference's golden values."""
     import numpy as np
