@@ -268,6 +268,26 @@ void accuracy_count(const void* z, bool z_bf16, int B, int C, const int64_t* lab
 void gap_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y16, float* y32, hipStream_t s);
 void gap_bwd(const void* dy, bool dy_bf16, int N, int HW, int C, uint16_t* dx, hipStream_t s);
 
+// fused classifier head (head.hip): gap -> FC -> softmax xent -> unit-seed input gradient, one block per
+// sample; feat [N][C] bf16 and dz [N][O] bf16 are kept for dW / db; state = 3 zeroed u64 (self-resetting)
+struct HeadXentArgs {
+  const uint16_t* x = nullptr;       // [N][HW][C] bf16
+  const uint16_t* w = nullptr;       // [O][C] bf16
+  const float* b = nullptr;          // [O] f32 or null
+  const int64_t* labels = nullptr;   // [N]
+  uint16_t* feat = nullptr;          // [N][C] pooled features (bf16)
+  uint16_t* dz = nullptr;            // [N][O] (p - onehot) * gscale (bf16)
+  uint16_t* dfeat = nullptr;         // [N][HW][C] input gradient (bf16)
+  float* loss = nullptr;             // [1] batch mean
+  unsigned long long* state = nullptr;
+  int C = 0, HW = 0, O = 0;
+  float gscale = 0.f;
+};
+bool head_xent_ok(int C, int O, int HW);
+void head_xent_fwd(const HeadXentArgs& args, int N, hipStream_t s);
+// dW [O][C] += dz^T feat, db += colsum(dz) (plain read-modify-write: one block per 8 channels)
+void head_wgrad(const uint16_t* dz, const uint16_t* feat, int N, int C, int O, float* dw, float* db, hipStream_t s);
+
 // ---------------------------------------------------------------- optimizers (flat buffers)
 void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, float* v, int64_t n,
                      const float* lr, float gscale, float wd, float b1, float b2, float eps, const float* step,

@@ -964,6 +964,49 @@ std::tuple<Tensor, Tensor> softmax_xent_mean(Tensor z, optional<Tensor> lab_idx,
   return {loss, dz};
 }
 
+// Fused classifier head (head.hip): returns (mean loss, dfeat [N,H,W,C], feat [N,C], dz [N,O]); the
+// input gradient is for a unit seed (the caller's promise), feat / dz feed linear_small_bwd's dW / db.
+// state: int64 [3] zeros, owned by the caller across launches (the kernel leaves it zero).
+bool head_xent_supported(int64_t C, int64_t O, int64_t HW) { return tfx::head_xent_ok((int)C, (int)O, (int)HW); }
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> head_xent(Tensor x, Tensor w, optional<Tensor> b, Tensor labels,
+                                                     Tensor state) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 4, "head_xent expects NHWC features");
+  const int64_t N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3), O = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == C, "head_xent: W [O, C]");
+  TORCH_CHECK(tfx::head_xent_ok((int)C, (int)O, (int)HW) && N >= 1 && N <= 4095 && N * HW * C < (int64_t(1) << 31),
+              "head_xent: unsupported shape");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.numel() == N && labels.is_contiguous(),
+              "head_xent: int64 labels [N]");
+  TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kLong && state.numel() >= 3 && state.is_contiguous(),
+              "head_xent: int64 state [3]");
+  if (b.has_value() && b->defined()) { CHECK_F32(*b); TORCH_CHECK(b->numel() == O, "head_xent bias"); }
+  check_aligned16(x, "x"); check_aligned16(w, "w");
+  auto loss = at::empty({}, x.options().dtype(at::kFloat));
+  auto dfeat = at::empty_like(x);
+  auto feat = at::empty({N, C}, x.options());
+  auto dz = at::empty({N, O}, x.options());
+  tfx::HeadXentArgs a;
+  a.x = bf(x); a.w = bf(w); a.b = fp(b); a.labels = labels.data_ptr<int64_t>();
+  a.feat = bfm(feat); a.dz = bfm(dz); a.dfeat = bfm(dfeat); a.loss = loss.data_ptr<float>();
+  a.state = reinterpret_cast<unsigned long long*>(state.data_ptr<int64_t>());
+  a.C = (int)C; a.HW = (int)HW; a.O = (int)O; a.gscale = 1.0f / (float)N;
+  tfx::head_xent_fwd(a, (int)N, cur_stream());
+  return {loss, dfeat, feat, dz};
+}
+
+// the fused head's parameter gradients: dw [O, C] += dz^T feat, db [O] += colsum(dz) (f32, in place)
+void head_wgrad(Tensor dz, Tensor feat, optional<Tensor> dw, optional<Tensor> db) {
+  CHECK_DEV(dz); CHECK_BF16(dz); CHECK_CONTIG(dz); CHECK_BF16(feat); CHECK_CONTIG(feat);
+  const int64_t N = dz.size(0), O = dz.size(1), C = feat.size(1);
+  TORCH_CHECK(feat.size(0) == N && C % 8 == 0 && O >= 1 && O <= 16, "head_wgrad shapes");
+  if (dw.has_value() && dw->defined()) { CHECK_F32(*dw); TORCH_CHECK(dw->numel() == O * C && dw->is_contiguous(), "dw"); }
+  if (db.has_value() && db->defined()) { CHECK_F32(*db); TORCH_CHECK(db->numel() == O && db->is_contiguous(), "db"); }
+  check_aligned16(feat, "feat");
+  tfx::head_wgrad(bf(dz), bf(feat), (int)N, (int)C, (int)O, fpm(dw), fpm(db), cur_stream());
+}
+
 Tensor accuracy_count(Tensor z, optional<Tensor> lab_idx, optional<Tensor> lab_dense) {
   CHECK_DEV(z); CHECK_CONTIG(z);
   const bool zb = z.scalar_type() == at::kBFloat16;
@@ -1643,6 +1686,9 @@ TORCH_LIBRARY(tfx, m) {
         "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);
   m.def("softmax_xent", &softmax_xent);
   m.def("softmax_xent_mean", &softmax_xent_mean);
+  m.def("head_xent", &head_xent);
+  m.def("head_wgrad", &head_wgrad);
+  m.def("head_xent_supported", &head_xent_supported);
   m.def("accuracy_count", &accuracy_count);
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);

@@ -184,7 +184,8 @@ class ResNetCifar:
             self.stem.w.master[..., 3:] = 0
         self.store.refresh_shadow()
 
-    def __call__(self, x: torch.Tensor, training: bool = True) -> torch.Tensor:
+    def features(self, x: torch.Tensor, training: bool = True) -> torch.Tensor:
+        """Stem and residual stages: the NHWC input of the classifier head."""
         o = self.stem_bn.after_conv(self.stem, x, training, relu=True)
         for i, blk in enumerate(self.blocks):
             if isinstance(blk, Bottleneck):
@@ -192,8 +193,18 @@ class ResNetCifar:
                 o = blk(o, training, defer_tail=isinstance(nxt, Bottleneck))
             else:
                 o = blk(o, training)
-        f = ops.global_avg_pool(o)
+        return o
+
+    def __call__(self, x: torch.Tensor, training: bool = True) -> torch.Tensor:
+        f = ops.global_avg_pool(self.features(x, training))
         return ops.linear(f, self.fc_w, self.fc_b)
+
+    def training_loss(self, x: torch.Tensor, labels: torch.Tensor, naive: bool = False,
+                      unit_seed: bool = False) -> torch.Tensor:
+        """Mean softmax cross-entropy of a training forward; the head (pool, FC, loss and, for a unit
+        seed, its input gradient) is one launch on the GPU (ops.classifier_head_xent)."""
+        return ops.classifier_head_xent(self.features(x, True), self.fc_w, self.fc_b, labels, naive=naive,
+                                        unit_seed=unit_seed)
 
 
 def build_resnet_cifar(device="cuda", depth=50, num_classes=10, dtype=torch.bfloat16, seed=0) -> Tuple[VariableStore, ResNetCifar]:

@@ -1066,6 +1066,66 @@ def softmax_cross_entropy(logits, labels, naive: bool = False, unit_seed: bool =
     return _SoftmaxXent.apply(logits, labels, naive, unit_seed)
 
 
+# ---- fused classifier head (training step): gap -> linear -> mean softmax xent, one launch (head.hip)
+_FUSE_HEAD = True  # test / A-B hook: False composes global_avg_pool, linear and softmax_cross_entropy
+HEAD_FUSED_CALLS = [0]
+_HEAD_STATE = {}
+
+
+def _head_state(device) -> torch.Tensor:
+    """The fused head's self-resetting loss accumulator (3 zeroed int64 per device, left zero by every
+    launch): allocated once, outside any graph capture's private pool when possible."""
+    st = _HEAD_STATE.get(device)
+    if st is None:
+        st = torch.zeros(3, dtype=torch.int64, device=device)
+        _HEAD_STATE[device] = st
+    return st
+
+
+class _HeadXent(torch.autograd.Function):
+    """Mean softmax cross-entropy of ``linear(global_avg_pool(feat))`` for a unit-seeded backward: the
+    forward launch also produces the input gradient (the loss is the graph's root), so backward only
+    accumulates dW += dz^T f and db += colsum(dz) (head_wgrad, one small launch)."""
+
+    @staticmethod
+    def forward(ctx, feat, anchor, w: Variable, b: Optional[Variable], labels):
+        ctx.w, ctx.b = w, b
+        loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, b.master if b is not None else None, labels,
+                                                     _head_state(feat.device))
+        ctx.save_for_backward(dfeat, f, dz)
+        HEAD_FUSED_CALLS[0] += 1
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        dfeat, f, dz = ctx.saved_tensors
+        w, b = ctx.w, ctx.b
+        bias_grad = b.grad if (b is not None and b.trainable) else None
+        if w.trainable or bias_grad is not None:
+            torch.ops.tfx.head_wgrad(dz, f, w.grad if w.trainable else None, bias_grad)
+        _grad_ready(w if w.trainable else None, b if bias_grad is not None else None)
+        return dfeat, None, None, None, None
+
+
+def classifier_head_xent(feat, w: Variable, b: Optional[Variable], labels, naive: bool = False,
+                         unit_seed: bool = False) -> torch.Tensor:
+    """``softmax_cross_entropy(linear(global_avg_pool(feat), w, b), labels)`` -- the training head of an
+    image classifier (NHWC ``feat``, int64 ``labels``).  With ``unit_seed`` (the loss is the root of
+    ``loss.backward()``) on the GPU it runs as ONE launch that also forms the input gradient
+    (csrc/kernels/head.hip); otherwise, and for TF1's naive loss, the three ops compose."""
+    fused = (_FUSE_HEAD and unit_seed and not naive and feat.is_cuda and feat.dim() == 4
+             and feat.dtype == torch.bfloat16 and labels.dtype == torch.long and labels.is_cuda
+             and w.value.dtype == torch.bfloat16 and w.value.dim() == 2 and w.value.is_contiguous()
+             and _native.use_native(feat))
+    if fused:
+        n, h, wd, c = feat.shape
+        fused = bool(torch.ops.tfx.head_xent_supported(c, w.shape[0], h * wd)) and labels.numel() == n <= 4095
+    if fused:
+        return _HeadXent.apply(_settle(feat).contiguous(), w.store.anchor, w, b, labels.contiguous())
+    logits = linear(global_avg_pool(feat), w, b)
+    return softmax_cross_entropy(logits, labels, naive=naive, unit_seed=unit_seed)
+
+
 def accuracy(logits, labels) -> torch.Tensor:
     """Fraction of rows with argmax(logits) == label (tf.equal(argmax, argmax) + mean)."""
     if _native.use_native(logits):

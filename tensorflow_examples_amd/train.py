@@ -34,8 +34,12 @@ class ClassifierTrainer:
         reset_pending_slot_reductions()  # nothing deferred survives an abandoned step
         self.store.zero_grad()
         with trace.range("forward"):
-            logits = self.model(x, training=True)
-            loss = ops.softmax_cross_entropy(logits, y, naive=self.naive, unit_seed=True)  # seeded by _one
+            head = getattr(self.model, "training_loss", None)
+            if head is not None:  # the model fuses its classifier head with the loss (seeded by _one)
+                loss = head(x, y, naive=self.naive, unit_seed=True)
+            else:
+                logits = self.model(x, training=True)
+                loss = ops.softmax_cross_entropy(logits, y, naive=self.naive, unit_seed=True)  # seeded by _one
         with trace.range("backward"):
             # a persistent unit seed gradient: no ones-fill launch per step (graph-safe: never written)
             one = self._one
