@@ -101,6 +101,11 @@ struct IgemmArgs {
   float* sr2_dgamma = nullptr;
   float* sr2_dbeta = nullptr;
   int sr2_C = 0;
+  // optional A-operand transform on load: A[m][k] -> relu(A * a_scale[k] + a_shift[k]) (a plain ReLU
+  // BN applied by its consumer: the BN output is never written).  1x1 stride-1 forward convs with a
+  // single k-tile (K <= 64) on the register-staged pipeline only (igemm_launch checks).
+  const float* a_scale = nullptr;
+  const float* a_shift = nullptr;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;
 };
@@ -119,6 +124,9 @@ struct PwExpandArgs {
   const uint16_t* a2 = nullptr;     // [M][CN] conv3 input
   const uint16_t* w = nullptr;      // [CW][CN] conv3 weight
   uint16_t* dA2 = nullptr;          // [M][CN] out
+  // a2_save set: a2 holds BN2's INPUT y2 and conv3's input is relu(y2 * scale + shift) with BN2's
+  // [4][CN] save -- formed on load (the forward applied BN2 on load too: a2 was never written)
+  const float* a2_save = nullptr;
   const uint16_t* y2 = nullptr;     // [M][CN] BN2 input (null: no BN2 partials)
   const float* save2 = nullptr;     // [4][CN]
   int relu2 = 0;
@@ -146,7 +154,7 @@ struct PwSqueezeArgs {
   int M = 0, CI = 0, CO = 0;
 };
 bool pw_fwd_squeeze_ok(int CI, int CO, int64_t M);
-int pw_fwd_squeeze_grid(int64_t M);
+int pw_fwd_squeeze_grid(int CI, int CO, int64_t M);
 void pw_fwd_squeeze(const PwSqueezeArgs& args, int nblocks, hipStream_t s);
 // Stage-1 3x3 conv (64 -> 64, stride 1, pad 1, width 32) with its BN layers fused (conv3x3_fused.hip).
 // Forward: y = conv(relu(x sc_in + sh_in)) with BN statistics of y added into slots [NSLOT][2][64].

@@ -13,6 +13,8 @@
 
 namespace tfx {
 
+constexpr int BKT_HOST = 64;  // k-tile depth of igemm_impl.h (BKT)
+
 // ------------------------------------------------------------------ measured launch configurations
 // Written at import (tensorflow_examples_amd/ops/tuning.py loads the committed table) or by the
 // tuner; read on every launch.  A mutex keeps the rare writes and the reads apart (autograd's device
@@ -112,6 +114,12 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
       fprintf(stderr, "igemm_launch: unsupported fused-BN epilogue configuration\n");
       abort();
     }
+  }
+  // the A-operand BN transform: single-k-tile pointwise forward with the fused statistics epilogue
+  if (a.a_scale && !(a.stats && mode == MODE_FWD && a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 &&
+                     a.pw == 0 && a.K <= BKT_HOST && a.K % 8 == 0 && a.a_shift)) {
+    fprintf(stderr, "igemm_launch: A-operand transform needs a 1x1 stride-1 forward with K <= 64 and BN stats\n");
+    abort();
   }
   // 1x1 stride-1 unpadded convs (two thirds of ResNet-50's) are plain GEMMs over the NHWC rows:
   // dense loaders instead of the im2col / parity gathers -- no per-row address decode at all.

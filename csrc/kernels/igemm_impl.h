@@ -770,6 +770,32 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   } else if constexpr (STG == 1) {  // host guarantees a single k-tile
     issue(kt0, sa0, sb0);
     epi_prefetch();
+    if constexpr (AKIND == KM_DENSE && EPI == EPI_STATS) {
+      // consumer-applied ReLU BN (IgemmArgs a_scale): the thread's chunk is channels c0 .. c0+7 of the
+      // single k-tile; rows past M stay zero (their loads returned zeros, not the BN of zero)
+      if (a.a_scale) {
+        // two 16-B loads each, unconditional (a per-element guard compiles to branches that drain
+        // vmcnt); K < 64: chunks past K read the last 8 entries -- their A values meet zero-filled B
+        const int cc = min(la.c0, a.K - 8);
+        const float4 s0 = *reinterpret_cast<const float4*>(a.a_scale + cc);
+        const float4 s1 = *reinterpret_cast<const float4*>(a.a_scale + cc + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(a.a_shift + cc);
+        const float4 h1 = *reinterpret_cast<const float4*>(a.a_shift + cc + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int i = 0; i < LA::NP; ++i) {
+          float f[8];
+          unpack8(__builtin_bit_cast(U4, sa0[i]), f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f);
+          const uint32_t keep = la.ctx0[i] >= 0 ? 0xffffffffu : 0u;  // bit mask, not a select: no branch
+          U4 p = pack8(f);
+          p.x &= keep; p.y &= keep; p.z &= keep; p.w &= keep;
+          sa0[i] = __builtin_bit_cast(u32x4_t, p);
+        }
+      }
+    }
     stage_store(0, sa0, sb0);
     __syncthreads();
     compute(0);
@@ -1236,7 +1262,7 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   const bool swap = a.out_mode == OUT_BF16 || a.trans_out;
   constexpr int STAGE_B = (BM + BN) * BKT * 2;
   constexpr int G3 = KS * 3 * STAGE_B <= 163840 ? 3 : 2;
-  const int gls = g_tc.gls >= 0 ? g_tc.gls : 0;
+  const int gls = (g_tc.gls >= 0 && !a.a_scale) ? g_tc.gls : 0;  // the A transform is register-path only
   if (gls > 0) {
     // LDS-DMA ring: single k-tile -> GLS 1; otherwise the deepest ring (<= 3) that fits the LDS
     const bool single = nkt == 1 && splits == 1;

@@ -111,6 +111,16 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
     }
   };
 
+  // a2_save: conv3's input is relu(BN2(y2)) formed on load from y2 (a.a2 holds y2); this thread's
+  // narrow chunk is channels 8 (t % NTPR) .. +7
+  const bool a2_bn = a.a2_save != nullptr;
+  float a2s[8], a2h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = 8 * (t % C::NTPR) + k;
+    a2s[k] = a2_bn ? a.a2_save[2 * CN + c] : 1.f;
+    a2h[k] = a2_bn ? a.a2_save[3 * CN + c] : 0.f;
+  }
   // dgrad wave tile: rows 16 (wv & 1), columns DCOLS (wv >> 1); SWAP orientation -> lane holds row
   // (lane & 15), columns dcb + (lane >> 4) * 4 + r of each 16-col tile
   const int drb = 16 * (wv & 1), dcb = C::DCOLS * (wv >> 1);
@@ -200,7 +210,15 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
     }
     if (t < C::NLD) {
       const int row = t / C::NTPR, cc = t % C::NTPR;
-      *reinterpret_cast<pw_u32x4*>(slot + C::T_BYTES + pw_mn<CN>(row, cc)) = s.a2;
+      pw_u32x4 v = s.a2;
+      if (a2_bn) {  // uniform: BN2 + ReLU of the staged y2 piece (rows past M are never stored)
+        float f[8];
+        unpack8(__builtin_bit_cast(U4, v), f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], a2s[k], a2h[k]), 0.f);
+        v = __builtin_bit_cast(pw_u32x4, pack8(f));
+      }
+      *reinterpret_cast<pw_u32x4*>(slot + C::T_BYTES + pw_mn<CN>(row, cc)) = v;
     }
   };
   auto compute = [&](const char* slot, int tile) {

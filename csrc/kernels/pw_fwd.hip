@@ -22,30 +22,33 @@
 namespace tfx {
 namespace {
 
-// CI = wide input channels (the tail's width), CO = conv1's output channels
+// CI = wide input channels (the tail's width), CO = conv1's output channels, BM = rows per m-tile
+// (32; 16 when W1 is 128 KB -- ResNet-50 stage 2, 512 -> 128: two 16 KB tile slots + W1 = all 160 KB)
 template <int CI, int CO>
 struct PwSqueezeCfg {
+  static constexpr int BM = CI * CO * 2 > 64 * 1024 ? 16 : PW_BM;
+  static constexpr int RG = BM / 16;                   // 16-row groups per tile
   static constexpr int NCH = CI / 64;                  // 64-channel chunks of the wide tile
   static constexpr int TPR = CI / 8;                   // threads per wide row (16-B chunks)
-  static constexpr int LPT = PW_BM * TPR / PW_NT;      // wide 16-B loads per thread per tensor per tile
+  static constexpr int LPT = BM * TPR / PW_NT;         // wide 16-B loads per thread per tensor per tile
   static constexpr int RSTEP = PW_NT / TPR;            // rows between a thread's loads
-  static constexpr int T_BYTES = NCH * PW_BM * 128;    // `out` tile, K-major in 64-channel chunks
+  static constexpr int T_BYTES = NCH * BM * 128;       // `out` tile, K-major in 64-channel chunks
   static constexpr int W_BYTES = NCH * CO * 128;       // W1 image (rows = output channel), resident
-  static constexpr int DCOLS = CO / 4;                 // columns per wave (2 row groups x 4 col groups)
+  static constexpr int DCOLS = CO * RG / 8;            // columns per wave (RG row groups x 8/RG col groups)
   static constexpr int DTN = DCOLS / 16;
-  static_assert(LPT >= 1 && PW_BM * TPR % PW_NT == 0, "wide tile mapping");
-  static_assert(DTN >= 1, "column mapping");
+  static_assert(LPT >= 1 && BM * TPR % PW_NT == 0, "wide tile mapping");
+  static_assert(DTN >= 1 && DCOLS % 16 == 0, "column mapping");
   static_assert(2 * T_BYTES + W_BYTES <= 160 * 1024, "LDS budget");
 };
 
 template <int CI, int CO, bool RBN>
 __global__ void __launch_bounds__(PW_NT, 1) pw_fwd_squeeze_kernel(PwSqueezeArgs a) {
   using C = PwSqueezeCfg<CI, CO>;
-  constexpr int NCH = C::NCH, LPT = C::LPT, TPR = C::TPR;
+  constexpr int NCH = C::NCH, LPT = C::LPT, TPR = C::TPR, BM = C::BM;
   __shared__ __attribute__((aligned(16))) char smem[2 * C::T_BYTES + C::W_BYTES];
   char* wimg = smem + 2 * C::T_BYTES;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int ntiles = a.M / PW_BM;
+  const int ntiles = a.M / BM;
 
   // ---- per-thread wide-channel group (fixed for the launch) and the tail's affine maps
   const int chc = t % TPR, c0 = 8 * chc, r0 = t / TPR;
@@ -71,9 +74,9 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_fwd_squeeze_kernel(PwSqueezeArgs 
   const __amdgpu_buffer_rsrc_t ro = pw_rsrc(a.out, wide), rm = pw_rsrc(a.mask, (int64_t)a.M * CI / 8);
   const __amdgpu_buffer_rsrc_t r1 = pw_rsrc(a.y1, (int64_t)a.M * CO * 2);
 
-  // wave tile: rows 16 (wv & 1), columns DCOLS (wv >> 1); SWAP orientation -> lane holds row
+  // wave tile: rows 16 (wv % RG), columns DCOLS (wv / RG); SWAP orientation -> lane holds row
   // (lane & 15), columns cb + (lane >> 4) * 4 + r of each 16-col tile
-  const int rb = 16 * (wv & 1), cb = C::DCOLS * (wv >> 1);
+  const int rb = 16 * (wv % C::RG), cb = C::DCOLS * (wv / C::RG);
   float bs[C::DTN][4], bq[C::DTN][4];  // BN1 statistics of this lane's columns, whole launch
 #pragma unroll
   for (int j = 0; j < C::DTN; ++j)
@@ -89,7 +92,7 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_fwd_squeeze_kernel(PwSqueezeArgs 
     const bool ok = tile < ntiles;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int row = tile * PW_BM + r0 + C::RSTEP * i;
+      const int row = tile * BM + r0 + C::RSTEP * i;
       const uint32_t off = ok ? (uint32_t)(row * CI + c0) * 2u : 0x80000000u;
       s.y[i] = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
       s.r[i] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
@@ -112,8 +115,8 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_fwd_squeeze_kernel(PwSqueezeArgs 
         yf[k] = fmaxf(z, 0.f);
       }
       const U4 o = pack8(yf);
-      const int lrow = r0 + C::RSTEP * i, row = tile * PW_BM + lrow;
-      *reinterpret_cast<U4*>(slot + (chc >> 3) * (PW_BM * 128) + pw_kmaj(lrow, chc & 7)) = o;
+      const int lrow = r0 + C::RSTEP * i, row = tile * BM + lrow;
+      *reinterpret_cast<U4*>(slot + (chc >> 3) * (BM * 128) + pw_kmaj(lrow, chc & 7)) = o;
       if (tile < ntiles) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pw_u32x4, o), ro, (uint32_t)(row * CI + c0) * 2u, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, rm, (uint32_t)(row * TPR + chc), 0, 0);
@@ -126,14 +129,14 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_fwd_squeeze_kernel(PwSqueezeArgs 
     for (int j = 0; j < C::DTN; ++j) acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kc = 0; kc < CI / 32; ++kc) {  // 32-deep k-steps over the wide channels
-      const bf16x8_t fa = pw_frag_kmaj(slot, (kc >> 1) * (PW_BM * 128), rb, 4 * (kc & 1), lane);
+      const bf16x8_t fa = pw_frag_kmaj(slot, (kc >> 1) * (BM * 128), rb, 4 * (kc & 1), lane);
 #pragma unroll
       for (int j = 0; j < C::DTN; ++j) {
         const bf16x8_t fb = pw_frag_kmaj(wimg, (kc >> 1) * (CO * 128), cb + 16 * j, 4 * (kc & 1), lane);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, acc[j], 0, 0, 0);  // SWAP
       }
     }
-    const int row = tile * PW_BM + rb + (lane & 15);
+    const int row = tile * BM + rb + (lane & 15);
 #pragma unroll
     for (int j = 0; j < C::DTN; ++j) {
       const int col = cb + 16 * j + (lane >> 4) * 4;
@@ -189,10 +192,15 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_fwd_squeeze_kernel(PwSqueezeArgs 
 }  // namespace
 
 bool pw_fwd_squeeze_ok(int CI, int CO, int64_t M) {
-  return CI == 256 && (CO == 64 || CO == 128) && M % PW_BM == 0 && M > 0 && (int64_t)M * CI < (1ll << 30);
+  const bool s1 = CI == 256 && (CO == 64 || CO == 128), s2 = CI == 512 && CO == 128;
+  const int bm = s2 ? PwSqueezeCfg<512, 128>::BM : PW_BM;
+  return (s1 || s2) && M % bm == 0 && M > 0 && (int64_t)M * CI < (1ll << 30);
 }
 
-int pw_fwd_squeeze_grid(int64_t M) { return (int)std::min<int64_t>(256, M / PW_BM); }
+int pw_fwd_squeeze_grid(int CI, int CO, int64_t M) {
+  const int bm = (CI == 512 && CO == 128) ? PwSqueezeCfg<512, 128>::BM : PW_BM;
+  return (int)std::min<int64_t>(256, M / bm);
+}
 
 void pw_fwd_squeeze(const PwSqueezeArgs& args, int nblocks, hipStream_t s) {
   const bool rbn = args.save_r != nullptr;
@@ -203,6 +211,8 @@ void pw_fwd_squeeze(const PwSqueezeArgs& args, int nblocks, hipStream_t s) {
     TFX_PWF(256, 64)
   } else if (args.CI == 256 && args.CO == 128) {
     TFX_PWF(256, 128)
+  } else if (args.CI == 512 && args.CO == 128) {
+    TFX_PWF(512, 128)
   } else {
     abort();
   }

@@ -263,6 +263,33 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   return {y, save};
 }
 
+// conv_fwd_bn of relu(x * in_save[2C..3C) + in_save[3C..4C)) -- a plain ReLU BN applied on load by this
+// 1x1 stride-1 conv (C <= 64: one k-tile), so the BN output is never written.  Returns (y, save).
+std::tuple<Tensor, Tensor> conv_fwd_bn_in(Tensor x, Tensor in_save, Tensor w, Tensor ws, optional<Tensor> gamma,
+                                          optional<Tensor> beta, optional<Tensor> run_mean, optional<Tensor> run_var,
+                                          double momentum, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
+  CHECK_F32(in_save); CHECK_CONTIG(in_save);
+  auto g = geom(x.sizes().vec(), w.sizes().vec(), 1, 0, 1);
+  TORCH_CHECK(g.R == 1 && g.S == 1 && g.C <= 64 && in_save.numel() == 4 * g.C,
+              "conv_fwd_bn_in: 1x1 conv with <= 64 input channels and the input BN's [4][C] save");
+  auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
+  auto save = at::empty({4 * g.Ko}, x.options().dtype(at::kFloat));
+  auto a = conv_args(g, 1, 0, 1);
+  a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
+  a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
+  a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.C; a.ldb = a.K; a.ldc = g.Ko;
+  a.out_mode = tfx::OUT_BF16;
+  check_bn_ws(ws, g.Ko);
+  a.stats = ws.data_ptr<float>();
+  a.a_scale = in_save.data_ptr<float>() + 2 * g.C;
+  a.a_shift = in_save.data_ptr<float>() + 3 * g.C;
+  tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
+  tfx::bn_finalize(a.stats, a.M, g.Ko, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
+                   fpm(run_var), save.data_ptr<float>(), cur_stream());
+  return {y, save};
+}
+
 // Block tail + the next block's conv1 (1x1, CI -> CO) forward in one launch (pw_fwd.hip): writes the
 // tail's output `out` and ReLU mask bits into the given buffers (allocated by the tail BN, which
 // deferred its apply), then finalizes BN1 from the epilogue statistics as conv_fwd_bn does.
@@ -292,7 +319,7 @@ std::tuple<Tensor, Tensor> pw_fwd_squeeze(Tensor y3, Tensor save3, Tensor res, o
     TORCH_CHECK(res_save->numel() == 4 * CI, "pw_fwd_squeeze: res_save");
     a.save_r = res_save->data_ptr<float>();
   }
-  tfx::pw_fwd_squeeze(a, tfx::pw_fwd_squeeze_grid(M), cur_stream());
+  tfx::pw_fwd_squeeze(a, tfx::pw_fwd_squeeze_grid((int)CI, (int)CO, M), cur_stream());
   tfx::bn_finalize(a.slots1, M, (int)CO, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
                    fpm(run_var), save.data_ptr<float>(), cur_stream());
   return {y1, save};
@@ -554,7 +581,7 @@ std::tuple<Tensor, Tensor, Tensor> pw_bwd_expand(Tensor g, Tensor y3, Tensor mas
                                                  optional<Tensor> dgamma2, optional<Tensor> dbeta2,
                                                  optional<Tensor> ysc, optional<Tensor> save_sc,
                                                  optional<Tensor> slots_sc, optional<Tensor> dgamma_sc,
-                                                 optional<Tensor> dbeta_sc) {
+                                                 optional<Tensor> dbeta_sc, optional<Tensor> a2_save) {
   CHECK_DEV(g); CHECK_BF16(g); CHECK_CONTIG(g); CHECK_BF16(y3); CHECK_CONTIG(y3); CHECK_BF16(a2); CHECK_CONTIG(a2);
   CHECK_BF16(w); CHECK_CONTIG(w); CHECK_F32(dw); CHECK_CONTIG(dw); CHECK_F32(save3); CHECK_F32(red3);
   const int64_t CW = w.size(0), CN = w.size(-1), M = a2.numel() / CN;
@@ -567,6 +594,11 @@ std::tuple<Tensor, Tensor, Tensor> pw_bwd_expand(Tensor g, Tensor y3, Tensor mas
   tfx::PwExpandArgs a;
   a.g = bf(g); a.y3 = bf(y3); a.mask3 = mask3.data_ptr<uint8_t>(); a.save3 = save3.data_ptr<float>();
   a.red3 = red3.data_ptr<float>(); a.a2 = bf(a2); a.w = bf(w); a.dA2 = bfm(dA2); a.M = (int)M; a.CN = (int)CN;
+  if (a2_save.has_value() && a2_save->defined()) {  // a2 = BN2's input: conv3's input formed on load
+    CHECK_F32(*a2_save); CHECK_CONTIG(*a2_save);
+    TORCH_CHECK(a2_save->numel() == 4 * CN, "pw_bwd_expand: a2_save = BN2's [4][CN] save");
+    a.a2_save = a2_save->data_ptr<float>();
+  }
   Tensor red2 = at::empty({0}, g.options().dtype(at::kFloat));
   const bool bnb = y2.has_value() && y2->defined();
   if (bnb) {
@@ -1666,6 +1698,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);
+  m.def("conv_fwd_bn_in", &conv_fwd_bn_in);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
         "Tensor bn_x, Tensor bn_save, Tensor? bn_mask, bool relu, Tensor ws, Tensor? dgamma, Tensor? dbeta, "
         "Tensor? addend_mask=None, bool reduce=True, bool addend_s2=False, Tensor? wflip=None) -> (Tensor, Tensor)",

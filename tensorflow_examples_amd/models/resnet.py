@@ -118,7 +118,8 @@ class Bottleneck:
         # BN1's apply is left to conv2 (a stage-1 3x3 conv applies it on load: conv3x3_fused.hip)
         o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons, fuse_input_bn_backward=cons is not None,
                                defer_apply=True)
-        o = self.b2.after_conv(self.c2, o, training, relu=True, fuse_input_bn_backward=True)
+        # BN2's apply is left to conv3 too (a single-k-tile 1x1 conv applies it on load; else materialised)
+        o = self.b2.after_conv(self.c2, o, training, relu=True, fuse_input_bn_backward=True, defer_apply=True)
         o3_fuse = True
         if self.proj is None:
             return self.b3.after_conv(self.c3, o, training, relu=True, residual=x, residual_sink=prod,

@@ -188,6 +188,18 @@ def _conv3_fused_ok(x, w, stride, pad, dil, stats_into) -> bool:
     return bool(torch.ops.tfx.conv3x3_fused_supported(n, h, wd, c, sh[0]))
 
 
+PW_APPLY_CALLS = [0]  # 1x1 forwards that applied their input BN on load (tests)
+_BN_ON_LOAD_1X1 = True  # A/B hook: False materialises a deferred plain BN before its 1x1 consumer
+
+
+def _pw_apply_ok(x, w, stride, pad, dil, stats_into) -> bool:
+    """Can this 1x1 conv apply its input's plain ReLU BN on load (one k-tile: <= 64 input channels)?"""
+    sh = w.shape
+    return (stride == 1 and pad == 0 and dil == 1 and isinstance(stats_into, BNWorkspace) and len(sh) == 4
+            and sh[1] == 1 and sh[2] == 1 and sh[3] == x.shape[-1] and x.shape[-1] <= 64 and x.shape[-1] % 8 == 0
+            and x.is_contiguous() and _DEFER_BN_IN and _BN_ON_LOAD_1X1)
+
+
 def _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into) -> bool:
     """Can this conv's forward run fused with the deferred tail ``tp`` of its input (pw_fwd.hip)?"""
     sh = w.shape
@@ -250,6 +262,15 @@ class _Conv2d(torch.autograd.Function):
                     ctx.pending_in = tp
                     CONV3_FWD_CALLS[0] += 1
                     return y
+                if tp.res is None and _pw_apply_ok(x, w, stride, pad, dil, stats_into):
+                    # a plain ReLU BN applied on load by this single-k-tile 1x1 conv (igemm a_scale):
+                    # x stays unwritten (the fused backward forms it on load too)
+                    ws = stats_into
+                    y, ws.pending_save = torch.ops.tfx.conv_fwd_bn_in(tp.x, tp.save, w.value, ws.get(x.device),
+                                                                      *ws.finalize_args)
+                    ctx.pending_in = tp
+                    PW_APPLY_CALLS[0] += 1
+                    return y
                 if _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into):
                     # the previous block's tail apply + this conv + its BN statistics in one launch:
                     # x (and the tail's mask bits) are written here (pw_fwd.hip)
@@ -289,7 +310,8 @@ class _Conv2d(torch.autograd.Function):
             CONV3_BWD_CALLS[0] += 1
             _grad_ready(w)
             return dx, None, None, None, None, None, None, None, None
-        if tp is not None:
+        if tp is not None and not (tp.res is None and lazy is not None and need_dx and ctx.native
+                                   and _pw_expand_ok(x, w, stride, pad, dil, lazy, ctx.sink)):
             tp.materialize()  # the forward applied the input BN on load only
         if ctx.native:
             if lazy is not None:
@@ -308,17 +330,21 @@ class _Conv2d(torch.autograd.Function):
                 if need_dx and _pw_expand_ok(x, w, stride, pad, dil, lazy, ctx.sink):
                     # the tail BN's backward apply + this conv's data AND weight gradient in one
                     # launch; dy never written (pw_bwd.hip).  The BN2 backward partials of dx ride along.
+                    # a2_lazy: the forward applied BN2 on load (x never written) -- formed on load here too
+                    a2_lazy = tp is not None and not tp.done and tp.res is None
                     bnb = ctx.bnb
                     use_bnb = bnb is not None and bnb.mask is None and not bnb.deferred and bnb.red is None \
                         and x.numel() * x.element_size() <= _BNB_MAX_BYTES
                     # projection block: the shortcut BN's backward reduction too (F3-SEC)
                     rb = lazy.sec if lazy.dy is None else None
                     dx, red2, red_sc = torch.ops.tfx.pw_bwd_expand(
-                        lazy.g.contiguous(), lazy.x, lazy.mask, lazy.save, lazy.red, x, w.value, w.grad,
+                        lazy.g.contiguous(), lazy.x, lazy.mask, lazy.save, lazy.red, tp.x if a2_lazy else x,
+                        w.value, w.grad,
                         bnb.x if use_bnb else None, bnb.save if use_bnb else None, bool(use_bnb and bnb.relu),
                         bnb.ws if use_bnb else None, bnb.dgamma if use_bnb else None,
                         bnb.dbeta if use_bnb else None, rb.x if rb else None, rb.save if rb else None,
-                        rb.ws if rb else None, rb.dgamma if rb else None, rb.dbeta if rb else None)
+                        rb.ws if rb else None, rb.dgamma if rb else None, rb.dbeta if rb else None,
+                        tp.save if a2_lazy else None)
                     if use_bnb:
                         bnb.red = red2
                     if rb is not None:

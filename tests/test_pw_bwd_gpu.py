@@ -19,8 +19,10 @@ def _bf(t):
 
 
 @pytest.mark.parametrize("shape", [(256, 32, 32, 64), (4, 8, 8, 64), (3, 4, 8, 64)])
-@pytest.mark.parametrize("bn2,sec", [(True, False), (False, False), (True, True)])
-def test_pw_bwd_expand_matches_reference(gpu, shape, bn2, sec):
+@pytest.mark.parametrize("bn2,sec,a2bn", [(True, False, False), (False, False, False), (True, True, False),
+                                         (True, False, True), (True, True, True)])
+def test_pw_bwd_expand_matches_reference(gpu, shape, bn2, sec, a2bn):
+    """a2bn: conv3's input is formed on load from BN2's input y2 (the forward applied BN2 on load)."""
     N, H, W, CN = shape
     CW = 4 * CN
     M = N * H * W
@@ -39,8 +41,10 @@ def test_pw_bwd_expand_matches_reference(gpu, shape, bn2, sec):
     y2 = _bf(torch.randn(N, H, W, CN, device=gpu) * 1.1 - 0.1)
     gam2, bet2 = torch.rand(CN, device=gpu) + 0.5, torch.randn(CN, device=gpu) * 0.3
     ws2 = torch.zeros(64 * 2 * CN, device=gpu)
-    _, save2, _ = torch.ops.tfx.bn_fwd_train(y2, gam2, bet2, None, None, 0.1, 1e-5, None, True, ws2, False)
+    a2_out, save2, _ = torch.ops.tfx.bn_fwd_train(y2, gam2, bet2, None, None, 0.1, 1e-5, None, True, ws2, False)
     assert ws2.abs().max().item() == 0.0
+    if a2bn:
+        a2 = a2_out  # the BN2 apply's bf16 output: what the kernel forms on load from y2
 
     # reference: the layer-wise chain, in fp32 from the same bf16 dy3 the apply pass writes
     dy3 = torch.ops.tfx.bn_bwd_apply(g, y3, None, save3, red3, True, mask3, False)[0]
@@ -60,9 +64,10 @@ def test_pw_bwd_expand_matches_reference(gpu, shape, bn2, sec):
     dw = torch.zeros(CW, 1, 1, CN, device=gpu)
     dg2, db2 = torch.zeros(CN, device=gpu), torch.zeros(CN, device=gpu)
     dA2, red2, redsc = torch.ops.tfx.pw_bwd_expand(
-        g, y3, mask3, save3, red3, a2, w, dw, y2 if bn2 else None, save2 if bn2 else None, True,
+        g, y3, mask3, save3, red3, y2 if a2bn else a2, w, dw, y2 if bn2 else None, save2 if bn2 else None, True,
         ws2 if bn2 else None, dg2 if bn2 else None, db2 if bn2 else None, ysc if sec else None,
-        savesc if sec else None, wssc if sec else None, dgsc if sec else None, dbsc if sec else None)
+        savesc if sec else None, wssc if sec else None, dgsc if sec else None, dbsc if sec else None,
+        save2 if a2bn else None)
     torch.cuda.synchronize()
     if sec:
         assert wssc.abs().max().item() == 0.0, "shortcut BN slots not restored to zero"
