@@ -296,6 +296,12 @@ void head_xent_fwd(const HeadXentArgs& args, int N, hipStream_t s);
 // dW [O][C] += dz^T feat, db += colsum(dz) (plain read-modify-write: one block per 8 channels)
 void head_wgrad(const uint16_t* dz, const uint16_t* feat, int N, int C, int O, float* dw, float* db, hipStream_t s);
 
+// CIFAR stem weight gradient (stem.hip): 3x3 s1 p1 conv of 32x32 images with 8 (padded) input channels,
+// Ko = 64: dw [Ko][3][3][8] +=, one block per image into copies of a zeroed workspace (re-zeroed)
+bool stem_wgrad_ok(int N, int H, int W, int C, int Ko);
+int stem_wgrad_ws_floats(int Ko);
+void stem_wgrad(const uint16_t* x, const uint16_t* dy, int N, int Ko, float* ws, float* dw, hipStream_t s);
+
 // ---------------------------------------------------------------- optimizers (flat buffers)
 void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, float* v, int64_t n,
                      const float* lr, float gscale, float wd, float b1, float b2, float eps, const float* step,

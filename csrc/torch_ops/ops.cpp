@@ -492,6 +492,27 @@ void conv_wgrad_impl(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad
   }
 }
 
+// CIFAR stem weight gradient (stem.hip): dw [64][3][3][8] += dY^T . im2col(x), 32x32 images, 8 channels
+bool stem_wgrad_supported(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ko) {
+  return tfx::stem_wgrad_ok((int)N, (int)H, (int)W, (int)C, (int)Ko);
+}
+
+int64_t stem_wgrad_ws_floats(int64_t Ko) { return tfx::stem_wgrad_ws_floats((int)Ko); }
+
+// ws: a zeroed f32 workspace of stem_wgrad_ws_floats(Ko) (left zero)
+void stem_wgrad(Tensor dy, Tensor x, Tensor dw, Tensor ws) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == x.size(0) && dy.size(1) == x.size(1) &&
+                  dy.size(2) == x.size(2), "stem_wgrad: NHWC x and dy of one image size");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), Ko = dy.size(3);
+  TORCH_CHECK(tfx::stem_wgrad_ok((int)N, (int)H, (int)W, (int)C, (int)Ko) && dw.numel() == Ko * 9 * C,
+              "stem_wgrad: unsupported shape");
+  check_aligned16(x, "x"); check_aligned16(dy, "dy");
+  CHECK_F32(ws); CHECK_CONTIG(ws);
+  TORCH_CHECK(ws.numel() >= tfx::stem_wgrad_ws_floats((int)Ko), "stem_wgrad: workspace too small");
+  tfx::stem_wgrad(bf(x), bf(dy), (int)N, (int)Ko, ws.data_ptr<float>(), dw.data_ptr<float>(), cur_stream());
+}
+
 void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t dil, bool accumulate) {
   conv_wgrad_impl(dy, x, dw, stride, pad, dil, accumulate, nullptr);
 }
@@ -1699,6 +1720,9 @@ TORCH_LIBRARY(tfx, m) {
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_fwd_bn_in", &conv_fwd_bn_in);
+  m.def("stem_wgrad", &stem_wgrad);
+  m.def("stem_wgrad_ws_floats", &stem_wgrad_ws_floats);
+  m.def("stem_wgrad_supported", &stem_wgrad_supported);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
         "Tensor bn_x, Tensor bn_save, Tensor? bn_mask, bool relu, Tensor ws, Tensor? dgamma, Tensor? dbeta, "
         "Tensor? addend_mask=None, bool reduce=True, bool addend_s2=False, Tensor? wflip=None) -> (Tensor, Tensor)",

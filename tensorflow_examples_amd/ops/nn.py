@@ -188,6 +188,31 @@ def _conv3_fused_ok(x, w, stride, pad, dil, stats_into) -> bool:
     return bool(torch.ops.tfx.conv3x3_fused_supported(n, h, wd, c, sh[0]))
 
 
+STEM_WGRAD_CALLS = [0]  # stem weight gradients by stem.hip (tests)
+_STEM_WGRAD = True  # A/B hook: False runs the stem's weight gradient on the generic implicit GEMM
+
+
+_STEM_WS = {}
+
+
+def _stem_ws(device, ko) -> torch.Tensor:
+    """stem.hip's zeroed dW workspace copies (left zero by every launch), one per device."""
+    ws = _STEM_WS.get(device)
+    if ws is None:
+        ws = torch.zeros(int(torch.ops.tfx.stem_wgrad_ws_floats(ko)), dtype=torch.float32, device=device)
+        _STEM_WS[device] = ws
+    return ws
+
+
+def _stem_ok(x, w, stride, pad, dil) -> bool:
+    sh = w.shape
+    if not (stride == 1 and pad == 1 and dil == 1 and x.dim() == 4 and len(sh) == 4 and sh[1] == 3 and sh[2] == 3
+            and sh[3] == x.shape[-1]):
+        return False
+    n, h, wd, c = x.shape
+    return bool(torch.ops.tfx.stem_wgrad_supported(n, h, wd, c, sh[0]))
+
+
 PW_APPLY_CALLS = [0]  # 1x1 forwards that applied their input BN on load (tests)
 _BN_ON_LOAD_1X1 = True  # A/B hook: False materialises a deferred plain BN before its 1x1 consumer
 
@@ -355,6 +380,12 @@ class _Conv2d(torch.autograd.Function):
                 gy = lazy.materialize()
             gy = gy.contiguous()
             sink = ctx.sink
+            if not need_dx and w.trainable and _STEM_WGRAD and not _PENDING_SR and _stem_ok(x, w, stride, pad, dil):
+                # the CIFAR stem (8 padded input channels, no input gradient): one block per image (stem.hip)
+                torch.ops.tfx.stem_wgrad(gy, x.contiguous(), w.grad, _stem_ws(gy.device, w.shape[0]))
+                STEM_WGRAD_CALLS[0] += 1
+                _grad_ready(w)
+                return None, None, None, None, None, None, None, None, None
             dx = None
             sr_bnb = None
             if need_dx:
