@@ -301,6 +301,8 @@ void head_wgrad(const uint16_t* dz, const uint16_t* feat, int N, int C, int O, f
 bool stem_wgrad_ok(int N, int H, int W, int C, int Ko);
 int stem_wgrad_ws_floats(int Ko);
 void stem_wgrad(const uint16_t* x, const uint16_t* dy, int N, int Ko, float* ws, float* dw, hipStream_t s);
+// ... and its forward: y [N][32][32][Ko] bf16, BN statistics of y into slots [NSLOT][2][Ko]
+void stem_fwd(const uint16_t* x, const uint16_t* w, int N, int Ko, uint16_t* y, float* slots, hipStream_t s);
 
 // ---------------------------------------------------------------- optimizers (flat buffers)
 void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, float* v, int64_t n,

@@ -1,5 +1,5 @@
-// Weight gradient of the CIFAR ResNet stem (3x3, stride 1, pad 1, 8 padded input channels, 32x32
-// images) for gfx950.
+// The CIFAR ResNet stem (3x3, stride 1, pad 1, 8 padded input channels, 32x32 images, 64 outputs) for
+// gfx950: its weight gradient, and (below) its forward with the BN statistics.
 //
 // As an implicit GEMM this is dW[Ko][72] = dY^T[Ko][P] . im2col(X)[P][72] over P = N*32*32 pixels: the
 // generic kernels tile its 72 columns into a 128-wide tile (44 % padding), gather im2col pieces of
@@ -112,6 +112,90 @@ __global__ void __launch_bounds__(ST_NT) stem_wgrad_kernel(const uint16_t* __res
   }
 }
 
+// ---- forward: y[n][y][x][ko] = sum over (r, s, c) of X[n][y+r-1][x+s-1][c] W[ko][r][s][c], and the
+// BN statistics of the bf16 y (igemm.hip EPI_STATS math) into the BN layer's slots.  One block per
+// image: the bordered image and W go to LDS once; per output row each wave (one 16-wide ko tile, its 3
+// B fragments held in registers for the whole image) reads 6 A fragments -- a pixel's 8 channels of one
+// tap are 16 contiguous bytes of the image, so no im2col -- and runs 6 MFMAs into y^T tiles (lanes hold
+// 4 consecutive ko: 8-byte bf16 stores).  No barrier after the staging: the block is store-bound.
+template <int KO>
+__global__ void __launch_bounds__(ST_NT) stem_fwd_kernel(const uint16_t* __restrict__ x,
+                                                         const uint16_t* __restrict__ w, int N,
+                                                         uint16_t* __restrict__ y, float* __restrict__ slots) {
+  static_assert(KO == 64, "one 16-wide ko tile per wave");
+  constexpr int H = ST_W, XB = ST_HW * ST_HW * 16;
+  __shared__ __attribute__((aligned(16))) char ximg[XB + 16];  // + a zero pixel for the padded taps
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int n = blockIdx.x;
+  const int64_t img_px = (int64_t)H * ST_W;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(x), 0,
+                                                                      (int)(N * img_px * 8 * 2), 0x00020000);
+  constexpr uint32_t BADO = 0x80000000u;
+  U4 xv[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int p = t + ST_NT * i, py = p / ST_HW, px = p % ST_HW;
+    const bool in = (p < ST_HW * ST_HW) & (py >= 1) & (py <= H) & (px >= 1) & (px <= ST_W);
+    const uint32_t o = in ? (uint32_t)((n * img_px + (py - 1) * ST_W + (px - 1)) * 16) : BADO;
+    xv[i] = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(rx, o, 0, 0));
+  }
+  // B fragments: lane holds W[ko = 16 wv + (lane & 15)][tap = 4 ks + (lane >> 4)][c 0..7]; taps 9..11 zero
+  bf16x8_t fb[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int tap = 4 * ks + (lane >> 4), ko = 16 * wv + (lane & 15);
+    U4 v = U4{0u, 0u, 0u, 0u};
+    if (tap < 9) v = *reinterpret_cast<const U4*>(w + (ko * 9 + tap) * 8);
+    fb[ks] = __builtin_bit_cast(bf16x8_t, v);
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int p = t + ST_NT * i;
+    *reinterpret_cast<U4*>(ximg + (p < ST_HW * ST_HW ? p * 16 : XB)) = xv[i];  // past the image: the zero pixel
+  }
+  if (t == 0) *reinterpret_cast<U4*>(ximg + XB) = U4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  float bs[4] = {0.f, 0.f, 0.f, 0.f}, bq[4] = {0.f, 0.f, 0.f, 0.f};
+  const int ko0 = 16 * wv + 4 * (lane >> 4);
+  uint16_t* yimg = y + (int64_t)n * img_px * KO;
+#pragma unroll 2
+  for (int yy = 0; yy < H; ++yy) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int px = 16 * mt + (lane & 15);
+      f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int tap = 4 * ks + (lane >> 4), r = tap / 3, s = tap - 3 * r;
+        const int off = tap < 9 ? ((yy + r) * ST_HW + px + s) * 16 : XB;
+        const bf16x8_t fa = *(const __attribute__((address_space(3))) bf16x8_t*)(
+            (__attribute__((address_space(3))) char*)ximg + off);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks], fa, acc, 0, 0, 0);  // y^T: rows ko, cols px
+      }
+      const uint32_t lo = pack_bf16x2(acc[0], acc[1]), hi = pack_bf16x2(acc[2], acc[3]);
+      *reinterpret_cast<uint2*>(yimg + (yy * ST_W + px) * KO + ko0) = make_uint2(lo, hi);
+      const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u), __uint_as_float(hi << 16),
+                          __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bs[r] += v[r];
+        bq[r] = fmaf(v[r], v[r], bq[r]);
+      }
+    }
+  }
+  // the 16 lanes of a DPP row hold the same 4 ko (different pixels): reduce, one atomic pair per ko
+  float* slot = slots + (size_t)(n % NSLOT) * 2 * KO;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float sv = row16_sum(bs[r]), qv = row16_sum(bq[r]);
+    if ((lane & 15) == 0) {
+      atomicAdd(slot + ko0 + r, sv);
+      atomicAdd(slot + KO + ko0 + r, qv);
+    }
+  }
+}
+
 // dw[e] += sum of the ST_COPIES workspace copies of element e, which are re-zeroed
 __global__ void __launch_bounds__(256) stem_reduce_kernel(float* __restrict__ ws, int E, float* __restrict__ dw) {
   const int e = blockIdx.x * 256 + threadIdx.x;
@@ -135,6 +219,11 @@ bool stem_wgrad_ok(int N, int H, int W, int C, int Ko) {
 }
 
 int stem_wgrad_ws_floats(int Ko) { return ST_COPIES * Ko * 72; }
+
+void stem_fwd(const uint16_t* x, const uint16_t* w, int N, int Ko, uint16_t* y, float* slots, hipStream_t s) {
+  (void)Ko;
+  stem_fwd_kernel<64><<<N, ST_NT, 0, s>>>(x, w, N, y, slots);
+}
 
 void stem_wgrad(const uint16_t* x, const uint16_t* dy, int N, int Ko, float* ws, float* dw, hipStream_t s) {
   stem_wgrad_kernel<64><<<N, ST_NT, 0, s>>>(x, dy, N, ws);

@@ -240,6 +240,8 @@ void check_bn_ws(const Tensor& ws, int64_t C) {
   TORCH_CHECK(ws.numel() >= tfx::NSLOT * 2 * C, "BN workspace too small for the fused epilogue");
 }
 
+bool g_stem_fwd = true;  // conv_fwd_bn routes the CIFAR stem (8 channels, 32x32, 64 outputs) to stem.hip
+
 // conv forward whose epilogue produces the following BN's batch statistics, then the finalize:
 // returns (y, save = [mean | invstd | scale | shift]) and updates the running statistics -- the BN
 // then only applies (bn_apply_train).
@@ -257,10 +259,23 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   a.out_mode = tfx::OUT_BF16;
   check_bn_ws(ws, g.Ko);
   a.stats = ws.data_ptr<float>();
-  tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
+  if (g_stem_fwd && stride == 1 && pad == 1 && dil == 1 && g.R == 3 && g.S == 3 &&
+      tfx::stem_wgrad_ok((int)g.N, (int)g.H, (int)g.W, (int)g.C, (int)g.Ko)) {
+    check_aligned16(x, "x"); check_aligned16(w, "w");
+    tfx::stem_fwd(bf(x), bf(w), (int)g.N, (int)g.Ko, bfm(y), a.stats, cur_stream());  // the CIFAR stem (stem.hip)
+  } else {
+    tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
+  }
   tfx::bn_finalize(a.stats, a.M, g.Ko, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
                    fpm(run_var), save.data_ptr<float>(), cur_stream());
   return {y, save};
+}
+
+// A/B hook for the stem forward kernel; returns the previous setting
+bool conv_stem_fwd(bool on) {
+  const bool prev = g_stem_fwd;
+  g_stem_fwd = on;
+  return prev;
 }
 
 // conv_fwd_bn of relu(x * in_save[2C..3C) + in_save[3C..4C)) -- a plain ReLU BN applied on load by this
@@ -1721,6 +1736,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_fwd_bn_in", &conv_fwd_bn_in);
   m.def("stem_wgrad", &stem_wgrad);
+  m.def("conv_stem_fwd", &conv_stem_fwd);
   m.def("stem_wgrad_ws_floats", &stem_wgrad_ws_floats);
   m.def("stem_wgrad_supported", &stem_wgrad_supported);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "
