@@ -288,10 +288,19 @@ struct HeadXentArgs {
   uint16_t* dfeat = nullptr;         // [N][HW][C] input gradient (bf16)
   float* loss = nullptr;             // [1] batch mean
   unsigned long long* state = nullptr;
+  // tail mode (y3 set): x is not read; the input is relu(y3 * scale + shift + res) of the last block's
+  // tail BN (save3 = its [4][C] save), its mask bits are written to mask [N*HW][C/8] and its backward
+  // partials written to bn_rows [N][2][C] (head_rows_reduce sums them)
+  const uint16_t* y3 = nullptr;
+  const uint16_t* res = nullptr;
+  const float* save3 = nullptr;
+  uint8_t* mask = nullptr;
+  float* bn_rows = nullptr;
   int C = 0, HW = 0, O = 0;
   float gscale = 0.f;
 };
 bool head_xent_ok(int C, int O, int HW);
+void head_rows_reduce(const float* rows, int N, int C, float* red, float* dgamma, float* dbeta, hipStream_t s);
 void head_xent_fwd(const HeadXentArgs& args, int N, hipStream_t s);
 // dW [O][C] += dz^T feat, db += colsum(dz) (plain read-modify-write: one block per 8 channels)
 void head_wgrad(const uint16_t* dz, const uint16_t* feat, int N, int C, int O, float* dw, float* db, hipStream_t s);

@@ -5,7 +5,8 @@
 // Layer-wise the head of ResNet-50/CIFAR is five launches (gap_fwd, a 2-block bf16 GEMM that walks
 // K = 2048 serially, softmax_xent_mean, linear_small_bwd, gap_bwd: 76 us of a 7.5 ms step,
 // profiles/r03_f1/step_trace_conv3.txt).  Forward, one block per sample (rows are independent once
-// the batch mean is taken out of the loss gradient: dz = (p - y) / B):
+// the batch mean is taken out of the loss gradient: dz = (p - y) / B; 1024 threads = 4 pixel groups
+// x 256 channel lanes, so a sample's pixels stream in parallel, reduced through LDS):
 //   f      = bf16(mean_hw x[n])                     (written: the FC weight gradient needs it)
 //   z      = bf16(W f + b)                          (DPP row sums, then 16 partials per class in LDS)
 //   loss_n = logsumexp(z) - z[label],  dz = bf16((p - onehot) / B)   (dz written for dW / db)
@@ -20,6 +21,12 @@
 // before the block's dfeat stores, so its round trip hides behind them; no release/acquire fences
 // (atomics complete at the memory side).  A non-finite or huge row loss sets a flag word first: the
 // mean is then NaN.
+// TAIL: the head's input is the last block's tail BN output, never written -- out = relu(y3 sc + sh + res)
+// is formed per pixel while pooling (bf16, exactly the apply pass's values) with its ReLU mask bits
+// stored for the BN's backward, and that BN's backward partials (sum g', sum g' xhat over g' = dfeat *
+// mask: per channel d * sum_hw mask, d * sum_hw mask xhat, d the pixel-constant input gradient) are
+// written as one row per sample (no atomics), summed by head_rows_reduce in the backward -- the apply
+// pass and the BN's backward reduction pass disappear.
 // Reference: R/distributed/distributed.py:96-102 (the loss the reference builds op by op); north-star
 // ResNet-50 head (BASELINE.json config 3).
 #include "tfx_common.h"
@@ -28,7 +35,11 @@
 namespace tfx {
 namespace {
 
-constexpr int HEAD_NT = 256;
+constexpr int HEAD_NT = 256;                             // channel lanes: 8 channels each
+constexpr int HEAD_PG = 4;                               // forward: pixel groups of HEAD_NT threads
+constexpr int HEAD_FT = HEAD_NT * HEAD_PG;               // forward block
+constexpr int HEAD_U = 4;                                // pixels in flight per thread
+constexpr int HEAD_UT = 4;                               // ... in TAIL mode (two operands)
 constexpr int HEAD_CNT_BITS = 12;                        // done count (N <= 4095)
 constexpr double HEAD_FIX = 16777216.0;                 // 2^24 per unit of loss
 constexpr float HEAD_ROW_MAX = 1e6f;                    // 4095 rows x 1e6 x 2^24 < 2^64 / 2^12
@@ -38,57 +49,142 @@ __device__ __forceinline__ void head_lds_sync() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int OMAX>
-__global__ void __launch_bounds__(HEAD_NT) head_xent_fwd_kernel(HeadXentArgs a) {
+template <int OMAX, bool TAIL>
+__global__ void __launch_bounds__(HEAD_FT) head_xent_fwd_kernel(HeadXentArgs a) {
   __shared__ float part[HEAD_NT / 16][OMAX];  // one partial per DPP row (16 lanes)
   __shared__ float dzs[OMAX];
-  const int n = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  // per pixel group: pooled sums (TAIL: + sum_hw mask, sum_hw mask * xhat), [quantity][group][k][t]
+  __shared__ float red[TAIL ? 3 : 1][HEAD_PG][8][HEAD_NT];
+  __shared__ U4 dlds[HEAD_NT];  // the packed pixel-constant dfeat of each 8-channel group
+  __shared__ float bsh[OMAX];
+  const int n = blockIdx.x, tt = threadIdx.x, t = tt & (HEAD_NT - 1), pg = tt / HEAD_NT, lane = tt & 63;
   const int C8 = a.C >> 3, O = a.O;
-  const bool own = t < C8;  // this thread's 8 channels (C <= 8 * HEAD_NT, host check)
+  const bool own = t < C8;   // this thread's 8 channels (C <= 8 * HEAD_NT, host check)
+  const bool lead = pg == 0;  // wave-uniform: pixel group 0 computes the logits and dfeat
   const float inv_hw = 1.f / (float)a.HW;
-  const U4* xr = reinterpret_cast<const U4*>(a.x + (int64_t)n * a.HW * a.C);
   const U4 zero = U4{0u, 0u, 0u, 0u};
+  // every load below is unconditional at a clamped index (a select around a load compiles to a branch
+  // that drains the load counter): a thread past C reads channel group 0, a padding pixel the last one
+  const int tc = own ? t : 0;
+  const int64_t lab = a.labels[n];
+  const float bias = a.b ? a.b[min(tt, O - 1)] : 0.f;
 
-  // ---- W columns of this thread's channels (L2-resident, independent of x: issued first)
-  U4 wraw[OMAX];
-#pragma unroll
-  for (int j = 0; j < OMAX; ++j) wraw[j] = (j < O && own) ? reinterpret_cast<const U4*>(a.w + (int64_t)j * a.C)[t] : zero;
-  // ---- pooled features: 16 pixels' loads in flight per step
+  // ---- pooled partials of this pixel group: pixels pg, pg + PG, ... (HEAD_U of them in flight)
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int p = 0; p < a.HW; p += 16) {
-    U4 v[16];
+  if constexpr (!TAIL) {
+    const U4* xr = reinterpret_cast<const U4*>(a.x + (int64_t)n * a.HW * a.C);
+    for (int p = pg; p < a.HW; p += HEAD_PG * HEAD_U) {
+      U4 v[HEAD_U];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = (own && p + q < a.HW) ? xr[(int64_t)(p + q) * C8 + t] : zero;
+      for (int q = 0; q < HEAD_U; ++q) {
+        const int pp = p + HEAD_PG * q;
+        v[q] = xr[(int64_t)min(pp, a.HW - 1) * C8 + tc];
+      }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      float e[8];
-      unpack8(v[q], e);
+      for (int q = 0; q < HEAD_U; ++q) {
+        if (p + HEAD_PG * q >= a.HW) break;
+        float e[8];
+        unpack8(v[q], e);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s[k] += e[k];
+        for (int k = 0; k < 8; ++k) s[k] += e[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[0][pg][k][t] = s[k];
+  } else {
+    float sc[8], sh[8], mu[8], is[8], cnt[8], sxh[8];  // cnt / sxh: sum_hw mask, sum_hw mask * xhat
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = 8 * tc + k;
+      mu[k] = a.save3[c];
+      is[k] = a.save3[a.C + c];
+      sc[k] = a.save3[2 * a.C + c];
+      sh[k] = a.save3[3 * a.C + c];
+      cnt[k] = sxh[k] = 0.f;
+    }
+    const U4* yr = reinterpret_cast<const U4*>(a.y3 + (int64_t)n * a.HW * a.C);
+    const U4* rr = reinterpret_cast<const U4*>(a.res + (int64_t)n * a.HW * a.C);
+    for (int p = pg; p < a.HW; p += HEAD_PG * HEAD_UT) {
+      U4 vy[HEAD_UT], vr[HEAD_UT];
+#pragma unroll
+      for (int q = 0; q < HEAD_UT; ++q) {
+        const int pp = p + HEAD_PG * q;
+        const int64_t i = (int64_t)min(pp, a.HW - 1) * C8 + tc;
+        vy[q] = yr[i];
+        vr[q] = rr[i];
+      }
+#pragma unroll
+      for (int q = 0; q < HEAD_UT; ++q) {
+        const int pp = p + HEAD_PG * q;
+        if (pp >= a.HW) break;  // a padding pixel would add relu(shift)
+        float ey[8], er[8], o[8];
+        unpack8(vy[q], ey);
+        unpack8(vr[q], er);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float z = fmaf(ey[k], sc[k], sh[k]) + er[k];  // bn_apply_vec's math
+          const bool on = z > 0.f;
+          bits |= (on ? 1u : 0u) << k;
+          o[k] = fmaxf(z, 0.f);
+          cnt[k] += on ? 1.f : 0.f;
+          sxh[k] += on ? (ey[k] - mu[k]) * is[k] : 0.f;
+        }
+        float ob[8];
+        unpack8(pack8(o), ob);  // the bf16 values the apply pass would have written
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += ob[k];
+        if (own) a.mask[((int64_t)n * a.HW + pp) * C8 + t] = (uint8_t)bits;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[0][pg][k][t] = s[k];
+      red[1][pg][k][t] = cnt[k];
+      red[2][pg][k][t] = sxh[k];
     }
   }
+  // ---- W columns of this thread's channels (L2-resident; the lead waves only, in flight over the sync)
+  // (rows past O read row O-1 and are never used; a thread past C reads real channels, times f = 0)
+  U4 wraw[OMAX];
+  if (lead) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) s[k] *= inv_hw;
-  const U4 fb = pack8(s);  // the layer-wise gap_fwd output (bf16)
-  float f[8];
-  unpack8(fb, f);
-  if (own) reinterpret_cast<U4*>(a.feat + (int64_t)n * a.C)[t] = fb;
+    for (int j = 0; j < OMAX; ++j) wraw[j] = reinterpret_cast<const U4*>(a.w + (int64_t)min(j, O - 1) * a.C)[tc];
+  }
+  if (tt < OMAX) bsh[tt] = bias;
+  __syncthreads();
 
   // ---- logits: per-thread partial dots, DPP row sums, 16 partials per class through LDS
-  float w[OMAX][8];
+  float f[8];
+  if (lead) {
 #pragma unroll
-  for (int j = 0; j < OMAX; ++j) {
-    unpack8(wraw[j], w[j]);
-    float d = 0.f;
+    for (int k = 0; k < 8; ++k) {
+      float v = red[0][0][k][t];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d = fmaf(w[j][k], f[k], d);
-    d = row16_sum(d);
-    if ((lane & 15) == 0) part[t >> 4][j] = d;
+      for (int g = 1; g < HEAD_PG; ++g) v += red[0][g][k][t];
+      s[k] = v * inv_hw;
+    }
+    const U4 fb = pack8(s);  // the layer-wise gap_fwd output (bf16)
+    unpack8(fb, f);
+    if (!own)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = 0.f;
+    if (own) reinterpret_cast<U4*>(a.feat + (int64_t)n * a.C)[t] = fb;
+#pragma unroll
+    for (int j = 0; j < OMAX; ++j) {
+      float w[8];
+      unpack8(wraw[j], w);
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d = fmaf(w[k], f[k], d);
+      d = row16_sum(d);  // classes past O: never read
+      if ((lane & 15) == 0) part[t >> 4][j] = d;
+    }
   }
   head_lds_sync();
   unsigned long long prev = 0ull, mine = 0ull;
   float lrow = 0.f;
-  if (t == 0) {
+  if (tt == 0) {
     float z[OMAX];
     float m = -INFINITY;
 #pragma unroll
@@ -97,7 +193,7 @@ __global__ void __launch_bounds__(HEAD_NT) head_xent_fwd_kernel(HeadXentArgs a) 
         float acc = 0.f;
 #pragma unroll
         for (int r = 0; r < HEAD_NT / 16; ++r) acc += part[r][j];
-        if (a.b) acc += a.b[j];
+        acc += bsh[j];
         z[j] = bf16_to_f32(f32_to_bf16(acc));  // the layer-wise GEMM's bf16 logits
         m = fmaxf(m, z[j]);
       }
@@ -107,7 +203,6 @@ __global__ void __launch_bounds__(HEAD_NT) head_xent_fwd_kernel(HeadXentArgs a) 
     for (int j = 0; j < OMAX; ++j)
       if (j < O) sum += __expf(z[j] - m);
     const float inv_s = 1.f / sum, lse = m + __logf(sum);
-    const int64_t lab = a.labels[n];
 #pragma unroll
     for (int j = 0; j < OMAX; ++j) {
       if (j < O) {
@@ -128,21 +223,43 @@ __global__ void __launch_bounds__(HEAD_NT) head_xent_fwd_kernel(HeadXentArgs a) 
     prev = __hip_atomic_fetch_add(a.state, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   head_lds_sync();
-  // ---- dfeat = bf16(bf16(dz W) / HW) over every pixel (the layer-wise linear dx, then gap_bwd)
-  float d[8];
+  // ---- dfeat = bf16(bf16(dz W) / HW) (the layer-wise linear dx, then gap_bwd): lead waves form it
+  if (lead) {
+    float d[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float acc = 0.f;
+    for (int j = 0; j < OMAX; ++j) {
+      float w[8];
+      unpack8(wraw[j], w);
+      const float g = j < O ? dzs[j] : 0.f;
 #pragma unroll
-    for (int j = 0; j < OMAX; ++j) acc = fmaf(j < O ? dzs[j] : 0.f, w[j][k], acc);
-    d[k] = bf16_to_f32(f32_to_bf16(acc)) * inv_hw;
+      for (int k = 0; k < 8; ++k) d[k] = fmaf(g, w[k], d[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = bf16_to_f32(f32_to_bf16(d[k])) * inv_hw;
+    dlds[t] = pack8(d);
   }
-  const U4 o = pack8(d);
+  head_lds_sync();
+  // ... every pixel group stores its pixels
   U4* dr = reinterpret_cast<U4*>(a.dfeat + (int64_t)n * a.HW * a.C);
-  if (own)
-    for (int p = 0; p < a.HW; ++p) dr[(int64_t)p * C8 + t] = o;
+  if (own) {
+    const U4 o = dlds[t];
+    for (int p = pg; p < a.HW; p += HEAD_PG) dr[(int64_t)p * C8 + t] = o;
+  }
+  if constexpr (TAIL) {
+    // the tail BN's backward partials of this sample, g' = dfeat * mask with dfeat pixel-constant:
+    // row n of [N][sum g' | sum g' xhat] (plain stores; head_rows_reduce sums the rows)
+    float* row = a.bn_rows + (size_t)n * 2 * a.C;
+    const uint16_t* dh = reinterpret_cast<const uint16_t*>(dlds);
+    for (int v = tt; v < 2 * a.C; v += HEAD_FT) {
+      const int kind = v >= a.C ? 1 : 0, c = v - kind * a.C;
+      float tot = 0.f;
+#pragma unroll
+      for (int g = 0; g < HEAD_PG; ++g) tot += red[1 + kind][g][c & 7][c >> 3];
+      row[v] = bf16_to_f32(dh[c]) * tot;
+    }
+  }
   // ---- the last block to count in finishes the mean (its returned word + its own = every row)
-  if (t == 0) {
+  if (tt == 0) {
     const unsigned long long tot = prev + mine;
     const unsigned long long cnt = tot & ((1ull << HEAD_CNT_BITS) - 1);
     if (cnt == (unsigned long long)gridDim.x) {
@@ -209,13 +326,56 @@ __global__ void __launch_bounds__(HEAD_NT) head_wgrad_kernel(const uint16_t* __r
   }
 }
 
+// red[v] = sum_n rows[n][v] over v < 2C ([sum g' | sum g' xhat]); dbeta += red[:C], dgamma += red[C:].
+// Block = 64 columns x 4 row groups, 8 rows in flight per thread, LDS sum of the 4 groups.
+__global__ void __launch_bounds__(256) head_rows_reduce_kernel(const float* __restrict__ rows, int N, int C,
+                                                               float* __restrict__ red, float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta) {
+  __shared__ float part[4][64];
+  const int t = threadIdx.x, col = t & 63, rg = t >> 6;
+  const int v = blockIdx.x * 64 + col, V = 2 * C;
+  float acc = 0.f;
+  if (v < V) {
+    int r = rg;
+    for (; r + 4 * 7 < N; r += 4 * 8) {
+      float x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x[q] = rows[(size_t)(r + 4 * q) * V + v];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc += x[q];
+    }
+    for (; r < N; r += 4) acc += rows[(size_t)r * V + v];
+  }
+  part[rg][col] = acc;
+  __syncthreads();
+  if (rg == 0 && v < V) {
+    const float tot = ((part[0][col] + part[1][col]) + part[2][col]) + part[3][col];
+    red[v] = tot;
+    if (v < C) {
+      if (dbeta) dbeta[v] += tot;
+    } else if (dgamma) {
+      dgamma[v - C] += tot;
+    }
+  }
+}
+
 }  // namespace
+
+void head_rows_reduce(const float* rows, int N, int C, float* red, float* dgamma, float* dbeta, hipStream_t s) {
+  head_rows_reduce_kernel<<<(2 * C + 63) / 64, 256, 0, s>>>(rows, N, C, red, dgamma, dbeta);
+}
 
 bool head_xent_ok(int C, int O, int HW) { return C % 8 == 0 && C <= 8 * HEAD_NT && O >= 1 && O <= 16 && HW >= 1; }
 
 void head_xent_fwd(const HeadXentArgs& args, int N, hipStream_t s) {
-  if (args.O <= 10) head_xent_fwd_kernel<10><<<N, HEAD_NT, 0, s>>>(args);  // CIFAR-10
-  else head_xent_fwd_kernel<16><<<N, HEAD_NT, 0, s>>>(args);
+  const bool tail = args.y3 != nullptr;
+  if (args.O <= 10) {  // CIFAR-10
+    if (tail) head_xent_fwd_kernel<10, true><<<N, HEAD_FT, 0, s>>>(args);
+    else head_xent_fwd_kernel<10, false><<<N, HEAD_FT, 0, s>>>(args);
+  } else {
+    if (tail) head_xent_fwd_kernel<16, true><<<N, HEAD_FT, 0, s>>>(args);
+    else head_xent_fwd_kernel<16, false><<<N, HEAD_FT, 0, s>>>(args);
+  }
 }
 
 void head_wgrad(const uint16_t* dz, const uint16_t* feat, int N, int C, int O, float* dw, float* db, hipStream_t s) {

@@ -1037,8 +1037,24 @@ std::tuple<Tensor, Tensor> softmax_xent_mean(Tensor z, optional<Tensor> lab_idx,
 // state: int64 [3] zeros, owned by the caller across launches (the kernel leaves it zero).
 bool head_xent_supported(int64_t C, int64_t O, int64_t HW) { return tfx::head_xent_ok((int)C, (int)O, (int)HW); }
 
+// the fused head's tail-BN backward rows [N][2C] -> red [2C]; dbeta += red[:C], dgamma += red[C:]
+Tensor head_rows_reduce(Tensor rows, int64_t C, optional<Tensor> dgamma, optional<Tensor> dbeta) {
+  CHECK_DEV(rows); CHECK_F32(rows); CHECK_CONTIG(rows);
+  TORCH_CHECK(C > 0 && rows.numel() % (2 * C) == 0, "head_rows_reduce: rows [N][2C]");
+  for (const auto* o : {&dgamma, &dbeta})
+    if (o->has_value() && (*o)->defined()) {
+      CHECK_F32(**o); TORCH_CHECK((*o)->numel() == C && (*o)->is_contiguous(), "head_rows_reduce: dgamma/dbeta [C]");
+    }
+  auto red = at::empty({2 * C}, rows.options());
+  tfx::head_rows_reduce(rows.data_ptr<float>(), (int)(rows.numel() / (2 * C)), (int)C, red.data_ptr<float>(),
+                        fpm(dgamma), fpm(dbeta), cur_stream());
+  return red;
+}
+
 std::tuple<Tensor, Tensor, Tensor, Tensor> head_xent(Tensor x, Tensor w, optional<Tensor> b, Tensor labels,
-                                                     Tensor state) {
+                                                     Tensor state, optional<Tensor> y3, optional<Tensor> res,
+                                                     optional<Tensor> save3, optional<Tensor> mask,
+                                                     optional<Tensor> bn_rows) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 4, "head_xent expects NHWC features");
   const int64_t N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3), O = w.size(0);
@@ -1060,6 +1076,23 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> head_xent(Tensor x, Tensor w, optiona
   a.feat = bfm(feat); a.dz = bfm(dz); a.dfeat = bfm(dfeat); a.loss = loss.data_ptr<float>();
   a.state = reinterpret_cast<unsigned long long*>(state.data_ptr<int64_t>());
   a.C = (int)C; a.HW = (int)HW; a.O = (int)O; a.gscale = 1.0f / (float)N;
+  if (y3.has_value() && y3->defined()) {
+    // tail mode: x (the unwritten tail output) only gives the shape
+    TORCH_CHECK(res.has_value() && save3.has_value() && mask.has_value() && bn_rows.has_value(),
+                "head_xent tail mode: y3, res, save3, mask, bn_rows");
+    for (const Tensor* tt : {&*y3, &*res}) {
+      CHECK_BF16(*tt); CHECK_CONTIG(*tt);
+      TORCH_CHECK(tt->sizes() == x.sizes(), "head_xent tail: y3 / res shape");
+      check_aligned16(*tt, "tail operand");
+    }
+    CHECK_F32(*save3); TORCH_CHECK(save3->numel() == 4 * C, "head_xent tail: save3");
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() * 8 == x.numel(),
+                "head_xent tail: mask");
+    CHECK_F32(*bn_rows); CHECK_CONTIG(*bn_rows);
+    TORCH_CHECK(bn_rows->numel() == N * 2 * C, "head_xent tail: bn rows [N][2][C]");
+    a.y3 = bf(*y3); a.res = bf(*res); a.save3 = save3->data_ptr<float>(); a.mask = mask->data_ptr<uint8_t>();
+    a.bn_rows = bn_rows->data_ptr<float>();
+  }
   tfx::head_xent_fwd(a, (int)N, cur_stream());
   return {loss, dfeat, feat, dz};
 }
@@ -1759,7 +1792,10 @@ TORCH_LIBRARY(tfx, m) {
         "Tensor? dbeta, Tensor? mask, bool want_dres=True) -> (Tensor, Tensor, Tensor)", &bn_bwd);
   m.def("softmax_xent", &softmax_xent);
   m.def("softmax_xent_mean", &softmax_xent_mean);
-  m.def("head_xent", &head_xent);
+  m.def("head_xent(Tensor x, Tensor w, Tensor? b, Tensor labels, Tensor state, Tensor? y3=None, Tensor? res=None, "
+        "Tensor? save3=None, Tensor? mask=None, Tensor? bn_rows=None) -> (Tensor, Tensor, Tensor, Tensor)",
+        &head_xent);
+  m.def("head_rows_reduce", &head_rows_reduce);
   m.def("head_wgrad", &head_wgrad);
   m.def("head_xent_supported", &head_xent_supported);
   m.def("accuracy_count", &accuracy_count);

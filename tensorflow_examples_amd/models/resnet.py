@@ -185,13 +185,15 @@ class ResNetCifar:
             self.stem.w.master[..., 3:] = 0
         self.store.refresh_shadow()
 
-    def features(self, x: torch.Tensor, training: bool = True) -> torch.Tensor:
-        """Stem and residual stages: the NHWC input of the classifier head."""
+    def features(self, x: torch.Tensor, training: bool = True, defer_last: bool = False) -> torch.Tensor:
+        """Stem and residual stages: the NHWC input of the classifier head.  ``defer_last``: the caller's
+        head applies the last block's tail BN itself (ops.classifier_head_xent); anything else that reads
+        the output first materialises it (ops.nn.TailPending)."""
         o = self.stem_bn.after_conv(self.stem, x, training, relu=True)
         for i, blk in enumerate(self.blocks):
             if isinstance(blk, Bottleneck):
                 nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
-                o = blk(o, training, defer_tail=isinstance(nxt, Bottleneck))
+                o = blk(o, training, defer_tail=isinstance(nxt, Bottleneck) or (nxt is None and defer_last))
             else:
                 o = blk(o, training)
         return o
@@ -204,8 +206,8 @@ class ResNetCifar:
                       unit_seed: bool = False) -> torch.Tensor:
         """Mean softmax cross-entropy of a training forward; the head (pool, FC, loss and, for a unit
         seed, its input gradient) is one launch on the GPU (ops.classifier_head_xent)."""
-        return ops.classifier_head_xent(self.features(x, True), self.fc_w, self.fc_b, labels, naive=naive,
-                                        unit_seed=unit_seed)
+        return ops.classifier_head_xent(self.features(x, True, defer_last=True), self.fc_w, self.fc_b, labels,
+                                        naive=naive, unit_seed=unit_seed)
 
 
 def build_resnet_cifar(device="cuda", depth=50, num_classes=10, dtype=torch.bfloat16, seed=0) -> Tuple[VariableStore, ResNetCifar]:

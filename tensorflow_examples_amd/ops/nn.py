@@ -988,7 +988,7 @@ class _GlobalAvgPool(torch.autograd.Function):
         ctx.shape = x.shape
         ctx.native = _native.use_native(x)
         if ctx.native:
-            return torch.ops.tfx.gap_fwd(x.contiguous(), False)
+            return torch.ops.tfx.gap_fwd(_settle(x).contiguous(), False)
         return x.mean(dim=(1, 2))
 
     @staticmethod
@@ -1125,7 +1125,9 @@ def softmax_cross_entropy(logits, labels, naive: bool = False, unit_seed: bool =
 
 # ---- fused classifier head (training step): gap -> linear -> mean softmax xent, one launch (head.hip)
 _FUSE_HEAD = True  # test / A-B hook: False composes global_avg_pool, linear and softmax_cross_entropy
+_HEAD_TAIL = True  # test / A-B hook: False materialises a deferred last tail before the fused head
 HEAD_FUSED_CALLS = [0]
+HEAD_TAIL_CALLS = [0]
 _HEAD_STATE = {}
 
 
@@ -1145,10 +1147,22 @@ class _HeadXent(torch.autograd.Function):
     accumulates dW += dz^T f and db += colsum(dz) (head_wgrad, one small launch)."""
 
     @staticmethod
-    def forward(ctx, feat, anchor, w: Variable, b: Optional[Variable], labels):
-        ctx.w, ctx.b = w, b
-        loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, b.master if b is not None else None, labels,
-                                                     _head_state(feat.device))
+    def forward(ctx, feat, anchor, w: Variable, b: Optional[Variable], labels, tail):
+        # tail = (TailPending, BNBackwardFusion) of the last block's unwritten tail BN output: the kernel
+        # forms it while pooling, writes its mask bits and that BN's backward partials (head.hip TAIL)
+        ctx.w, ctx.b, ctx.tail_bnb = w, b, None
+        bias = b.master if b is not None else None
+        if tail is not None:
+            tp, bnb = tail
+            rows = torch.empty(2 * feat.numel() // (feat.shape[1] * feat.shape[2]), dtype=torch.float32,
+                               device=feat.device)
+            loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, bias, labels, _head_state(feat.device), tp.x,
+                                                         tp.res, tp.save, tp.mask, rows)
+            ctx.tail_bnb, ctx.tail_rows = bnb, rows
+            HEAD_TAIL_CALLS[0] += 1
+        else:
+            loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, bias, labels, _head_state(feat.device), None,
+                                                         None, None, None, None)
         ctx.save_for_backward(dfeat, f, dz)
         HEAD_FUSED_CALLS[0] += 1
         return loss
@@ -1157,11 +1171,29 @@ class _HeadXent(torch.autograd.Function):
     def backward(ctx, g):
         dfeat, f, dz = ctx.saved_tensors
         w, b = ctx.w, ctx.b
+        bnb = ctx.tail_bnb
+        if bnb is not None:  # the tail BN's backward reduction: the forward wrote its per-sample partials
+            bnb.red = torch.ops.tfx.head_rows_reduce(ctx.tail_rows, bnb.x.shape[-1], bnb.dgamma, bnb.dbeta)
+            ctx.tail_rows = None
         bias_grad = b.grad if (b is not None and b.trainable) else None
         if w.trainable or bias_grad is not None:
             torch.ops.tfx.head_wgrad(dz, f, w.grad if w.trainable else None, bias_grad)
         _grad_ready(w if w.trainable else None, b if bias_grad is not None else None)
-        return dfeat, None, None, None, None
+        return dfeat, None, None, None, None, None
+
+
+def _head_tail(feat):
+    """(TailPending, BNBackwardFusion) when ``feat`` is a ReLU + identity-residual tail BN's output that
+    was never written and whose backward reduction nobody owes yet: the fused head takes both over."""
+    tp = getattr(feat, "_tfx_tail", None)
+    bnb = getattr(feat, "_tfx_bnb", None)
+    if not _HEAD_TAIL or tp is None or tp.done or bnb is None:
+        return None
+    if tp.res is None or tp.res_save is not None or tp.mask is None or bnb.mask is not tp.mask or not bnb.relu:
+        return None
+    if bnb.deferred or bnb.red is not None or bnb.sr_pending or bnb.x is not tp.x:
+        return None
+    return tp, bnb
 
 
 def classifier_head_xent(feat, w: Variable, b: Optional[Variable], labels, naive: bool = False,
@@ -1178,7 +1210,9 @@ def classifier_head_xent(feat, w: Variable, b: Optional[Variable], labels, naive
         n, h, wd, c = feat.shape
         fused = bool(torch.ops.tfx.head_xent_supported(c, w.shape[0], h * wd)) and labels.numel() == n <= 4095
     if fused:
-        return _HeadXent.apply(_settle(feat).contiguous(), w.store.anchor, w, b, labels.contiguous())
+        tail = _head_tail(feat)
+        return _HeadXent.apply(feat if tail is not None else _settle(feat).contiguous(), w.store.anchor, w, b,
+                               labels.contiguous(), tail)
     logits = linear(global_avg_pool(feat), w, b)
     return softmax_cross_entropy(logits, labels, naive=naive, unit_seed=unit_seed)
 

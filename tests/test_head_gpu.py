@@ -108,3 +108,80 @@ def test_head_xent_nonfinite_loss_is_nan(gpu):
     assert int(state.abs().sum().item()) == 0
     ok = torch.ops.tfx.head_xent(feat.nan_to_num(posinf=0.0), w.value, b.master, labels, state)[0]
     assert torch.isfinite(ok).item()
+
+
+@pytest.mark.parametrize("N,H,W,C,O", [(128, 4, 4, 2048, 10), (5, 3, 3, 64, 16)])
+def test_head_xent_tail_mode_matches_applied_input(gpu, N, H, W, C, O):
+    """Tail mode: the head forms relu(y3 * scale + shift + res) itself -- same loss / dfeat / features as
+    the head over the applied (bf16) output, the apply pass's mask bits, and the tail BN's backward
+    partials (sum g', sum g' xhat) as per-sample rows that head_rows_reduce sums (+= dbeta / dgamma)."""
+    torch.manual_seed(5)
+    y3 = torch.randn(N, H, W, C, device=gpu).to(torch.bfloat16)
+    res = torch.randn(N, H, W, C, device=gpu).clamp_min(0).to(torch.bfloat16)
+    mu, var = y3.float().mean((0, 1, 2)), y3.float().var((0, 1, 2), unbiased=False)
+    inv = torch.rsqrt(var + 1e-5)
+    gam, bet = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.3
+    save = torch.cat([mu, inv, gam * inv, bet - mu * gam * inv]).contiguous()
+    out = torch.empty_like(y3)
+    mask_ref = torch.empty(y3.numel() // 8, dtype=torch.uint8, device=gpu)
+    torch.ops.tfx.bn_apply_into(y3, res, save, None, out, mask_ref)
+    labels = torch.randint(0, O, (N,), device=gpu)
+    st, w, b = _store(gpu, O, C)
+    state = opsnn._head_state(gpu)
+    ref = torch.ops.tfx.head_xent(out, w.value, b.master, labels, state)
+    mask = torch.zeros_like(mask_ref)
+    rows = torch.empty(N * 2 * C, device=gpu)
+    got = torch.ops.tfx.head_xent(torch.empty_like(y3), w.value, b.master, labels, state, y3, res, save, mask, rows)
+    dg, db = torch.full((C,), 0.5, device=gpu), torch.full((C,), -0.25, device=gpu)
+    red = torch.ops.tfx.head_rows_reduce(rows, C, dg, db)
+    torch.cuda.synchronize()
+    assert torch.equal(mask, mask_ref)
+    assert got[0].item() == ref[0].item()
+    for a, r in zip(got[1:], ref[1:]):
+        assert torch.equal(a, r)
+    m = ((mask_ref.view(-1, 1) >> torch.arange(8, device=gpu, dtype=torch.uint8)) & 1).view(N, H, W, C).float()
+    gp = got[1].float() * m
+    xhat = (y3.float() - mu) * inv
+    ref_red = torch.stack([gp.sum((0, 1, 2)), (gp * xhat).sum((0, 1, 2))])
+    assert _rel(red.view(2, C), ref_red) < 1e-4
+    assert _rel(rows.view(N, 2, C).sum(0), ref_red) < 1e-4
+    assert _rel(db, ref_red[0] - 0.25) < 1e-4 and _rel(dg, ref_red[1] + 0.5) < 1e-4
+
+
+def test_resnet_head_takes_over_last_tail(gpu):
+    """ResNet-50/CIFAR training_loss: the fused head applies the last block's tail BN and reduces its
+    backward (HEAD_TAIL_CALLS).  A random-init bf16 ResNet-50 amplifies the f32-atomic order noise of
+    its BN statistics from layer to layer, so the gradients are compared with the materialised-tail
+    path per variable against the noise floor of two runs of the same path (as
+    test_resnet_gpu.test_deferred_slot_reductions_fallback_and_off_agree)."""
+    from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
+    img = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, device=gpu)
+    lab = torch.randint(0, 10, (32,), device=gpu)
+    st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=7)
+
+    def run(tail):
+        old = opsnn._HEAD_TAIL
+        opsnn._HEAD_TAIL = tail
+        try:
+            st.zero_grad()
+            n0 = opsnn.HEAD_TAIL_CALLS[0]
+            loss = m.training_loss(to_model_input(img), lab, unit_seed=True)
+            loss.backward()
+            torch.cuda.synchronize()
+            assert (opsnn.HEAD_TAIL_CALLS[0] - n0) == (1 if tail else 0)
+            assert not opsnn._PENDING_SR
+            return loss.item(), st.grad.clone()
+        finally:
+            opsnn._HEAD_TAIL = old
+
+    l0, g0 = run(False)
+    l1, g1 = run(False)
+    l2, g2 = run(True)
+    assert torch.isfinite(g2).all()
+    assert abs(l2 - l0) <= 4 * abs(l1 - l0) + 1e-2, (l0, l1, l2)
+    for v in st.trainable():
+        sl = slice(v.offset, v.offset + v.numel)
+        n = g0[sl].norm().item() + 1e-12
+        noise = (g1[sl] - g0[sl]).norm().item() / n
+        e = (g2[sl] - g0[sl]).norm().item() / n
+        assert e <= max(4 * noise, 1e-3), (v.name, e, noise)
