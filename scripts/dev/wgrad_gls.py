@@ -1,0 +1,48 @@
+"""Weight-gradient launch configurations at the ResNet-50/CIFAR bench shapes: the tuned/auto choice vs
+forced (tile, ks, gls, want) candidates (profiles/r03_w8).  Checks each result
+against the auto configuration's."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "scripts"))
+from tensorflow_examples_amd.ops import _native, tuning  # noqa: E402
+from operand_major_bench import graph_us  # noqa: E402
+
+assert _native.load()
+tuning.load()
+FAMS = (6, 7, 8)
+CANDS = [None, (1, 2, 2, 256), (2, 2, 3, 256), (1, 1, 3, 256), (2, 1, 3, 256)]
+SHAPES = [(256, 32, 32, 64, 64, 3, 1), (256, 16, 16, 128, 128, 3, 1), (256, 8, 8, 256, 256, 3, 1),
+          (256, 4, 4, 512, 512, 3, 1), (256, 32, 32, 64, 256, 1, 1), (256, 8, 8, 256, 1024, 1, 1),
+          (256, 8, 8, 1024, 256, 1, 1), (256, 16, 16, 128, 512, 1, 1), (256, 4, 4, 2048, 512, 1, 1)]
+
+
+def force(c):
+    torch.ops.tfx.igemm_tune_force(-1, 0, 0, -1, 0)
+    if c is not None:
+        for f in FAMS:
+            torch.ops.tfx.igemm_tune_force(f, *c)
+
+
+for (N, H, W, C, K, R, st) in SHAPES:
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    gy = torch.randn(N, (H - 1) // st + 1, (W - 1) // st + 1, K, device="cuda").bfloat16()
+    ref = None
+    line = []
+    for c in CANDS:
+        force(c)
+        dw = torch.zeros(K, R, R, C, device="cuda")
+        torch.ops.tfx.conv_wgrad(gy, x, dw, st, R // 2, 1, True)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = dw.clone()
+            err = 0.0
+        else:
+            err = ((dw - ref).norm() / ref.norm()).item()
+        t = graph_us(lambda: torch.ops.tfx.conv_wgrad(gy, x, dw, st, R // 2, 1, True))
+        line.append(f"{str(c):>16}: {t:6.1f}us e{err:.0e}")
+    force(None)
+    print([N, H, W, C, K, R, st], " | ".join(line), flush=True)
