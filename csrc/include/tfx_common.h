@@ -72,6 +72,15 @@ __device__ __forceinline__ float wave_max(float v) {
 // Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5, T1):
 // blocks b and b+8 share an XCD's L2 under round-robin dispatch, so hand each XCD a
 // contiguous run of logical tiles.  Pure speed: correctness never depends on placement.
+// p[i], or 0 for a null p, as a buffer load whose resource has no records when p is null: no branch
+// around the load (a branch -- even on a uniform condition -- makes the waitcnt pass drain the load
+// counter at its join, serialising the loads behind it)
+__device__ __forceinline__ float ld_f32_or0(const float* p, int i) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, p ? 0x7fffffff : 0, 0x00020000);
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)i * 4u, 0, 0));
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int nx = 8;
   if (nwg < nx) return bid;

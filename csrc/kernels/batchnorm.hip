@@ -105,18 +105,26 @@ __device__ __forceinline__ void slot_sum_consume(float* __restrict__ slots, int 
   float vs[NSLOT / 16], vq[NSLOT / 16];
   s = 0.f;
   q = 0.f;
+  // loads unconditional at a clamped channel (a branch around them would drain the load counter
+  // before the caller's own loads return); the sums of a thread past C are never used
+  const int cc = min(c, C - 1);
+#pragma unroll
+  for (int i = 0; i < NSLOT / 16; ++i) {
+    const float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
+    vs[i] = p[cc];
+    vq[i] = p[C + cc];
+  }
+#pragma unroll
+  for (int i = 0; i < NSLOT / 16; ++i) {
+    s += vs[i];
+    q += vq[i];
+  }
+  __shared__ float rs[256], rq[256];
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  // the re-zeroing stores go out after the sums consumed the loads, and the barrier waits for LDS only
+  // (__syncthreads' fence would also wait for these stores to complete)
   if (c < C) {
-#pragma unroll
-    for (int i = 0; i < NSLOT / 16; ++i) {
-      const float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
-      vs[i] = p[c];
-      vq[i] = p[C + c];
-    }
-#pragma unroll
-    for (int i = 0; i < NSLOT / 16; ++i) {
-      s += vs[i];
-      q += vq[i];
-    }
 #pragma unroll
     for (int i = 0; i < NSLOT / 16; ++i) {
       float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
@@ -124,10 +132,8 @@ __device__ __forceinline__ void slot_sum_consume(float* __restrict__ slots, int 
       p[C + c] = 0.f;
     }
   }
-  __shared__ float rs[256], rq[256];
-  rs[threadIdx.x] = s;
-  rq[threadIdx.x] = q;
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   if (ty == 0) {
 #pragma unroll
     for (int k = 1; k < 16; ++k) {
@@ -144,16 +150,12 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(float* __restrict__ sl
   const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   // parameter / running-stat loads issued before the slot reduction: one memory round trip per
   // kernel instead of two (these launches are latency-bound, ~100 of them per ResNet-50 step)
+  // (unconditional loads at a clamped channel: no branch around them, see slot_sum_consume)
   const bool own = (threadIdx.x >> 4) == 0 && c < C;
-  float g = 1.f, b = 0.f, rm = 0.f, rv = 0.f;
-  if (own) {
-    if (gamma) g = gamma[c];
-    if (beta) b = beta[c];
-    if (run_mean) {
-      rm = run_mean[c];
-      rv = run_var[c];
-    }
-  }
+  const int cc = min(c, C - 1);
+  const float g0 = ld_f32_or0(gamma, cc), b = ld_f32_or0(beta, cc);
+  const float rm = ld_f32_or0(run_mean, cc), rv = ld_f32_or0(run_var, cc);
+  const float g = gamma ? g0 : 1.f;
   float sum, sq;
   slot_sum_consume(slots, C, c, sum, sq);
   if (!own) return;
@@ -179,11 +181,8 @@ __global__ void __launch_bounds__(256) bn_slot_reduce_kernel(float* __restrict__
                                                              float* __restrict__ dbeta) {
   const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool own = (threadIdx.x >> 4) == 0 && c < C;
-  float db = 0.f, dg = 0.f;  // loaded before the slot reduction (one round trip, see finalize)
-  if (own) {
-    if (dbeta) db = dbeta[c];
-    if (dgamma) dg = dgamma[c];
-  }
+  const int cc = min(c, C - 1);  // loaded before the slot reduction (one round trip, see finalize)
+  const float db = ld_f32_or0(dbeta, cc), dg = ld_f32_or0(dgamma, cc);
   float s, q;
   slot_sum_consume(slots, C, c, s, q);
   if (own) {

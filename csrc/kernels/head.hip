@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(HEAD_FT) head_xent_fwd_kernel(HeadXentArgs a) 
   // that drains the load counter): a thread past C reads channel group 0, a padding pixel the last one
   const int tc = own ? t : 0;
   const int64_t lab = a.labels[n];
-  const float bias = a.b ? a.b[min(tt, O - 1)] : 0.f;
+  const float bias = ld_f32_or0(a.b, min(tt, O - 1));
 
   // ---- pooled partials of this pixel group: pixels pg, pg + PG, ... (HEAD_U of them in flight)
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};

@@ -382,32 +382,40 @@ __device__ __forceinline__ void sr_block(float* __restrict__ slots, float* __res
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int c = sb * 16 + tx;
   const bool own = ty == 0 && c < C;
-  float db = 0.f, dg = 0.f;
-  if (own) {
-    if (dbeta) db = dbeta[c];
-    if (dgamma) dg = dgamma[c];
-  }
+  // every load unconditional (clamped channel; null dgamma / dbeta through record-less resources): a
+  // branch around a load makes the waitcnt pass drain the load counter at its join -- two round trips
+  const int cc = min(c, C - 1);
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(dgamma, dgamma ? 0x7fffffff : 0);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(dbeta, dbeta ? 0x7fffffff : 0);
+  const float db = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (uint32_t)cc * 4u, 0, 0));
+  const float dg = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, (uint32_t)cc * 4u, 0, 0));
   float s = 0.f, q = 0.f;
+  float vs[NSLOT / 16], vq[NSLOT / 16];
+#pragma unroll
+  for (int i = 0; i < NSLOT / 16; ++i) {
+    const float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
+    vs[i] = p[cc];
+    vq[i] = p[C + cc];
+  }
+#pragma unroll
+  for (int i = 0; i < NSLOT / 16; ++i) {
+    s += vs[i];
+    q += vq[i];
+  }
+  red2[threadIdx.x] = s;
+  red2[256 + threadIdx.x] = q;
   if (c < C) {
-    float vs[NSLOT / 16], vq[NSLOT / 16];
 #pragma unroll
     for (int i = 0; i < NSLOT / 16; ++i) {
-      const float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
-      vs[i] = p[c];
-      vq[i] = p[C + c];
-    }
-#pragma unroll
-    for (int i = 0; i < NSLOT / 16; ++i) {
-      s += vs[i];
-      q += vq[i];
       float* p = slots + (size_t)(ty + 16 * i) * 2 * C;
       p[c] = 0.f;  // the workspace is zero again for its next use
       p[C + c] = 0.f;
     }
   }
-  red2[threadIdx.x] = s;
-  red2[256 + threadIdx.x] = q;
-  __syncthreads();  // the waves still running: threads >= 256 of an 8-wave block have exited
+  // LDS-only barrier (a fence would wait for the zeroing stores); the waves still running: threads
+  // >= 256 of an 8-wave block have exited
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   if (own) {
 #pragma unroll
     for (int k = 1; k < 16; ++k) {

@@ -5,11 +5,12 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from tensorflow_examples_amd.ops import _native  # noqa: E402
+from tensorflow_examples_amd.ops import _native, tuning  # noqa: E402
 
 N, H, W, C, K, R, st = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "256,16,16,128,128,3,1").split(",")]
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 assert _native.load()
+tuning.load()  # the measured launch table, as in the training step
 pad = R // 2
 x = torch.randn(N, H, W, C, device="cuda").bfloat16()
 w = (torch.randn(K, R, R, C, device="cuda") * 0.05).bfloat16()
