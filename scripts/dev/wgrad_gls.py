@@ -14,7 +14,7 @@ from operand_major_bench import graph_us  # noqa: E402
 assert _native.load()
 tuning.load()
 FAMS = (6, 7, 8)
-CANDS = [None, (1, 2, 2, 256), (2, 2, 3, 256), (1, 1, 3, 256), (2, 1, 3, 256)]
+CANDS = [None]
 SHAPES = [(256, 32, 32, 64, 64, 3, 1), (256, 16, 16, 128, 128, 3, 1), (256, 8, 8, 256, 256, 3, 1),
           (256, 4, 4, 512, 512, 3, 1), (256, 32, 32, 64, 256, 1, 1), (256, 8, 8, 256, 1024, 1, 1),
           (256, 8, 8, 1024, 256, 1, 1), (256, 16, 16, 128, 512, 1, 1), (256, 4, 4, 2048, 512, 1, 1)]
