@@ -143,7 +143,8 @@ elif FLAGS.job_name == "worker":
     print("Variables initialized ...")
 
     sv = Supervisor(is_chief=(FLAGS.task_index == 0), client=client, logdir=FLAGS.logdir or None,
-                    recovery_wait_secs=FLAGS.recovery_wait_secs)
+                    recovery_wait_secs=FLAGS.recovery_wait_secs,
+                    graph_nodes=lambda: model.graph_nodes(lambda n: client.shard_map().get(n, "")))
 
     begin_time = time.time()
     frequency = 100

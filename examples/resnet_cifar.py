@@ -18,7 +18,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from tensorflow_examples_amd import app, ops  # noqa: E402
-from tensorflow_examples_amd.ckpt import Saver, latest_checkpoint  # noqa: E402
+from tensorflow_examples_amd.ckpt import Saver, latest_checkpoint, store_graph_nodes, write_graph  # noqa: E402
 from tensorflow_examples_amd.data.cifar import augment_model_input, load_cifar10  # noqa: E402
 from tensorflow_examples_amd.data.pipeline import DevicePrefetcher, batches  # noqa: E402
 from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
@@ -64,6 +64,8 @@ def main(_):
     if FLAGS.logdir and latest_checkpoint(FLAGS.logdir):
         tensors = Saver().restore(store, latest_checkpoint(FLAGS.logdir))
         start_step = int(float(tensors["global_step"])) if "global_step" in tensors else 0
+    if FLAGS.logdir and rank == 0:
+        write_graph(FLAGS.logdir, store_graph_nodes(store))  # graph.pbtxt, as TF1's Supervisor writes it
     broadcast_variables(store)
     dp = GradAllReduce(store, bucket_bytes=int(FLAGS.bucket_mb * (1 << 20))) if world > 1 else None
     trainer = ClassifierTrainer(store, model, opt, dp)

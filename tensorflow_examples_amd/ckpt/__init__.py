@@ -5,11 +5,15 @@
     <dir>/checkpoint                          text: model_checkpoint_path / all_model_checkpoint_paths
     <dir>/model.ckpt-N.index                  JSON index: name -> dtype, shape, crc32c (format tfx-ckpt-v1)
     <dir>/model.ckpt-N.data-00000-of-00001    safetensors container with every tensor (f32)
-    <dir>/model.ckpt-N.meta                   JSON "meta graph": variable list + user metadata
+    <dir>/model.ckpt-N.meta                   MetaGraphDef protobuf (graph_def, saver_def, collections)
+    <dir>/graph.pbtxt                         text GraphDef (write_graph; TF1's Supervisor writes it)
 
 Variables keep their TF names (``global_step``, ``weights/Variable``, ``biases/Variable_1``, ...).
 The data file is safetensors (loaded with the safe loader, nothing executable); CRC32C of every
-tensor is verified on restore.  ``export_saved_model`` writes the SavedModel-shaped directory
+tensor is verified on restore.  ``.meta`` is a binary MetaGraphDef encoded by ``summary.meta_graph_def``:
+the graph (one ``VariableV2`` node per variable unless the caller passes the model's nodes), TF1's
+default SaverDef, the ``variables`` / ``trainable_variables`` collections (serialized VariableDefs)
+and a ``tfx_meta`` collection holding the caller's metadata as JSON; ``read_meta_graph`` parses it.  ``export_saved_model`` writes the SavedModel-shaped directory
 ``saved_model.pb`` + ``variables/variables.{index,data-00000-of-00001}``; ``saved_model.pb`` here is
 our container (magic ``TFXSM001`` + JSON signature/meta), not a TF protobuf.
 The reference's Supervisor builds a default Saver but never saves without ``logdir``
@@ -26,7 +30,7 @@ from typing import Dict, List, Optional
 import torch
 from safetensors.torch import load_file, save_file
 
-from .. import runtime
+from .. import runtime, summary
 
 FORMAT = "tfx-ckpt-v1"
 SM_MAGIC = b"TFXSM001"
@@ -36,7 +40,13 @@ def _crc(t: torch.Tensor) -> int:
     return runtime.crc32c(t.detach().cpu().contiguous().numpy().tobytes())
 
 
-def _write_tensors(prefix: str, tensors: Dict[str, torch.Tensor], meta: Optional[dict]) -> None:
+def _default_nodes(names: List[str]) -> List[Dict]:
+    return [{"name": n, "op": "VariableV2", "inputs": [], "device": ""} for n in names]
+
+
+def _write_tensors(prefix: str, tensors: Dict[str, torch.Tensor], meta: Optional[dict],
+                   graph_nodes: Optional[List[Dict]] = None, trainable: Optional[Dict[str, bool]] = None,
+                   max_to_keep: int = 5) -> None:
     cpu = {k: v.detach().cpu().contiguous() for k, v in tensors.items()}
     save_file(cpu, prefix + ".data-00000-of-00001", metadata={"format": FORMAT})
     index = {"format": FORMAT, "num_shards": 1,
@@ -44,8 +54,56 @@ def _write_tensors(prefix: str, tensors: Dict[str, torch.Tensor], meta: Optional
                          for k, v in cpu.items()}}
     with open(prefix + ".index", "w") as f:
         json.dump(index, f, indent=1, sort_keys=True)
-    with open(prefix + ".meta", "w") as f:
-        json.dump({"format": FORMAT, "variables": sorted(cpu), "meta": meta or {}, "time": time.time()}, f, indent=1)
+    names = sorted(cpu)
+    trainable = trainable or {}
+    nodes = graph_nodes if graph_nodes is not None else _default_nodes(names)
+    tr = [n for n in names if trainable.get(n, False)]
+    body = summary.meta_graph_def(
+        summary.graph_def(nodes), saver=summary.saver_def(max_to_keep),
+        collections={"variables": [summary.variable_def(n, trainable.get(n, False)) for n in names],
+                     "trainable_variables": [summary.variable_def(n, True) for n in tr],
+                     "tfx_meta": [json.dumps({"format": FORMAT, "meta": meta or {}, "time": time.time()}).encode()]})
+    with open(prefix + ".meta", "wb") as f:
+        f.write(body)
+
+
+def read_meta_graph(prefix_or_path: str) -> dict:
+    """Parse a checkpoint's ``.meta`` (MetaGraphDef): nodes, saver, variable names, user metadata."""
+    path = prefix_or_path if prefix_or_path.endswith(".meta") else prefix_or_path + ".meta"
+    with open(path, "rb") as f:
+        mg = summary.parse_meta_graph_def(f.read())
+    colls = mg["collections"]
+    mg["variables"] = [summary.parse_variable_def(b)["variable_name"].rsplit(":", 1)[0]
+                       for b in colls.get("variables", [])]
+    mg["trainable_variables"] = [summary.parse_variable_def(b)["variable_name"].rsplit(":", 1)[0]
+                                 for b in colls.get("trainable_variables", [])]
+    tm = colls.get("tfx_meta")
+    mg["meta"] = json.loads(tm[0])["meta"] if tm else {}
+    return mg
+
+
+def write_graph(logdir: str, nodes: List[Dict], name: str = "graph.pbtxt") -> str:
+    """``<logdir>/graph.pbtxt``: the text GraphDef TF1's Supervisor writes when logdir is set
+    (R/distributed/distributed.py:129-131)."""
+    os.makedirs(logdir, exist_ok=True)
+    path = os.path.join(logdir, name)
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write(summary.graph_def_pbtxt(nodes))
+    os.replace(tmp, path)
+    return path
+
+
+def read_graph(path: str) -> List[Dict]:
+    with open(path) as f:
+        return summary.parse_graph_pbtxt(f.read())
+
+
+def store_graph_nodes(store, device_of=lambda name: "") -> List[Dict]:
+    """GraphDef nodes of a VariableStore's variables (VariableV2 each, creation order)."""
+    out = [{"name": v.name, "op": "VariableV2", "inputs": [], "device": device_of(v.name)} for v in store.vars]
+    out += [{"name": n, "op": "VariableV2", "inputs": [], "device": device_of(n)} for n in store.state]
+    return out
 
 
 def read_checkpoint(prefix: str, verify: bool = True) -> Dict[str, torch.Tensor]:
@@ -67,7 +125,7 @@ class Saver:
         self._kept: List[str] = []
 
     def save(self, store, save_path: str, global_step: Optional[int] = None, extra: Optional[Dict] = None,
-             meta: Optional[dict] = None) -> str:
+             meta: Optional[dict] = None, graph_nodes: Optional[List[Dict]] = None) -> str:
         prefix = f"{save_path}-{int(global_step)}" if global_step is not None else save_path
         d = os.path.dirname(os.path.abspath(prefix))
         os.makedirs(d, exist_ok=True)
@@ -76,7 +134,8 @@ class Saver:
             tensors.setdefault("global_step", torch.tensor(float(global_step)))
         for k, v in (extra or {}).items():
             tensors[k] = torch.as_tensor(v)
-        _write_tensors(prefix, tensors, meta)
+        trainable = {v.name: bool(v.trainable) for v in getattr(store, "vars", [])}
+        _write_tensors(prefix, tensors, meta, graph_nodes, trainable, self.max_to_keep)
         self._kept = [p for p in _read_state(d) if p != prefix] + [prefix]
         while self.max_to_keep and len(self._kept) > self.max_to_keep:
             old = self._kept.pop(0)
@@ -154,4 +213,5 @@ def load_saved_model(store, export_dir: str) -> dict:
     return meta
 
 
-__all__ = ["Saver", "latest_checkpoint", "read_checkpoint", "export_saved_model", "load_saved_model"]
+__all__ = ["Saver", "latest_checkpoint", "read_checkpoint", "export_saved_model", "load_saved_model",
+           "read_meta_graph", "write_graph", "read_graph", "store_graph_nodes"]

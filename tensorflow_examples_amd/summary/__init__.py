@@ -87,15 +87,130 @@ def graph_def(nodes: Sequence[Dict]) -> bytes:
     return bytes(out)
 
 
-def meta_graph_def(graph: bytes, tags: Sequence[str] = ()) -> bytes:
-    """Minimal MetaGraphDef: meta_info_def { meta_graph_version, tags*, tensorflow_version,
+def _varint_field(field: int, v: int) -> bytes:
+    return _varint(field << 3) + _varint(int(v))
+
+
+def saver_def(max_to_keep: int = 5) -> bytes:
+    """SaverDef { filename_tensor_name, save_tensor_name, restore_op_name, max_to_keep, sharded,
+    keep_checkpoint_every_n_hours, version: V2 } with the names TF1's default Saver uses."""
+    return (_bytes_field(1, b"save/Const:0") + _bytes_field(2, b"save/control_dependency:0") +
+            _bytes_field(3, b"save/restore_all") + _varint_field(4, max_to_keep) + _varint_field(5, 1) +
+            b"\x35" + struct.pack("<f", 10000.0) + _varint_field(7, 2))
+
+
+def variable_def(name: str, trainable: bool = True) -> bytes:
+    """VariableDef { variable_name, initializer_name, snapshot_name, trainable } (TF1 names)."""
+    return (_bytes_field(1, f"{name}:0".encode()) + _bytes_field(2, f"{name}/Assign".encode()) +
+            _bytes_field(3, f"{name}/read:0".encode()) + _varint_field(7, 1 if trainable else 0))
+
+
+def meta_graph_def(graph: bytes, tags: Sequence[str] = (), saver: Optional[bytes] = None,
+                   collections: Optional[Dict[str, Sequence[bytes]]] = None) -> bytes:
+    """MetaGraphDef: meta_info_def { meta_graph_version, tags*, tensorflow_version,
     tensorflow_git_version } + graph_def (what TF1's FileWriter(graph=...) writes after the GraphDef
-    event, R/distributed/distributed.py:138)."""
+    event, R/distributed/distributed.py:138), plus -- for a checkpoint's ``.meta`` (what TF1's
+    Saver.save writes next to the data) -- saver_def and collection_def entries
+    ``name -> CollectionDef { bytes_list { value* } }`` (e.g. "variables" = serialized VariableDefs)."""
     info = _bytes_field(1, b"v1")
     for t in tags:
         info += _bytes_field(4, t.encode())
     info += _bytes_field(5, b"tensorflow_examples_amd") + _bytes_field(6, b"mi355x-native")
-    return _bytes_field(1, info) + _bytes_field(2, bytes(graph))
+    out = _bytes_field(1, info) + _bytes_field(2, bytes(graph))
+    if saver is not None:
+        out += _bytes_field(3, saver)
+    for key, values in (collections or {}).items():
+        blist = b"".join(_bytes_field(1, bytes(v)) for v in values)
+        entry = _bytes_field(1, key.encode()) + _bytes_field(2, _bytes_field(2, blist))
+        out += _bytes_field(4, entry)
+    return out
+
+
+def parse_graph_def(b: bytes) -> List[Dict]:
+    """Nodes of a binary GraphDef as {"name", "op", "inputs", "device"} dicts (inverse of graph_def)."""
+    nodes = []
+    for nb in _parse(bytes(b)).get(1, []):
+        f = _parse(nb)
+        nodes.append({"name": f[1][0].decode(), "op": f.get(2, [b""])[0].decode(),
+                      "inputs": [i.decode() for i in f.get(3, [])],
+                      "device": f.get(4, [b""])[0].decode()})
+    return nodes
+
+
+def parse_meta_graph_def(b: bytes) -> Dict:
+    """A MetaGraphDef as {"meta_info": {...}, "nodes": [...], "saver": {...}, "collections": {...}}."""
+    f = _parse(bytes(b))
+    info = _parse(f[1][0]) if 1 in f else {}
+    out = {"meta_info": {"meta_graph_version": info.get(1, [b""])[0].decode(),
+                         "tags": [t.decode() for t in info.get(4, [])],
+                         "tensorflow_version": info.get(5, [b""])[0].decode()},
+           "nodes": parse_graph_def(f[2][0]) if 2 in f else [], "saver": None, "collections": {}}
+    if 3 in f:
+        s = _parse(f[3][0])
+        out["saver"] = {"filename_tensor_name": s[1][0].decode(), "save_tensor_name": s[2][0].decode(),
+                        "restore_op_name": s[3][0].decode(), "max_to_keep": s.get(4, [0])[0],
+                        "version": s.get(7, [0])[0]}
+    for eb in f.get(4, []):
+        e = _parse(eb)
+        coll = _parse(e[2][0])
+        vals = _parse(coll[2][0]).get(1, []) if 2 in coll else []
+        out["collections"][e[1][0].decode()] = [bytes(v) for v in vals]
+    return out
+
+
+def parse_variable_def(b: bytes) -> Dict:
+    f = _parse(bytes(b))
+    return {"variable_name": f[1][0].decode(), "initializer_name": f.get(2, [b""])[0].decode(),
+            "snapshot_name": f.get(3, [b""])[0].decode(), "trainable": bool(f.get(7, [0])[0])}
+
+
+def _pbtxt_str(s: str) -> str:
+    return '"' + s.replace("\\", "\\\\").replace('"', '\\"') + '"'
+
+
+def graph_def_pbtxt(nodes: Sequence[Dict]) -> str:
+    """The text-format GraphDef TF1's Supervisor writes as ``<logdir>/graph.pbtxt``."""
+    lines = []
+    for n in nodes:
+        lines.append("node {")
+        lines.append(f"  name: {_pbtxt_str(n['name'])}")
+        lines.append(f"  op: {_pbtxt_str(n['op'])}")
+        for i in n.get("inputs", []):
+            lines.append(f"  input: {_pbtxt_str(i)}")
+        if n.get("device"):
+            lines.append(f"  device: {_pbtxt_str(n['device'])}")
+        lines.append("}")
+    lines += ["versions {", "  producer: 26", "}"]
+    return "\n".join(lines) + "\n"
+
+
+def parse_graph_pbtxt(text: str) -> List[Dict]:
+    """Reader for :func:`graph_def_pbtxt`'s output (node blocks of name / op / input / device)."""
+    import re
+    nodes, cur, depth = [], None, 0
+    for raw in text.splitlines():
+        line = raw.strip()
+        if not line:
+            continue
+        if line.endswith("{"):
+            depth += 1
+            if depth == 1 and line.startswith("node"):
+                cur = {"name": "", "op": "", "inputs": [], "device": ""}
+            continue
+        if line == "}":
+            depth -= 1
+            if depth == 0 and cur is not None:
+                nodes.append(cur)
+                cur = None
+            continue
+        m = re.match(r'(\w+):\s*"((?:[^"\\]|\\.)*)"$', line)
+        if cur is not None and m:
+            k, v = m.group(1), m.group(2).replace('\\"', '"').replace("\\\\", "\\")
+            if k == "input":
+                cur["inputs"].append(v)
+            elif k in ("name", "op", "device"):
+                cur[k] = v
+    return nodes
 
 
 # ---------------------------------------------------------------- writer
@@ -228,4 +343,5 @@ def summary_iterator(path: str) -> Iterator[Dict]:
 
 
 __all__ = ["Summary", "scalar", "merge_all", "FileWriter", "summary_iterator", "read_records", "graph_def",
-           "meta_graph_def", "reset_registry"]
+           "meta_graph_def", "reset_registry", "saver_def", "variable_def", "parse_graph_def",
+           "parse_meta_graph_def", "parse_variable_def", "graph_def_pbtxt", "parse_graph_pbtxt"]
