@@ -58,6 +58,9 @@ def parse(argv=None):
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--allreduce-dtype", choices=["f32", "bf16"], default="f32",
+                    help="gradient wire format of the bucketed all-reduce: f32, or bf16 (cast per bucket into a "
+                         "persistent bf16 twin, reduced in place, read by the optimizer directly)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="capture the whole step in a HIP graph and replay it (default on; for N>1 the bucketed "
                          "RCCL all-reduces are captured too -- measured on a 1-rank RCCL group: 8.09-8.16 ms graph vs "
@@ -137,7 +140,8 @@ def run(a):
         store, model = build_resnet_cifar(device=dev, depth=a.depth, dtype=dtype, seed=0)
         broadcast_variables(store)
         opt = MomentumOptimizer(store, a.lr, momentum=0.9, weight_decay=5e-4)
-        dp = GradAllReduce(store, bucket_bytes=int(a.bucket_mb * (1 << 20))) if dist.is_initialized() else None
+        dp = GradAllReduce(store, bucket_bytes=int(a.bucket_mb * (1 << 20)),
+                           compress_bf16=a.allreduce_dtype == "bf16") if dist.is_initialized() else None
         trainer = ClassifierTrainer(store, model, opt, dp)
 
         label_fuse = os.environ.get("TFX_LABEL_FUSE", "1") == "1"  # 0: separate label copy (A/B)
@@ -200,6 +204,8 @@ def run(a):
         time.sleep(1e6)
     for i in range(a.warmup):
         loss = step(i)
+    if rank == 0 and a.impl == "native" and getattr(trainer, "plan", None) is not None:
+        print(trainer.plan.table(), file=sys.stderr, flush=True)  # the fusion plan the step runs (stderr)
     sync()
     if world > 1:
         dist.barrier(group=ctl)
@@ -251,6 +257,7 @@ def run(a):
                 "impl": a.impl,
                 "optimizer": "momentum-SGD 0.9, wd 5e-4 (fused flat-buffer kernel)" if a.impl == "native" else "torch.optim.SGD foreach",
                 "allreduce_bucket_mb": a.bucket_mb,
+                "allreduce_dtype": a.allreduce_dtype,
                 "hip_graph": bool(a.impl == "native" and graphed),
                 "host_input": a.host_input if ring is not None else False,
                 "params": nparams,

@@ -316,7 +316,7 @@ void stem_fwd(const uint16_t* x, const uint16_t* w, int N, int Ko, uint16_t* y, 
 // ---------------------------------------------------------------- optimizers (flat buffers)
 void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, float* v, int64_t n,
                      const float* lr, float gscale, float wd, float b1, float b2, float eps, const float* step,
-                     const float* sumsq, float max_norm, uint16_t* pbf, hipStream_t s);
+                     const float* sumsq, float max_norm, uint16_t* pbf, const int* skip, hipStream_t s);
 void sumsq_flat(const void* g, bool g_bf16, int64_t n, float* out, hipStream_t s);
 void cast_f32_bf16(const float* x, int64_t n, uint16_t* y, hipStream_t s);
 
@@ -369,6 +369,8 @@ void lstm_cell_bwd(const float* act, const float* c, const float* c_prev, const 
 // persistent whole-sequence recurrence (lstm_seq.hip): one launch per layer and direction
 int lstm_seq_sync_words(int B, int H);
 bool lstm_seq_supported(int B, int H, int num_cus);
+// resident workgroups (occupancy API x CUs) of the forward / backward kernels at hidden size H
+void lstm_seq_residency(int B, int H, int num_cus, int* fwd, int* bwd);
 // status: a sticky health word (set to 1 when a bounded hand-off wait expires; never cleared by the
 // launch) -- null = the sync buffer's own status word; spin_limit 0 = the default bound (tests force 1)
 void lstm_seq_fwd(const float* gx, const uint16_t* whh, int T, int B, int H, uint16_t* hbuf, float* cbuf, float* act,

@@ -42,7 +42,10 @@ constexpr int HEAD_U = 4;                                // pixels in flight per
 constexpr int HEAD_UT = 4;                               // ... in TAIL mode (two operands)
 constexpr int HEAD_CNT_BITS = 12;                        // done count (N <= 4095)
 constexpr double HEAD_FIX = 16777216.0;                 // 2^24 per unit of loss
-constexpr float HEAD_ROW_MAX = 1e6f;                    // 4095 rows x 1e6 x 2^24 < 2^64 / 2^12
+// a row's fixed-point loss is < HEAD_ROW_MAX x 2^24, and the word holds 64 - 12 = 52 bits of sum:
+// 4095 rows x 6.5e4 x 2^24 < 2^52 (2^28 / 4095 = 65552).  A row at or past it (a diverged loss)
+// takes the NaN-flag path instead of wrapping the word into a wrong finite mean.
+constexpr float HEAD_ROW_MAX = 6.5e4f;
 
 __device__ __forceinline__ void head_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

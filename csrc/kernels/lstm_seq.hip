@@ -36,6 +36,9 @@
 #include "tfx_common.h"
 #include "tfx_kernels.h"
 
+#include <algorithm>
+#include <cstdio>
+
 namespace tfx {
 namespace {
 
@@ -287,13 +290,46 @@ void ls_prepare(K k) {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LS_LDS);
 }
 
+// Workgroups of kernel k that can be resident at once on the whole device (occupancy API at the
+// launch's block size and dynamic LDS, x CUs).  The 96 KB of LDS caps it at one per CU, so the API's
+// known over-count at high SGPR use (MI355X_MICROARCH.md, correctness boundaries) cannot apply.
+template <typename K>
+int ls_resident(K k, int cus) {
+  ls_prepare(k);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k), 256, LS_LDS) !=
+      hipSuccess)
+    return 0;
+  return std::min(per_cu, 1) * cus;
+}
+
+// Co-residency of the grid is required (workgroups wait on each other): outside a graph capture the
+// launch is cooperative (the runtime refuses a grid that cannot be co-resident instead of starting
+// it); inside a capture -- where a cooperative launch is not recorded -- a plain launch, guarded by
+// the occupancy check of lstm_seq_supported and the bounded waits.
+template <typename K>
+void ls_launch(K k, dim3 grid, void** args, hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(s, &cs);
+  if (cs == hipStreamCaptureStatusNone) {
+    const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), grid, dim3(256), args,
+                                                    LS_LDS, s);
+    if (e == hipSuccess) return;
+    (void)hipGetLastError();  // clear it: the plain launch below reports its own errors
+    fprintf(stderr, "lstm_seq: cooperative launch refused (%s); plain launch with bounded waits\n",
+            hipGetErrorString(e));
+  }
+  TFX_HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(k), grid, dim3(256), args, LS_LDS, s));
+}
+
 template <int NK>
 void fwd_launch(dim3 grid, const float* gx, const uint16_t* whh, int T, int B, uint16_t* hbuf, float* cbuf,
                 float* act, float* hT, unsigned* sync, unsigned* status, unsigned limit, hipStream_t s) {
   static bool once = (ls_prepare(lstm_seq_fwd_kernel<NK>), true);
   (void)once;
   (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B, H_of<NK>()) * 4, s);
-  lstm_seq_fwd_kernel<NK><<<grid, 256, LS_LDS, s>>>(gx, whh, T, B, hbuf, cbuf, act, hT, sync, status, limit);
+  void* args[] = {&gx, &whh, &T, &B, &hbuf, &cbuf, &act, &hT, &sync, &status, &limit};
+  ls_launch(lstm_seq_fwd_kernel<NK>, grid, args, s);
 }
 
 template <int NK>
@@ -303,18 +339,39 @@ void bwd_launch(dim3 grid, const float* act, const float* cbuf, const uint16_t* 
   static bool once = (ls_prepare(lstm_seq_bwd_kernel<NK>), true);
   (void)once;
   (void)hipMemsetAsync(sync, 0, (size_t)lstm_seq_sync_words(B, H_of<NK>()) * 4, s);
-  lstm_seq_bwd_kernel<NK><<<grid, 256, LS_LDS, s>>>(act, cbuf, dH, dhT, dc_in, whh, T, B, dg, dc_out, dbias, sync,
-                                                    status, limit);
+  void* args[] = {&act, &cbuf, &dH, &dhT, &dc_in, &whh, &T, &B, &dg, &dc_out, &dbias, &sync, &status, &limit};
+  ls_launch(lstm_seq_bwd_kernel<NK>, grid, args, s);
+}
+
+template <int NK>
+void residency(int cus, int* f, int* b) {
+  *f = ls_resident(lstm_seq_fwd_kernel<NK>, cus);
+  *b = ls_resident(lstm_seq_bwd_kernel<NK>, cus);
 }
 
 }  // namespace
 
 int lstm_seq_sync_words(int B, int H) { return ((B / 16) * (H / 16) + 1) * LS_STRIDE; }
 
+void lstm_seq_residency(int B, int H, int num_cus, int* fwd, int* bwd) {
+  *fwd = *bwd = 0;
+  switch (H) {
+    case 128: residency<4>(num_cus, fwd, bwd); break;
+    case 256: residency<8>(num_cus, fwd, bwd); break;
+    case 512: residency<16>(num_cus, fwd, bwd); break;
+    case 1024: residency<32>(num_cus, fwd, bwd); break;
+    default: break;
+  }
+}
+
 bool lstm_seq_supported(int B, int H, int num_cus) {
   if (B <= 0 || B % 16 != 0) return false;
   if (H != 128 && H != 256 && H != 512 && H != 1024) return false;
-  return (int64_t)(B / 16) * (H / 16) <= num_cus;  // every workgroup resident at once (1 per CU)
+  // every workgroup resident at once: the occupancy API's count for both kernels, not just grid <= CUs
+  int f = 0, b = 0;
+  lstm_seq_residency(B, H, num_cus, &f, &b);
+  const int64_t grid = (int64_t)(B / 16) * (H / 16);
+  return grid <= num_cus && grid <= f && grid <= b;
 }
 
 void lstm_seq_fwd(const float* gx, const uint16_t* whh, int T, int B, int H, uint16_t* hbuf, float* cbuf, float* act,

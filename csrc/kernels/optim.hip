@@ -42,7 +42,10 @@ __global__ void __launch_bounds__(256) opt_kernel(float* __restrict__ p, const T
                                                   const float* __restrict__ lr_ptr, float gscale, float wd,
                                                   float b1, float b2, float eps, const float* __restrict__ step_ptr,
                                                   const float* __restrict__ sumsq, float max_norm,
-                                                  uint16_t* __restrict__ pbf) {
+                                                  uint16_t* __restrict__ pbf, const int* __restrict__ skip) {
+  // a nonzero skip word (e.g. the persistent LSTM's sticky health word: this step's gradients came
+  // from a launch that gave up on a hand-off) leaves parameters, moments and the shadow untouched
+  if (skip && *skip) return;
   const float lr = *lr_ptr;
   const float gs = gscale * clip_factor(sumsq, max_norm);
   float bc1 = 1.f, bc2 = 1.f;
@@ -111,11 +114,21 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const TG* __restrict__ g, in
   if (threadIdx.x == 0) atomicAdd(out, r[0] + r[1] + r[2] + r[3]);
 }
 
-// f32 -> bf16 copy (weights refresh) and bf16 -> f32
+// f32 -> bf16 copy (weights refresh, DP bf16 gradient buckets) and bf16 -> f32
 __global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restrict__ x, int64_t n,
                                                             uint16_t* __restrict__ y) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     y[i] = f32_to_bf16(x[i]);
+}
+
+// 8 elements per thread: two 16-B loads, one 16-B store (16-B aligned x and y, n8 = n / 8)
+__global__ void __launch_bounds__(256) cast_f32_bf16_vec_kernel(const float4* __restrict__ x, int64_t n8,
+                                                                U4* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const float4 a = x[2 * i], b = x[2 * i + 1];
+    const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    y[i] = pack8(f);
+  }
 }
 
 static inline int ogrid(int64_t n4) {
@@ -125,16 +138,16 @@ static inline int ogrid(int64_t n4) {
 
 void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, float* v, int64_t n,
                      const float* lr, float gscale, float wd, float b1, float b2, float eps, const float* step,
-                     const float* sumsq, float max_norm, uint16_t* pbf, hipStream_t s) {
+                     const float* sumsq, float max_norm, uint16_t* pbf, const int* skip, hipStream_t s) {
   const int64_t n4 = n / 4;  // host wrapper pads flat buffers to a multiple of 4 elements
   const int grid = ogrid(n4);
 #define TFX_OPT(K)                                                                                     \
   if (g_bf16)                                                                                          \
     opt_kernel<uint16_t, K><<<grid, 256, 0, s>>>(p, (const uint16_t*)g, m, v, n4, lr, gscale, wd, b1, b2, \
-                                                 eps, step, sumsq, max_norm, pbf);                     \
+                                                 eps, step, sumsq, max_norm, pbf, skip);               \
   else                                                                                                 \
     opt_kernel<float, K><<<grid, 256, 0, s>>>(p, (const float*)g, m, v, n4, lr, gscale, wd, b1, b2, eps, \
-                                              step, sumsq, max_norm, pbf);
+                                              step, sumsq, max_norm, pbf, skip);
   switch (kind) {
     case 0: TFX_OPT(0); break;
     case 1: TFX_OPT(1); break;
@@ -156,6 +169,12 @@ void sumsq_flat(const void* g, bool g_bf16, int64_t n, float* out, hipStream_t s
 }
 
 void cast_f32_bf16(const float* x, int64_t n, uint16_t* y, hipStream_t s) {
+  if (n % 8 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
+    const int64_t n8 = n / 8;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n8 + 1023) / 1024, 4096));
+    cast_f32_bf16_vec_kernel<<<grid, 256, 0, s>>>(reinterpret_cast<const float4*>(x), n8, reinterpret_cast<U4*>(y));
+    return;
+  }
   cast_f32_bf16_kernel<<<ogrid(n), 256, 0, s>>>(x, n, y);
 }
 

@@ -1230,7 +1230,7 @@ Tensor scale_by_scalar(Tensor x, Tensor scal, bool out_bf16) {
 // ------------------------------------------------------------------ optimizers
 void optimizer_apply(int64_t kind, Tensor p, Tensor g, optional<Tensor> m, optional<Tensor> v, Tensor lr,
                      double gscale, double wd, double b1, double b2, double eps, optional<Tensor> step,
-                     optional<Tensor> sumsq, double max_norm, optional<Tensor> pbf) {
+                     optional<Tensor> sumsq, double max_norm, optional<Tensor> pbf, optional<Tensor> skip_if) {
   CHECK_DEV(p); CHECK_F32(p); CHECK_CONTIG(p); CHECK_CONTIG(g);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() % 4 == 0, "flat buffers must match and be padded to 4");
   const bool gb = g.scalar_type() == at::kBFloat16;
@@ -1243,8 +1243,13 @@ void optimizer_apply(int64_t kind, Tensor p, Tensor g, optional<Tensor> m, optio
     TORCH_CHECK(pbf->numel() == p.numel(), "bf16 shadow size");
     pb = bfm(*pbf);
   }
+  const int* skip = nullptr;  // a device int32 word: nonzero -> the update is skipped on the device
+  if (skip_if.has_value() && skip_if->defined()) {
+    TORCH_CHECK(skip_if->is_cuda() && skip_if->scalar_type() == at::kInt && skip_if->numel() >= 1, "skip_if word");
+    skip = skip_if->data_ptr<int>();
+  }
   tfx::optimizer_apply(kind, p.data_ptr<float>(), g.data_ptr(), gb, fpm(m), fpm(v), p.numel(), lr.data_ptr<float>(),
-                       gscale, wd, b1, b2, eps, fp(step), fp(sumsq), max_norm, pb, cur_stream());
+                       gscale, wd, b1, b2, eps, fp(step), fp(sumsq), max_norm, pb, skip, cur_stream());
 }
 
 Tensor sumsq(Tensor g) {
@@ -1511,6 +1516,16 @@ bool lstm_seq_supported(int64_t B, int64_t H) {
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   return tfx::lstm_seq_supported((int)B, (int)H, cus);
+}
+
+// (resident workgroups the occupancy API allows for the forward / backward kernel, grid size)
+std::tuple<int64_t, int64_t, int64_t> lstm_seq_residency(int64_t B, int64_t H) {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  int f = 0, b = 0;
+  tfx::lstm_seq_residency((int)B, (int)H, cus, &f, &b);
+  return {f, b, (B / 16) * (H / 16)};
 }
 
 unsigned* lstm_status_ptr(const optional<Tensor>& status) {
@@ -1802,6 +1817,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("optimizer_apply", &optimizer_apply);
+  m.def("lstm_seq_residency", &lstm_seq_residency);
   m.def("affine_fwd", &affine_fwd);
   m.def("affine_bwd", &affine_bwd);
   m.def("sse_fwd", &sse_fwd);

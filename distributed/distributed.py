@@ -194,6 +194,9 @@ elif FLAGS.job_name == "worker":
                     if FLAGS.logdir and FLAGS.save_checkpoint_steps and local_steps % FLAGS.save_checkpoint_steps == 0:
                         cost, _, step = flush()
                         sv.save(step + 1)
+                    if fault.armed():
+                        # runner.step() only enqueued the replay: complete its pushes to the ps first
+                        torch.cuda.synchronize()
                     fault.after_step(local_steps)
                     if (count + 1) % frequency == 0 or i + 1 == batch_count:
                         cost, _, step = flush()

@@ -86,7 +86,7 @@ def main(_):
             if step % 50 == 0:
                 costs += float(loss)
                 iters += 1
-                trainer.check()  # a timed-out persistent-LSTM hand-off raises here, not silently trains on
+                trainer.check()  # a timed-out persistent-LSTM hand-off: steps skipped, per-step kernels from here
                 if rank == 0:
                     print("epoch %d step %d perplexity %.3f  %.0f tokens/sec" %
                           (ep + 1, step, math.exp(costs / iters), tokens / (time.time() - t0)), flush=True)

@@ -40,6 +40,7 @@ flags.DEFINE_float("bucket_mb", 32.0, "all-reduce bucket size (MB)")
 flags.DEFINE_string("logdir", "", "checkpoint directory (resume from the latest checkpoint in it)")
 flags.DEFINE_integer("synthetic_train", 50000, "synthetic training-set size when no data is found")
 flags.DEFINE_integer("eval_examples", 0, "evaluate on the first N test images (0 = all)")
+flags.DEFINE_integer("seed", 0, "weight-initialisation seed (also offsets the data shuffle)")
 flags.DEFINE_boolean("graph", True, "GPU: capture the training step (forward, backward with the bucketed RCCL "
                      "all-reduces, optimizer) in a HIP graph on the first batch and replay it (the capture's "
                      "warm-up trains on that batch 3 extra times); --nograph runs eager launches")
@@ -58,7 +59,7 @@ def main(_):
     xtr, ytr, xte, yte, synth = load_cifar10(FLAGS.data_dir or None, synthetic_train=FLAGS.synthetic_train)
     if rank == 0:
         print("CIFAR-10 %s: %d train / %d test" % ("synthetic" if synth else "binary", len(xtr), len(xte)))
-    store, model = build_resnet_cifar(device=dev, depth=FLAGS.depth, dtype=dtype, seed=0)
+    store, model = build_resnet_cifar(device=dev, depth=FLAGS.depth, dtype=dtype, seed=FLAGS.seed)
     opt = MomentumOptimizer(store, FLAGS.learning_rate * world, momentum=0.9, weight_decay=FLAGS.weight_decay)
     start_step = 0
     if FLAGS.logdir and latest_checkpoint(FLAGS.logdir):
@@ -76,7 +77,7 @@ def main(_):
     step, t0, seen = start_step, time.time(), 0
     want_graph = FLAGS.graph and dev.type == "cuda"
     for ep in range(FLAGS.epochs):
-        src = batches([xtr[shard], ytr[shard]], FLAGS.batch_size, seed=ep * 1000 + rank)
+        src = batches([xtr[shard], ytr[shard]], FLAGS.batch_size, seed=ep * 1000 + rank + 7919 * FLAGS.seed)
         for img, lab in DevicePrefetcher(src, dev):
             lr = FLAGS.learning_rate * world * (0.1 ** sum(step >= b for b in bounds))
             opt.set_learning_rate(lr)  # a device scalar: a replayed graph reads the new value
@@ -98,6 +99,8 @@ def main(_):
                 if rank == 0:
                     print("hip graph: %s" % ("replaying the captured step" if ok else "eager launches"), flush=True)
             loss = trainer.step(x, lab)
+            if rank == 0 and step == start_step and trainer.plan is not None:
+                print(trainer.plan.table(), flush=True)  # which fusion group ran which layer (ops/fusion.py)
             step += 1
             seen += img.shape[0]
             if rank == 0 and step % 50 == 0:

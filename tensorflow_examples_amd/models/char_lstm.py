@@ -19,6 +19,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from .. import ops
+from ..ops import rnn as rnn_ops
 from ..variables import Uniform, VariableStore, Zeros, Constant
 
 State = List[Tuple[torch.Tensor, torch.Tensor]]
@@ -87,19 +88,39 @@ class LMTrainer:
         logits, new_state = self.model(x, state)
         loss = ops.softmax_cross_entropy(logits, y.reshape(-1))
         loss.backward()
-        scale = 1.0
+        scale, grad = 1.0, None
         if self.dp is not None:
             self.dp.finish()
-            scale = self.dp.grad_scale
-        sumsq = self.opt.global_norm_sq() if self.max_norm > 0 else None
-        # the kernel clips on ||raw grad||; the raw DP grad is the SUM over ranks -> scale the bound
-        self.opt.apply_gradients(grad_scale=scale, sumsq=sumsq, max_norm=self.max_norm / scale)
+            scale, grad = self.dp.grad_scale, self.dp.reduced_grad
+        sumsq = self.opt.global_norm_sq(grad) if self.max_norm > 0 else None
+        # the kernel clips on ||raw grad||; the raw DP grad is the SUM over ranks -> scale the bound.
+        # GPU: the persistent LSTM's sticky health word guards the update (skipped on the device
+        # while it is set: a timed-out hand-off never reaches the weights)
+        dev = self.store.master.device
+        guard = rnn_ops.health_word(dev) if dev.type == "cuda" else None
+        if guard is not None and self.dp is not None:
+            # every rank skips together: a failed rank's gradient is inside everyone's all-reduced sum
+            # (a 4-byte MAX on the DP group, stream-ordered: no host sync)
+            import torch.distributed as dist
+            dist.all_reduce(guard, op=dist.ReduceOp.MAX, group=getattr(self.dp, "group", None))
+        self.opt.apply_gradients(grad_scale=scale, sumsq=sumsq, max_norm=self.max_norm / scale, skip_if=guard,
+                                 grad=grad)
         return loss.detach(), new_state
 
-    def check(self) -> None:
-        """Raise if a persistent LSTM launch timed out a hand-off since the last check (reads the
-        device health word: call it where the host synchronises anyway, e.g. when logging)."""
-        ops.check_lstm_health(self.store.master.device if self.store.master.is_cuda else None)
+    def check(self) -> bool:
+        """Look at the device health word (call it where the host synchronises anyway, e.g. when
+        logging).  If a persistent LSTM launch timed out a hand-off since the last check, the guarded
+        optimizer has skipped those steps; switch to the per-step kernels for the rest of the run,
+        report it and return True."""
+        dev = self.store.master.device if self.store.master.is_cuda else None
+        if dev is None:
+            return False
+        # under DP the word was MAX-reduced before every update, so all ranks see the same value here
+        failed = rnn_ops.recover_persistent_failure(dev)
+        if failed:
+            print("warning: persistent LSTM hand-off timed out; the affected steps were skipped on the device, "
+                  "continuing on the per-step recurrence kernels", flush=True)
+        return failed
 
 
 def build_char_lstm(device="cuda", vocab_size=65, embed=128, hidden=512, layers=2, dtype=torch.bfloat16,

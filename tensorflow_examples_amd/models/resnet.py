@@ -156,8 +156,16 @@ class Basic:
         return self.b2.after_conv(self.c2, o, training, relu=True, residual=sc, residual_is_bn=True)
 
 
+_ENV_APPLIED = False
+
+
 class ResNetCifar:
     def __init__(self, store: VariableStore, depth: int = 50, num_classes: int = 10, base_width: int = 64):
+        global _ENV_APPLIED
+        if not _ENV_APPLIED:  # TFX_FUSION profile (ops/fusion.py), once per process
+            _ENV_APPLIED = True
+            from ..ops import fusion
+            fusion.apply_env()
         kind, blocks = STAGES[depth]
         Block = Bottleneck if kind == "bottleneck" else Basic
         self.store = store

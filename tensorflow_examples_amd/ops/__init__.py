@@ -1,5 +1,5 @@
 """Op layer: autograd wrappers over the gfx950 HIP kernels (GPU) / PyTorch references (CPU)."""
-from . import _native
+from . import _native, fusion
 from .nn import (BNWorkspace, GradSink, accuracy, avg_pool2d, batch_norm, classifier_head_xent, conv2d, dense,
                  global_avg_pool, linear,
                  max_pool2d, scale_shift, softmax_cross_entropy, sum_squared_error)

@@ -14,12 +14,13 @@ launch a bucket's all-reduce as soon as its last gradient lands.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
 import torch.nn.functional as F
 
-from . import _native
+from . import _native, fusion
 from ..variables import Variable
 
 
@@ -200,7 +201,8 @@ def _stem_ws(device, ko) -> torch.Tensor:
     ws = _STEM_WS.get(device)
     if ws is None:
         ws = torch.zeros(int(torch.ops.tfx.stem_wgrad_ws_floats(ko)), dtype=torch.float32, device=device)
-        _STEM_WS[device] = ws
+        if not torch.cuda.is_current_stream_capturing():  # never cache a graph-pool tensor (see _head_state)
+            _STEM_WS[device] = ws
     return ws
 
 
@@ -226,8 +228,11 @@ def _pw_apply_ok(x, w, stride, pad, dil, stats_into) -> bool:
 
 
 def _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into) -> bool:
-    """Can this conv's forward run fused with the deferred tail ``tp`` of its input (pw_fwd.hip)?"""
+    """Can this conv's forward run fused with the deferred tail ``tp`` of its input (pw_fwd.hip)?
+    Only a residual + ReLU tail (residual and mask bits set): a plain deferred BN falls through."""
     sh = w.shape
+    if tp.res is None or tp.mask is None:
+        return False
     if not (stride == 1 and pad == 0 and dil == 1 and isinstance(stats_into, BNWorkspace) and len(sh) == 4
             and sh[1] == 1 and sh[2] == 1 and sh[3] == x.shape[-1] and x.is_contiguous()):
         return False
@@ -286,6 +291,7 @@ class _Conv2d(torch.autograd.Function):
                                                                          *ws.finalize_args)
                     ctx.pending_in = tp
                     CONV3_FWD_CALLS[0] += 1
+                    fusion.note("bn_on_load", w.name, "conv3x3_fwd_fused")
                     return y
                 if tp.res is None and _pw_apply_ok(x, w, stride, pad, dil, stats_into):
                     # a plain ReLU BN applied on load by this single-k-tile 1x1 conv (igemm a_scale):
@@ -295,6 +301,7 @@ class _Conv2d(torch.autograd.Function):
                                                                       *ws.finalize_args)
                     ctx.pending_in = tp
                     PW_APPLY_CALLS[0] += 1
+                    fusion.note("bn_on_load", w.name, "igemm_fwd_a_scale")
                     return y
                 if _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into):
                     # the previous block's tail apply + this conv + its BN statistics in one launch:
@@ -304,16 +311,22 @@ class _Conv2d(torch.autograd.Function):
                         tp.x, tp.save, tp.res, tp.res_save, w.value, x, tp.mask, ws.get(x.device), *ws.finalize_args)
                     tp.done = True
                     PW_SQUEEZE_CALLS[0] += 1
+                    fusion.note("block_boundary_fwd", w.name, "pw_fwd_squeeze")
                     return y
+                fusion.note("layerwise", w.name, "bn_apply_into")
                 tp.materialize()
             if isinstance(stats_into, BNWorkspace):
                 ws = stats_into
                 # epilogue statistics, then the finalize: the BN only applies
                 y, ws.pending_save = torch.ops.tfx.conv_fwd_bn(x.contiguous(), w.value, stride, pad, dil,
                                                                ws.get(x.device), *ws.finalize_args)
+                fusion.note("bn_epilogue", w.name, "stem_fwd" if (_STEM_WGRAD and _stem_ok(x, w, stride, pad, dil))
+                            else "igemm_fwd_stats")
                 return y
             if stats_into is not None:
+                fusion.note("bn_epilogue", w.name, "igemm_fwd_stats_only")
                 return torch.ops.tfx.conv_fwd_stats(x.contiguous(), w.value, stride, pad, dil, stats_into)
+            fusion.note("conv", w.name, "igemm_fwd")
             return torch.ops.tfx.conv_fwd(x.contiguous(), w.value, stride, pad, dil)
         return _conv_ref(x, w.value.to(x.dtype), stride, pad, dil)
 
@@ -333,6 +346,7 @@ class _Conv2d(torch.autograd.Function):
             dx, bnb.red = torch.ops.tfx.conv3x3_bwd_fused(lazy.g.contiguous(), lazy.x, lazy.save, lazy.red, tp.x,
                                                           tp.save, w.value, w.grad, bnb.ws, bnb.dgamma, bnb.dbeta)
             CONV3_BWD_CALLS[0] += 1
+            fusion.note("conv3_fused_bwd", w.name, "conv3x3_bwd_fused")
             _grad_ready(w)
             return dx, None, None, None, None, None, None, None, None
         if tp is not None and not (tp.res is None and lazy is not None and need_dx and ctx.native
@@ -350,6 +364,7 @@ class _Conv2d(torch.autograd.Function):
                         lazy.g.contiguous(), lazy.x, lazy.save, lazy.red, x, w.value, w.grad, add.contiguous(), amask,
                         bnb.x, bnb.save, bnb.mask, bnb.ws, bnb.dgamma, bnb.dbeta)
                     PW_SQUEEZE_BWD_CALLS[0] += 1
+                    fusion.note("lazy_bn_bwd", w.name, "pw_bwd_squeeze")
                     _grad_ready(w)
                     return dx, None, None, None, None, None, None, None, None
                 if need_dx and _pw_expand_ok(x, w, stride, pad, dil, lazy, ctx.sink):
@@ -375,8 +390,10 @@ class _Conv2d(torch.autograd.Function):
                     if rb is not None:
                         rb.red, rb.sec_lazy = red_sc, None
                     PW_EXPAND_CALLS[0] += 1
+                    fusion.note("lazy_bn_bwd", w.name, "pw_bwd_expand")
                     _grad_ready(w)
                     return dx, None, None, None, None, None, None, None, None
+                fusion.note("layerwise", w.name, "bn_bwd_apply")
                 gy = lazy.materialize()
             gy = gy.contiguous()
             sink = ctx.sink
@@ -384,6 +401,7 @@ class _Conv2d(torch.autograd.Function):
                 # the CIFAR stem (8 padded input channels, no input gradient): one block per image (stem.hip)
                 torch.ops.tfx.stem_wgrad(gy, x.contiguous(), w.grad, _stem_ws(gy.device, w.shape[0]))
                 STEM_WGRAD_CALLS[0] += 1
+                fusion.note("stem_kernels", w.name, "stem_wgrad")
                 _grad_ready(w)
                 return None, None, None, None, None, None, None, None, None
             dx = None
@@ -395,6 +413,7 @@ class _Conv2d(torch.autograd.Function):
                     # dx is the complete gradient of the BN output x: the epilogue also reduces
                     # that BN's backward (sum g', sum g' xhat, dgamma, dbeta) -- see BNBackwardFusion
                     add, amask, s2 = _unpack_sink(sink.take()) if sink is not None else (None, None, False)
+                    fusion.note("bn_epilogue", w.name, "igemm_dgrad_bnb" + ("+addend" if add is not None else ""))
                     if w.trainable:
                         # partials stay in the slots; the weight-gradient launch below reduces them in
                         # tail blocks of its grid (conv_wgrad_sr): no bn_slot_reduce launch
@@ -409,6 +428,7 @@ class _Conv2d(torch.autograd.Function):
                 elif sink is not None and sink.mode == "consume":
                     # last consumer of x in backward order: fold the other branch's gradient in
                     add, amask, s2 = _unpack_sink(sink.take())
+                    fusion.note("grad_sink", w.name, "igemm_dgrad_addend")
                     dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, add, amask, s2,
                                                   _wflip(w, stride, pad, dil))
                 elif sink is not None and sink.accept_s2 and stride == 2 and pad == 0 and w.shape[1] == 1 \
@@ -418,6 +438,7 @@ class _Conv2d(torch.autograd.Function):
                     n, h, wd, c = x.shape
                     dxc = torch.ops.tfx.conv_dgrad(gy, w.value, [n, gy.shape[1], gy.shape[2], c], 1, 0, dil, None)
                     sink.put(("s2", dxc))
+                    fusion.note("s2_addend", w.name, "igemm_dgrad_compact")
                     dx = None
                 else:
                     dx = torch.ops.tfx.conv_dgrad(gy, w.value, list(x.shape), stride, pad, dil, None, None, False,
@@ -446,9 +467,11 @@ class _Conv2d(torch.autograd.Function):
                         t1.red = r1
                     if t2 is not None:
                         t2.red, t2.sr_pending = r2, False
+                    fusion.note("deferred_slot_reduce", w.name, "igemm_wgrad_sr%d" % ((t1 is not None) + (t2 is not None)))
                     _grad_ready(w)
                 else:
                     torch.ops.tfx.conv_wgrad(gy, x, w.grad, stride, pad, dil, True)
+                    fusion.note("conv", w.name, "igemm_wgrad")
                     _grad_ready(w)
             return dx, None, None, None, None, None, None, None, None
         dx = _ref_param_grads(lambda xx, ww: _conv_ref(xx, ww, stride, pad, dil), x, [w], gy, need_dx)
@@ -1128,6 +1151,7 @@ _FUSE_HEAD = True  # test / A-B hook: False composes global_avg_pool, linear and
 _HEAD_TAIL = True  # test / A-B hook: False materialises a deferred last tail before the fused head
 HEAD_FUSED_CALLS = [0]
 HEAD_TAIL_CALLS = [0]
+_CHECK_SEED = os.environ.get("TFX_CHECK_SEED", "0") == "1"
 _HEAD_STATE = {}
 
 
@@ -1137,7 +1161,10 @@ def _head_state(device) -> torch.Tensor:
     st = _HEAD_STATE.get(device)
     if st is None:
         st = torch.zeros(3, dtype=torch.int64, device=device)
-        _HEAD_STATE[device] = st
+        # a tensor allocated during a capture lives in that graph's private pool: never cache it (the
+        # zero fill is then recorded in the graph, so each replay still starts from a zero word)
+        if not torch.cuda.is_current_stream_capturing():
+            _HEAD_STATE[device] = st
     return st
 
 
@@ -1160,15 +1187,22 @@ class _HeadXent(torch.autograd.Function):
                                                          tp.res, tp.save, tp.mask, rows)
             ctx.tail_bnb, ctx.tail_rows = bnb, rows
             HEAD_TAIL_CALLS[0] += 1
+            fusion.note("head_tail", w.name, "head_xent_tail")
         else:
             loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, bias, labels, _head_state(feat.device), None,
                                                          None, None, None, None)
         ctx.save_for_backward(dfeat, f, dz)
         HEAD_FUSED_CALLS[0] += 1
+        fusion.note("fused_head", w.name, "head_xent")
         return loss
 
     @staticmethod
     def backward(ctx, g):
+        # unit-seed contract (classifier_head_xent): dfeat, dW, db and the tail BN's dgamma / dbeta were
+        # formed in the forward for a seed of exactly 1 -- a scaled seed is NOT applied.  Callers that
+        # scale the loss use unit_seed=False (the composed ops).  TFX_CHECK_SEED=1 verifies it (syncs).
+        if _CHECK_SEED and float(g) != 1.0:
+            raise RuntimeError("fused classifier head: backward seed %r != 1 (use unit_seed=False)" % float(g))
         dfeat, f, dz = ctx.saved_tensors
         w, b = ctx.w, ctx.b
         bnb = ctx.tail_bnb
@@ -1201,7 +1235,9 @@ def classifier_head_xent(feat, w: Variable, b: Optional[Variable], labels, naive
     """``softmax_cross_entropy(linear(global_avg_pool(feat), w, b), labels)`` -- the training head of an
     image classifier (NHWC ``feat``, int64 ``labels``).  With ``unit_seed`` (the loss is the root of
     ``loss.backward()``) on the GPU it runs as ONE launch that also forms the input gradient
-    (csrc/kernels/head.hip); otherwise, and for TF1's naive loss, the three ops compose."""
+    (csrc/kernels/head.hip); otherwise, and for TF1's naive loss, the three ops compose.  On the fused
+    path the gradients are formed for a backward seed of exactly 1: a scaled seed (loss scaling,
+    ``(loss * k).backward()``) is not applied -- such callers pass ``unit_seed=False``."""
     fused = (_FUSE_HEAD and unit_seed and not naive and feat.is_cuda and feat.dim() == 4
              and feat.dtype == torch.bfloat16 and labels.dtype == torch.long and labels.is_cuda
              and w.value.dtype == torch.bfloat16 and w.value.dim() == 2 and w.value.is_contiguous()

@@ -24,12 +24,20 @@ become one.  ``TFX_LSTM_PERSISTENT=0`` selects the per-step kernels above.
 Gate order: i, f, g, o (f gets ``forget_bias`` added in the pointwise kernel through ``b``).
 The whole step is HIP-graph capturable (no host syncs), which removes the per-step launch cost.
 
-Failure reporting of the persistent kernels: their inter-workgroup waits are bounded (a workgroup
-that is not resident -- CUs taken by another stream or process, e.g. RCCL kernels under DP -- would
-otherwise hang the grid).  On expiry a launch sets a per-device STICKY health word and drains; its
-results are invalid.  The training step never synchronises on it: :func:`check_lstm_health` reads
-it at the caller's own sync points (the examples' log cadence, LMTrainer.check) and raises
-:class:`LSTMHandoffError`, so a timed-out hand-off cannot silently train on wrong gradients.
+Co-residency of the persistent grid: :func:`_persistent` accepts a shape only when the occupancy API
+(x CUs) admits every workgroup of both kernels at once, and an eager launch is cooperative (the
+runtime refuses a grid that cannot be co-resident); a captured launch relies on that check.
+
+Failure handling of the persistent kernels: their inter-workgroup waits are still bounded (a
+workgroup kept off the device -- CUs taken by another stream or process, e.g. RCCL kernels under DP
+-- would otherwise hang the grid).  On expiry a launch sets a per-device STICKY health word and
+drains; its results are invalid.  The training step never synchronises on it, but it cannot
+corrupt the weights either: the fused optimizer takes the word as its ``skip_if`` and skips the
+update ON THE DEVICE while it is set (LMTrainer), so a bad step -- and any step until the host
+looks -- leaves parameters and moments unchanged.  At the caller's own sync points
+:func:`recover_persistent_failure` (LMTrainer.check) clears the word and switches this process to the
+per-step kernels for the rest of the run; :func:`check_lstm_health` instead raises
+:class:`LSTMHandoffError` for callers that want to stop.
 """
 from __future__ import annotations
 
@@ -78,6 +86,34 @@ def _health(dev: torch.device) -> torch.Tensor:
     return h
 
 
+def health_word(device) -> torch.Tensor:
+    """The device's sticky persistent-LSTM health word (int32, 0 = healthy): pass it as the optimizer's
+    ``skip_if`` so a step whose recurrence gave up on a hand-off is not applied."""
+    return _health(torch.device(device))
+
+
+# set once a persistent launch failed in this process: every later layer runs the per-step kernels
+_PERSISTENT_OFF = False
+PERSISTENT_LAUNCHES = [0]  # persistent fwd + bwd launches (tests)
+
+
+def recover_persistent_failure(device=None) -> bool:
+    """If a persistent launch on ``device`` (default: every device) timed out a hand-off since the last
+    look: clear the health word, switch this process to the per-step kernels, return True.  The steps
+    in between were skipped by the guarded optimizer (their updates are lost, never applied wrong)."""
+    global _PERSISTENT_OFF
+    devs = [torch.device(device).index or 0] if device is not None else list(_HEALTH)
+    failed = False
+    for d in devs:
+        h = _HEALTH.get(d)
+        if h is not None and int(h.item()) != 0:
+            h.zero_()
+            failed = True
+    if failed:
+        _PERSISTENT_OFF = True
+    return failed
+
+
 def check_lstm_health(device=None, reset: bool = True) -> None:
     """Raise :class:`LSTMHandoffError` if any persistent LSTM launch on ``device`` (default: all)
     timed out a hand-off since the last check.  Reads the device health word: call it where the host
@@ -94,7 +130,7 @@ def check_lstm_health(device=None, reset: bool = True) -> None:
 
 
 def _persistent(B: int, H: int, dev: torch.device) -> bool:
-    if os.environ.get("TFX_LSTM_PERSISTENT", "1") == "0" or not _native.use_native_device(dev):
+    if _PERSISTENT_OFF or os.environ.get("TFX_LSTM_PERSISTENT", "1") == "0" or not _native.use_native_device(dev):
         return False
     key = (B, H, dev.index or 0)
     if key not in _SEQ_OK:
@@ -130,6 +166,7 @@ class _LSTMLayer(torch.autograd.Function):
         gx = gx.view(T, B, 4 * H)
         ctx.persistent = _persistent(B, H, dev)
         if ctx.persistent:
+            PERSISTENT_LAUNCHES[0] += 1
             _LSTMLayer.last_status["fwd"] = torch.ops.tfx.lstm_seq_fwd(gx, w_hh.value, hbuf, cbuf, act, hT,
                                                                        _health(dev), int(_SPIN_LIMIT or 0))
         else:
@@ -172,6 +209,7 @@ class _LSTMLayer(torch.autograd.Function):
             dH16 = gout.to(torch.bfloat16).contiguous() if gout is not None else None
             dhT = g_hT.float().contiguous() if g_hT is not None else None
             dc_in = g_cT.float().contiguous() if g_cT is not None else None
+            PERSISTENT_LAUNCHES[0] += 1
             _LSTMLayer.last_status["bwd"] = torch.ops.tfx.lstm_seq_bwd(
                 act, cbuf, dH16, dhT, dc_in, w_hh.value, dg, None, b.grad if b.trainable else None,
                 _health(xf.device), int(_SPIN_LIMIT or 0))
@@ -217,4 +255,4 @@ def lstm_layer(x: torch.Tensor, w_ih: Variable, w_hh: Variable, b: Variable,
     return out, (hT.detach(), cT.detach())
 
 
-__all__ = ["lstm_layer", "check_lstm_health", "LSTMHandoffError"]
+__all__ = ["lstm_layer", "check_lstm_health", "LSTMHandoffError", "health_word", "recover_persistent_failure"]

@@ -58,9 +58,14 @@ class Optimizer:
             sv.clear()
 
     def apply_gradients(self, grad_scale: float = 1.0, sumsq: Optional[torch.Tensor] = None,
-                        max_norm: float = 0.0) -> None:
+                        max_norm: float = 0.0, skip_if: Optional[torch.Tensor] = None,
+                        grad: Optional[torch.Tensor] = None) -> None:
         """p <- update(p, grad_scale * g); refreshes the bf16 shadow. ``sumsq`` (device scalar
-        ||g||^2) enables clip-by-global-norm at ``max_norm``."""
+        ||g||^2) enables clip-by-global-norm at ``max_norm``.  ``skip_if`` (a device int32 word, GPU):
+        when it is nonzero at execution time the update is skipped ON THE DEVICE -- parameters,
+        moments and shadow unchanged (the persistent LSTM's health word guards its steps this way).
+        ``grad``: the flat gradient buffer to apply instead of the store's f32 one (same layout; f32 or
+        bf16 -- the DP bf16 wire format hands its all-reduced bf16 buffer straight to the kernel)."""
         st = self.store
         self.iterations += 1
         if self.kind >= ADAM:  # only the bias corrections read the device step counter (one launch less)
@@ -70,12 +75,13 @@ class Optimizer:
         if not st.vars:
             return
         if _native.use_native(st.master):
-            torch.ops.tfx.optimizer_apply(self.kind, st.master, st.grad, self.m, self.v, self.lr_t, grad_scale,
+            torch.ops.tfx.optimizer_apply(self.kind, st.master, st.grad if grad is None else grad, self.m, self.v,
+                                          self.lr_t, grad_scale,
                                           self.wd, self.b1, self.b2, self.eps, self.step_t, sumsq, max_norm,
-                                          st.shadow)
+                                          st.shadow, skip_if)
             return
         with torch.no_grad():
-            g = st.grad * grad_scale
+            g = (st.grad if grad is None else grad.float()) * grad_scale
             if sumsq is not None:
                 nrm = float(sumsq.sqrt())
                 if nrm > max_norm:
@@ -98,11 +104,11 @@ class Optimizer:
                 p.sub_(lr * upd)
             st.refresh_shadow()
 
-    def global_norm_sq(self) -> torch.Tensor:
-        st = self.store
-        if _native.use_native(st.grad):
-            return torch.ops.tfx.sumsq(st.grad)
-        return (st.grad.double() ** 2).sum().float().reshape(1)
+    def global_norm_sq(self, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
+        g = self.store.grad if grad is None else grad
+        if _native.use_native(g):
+            return torch.ops.tfx.sumsq(g)
+        return (g.double() ** 2).sum().float().reshape(1)
 
 
 class GradientDescentOptimizer(Optimizer):

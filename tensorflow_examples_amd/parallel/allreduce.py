@@ -16,7 +16,11 @@ Design for one MI355X node (8 GPUs, 7 point-to-point xGMI links of ~153 GB/s per
   RCCL's launch/latency cost yet small enough that the first bucket starts early in
   backward (ResNet-50: 94 MB of f32 gradients -> 3 buckets);
 * averaging is folded into the optimizer (``grad_scale = 1/world``), no extra pass;
-* optional bf16 compression halves the bytes on the wire (cast, reduce, cast back).
+* optional bf16 wire format (``compress_bf16``) halves the bytes on the wire: a persistent flat bf16
+  twin of the grad buffer (same layout, allocated once -- no per-bucket allocation, graph-safe), each
+  bucket cast into it by one vectorised launch right before its collective, reduced IN PLACE in bf16,
+  and the fused optimizer reads the reduced bf16 gradients directly into the f32 master update
+  (``reduced_grad``) -- no cast back, 47 MB less for the optimizer to read (ResNet-50).
 
 The reference has no synchronous DP at all -- only a commented-out
 ``SyncReplicasOptimizer`` remnant (R/distributed/distributed.py:110-113); this is the
@@ -52,6 +56,9 @@ class GradAllReduce:
         self.force = bool(force_collective) and dist.is_initialized()
         self.overlap = overlap
         self.compress = compress_bf16
+        # the bf16 twin of the flat grad buffer (zeros outside the buckets: padding and frozen vars)
+        self.grad16 = torch.zeros_like(store.grad, dtype=torch.bfloat16) if compress_bf16 else None
+        self._used16 = False
         elem = store.grad.element_size()
         cap = max(1, bucket_bytes // elem)
         tail_cap = max(1, tail_bytes // elem)
@@ -110,11 +117,6 @@ class GradAllReduce:
         e = self.store.grad.element_size()
         return [(hi - lo) * e for lo, hi in self.buckets]
 
-    def start_step(self) -> None:
-        self._pending = [len(m) for m in self.members]
-        self._launched = [False] * len(self.buckets)
-        self._works = []
-
     def reset(self) -> None:
         """Abandon a step that failed part-way through backward (e.g. a HIP-graph capture error):
         its queued Work objects may be captured, never-executed collectives, so they are dropped
@@ -146,9 +148,13 @@ class GradAllReduce:
         # issued from the compute stream right after the bucket's last gradient kernel: RCCL runs it
         # on its own stream, ordered after that kernel, beside the rest of backward
         if self.compress:
-            tmp = view.to(torch.bfloat16)
-            work = dist.all_reduce(tmp, op=op, group=self.group, async_op=True)
-            self._works.append((work, view, tmp))
+            g16 = self.grad16[lo:hi]
+            if view.is_cuda:
+                torch.ops.tfx.cast_f32_bf16(view, g16)
+            else:
+                g16.copy_(view)
+            self._used16 = True
+            self._works.append((dist.all_reduce(g16, op=op, group=self.group, async_op=True), None, None))
         else:
             self._works.append((dist.all_reduce(view, op=op, group=self.group, async_op=True), None, None))
 
@@ -161,11 +167,25 @@ class GradAllReduce:
             work.wait()
             if view is not None:
                 view.copy_(tmp)
-        self.start_step()
+        self._pending = [len(m) for m in self.members]
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+
+    def start_step(self) -> None:
+        self._pending = [len(m) for m in self.members]
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+        self._used16 = False
 
     @property
     def grad_scale(self) -> float:
         return 1.0 / self.world
+
+    @property
+    def reduced_grad(self) -> Optional[torch.Tensor]:
+        """The flat buffer holding the all-reduced gradients for the optimizer: the bf16 twin when the
+        bf16 wire format ran collectives this step, else None (the f32 grad buffer itself)."""
+        return self.grad16 if (self.compress and self._used16) else None
 
 
 def broadcast_variables(store: VariableStore, src: int = 0, group=None) -> None:

@@ -28,8 +28,18 @@ class ClassifierTrainer:
         self.graph = None
         self._static = None
         self._one = None
+        self.plan = None  # ops.fusion.record of the first step: which fusion group ran which layer
 
     def _step(self, x, y):
+        if self.plan is None and not (x.is_cuda and torch.cuda.is_current_stream_capturing()):
+            from .ops import fusion
+            with fusion.record() as rec:
+                loss = self._step_impl(x, y)
+            self.plan = rec
+            return loss
+        return self._step_impl(x, y)
+
+    def _step_impl(self, x, y):
         # roctx ranges (TFX_ROCTX=1) label the phases on a rocprofv3 --marker-trace timeline
         reset_pending_slot_reductions()  # nothing deferred survives an abandoned step
         self.store.zero_grad()
@@ -48,13 +58,13 @@ class ClassifierTrainer:
                 if not (one.is_cuda and torch.cuda.is_current_stream_capturing()):  # not from a graph pool
                     self._one = one
             loss.backward(one)
-        scale = 1.0
+        scale, grad = 1.0, None
         if self.dp is not None:
             with trace.range("allreduce_wait"):
                 self.dp.finish()
-            scale = self.dp.grad_scale
+            scale, grad = self.dp.grad_scale, self.dp.reduced_grad
         with trace.range("optimizer"):
-            self.opt.apply_gradients(grad_scale=scale)
+            self.opt.apply_gradients(grad_scale=scale, grad=grad)
         return loss.detach()
 
     def input_buffer(self):

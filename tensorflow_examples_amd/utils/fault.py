@@ -40,6 +40,12 @@ def _die(what: str) -> None:
     os._exit(FAULT_EXIT_CODE)
 
 
+def armed() -> bool:
+    """True when a fault is configured (callers that enqueue work asynchronously -- a replayed HIP
+    graph -- must complete it before :func:`after_step`, whose contract is steps *completed*)."""
+    return _KIND is not None
+
+
 def before_init() -> None:
     if _KIND == "before_init":
         _die("before_init")

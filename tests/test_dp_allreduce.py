@@ -26,13 +26,13 @@ def _model(seed):
     return st, m
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, bf16=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     st, m = _model(seed=10 + rank)  # different init per rank: broadcast must fix it
     broadcast_variables(st)
-    dp = GradAllReduce(st, bucket_bytes=2048)  # several buckets
+    dp = GradAllReduce(st, bucket_bytes=2048, compress_bf16=bf16)  # several buckets
     opt = MomentumOptimizer(st, 0.1, momentum=0.9)
     x, y = _data()
     per = x.shape[0] // world
@@ -42,7 +42,9 @@ def _worker(rank, world, port, out):
         loss = ops.softmax_cross_entropy(m.logits(xs), ys, naive=False)
         loss.backward()
         dp.finish()
-        opt.apply_gradients(grad_scale=dp.grad_scale)
+        if bf16:
+            assert dp.reduced_grad is not None and dp.reduced_grad.dtype == torch.bfloat16
+        opt.apply_gradients(grad_scale=dp.grad_scale, grad=dp.reduced_grad)
     out[rank] = (st.master.clone(), len(dp.buckets))
     dist.destroy_process_group()
 
@@ -146,3 +148,23 @@ def test_reset_after_mid_backward_failure_reduces_each_bucket_once():
         assert nb >= 2
         assert clean[0] == list(range(nb)) and recovered[0] == list(range(nb))
         assert torch.equal(clean[1], recovered[1])
+
+
+def test_dp_bf16_wire_format_vs_f32_reduce():
+    """The bf16 wire format (persistent bf16 twin, in-place bf16 reduce, optimizer reads it) tracks the
+    f32 reduce within bf16 rounding, and replicas stay identical."""
+    res = {}
+    for bf16 in (False, True):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        mgr = mp.Manager()
+        out = mgr.dict()
+        mp.start_processes(_worker, args=(2, port, out, bf16), nprocs=2, join=True, start_method="spawn")
+        assert torch.equal(out[0][0], out[1][0])
+        res[bf16] = out[0][0]
+    st, _ = _model(seed=10)
+    d32, d16 = res[False] - st.master, res[True] - st.master
+    rel = ((d16 - d32).norm() / d32.norm()).item()
+    assert 0 < rel < 2e-2, rel

@@ -117,20 +117,23 @@ from tensorflow_examples_amd.train import ClassifierTrainer
 dev = init_distributed(device="cuda")  # TFX_DP_FORCE_COLLECTIVE=1: 1-rank RCCL process group
 assert dist.is_initialized() and dist.get_backend() == "nccl", dist.get_backend()
 g = torch.Generator().manual_seed(0)
-img = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, generator=g).to(dev)
-lab = torch.randint(0, 10, (16,), generator=g).to(dev)
-x = to_model_input(img)
 # The all-reduce is a pre-multiplied sum by 2: at world size 1 every bucket's collective doubles its
 # gradient, so a bucket whose collective is dropped from the graph, or ordered before its weight
 # gradient lands, leaves a wrong gradient.  Without weight decay, momentum-SGD on 2g at lr is the
 # same trajectory as on g at 2 lr -- the reference run has no DP at all.
+DEPTH, BATCH = int(os.environ.get("DP_DEPTH", "18")), int(os.environ.get("DP_BATCH", "16"))
+BF16 = os.environ.get("DP_BF16", "0") == "1"
+BUCKET = int(float(os.environ.get("DP_BUCKET_MB", "2")) * (1 << 20))
+img = torch.randint(0, 256, (BATCH, 32, 32, 3), dtype=torch.uint8, generator=g).to(dev)
+lab = torch.randint(0, 10, (BATCH,), generator=g).to(dev)
+x = to_model_input(img)
 runs = {}
 for mode in ("ref", "eager", "graphed"):
-    store, model = build_resnet_cifar(device=dev, depth=18, dtype=torch.bfloat16, seed=0)
+    store, model = build_resnet_cifar(device=dev, depth=DEPTH, dtype=torch.bfloat16, seed=0)
     w0 = store.master.clone()
     dp = None
     if mode != "ref":
-        dp = GradAllReduce(store, bucket_bytes=2 << 20, premul=2.0)
+        dp = GradAllReduce(store, bucket_bytes=BUCKET, premul=2.0, compress_bf16=BF16)
         assert dp.force and len(dp.buckets) > 2
     lr = 0.02 if mode == "ref" else 0.01
     opt = MomentumOptimizer(store, lr, momentum=0.9)
@@ -156,16 +159,23 @@ for mode in ("eager", "graphed"):
     worst = max(((d[lo:hi] - ref[lo:hi]).norm() / ref[lo:hi].norm()).item() for lo, hi in buckets
                 if ref[lo:hi].norm() > 0)
     print("REL", mode, rel, "worst_bucket", worst, "buckets", len(buckets), flush=True)
-    assert rel < 2e-3 and worst < 1e-2, (mode, rel, worst)
+    # bf16 on the wire rounds every gradient to 8 significant bits (rel ~ 2^-9 per element)
+    lim = (1e-2, 3e-2) if BF16 else (2e-3, 1e-2)
+    assert rel < lim[0] and worst < lim[1], (mode, rel, worst)
 dist.destroy_process_group()
 """
 
 
-def test_dp_graph_capture_rccl_one_rank(gpu, tmp_path):
+@pytest.mark.parametrize("depth,batch,bf16,bucket_mb", [(18, 16, False, 2), (50, 256, False, 8), (50, 256, True, 8)],
+                         ids=["r18_b16_f32", "r50_b256_f32", "r50_b256_bf16"])
+def test_dp_graph_capture_rccl_one_rank(gpu, tmp_path, depth, batch, bf16, bucket_mb):
     """The DP step (bucketed RCCL all-reduces launched from grad-ready hooks) eager and captured in
     a HIP graph and replayed, on a 1-rank RCCL process group whose all-reduce is a pre-multiplied
     sum by 2: one step of each must equal one no-DP step at twice the learning rate, bucket by
-    bucket (split-K atomics make the runs differ in rounding only)."""
+    bucket (split-K atomics make the runs differ in rounding only).  ResNet-50 at batch 256 is the
+    bench's fused backward (deferred BN reductions and fused weight gradients fire the bucket hooks);
+    the bf16 variant runs the bf16 wire format (per-bucket cast into the persistent bf16 twin, reduced
+    in place, read by the optimizer)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -173,7 +183,8 @@ def test_dp_graph_capture_rccl_one_rank(gpu, tmp_path):
     script = tmp_path / "g.py"
     script.write_text(GRAPH_WORKER)
     env = dict(os.environ, ROOT=ROOT, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
-               MASTER_PORT=str(port), TFX_DP_FORCE_COLLECTIVE="1")
+               MASTER_PORT=str(port), TFX_DP_FORCE_COLLECTIVE="1", DP_DEPTH=str(depth), DP_BATCH=str(batch),
+               DP_BF16="1" if bf16 else "0", DP_BUCKET_MB=str(bucket_mb))
     p = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
     print(p.stdout, p.stderr[-3000:])
     assert p.returncode == 0, p.stderr[-3000:]

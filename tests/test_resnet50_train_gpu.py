@@ -1,0 +1,98 @@
+"""ResNet-50 (the headline model) through the round-3 fused kernels: the fused training loss at the
+bench's batch-256 shape against fp32 reference ops, and a short training run that must reach an
+accuracy far above chance while every fused path (block-boundary forward, fused conv1/conv3
+backward, stage-1 3x3 fwd/bwd, head tail mode) actually ran.
+
+Reference: success is judged by the final accuracy line, R/distributed/distributed.py:164."""
+import pytest
+import torch
+
+from tensorflow_examples_amd import ops
+from tensorflow_examples_amd.data.cifar import synthetic_cifar
+from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
+from tensorflow_examples_amd.ops import _native
+from tensorflow_examples_amd.ops import nn as nnops
+from tensorflow_examples_amd.optim import MomentumOptimizer
+from tensorflow_examples_amd.train import ClassifierTrainer
+
+pytestmark = pytest.mark.gpu
+
+_COUNTERS = ("PW_SQUEEZE_CALLS", "PW_SQUEEZE_BWD_CALLS", "PW_EXPAND_CALLS", "CONV3_FWD_CALLS", "CONV3_BWD_CALLS",
+             "HEAD_TAIL_CALLS", "HEAD_FUSED_CALLS", "PW_APPLY_CALLS", "STEM_WGRAD_CALLS")
+
+
+def _counts():
+    return {k: getattr(nnops, k)[0] for k in _COUNTERS}
+
+
+def test_resnet50_training_loss_batch256_vs_fp32_reference(gpu):
+    """bench.py's step: model.training_loss (fused head in TAIL mode: the last tail BN applied while
+    pooling, pool + FC + softmax-xent + unit-seed input gradient in one launch) + backward, at batch
+    256, against the PyTorch reference ops of the same model in fp32 on the GPU; per-variable gradient
+    error bounded by the bf16 noise floor (the reference ops run in bf16)."""
+    g = torch.Generator().manual_seed(21)
+    img = torch.randint(0, 256, (256, 32, 32, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 10, (256,), generator=g).to(gpu)
+    res = {}
+    before = _counts()
+    for mode, dt in (("native", torch.bfloat16), ("ref32", torch.float32), ("ref16", torch.bfloat16)):
+        st, m = build_resnet_cifar(device=gpu, depth=50, dtype=dt, seed=7)
+        if mode == "native":
+            w0 = st.master.bfloat16().float()
+        st.master.copy_(w0)
+        st.refresh_shadow()
+        st.zero_grad()
+        if mode == "native":
+            loss = m.training_loss(to_model_input(img.to(gpu)), lab, unit_seed=True)
+            loss.backward()
+        else:
+            with _native.reference_mode():
+                loss = ops.softmax_cross_entropy(m(to_model_input(img, dtype=dt).to(gpu), training=True), lab)
+                loss.backward()
+        torch.cuda.synchronize()
+        res[mode] = (float(loss), st)
+    after = _counts()
+    for k in ("HEAD_TAIL_CALLS", "PW_SQUEEZE_CALLS", "PW_EXPAND_CALLS", "PW_SQUEEZE_BWD_CALLS", "CONV3_FWD_CALLS",
+              "CONV3_BWD_CALLS"):
+        assert after[k] > before[k], (k, before, after)
+    (ln, sn), (l32, s32), (l16, s16) = res["native"], res["ref32"], res["ref16"]
+    assert abs(ln - l32) < 0.02 * abs(l32) + 0.02, (ln, l32)
+    bad = []
+    for v in s32.trainable():
+        gr = v.grad
+        en = ((sn.by_name[v.name].grad - gr).norm() / (gr.norm() + 1e-8)).item()
+        eb = ((s16.by_name[v.name].grad - gr).norm() / (gr.norm() + 1e-8)).item()
+        if en > 2.0 * eb + 0.02:
+            bad.append((v.name, en, eb))
+    assert not bad, bad[:5]
+
+
+def test_resnet50_trains_synthetic_cifar(gpu):
+    """A short ResNet-50 training run on synthetic CIFAR-10 (batch 128, 80 steps, momentum SGD) reaches a
+    test accuracy far above chance, every step on the fused kernel paths (counters checked)."""
+    xtr, ytr = synthetic_cifar(128 * 80, 0)
+    xte, yte = synthetic_cifar(2000, 1)
+    st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=0)
+    opt = MomentumOptimizer(st, 0.05, momentum=0.9, weight_decay=5e-4)
+    tr = ClassifierTrainer(st, m, opt)
+    xtr_d = torch.as_tensor(xtr, device=gpu)
+    ytr_d = torch.as_tensor(ytr, device=gpu)
+    before = _counts()
+    losses = []
+    for i in range(80):
+        sl = slice(128 * i, 128 * (i + 1))
+        losses.append(tr.step(to_model_input(xtr_d[sl]), ytr_d[sl]))
+    losses = [float(l) for l in losses]
+    after = _counts()
+    for k in ("HEAD_TAIL_CALLS", "PW_SQUEEZE_CALLS", "PW_EXPAND_CALLS", "PW_SQUEEZE_BWD_CALLS", "CONV3_FWD_CALLS",
+              "CONV3_BWD_CALLS", "STEM_WGRAD_CALLS"):
+        assert after[k] - before[k] >= 80, (k, before, after)
+    assert all(l == l for l in losses), losses
+    correct = 0
+    with torch.no_grad():
+        for i in range(0, len(xte), 500):
+            x = to_model_input(torch.as_tensor(xte[i:i + 500], device=gpu))
+            y = torch.as_tensor(yte[i:i + 500], device=gpu)
+            correct += float(ops.accuracy(m(x, training=False), y)) * len(y)
+    acc = correct / len(xte)
+    assert acc > 0.5, (acc, losses[::10])
