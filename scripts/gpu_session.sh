@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session, as named steps (STEPS="tests bench prof ..."): every GPU step runs under its
 # own time limit and the steps are chained -- a crash, abort or time-out ends the session (no further
-# GPU work), a failing test does not.  Output under gpurun_out/; copy what is worth keeping to profiles/.
+# GPU work), a failing test does not.  Output under $O/; copy what is worth keeping to profiles/.
 #   tests    pytest -m gpu (the whole GPU suite, one process)
 #   bench    bench.py --steps 20 --warmup 5 (the driver's 1-GPU command)
 #   prof     rocprofv3 --kernel-trace --stats over a short bench, summarised by scripts/kstats.py
@@ -10,9 +10,11 @@
 #   models   scripts/bench_models.py (LeNet-5, word2vec, char-LSTM)
 #   dpforce  the DP step on a 1-rank RCCL group under torch.distributed.run, graphed and eager
 set -u
-R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"
-mkdir -p gpurun_out
+# R = the tree to run (cwd: the repo root, or the frozen .snap copy of scripts/snap_submit.sh);
+# O = where results go (OUT, default R/gpurun_out -- gpurun merges $GRAFT_REPO_ROOT/gpurun_out back)
+R=$(pwd)
+O=${OUT:-$R/gpurun_out}
+mkdir -p "$O"
 export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
 STEPS=${STEPS:-"tests bench prof"}
@@ -20,48 +22,48 @@ for s in $STEPS; do
   case $s in
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread \
-        ${PYTEST_EXTRA:-} > gpurun_out/pytest_gpu.log 2>&1
-      rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+        ${PYTEST_EXTRA:-} > $O/pytest_gpu.log 2>&1
+      rc=$?; echo "pytest rc=$rc"; tail -5 $O/pytest_gpu.log
       [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     bench)
       for i in ${BENCH_REPS:-1}; do
-        timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$i.log 2>&1
-        rc=$?; echo "bench rc=$rc"; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_$i.log; [ $rc -eq 0 ] || exit $rc
+        timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_$i.log 2>&1
+        rc=$?; echo "bench rc=$rc"; grep -o '"ms_per_step": [0-9.]*' $O/bench_$i.log; [ $rc -eq 0 ] || exit $rc
       done ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- \
-        python3 "$R/bench.py" --steps 5 --warmup 2 > gpurun_out/prof.log 2>&1
-      rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/prof.log; exit $rc; }
-      f=$(find gpurun_out/prof -name '*kernel_stats.csv' | head -1)
-      python scripts/kstats.py "$f" auto 60 > gpurun_out/kernel_summary.txt; head -25 gpurun_out/kernel_summary.txt
-      kt=$(find gpurun_out/prof -name '*kernel_trace.csv' | head -1)
-      python scripts/step_trace.py "$kt" > gpurun_out/step_trace.txt; head -1 gpurun_out/step_trace.txt ;;
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
+        python3 "$R/bench.py" --steps 5 --warmup 2 > $O/prof.log 2>&1
+      rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/prof.log; exit $rc; }
+      f=$(find $O/prof -name '*kernel_stats.csv' | head -1)
+      python scripts/kstats.py "$f" auto 60 > $O/kernel_summary.txt; head -25 $O/kernel_summary.txt
+      kt=$(find $O/prof -name '*kernel_trace.csv' | head -1)
+      python scripts/step_trace.py "$kt" > $O/step_trace.txt; head -1 $O/step_trace.txt ;;
     pmc)
       i=0
       for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" \
                  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM TCC_HIT_sum TCC_MISS_sum" \
                  "FETCH_SIZE" "WRITE_SIZE"; do
         i=$((i+1))
-        timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$R/gpurun_out/pmc/p$i" -o p -- \
-          python3 "$R/bench.py" --steps 2 --warmup 1 --no-graph > gpurun_out/pmc_p$i.log 2>&1
-        rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_p$i.log; exit $rc; }
+        timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$O/pmc/p$i" -o p -- \
+          python3 "$R/bench.py" --steps 2 --warmup 1 --no-graph > $O/pmc_p$i.log 2>&1
+        rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/pmc_p$i.log; exit $rc; }
       done
-      python scripts/pmc_summary.py gpurun_out/pmc --steps 3 > gpurun_out/pmc_summary.txt; head -45 gpurun_out/pmc_summary.txt ;;
+      python scripts/pmc_summary.py $O/pmc --steps 3 > $O/pmc_summary.txt; head -45 $O/pmc_summary.txt ;;
     convs)
-      timeout -k 10 400 python scripts/conv_bench.py --out gpurun_out/conv_bench.json > gpurun_out/conv_bench.log 2>&1
-      rc=$?; echo "convs rc=$rc"; tail -3 gpurun_out/conv_bench.log; [ $rc -eq 0 ] || exit $rc ;;
+      timeout -k 10 400 python scripts/conv_bench.py --out $O/conv_bench.json > $O/conv_bench.log 2>&1
+      rc=$?; echo "convs rc=$rc"; tail -3 $O/conv_bench.log; [ $rc -eq 0 ] || exit $rc ;;
     models)
-      timeout -k 10 600 python scripts/bench_models.py > gpurun_out/bench_models.jsonl 2> gpurun_out/bench_models.err
-      rc=$?; echo "models rc=$rc"; cat gpurun_out/bench_models.jsonl; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_models.err; exit $rc; }
+      timeout -k 10 600 python scripts/bench_models.py > $O/bench_models.jsonl 2> $O/bench_models.err
+      rc=$?; echo "models rc=$rc"; cat $O/bench_models.jsonl; [ $rc -eq 0 ] || { tail -5 $O/bench_models.err; exit $rc; }
       ;;
     dpforce)
       for v in 1 0; do
         TFX_DP_FORCE_COLLECTIVE=1 TFX_DP_GRAPH=$v timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 2951$v bench.py --steps 20 --warmup 5 \
-          > gpurun_out/bench_dpforce_g$v.log 2>&1
-        rc=$?; echo "dpforce graph=$v rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_dpforce_g$v.log; exit $rc; }
+          > $O/bench_dpforce_g$v.log 2>&1
+        rc=$?; echo "dpforce graph=$v rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/bench_dpforce_g$v.log; exit $rc; }
       done
-      grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_dpforce_g*.log ;;
+      grep -o '"ms_per_step": [0-9.]*' $O/bench_dpforce_g*.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

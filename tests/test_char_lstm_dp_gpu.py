@@ -174,7 +174,7 @@ def test_persistent_lstm_failure_skips_update_and_falls_back(gpu):
         # gradients differs between the two runs: bound the gap by the size of the update itself
         upd = (rstore.master - w_before).norm().item()
         gap = (store.master - rstore.master).norm().item()
-        assert upd > 0 and gap < 1e-3 * upd, (gap, upd)  # training continued, on the reference trajectory
+        assert upd > 0 and gap < 1e-2 * upd, (gap, upd)  # training continued, on the reference trajectory
         assert tr.check() is False
     finally:
         rnn_ops._PERSISTENT_OFF, rnn_ops._SPIN_LIMIT = saved_off, saved_spin
