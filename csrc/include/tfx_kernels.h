@@ -106,6 +106,10 @@ struct IgemmArgs {
   // single k-tile (K <= 64) on the register-staged pipeline only (igemm_launch checks).
   const float* a_scale = nullptr;
   const float* a_shift = nullptr;
+  // im2col (KM_FWD_X) operand with C % 64 == 0 and R*S <= 32 (set by igemm_launch): every 64-deep
+  // k-tile lies in ONE filter tap, so the tap / channel decode is uniform (scalar) per k-tile and a
+  // row's padding test is one bit of a per-row tap-validity mask precomputed at the block's start
+  int tapmask = 0;
   // filled by the launcher
   int kps = 0, tiles_m = 0, tiles_n = 0;
 };

@@ -157,6 +157,9 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
         break;
     }
   }
+  // im2col operand (forward, flipped-filter data gradient) whose k-tiles each lie in one filter tap
+  if ((mode == MODE_FWD || mode == MODE_DGRAD_FLIP) && a.C % BKT_HOST == 0 && a.R * a.S <= 32 && !a.a_scale)
+    a.tapmask = 1;
   switch (mode) {
     case MODE_FWD: igemm_fwd_im2col(a, s); break;
     case MODE_DGRAD: igemm_dgrad_general(a, s); break;

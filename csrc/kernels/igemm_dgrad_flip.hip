@@ -6,5 +6,8 @@
 #include "igemm_impl.h"
 
 namespace tfx {
-void igemm_dgrad_flip(IgemmArgs& a, hipStream_t s) { launch_epi<KM_FWD_X, KM_DENSE, EPI_BNB>(a, s, FAM_DGRAD_FLIP); }
+void igemm_dgrad_flip(IgemmArgs& a, hipStream_t s) {
+  if (a.tapmask) launch_epi<KM_FWD_XT, KM_DENSE, EPI_BNB>(a, s, FAM_DGRAD_FLIP);  // Ko % 64 == 0
+  else launch_epi<KM_FWD_X, KM_DENSE, EPI_BNB>(a, s, FAM_DGRAD_FLIP);
+}
 }  // namespace tfx

@@ -6,11 +6,18 @@
 //   K-major kinds  (LDS image [rows][64 k], fragments by ds_read_b128):
 //     KM_DENSE     A[m*ld + k]
 //     KM_FWD_X     im2col(X) of an NHWC conv forward, gathered on the fly
+//     KM_FWD_XT    the same when C % 64 == 0 (every 64-deep k-tile inside one filter tap): the tap /
+//                  channel decode is uniform per k-tile (scalar), a row's padding test one bit of a
+//                  per-row tap-validity mask built at the block's start
 //     KM_DGRAD_DY  gather of dY for the conv data-gradient (stride via parity test)
 //   MN-major kinds (LDS image [64 k][cols], fragments by ds_read_b64_tr_b16, no transpose pass):
 //     MN_DENSE     A[k*ld + m]                (also dY^T for the weight gradient)
 //     MN_DGRAD_W   W[ko][r][s][c] read as B(k=(r,s,ko), n=c)
 //     MN_WGRAD_X   im2col(X) rows j=(n,p,q), columns (r,s,c)
+//     MN_WGRAD_XT  the same when a 64-pixel k-tile is whole output rows of one image or whole images
+//                  (P*Q % 64 == 0 and 64 % Q == 0, or 64 % (P*Q) == 0): each k-row's (p, q) offset
+//                  inside the tile is a per-thread constant, so per k-tile only the tile's (n0, p0) --
+//                  scalar -- and one bound test per piece remain
 // Ops: conv FWD = <KM_FWD_X, KM_DENSE>, DGRAD = <KM_DGRAD_DY, MN_DGRAD_W>,
 //      WGRAD = <MN_DENSE(dY), MN_WGRAD_X> or transposed <MN_WGRAD_X, MN_DENSE(dY)> (+trans_out),
 //      GEMM = any K/MN-major dense pair.
@@ -38,8 +45,8 @@ namespace tfx {
 
 namespace {
 
-enum { KM_DENSE = 0, KM_FWD_X = 1, KM_DGRAD_DY = 2, MN_DENSE = 10, MN_DGRAD_W = 11, MN_WGRAD_X = 12,
-       MN_DGRAD_W2 = 13 };
+enum { KM_DENSE = 0, KM_FWD_X = 1, KM_DGRAD_DY = 2, KM_FWD_XT = 3, MN_DENSE = 10, MN_DGRAD_W = 11,
+       MN_WGRAD_X = 12, MN_DGRAD_W2 = 13, MN_WGRAD_XT = 14 };
 enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_BNB = 2 };
 constexpr uint32_t BAD = 0x80000000u;  // byte offset beyond any num_records -> loads return 0
 constexpr int NT = 256, BKT = 64;
@@ -174,15 +181,32 @@ struct Loader {
           ctx0[i] = ok ? 0 : -1;
           base[i] = row * ld;
         } else {
-          const int GY = KIND == KM_FWD_X ? a.P : a.H, GX = KIND == KM_FWD_X ? a.Q : a.W;
+          constexpr bool IM2COL = KIND == KM_FWD_X || KIND == KM_FWD_XT;
+          const int GY = IM2COL ? a.P : a.H, GX = IM2COL ? a.Q : a.W;
           int n = row / (GY * GX), yx = row - n * GY * GX, y = yx / GX, x = yx - y * GX;
           // rows past M get a y far out of range: every bounds test below then fails (no flag register)
           constexpr int FAR = -(1 << 28);
-          if constexpr (KIND == KM_FWD_X) {
+          if constexpr (IM2COL) {
             ctx1[i] = ok ? y * a.sh - a.ph : FAR;
             ctx2[i] = x * a.sw - a.pw;
             // element offset of (n, iy0, ix0, 0): may be negative (padding), only used when in range
             base[i] = ((n * a.H + y * a.sh - a.ph) * a.W + ctx2[i]) * a.C;
+            if constexpr (KIND == KM_FWD_XT) {
+              // bit (r*S + s) = tap (r, s) of this row is inside the image (rows past M: none)
+              uint32_t vm = 0;
+              for (int r = 0; r < a.R; ++r) {
+                const bool yin = (unsigned)(ctx1[i] + r * a.dh) < (unsigned)a.H;
+                for (int s2 = 0; s2 < a.S; ++s2) {
+                  const bool xin = (unsigned)(ctx2[i] + s2 * a.dw) < (unsigned)a.W;
+                  vm |= (yin && xin ? 1u : 0u) << (r * a.S + s2);
+                }
+              }
+              ctx0[i] = (int)vm;
+              base[i] += c0;  // the thread's channel chunk is fixed: fold it into the row base
+              // opaque from here: hipcc otherwise re-derives base + dk per k-tile as
+              // ((nH + iy) W + ix) C -- two quarter-rate v_mul_lo_u32 per piece
+              asm volatile("" : "+v"(base[i]), "+v"(ctx0[i]));
+            }
           } else {
             ctx1[i] = ok ? y + a.ph : FAR;
             ctx2[i] = x + a.pw;
@@ -199,12 +223,13 @@ struct Loader {
         const int cj = base0 + 8 * ((l % CH) ^ mn_swz<ROWS>(r));
         col[j] = cj < lim ? cj : -1;
         if constexpr (KIND == MN_DENSE) base[j] = r * ld + cj;
-        if constexpr (KIND == MN_WGRAD_X) {
+        if constexpr (KIND == MN_WGRAD_X || KIND == MN_WGRAD_XT) {
           const int rs = cj < lim ? cj / a.C : 0;
           cc[j] = cj - rs * a.C;
           cr[j] = rs / a.S;
           cs[j] = rs - cr[j] * a.S;
         }
+        if constexpr (KIND == MN_WGRAD_XT) xt_init(a, j, r, cj < lim);
       }
     } else {
       r0 = t >> 2;
@@ -214,14 +239,32 @@ struct Loader {
         const int cj = base0 + 8 * ((t & 3) + 4 * j);
         col[j] = cj < lim ? cj : -1;
         if constexpr (KIND == MN_DENSE) base[j] = r0 * ld + cj;
-        if constexpr (KIND == MN_WGRAD_X) {
+        if constexpr (KIND == MN_WGRAD_X || KIND == MN_WGRAD_XT) {
           const int rs = cj < lim ? cj / a.C : 0;
           cc[j] = cj - rs * a.C;
           cr[j] = rs / a.S;
           cs[j] = rs - cr[j] * a.S;
         }
+        if constexpr (KIND == MN_WGRAD_XT) {
+          rk[j] = r0;
+          xt_init(a, j, r0, cj < lim);
+        }
       }
     }
+  }
+
+  // MN_WGRAD_XT: k-row r of a tile = pixel k0 + r with k0 % 64 == 0; under the kind's condition its
+  // image is n0 + r / PQ and its (p, q) = (p0 + (r % PQ) / Q, (r % PQ) % Q), with (n0, p0) uniform per
+  // k-tile.  base[j] = the element offset of (r / PQ, iy - p0 sh, ix, c) relative to image n0;
+  // cr[j] = that row's iy without the tile's p0 sh (FAR when the column or ix is out of range).
+  __device__ __forceinline__ void xt_init(const IgemmArgs& a, int j, int r, bool colok) {
+    const int PQ = a.P * a.Q;
+    const int nr = r / PQ, pq = r - nr * PQ, p = pq / a.Q, q = pq - p * a.Q;
+    const int iyc = p * a.sh - a.ph + cr[j] * a.dh, ix = q * a.sw - a.pw + cs[j] * a.dw;
+    const bool ok = colok && (unsigned)ix < (unsigned)a.W;
+    base[j] = ((nr * a.H + iyc) * a.W + ix) * a.C + cc[j];
+    cr[j] = ok ? iyc : -(1 << 28);
+    asm volatile("" : "+v"(base[j]), "+v"(cr[j]));  // keep them as values (no re-derivation per k-tile)
   }
 
   // byte offsets of this thread's NP 16-B pieces of k-tile k0 (BAD = zero fill)
@@ -236,6 +279,17 @@ struct Loader {
         for (int i = 0; i < NP; ++i) {
           const uint32_t o = (uint32_t)(base[i] + k) * 2u;
           off[i] = (kok & (ctx0[i] >= 0)) ? o : BAD;
+        }
+      } else if constexpr (KIND == KM_FWD_XT) {
+        // one tap per k-tile (C % 64 == 0): tap, channel base and the tap's element offset are uniform --
+        // scalar math on k0; per piece a mask bit and one add (K % 64 == 0: the k bound is uniform too)
+        const int tap = a.fd_C.div(k0), cb = k0 - tap * a.C, r = a.fd_S.div(tap), s = tap - r * a.S;
+        const int dk = ((r * a.dh) * a.W + s * a.dw) * a.C + cb;
+        const bool kok0 = k0 < kend;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const bool ok = kok0 & (((uint32_t)ctx0[i] >> tap) & 1u);
+          off[i] = ok ? (uint32_t)(base[i] + dk) * 2u : BAD;
         }
       } else if constexpr (KIND == KM_FWD_X) {
         const int rs = a.fd_C.div(k), c = k - mul24(rs, a.C), r = a.fd_S.div(rs), s = rs - mul24(r, a.S);
@@ -279,6 +333,12 @@ struct Loader {
           const int tap = mul24(a.cr0 + 2 * ri, a.wS) + a.cs0 + 2 * si;
           const int e0 = mul24(ko, a.wR * a.wS * a.C) + mul24(tap, a.C);
           off[j] = ok ? (uint32_t)(e0 + col[j]) * 2u : BAD;
+        } else if constexpr (KIND == MN_WGRAD_XT) {
+          const int n0 = a.fd_PQ.div(k0), p0 = a.fd_Q.div(k0 - n0 * a.P * a.Q);  // uniform
+          const int dys = p0 * a.sh, U = (n0 * a.H + dys) * a.W * a.C;
+          const int iy = cr[j] + dys;
+          const bool in = (k < kend) & ((unsigned)iy < (unsigned)a.H);
+          off[j] = in ? (uint32_t)(base[j] + U) * 2u : BAD;
         } else {  // MN_WGRAD_X
           const int PQ = a.P * a.Q;
           const int n = a.fd_PQ.div(k), pq = k - mul24(n, PQ), p = a.fd_Q.div(pq), q = pq - mul24(p, a.Q);
@@ -308,6 +368,15 @@ struct Loader {
         const int e0 = mul24(ko, a.wR * a.wS * a.C) + mul24(tap, a.C);
 #pragma unroll
         for (int j = 0; j < NP; ++j) off[j] = (kok & (col[j] >= 0)) ? (uint32_t)(e0 + col[j]) * 2u : BAD;
+      } else if constexpr (KIND == MN_WGRAD_XT) {
+        const int n0 = a.fd_PQ.div(k0), p0 = a.fd_Q.div(k0 - n0 * a.P * a.Q);  // uniform
+        const int dys = p0 * a.sh, U = (n0 * a.H + dys) * a.W * a.C;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+          const int iy = cr[j] + dys;
+          const bool in = kok & ((unsigned)iy < (unsigned)a.H);
+          off[j] = in ? (uint32_t)(base[j] + U) * 2u : BAD;
+        }
       } else {  // MN_WGRAD_X: pixel (n, p, q) of k, then per chunk its (r, s, c) tap
         const int PQ = a.P * a.Q;
         const int n = a.fd_PQ.div(k), pq = k - mul24(n, PQ), p = a.fd_Q.div(pq), q = pq - mul24(p, a.Q);
@@ -657,7 +726,9 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
 
   if constexpr (GL) {
     constexpr int NPT = LA::NP + LB::NP;  // LDS-DMA pieces per thread per k-tile
-    const int wv = t >> 6;
+    // the wave index as a scalar: every LDS-DMA destination (M0) is then computed once in SGPRs
+    // instead of a v_readfirstlane per piece and k-tile
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     // stage images of group G, stage S (compile-time: each read / DMA names its array directly)
     auto img_a = [&](auto G, auto S) -> char* {
       constexpr int g = decltype(G)::value, st = decltype(S)::value;
@@ -1313,6 +1384,9 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   constexpr int STAGE_B = (BM + BN) * BKT * 2;
   constexpr int G3 = KS * 3 * STAGE_B <= 163840 ? 3 : 2;
   const int gls = (g_tc.gls >= 0 && !a.a_scale) ? g_tc.gls : 0;  // the A transform is register-path only
+  // the general im2col gathers (C % 64 != 0 / pixel tiles crossing image rows: LeNet, odd stems) run the
+  // register pipeline only
+  if constexpr (AK != KM_FWD_X && AK != MN_WGRAD_X && BK != MN_WGRAD_X) {
   if (gls > 0) {
     // LDS-DMA ring: single k-tile -> GLS 1; otherwise the deepest ring (<= 3) that fits the LDS
     const bool single = nkt == 1 && splits == 1;
@@ -1329,6 +1403,7 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
     }
 #undef TFX_GL_LAUNCH
     return;
+  }
   }
   if constexpr (KS == 2) {
     if constexpr (EPI != EPI_PLAIN) {

@@ -96,3 +96,53 @@ def test_resnet50_trains_synthetic_cifar(gpu):
             correct += float(ops.accuracy(m(x, training=False), y)) * len(y)
     acc = correct / len(xte)
     assert acc > 0.5, (acc, losses[::10])
+
+
+def _bn_workspaces(model):
+    from tensorflow_examples_amd.models.resnet import _BN
+    out = []
+    for name, obj in _walk(model):
+        if isinstance(obj, _BN) and obj.ws.buf is not None:
+            out.append((name, obj.ws.buf))
+    return out
+
+
+def _walk(obj, prefix="model", seen=None):
+    seen = set() if seen is None else seen
+    if id(obj) in seen:
+        return
+    seen.add(id(obj))
+    yield prefix, obj
+    for k, v in list(getattr(obj, "__dict__", {}).items()):
+        if isinstance(v, list):
+            for i, e in enumerate(v):
+                if hasattr(e, "__dict__"):
+                    yield from _walk(e, "%s.%s[%d]" % (prefix, k, i), seen)
+        elif hasattr(v, "__dict__") and type(v).__module__.startswith("tensorflow_examples_amd.models"):
+            yield from _walk(v, "%s.%s" % (prefix, k), seen)
+
+
+@pytest.mark.parametrize("graphed", [False, True], ids=["eager", "graphed"])
+def test_resnet50_no_state_leaks_across_steps(gpu, graphed):
+    """Steps at learning rate 0 (weights frozen) on one batch must produce the same loss and gradients
+    every time: every BN slot workspace is zero again after a step (a fused kernel that leaves partial
+    sums behind corrupts the NEXT step's statistics -- invisible to single-step tests)."""
+    st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=1)
+    opt = MomentumOptimizer(st, 0.0, momentum=0.9)
+    tr = ClassifierTrainer(st, m, opt)
+    g = torch.Generator().manual_seed(3)
+    img = torch.randint(0, 256, (256, 32, 32, 3), dtype=torch.uint8, generator=g).to(gpu)
+    lab = torch.randint(0, 10, (256,), generator=g).to(gpu)
+    x = to_model_input(img)
+    if graphed:
+        tr.capture(x, lab, warmup=2)
+    losses, grads = [], []
+    for _ in range(3):
+        losses.append(float(tr.step(x, lab)))
+        torch.cuda.synchronize()
+        grads.append(st.grad.clone())
+        dirty = [(n, float(b.abs().max())) for n, b in _bn_workspaces(m) if float(b.abs().max()) != 0.0]
+        assert not dirty, dirty[:8]
+    for i in (1, 2):
+        rel = ((grads[i] - grads[0]).norm() / grads[0].norm()).item()
+        assert abs(losses[i] - losses[0]) < 1e-4 * abs(losses[0]) + 1e-5 and rel < 5e-3, (i, losses, rel)
