@@ -41,6 +41,9 @@ flags.DEFINE_string("logdir", "", "checkpoint directory (resume from the latest 
 flags.DEFINE_integer("synthetic_train", 50000, "synthetic training-set size when no data is found")
 flags.DEFINE_integer("eval_examples", 0, "evaluate on the first N test images (0 = all)")
 flags.DEFINE_integer("seed", 0, "weight-initialisation seed (also offsets the data shuffle)")
+flags.DEFINE_boolean("zero_init_residual", True, "start every residual branch's last BN at gamma = 0 (identity blocks "
+                     "at init; --nozero_init_residual for the plain random init)")
+flags.DEFINE_integer("warmup_steps", 50, "linear learning-rate warm-up over the first N steps (0 = none)")
 flags.DEFINE_boolean("graph", True, "GPU: capture the training step (forward, backward with the bucketed RCCL "
                      "all-reduces, optimizer) in a HIP graph on the first batch and replay it (the capture's "
                      "warm-up trains on that batch 3 extra times); --nograph runs eager launches")
@@ -59,7 +62,8 @@ def main(_):
     xtr, ytr, xte, yte, synth = load_cifar10(FLAGS.data_dir or None, synthetic_train=FLAGS.synthetic_train)
     if rank == 0:
         print("CIFAR-10 %s: %d train / %d test" % ("synthetic" if synth else "binary", len(xtr), len(xte)))
-    store, model = build_resnet_cifar(device=dev, depth=FLAGS.depth, dtype=dtype, seed=FLAGS.seed)
+    store, model = build_resnet_cifar(device=dev, depth=FLAGS.depth, dtype=dtype, seed=FLAGS.seed,
+                                      zero_init_residual=FLAGS.zero_init_residual)
     opt = MomentumOptimizer(store, FLAGS.learning_rate * world, momentum=0.9, weight_decay=FLAGS.weight_decay)
     start_step = 0
     if FLAGS.logdir and latest_checkpoint(FLAGS.logdir):
@@ -80,6 +84,8 @@ def main(_):
         src = batches([xtr[shard], ytr[shard]], FLAGS.batch_size, seed=ep * 1000 + rank + 7919 * FLAGS.seed)
         for img, lab in DevicePrefetcher(src, dev):
             lr = FLAGS.learning_rate * world * (0.1 ** sum(step >= b for b in bounds))
+            if FLAGS.warmup_steps and step < FLAGS.warmup_steps:
+                lr *= (step + 1) / FLAGS.warmup_steps
             opt.set_learning_rate(lr)  # a device scalar: a replayed graph reads the new value
             x = augment_model_input(img, dtype)  # crop + flip + normalise: one fused kernel on the GPU
             if want_graph:
