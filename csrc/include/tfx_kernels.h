@@ -68,6 +68,9 @@ struct IgemmArgs {
   int relu = 0;
   // optional per-column BN statistics of the (bf16-rounded) output: [NSLOT][2][N] f32, pre-zeroed
   float* stats = nullptr;
+  // rows of `stats` the epilogue adds into (tile row tm -> row tm % stat_slots): NSLOT, or fewer for
+  // a BN whose finalize is folded into its apply (bn_apply_fin reads only these rows per block)
+  int stat_slots = NSLOT;
   FastDiv fd_C, fd_S, fd_Ko, fd_PQ, fd_Q;
   int zero_out = 1;
   // MODE_DGRAD_CLS: one output-parity class (cph, cpw) of a stride-2 data gradient.  The GEMM rows
@@ -245,6 +248,12 @@ void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float
 void bn_slot_reduce(float* slots, int C, float* red, float* dgamma, float* dbeta, hipStream_t s);
 void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
                   const float* run_var, float* save, hipStream_t s);
+// the apply with the finalize folded in (bn_apply_fin_kernel): statistics in the first nsl (<= 16)
+// rows of slots ([NSLOT][2][C] + an int counter after them), re-zeroed by the last block
+bool bn_apply_fin_ok(int C);
+void bn_apply_fin(const uint16_t* x, const uint16_t* res, float* slots, int nsl, int64_t M, int C, const float* gamma,
+                  const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* save,
+                  bool relu, uint16_t* y, uint8_t* mask, hipStream_t s);
 // mask (optional, residual + ReLU on the C % 8 == 0 path): 1 bit per element, the ReLU mask of y
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
               uint16_t* y, uint8_t* mask, hipStream_t s);

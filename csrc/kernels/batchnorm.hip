@@ -272,6 +272,149 @@ __global__ void __launch_bounds__(256) bn_apply_gen_kernel(const uint16_t* __res
   }
 }
 
+// ------------------------------------------------------------------ apply with the finalize folded in
+// The producing conv's epilogue added the batch statistics into the first `nsl` (<= 16) slot rows
+// (IgemmArgs stat_slots).  Instead of a separate finalize launch (a dependent ~5 us launch per BN
+// layer, most of them on stage-3/4 tensors that the apply streams in a few us), every block of the
+// apply reduces those rows itself in its prologue -- nsl x 2C floats, L2-resident after the first
+// block of an XCD -- and keeps scale / shift in LDS.  Block 0 writes save = [mean|invstd|scale|shift]
+// (the backward reads it) and the running statistics.  The slot rows are re-zeroed by the LAST block
+// to finish reading them: each block bumps a counter (an int after the [NSLOT][2][C] rows) once its
+// slot loads have returned -- they are consumed before the barrier that precedes the add -- and the
+// block that reads grid-1 back zeroes the rows and the counter at its end, after its own apply
+// (the add's round trip overlaps the whole apply).  KM = ceil(nsl / threads-per-vector) load
+// rounds per thread, unrolled (a runtime loop would serialise the round trips).
+template <bool RES, bool RELU, int KM>
+__global__ void __launch_bounds__(256) bn_apply_fin_kernel(const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ res, float* __restrict__ slots,
+                                                           int nsl, int64_t M, int C, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float eps, float momentum,
+                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                           float* __restrict__ save, int64_t nvec,
+                                                           uint16_t* __restrict__ y, uint8_t* __restrict__ mask) {
+  __shared__ __attribute__((aligned(16))) float part[256 * 16];  // [thread][sum 8 | sq 8]
+  __shared__ __attribute__((aligned(16))) float ssc[2048], ssh[2048];
+  __shared__ int s_last;
+  const int t = threadIdx.x;
+  const int nv = C >> 3;    // channel vectors, 256 % nv == 0 (host)
+  const int tpv = 256 / nv;  // threads per vector
+  const int v = t % nv, pr = t / nv;
+  int* counter = reinterpret_cast<int*>(slots + (size_t)NSLOT * 2 * C);
+  // parameter / running-stat loads first: one memory round trip for the whole prologue
+  const int cv = v * 8;
+  float g8[8], b8[8], rm8[8], rv8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    g8[k] = gamma ? gamma[cv + k] : 1.f;
+    b8[k] = beta ? beta[cv + k] : 0.f;
+    rm8[k] = run_mean ? run_mean[cv + k] : 0.f;
+    rv8[k] = run_var ? run_var[cv + k] : 0.f;
+  }
+  float ps[8], pq[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ps[k] = pq[k] = 0.f;
+  {
+    float4 ld[KM][4];
+    float wt[KM];
+#pragma unroll
+    for (int i = 0; i < KM; ++i) {
+      const int s = pr + i * tpv;
+      wt[i] = s < nsl ? 1.f : 0.f;  // rows past nsl: clamped, weighted out (no branch around loads)
+      const float* p = slots + (size_t)min(s, nsl - 1) * 2 * C + cv;
+      ld[i][0] = *reinterpret_cast<const float4*>(p);
+      ld[i][1] = *reinterpret_cast<const float4*>(p + 4);
+      ld[i][2] = *reinterpret_cast<const float4*>(p + C);
+      ld[i][3] = *reinterpret_cast<const float4*>(p + C + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < KM; ++i) {
+      const float a[8] = {ld[i][0].x, ld[i][0].y, ld[i][0].z, ld[i][0].w, ld[i][1].x, ld[i][1].y, ld[i][1].z, ld[i][1].w};
+      const float b[8] = {ld[i][2].x, ld[i][2].y, ld[i][2].z, ld[i][2].w, ld[i][3].x, ld[i][3].y, ld[i][3].z, ld[i][3].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ps[k] = fmaf(a[k], wt[i], ps[k]);
+        pq[k] = fmaf(b[k], wt[i], pq[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    part[t * 16 + k] = ps[k];
+    part[t * 16 + 8 + k] = pq[k];
+  }
+  __syncthreads();
+  if (pr == 0) {
+    for (int j = 1; j < tpv; ++j) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ps[k] += part[(j * nv + v) * 16 + k];
+        pq[k] += part[(j * nv + v) * 16 + 8 + k];
+      }
+    }
+    const float inv_m = 1.f / (float)M;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = cv + k;
+      const float mean = ps[k] * inv_m;
+      const float var = fmaxf(pq[k] * inv_m - mean * mean, 0.f);
+      const float invstd = rsqrtf(var + eps);
+      const float sc = g8[k] * invstd, sh = b8[k] - mean * sc;
+      ssc[c] = sc;
+      ssh[c] = sh;
+      if (blockIdx.x == 0) {
+        save[c] = mean;
+        save[C + c] = invstd;
+        save[2 * C + c] = sc;
+        save[3 * C + c] = sh;
+        if (run_mean) {
+          const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+          run_mean[c] = (1.f - momentum) * rm8[k] + momentum * mean;
+          run_var[c] = (1.f - momentum) * rv8[k] + momentum * unb;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // every thread's slot loads were consumed before the barrier above: this block is done reading
+  int old = 0;
+  if (t == 0) old = atomicAdd(counter, 1);
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = ssc[cv + k];
+    sh[k] = ssh[cv + k];
+  }
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + t;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  auto one = [&](int64_t i) {
+    float f[8], r[8];
+    unpack8(reinterpret_cast<const U4*>(x)[i], f);
+    if (RES) unpack8(reinterpret_cast<const U4*>(res)[i], r);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float z = fmaf(f[k], sc[k], sh[k]);
+      if (RES) z += r[k];
+      bits |= (z > 0.f ? 1u : 0u) << k;
+      f[k] = RELU ? fmaxf(z, 0.f) : z;
+    }
+    reinterpret_cast<U4*>(y)[i] = pack8(f);
+    if (RES && RELU && mask) mask[i] = (uint8_t)bits;
+  };
+  int64_t i = i0;
+  for (; i + stride < nvec; i += 2 * stride) {
+    one(i);
+    one(i + stride);
+  }
+  if (i < nvec) one(i);
+  if (t == 0) s_last = old == (int)gridDim.x - 1;
+  __syncthreads();
+  if (s_last) {
+    for (int e = t; e < nsl * 2 * C / 4; e += 256) reinterpret_cast<float4*>(slots)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t == 0) *counter = 0;
+  }
+}
+
 // ------------------------------------------------------------------ backward reduce
 // RES && RELU: the ReLU mask comes from the forward's mask bits (``mask``, one byte per vector)
 template <bool RES, bool RELU, int U>
@@ -560,6 +703,35 @@ void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t
     const int g = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_apply_gen_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, n, C, y)));
   }
+}
+
+bool bn_apply_fin_ok(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0; }
+
+// grid cap of the folded apply: every block re-reads the nsl x 2C slot floats (L2 hits after the
+// first block per XCD), so fewer, fatter blocks than bn_apply's (4 vectors per thread, <= 4096):
+// at most g_fin_grid, and at most ~16 MB of prologue reads over the grid (>= 128 blocks)
+int g_fin_grid = 512;
+
+void bn_apply_fin(const uint16_t* x, const uint16_t* res, float* slots, int nsl, int64_t M, int C, const float* gamma,
+                  const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* save,
+                  bool relu, uint16_t* y, uint8_t* mask, hipStream_t s) {
+  const int64_t nvec = M * C / 8;
+  int cap = (int)((16ll << 20) / ((int64_t)nsl * 8 * C));
+  cap = cap < 128 ? 128 : (cap > g_fin_grid ? g_fin_grid : cap);
+  const int g0 = fixed_channel_grid(nvec, C), g = g0 < cap ? g0 : cap;  // C/8 divides 256: any grid keeps the channel period
+  const int tpv = 256 / (C / 8);
+  const int km = (nsl + tpv - 1) / tpv;
+  const bool has_res = res != nullptr;
+#define TFX_FIN_LAUNCH(KM_)                                                                                    \
+  TFX_DISPATCH_RR(has_res, relu, (bn_apply_fin_kernel<R_, L_, KM_><<<g, 256, 0, s>>>(                        \
+                                     x, res, slots, nsl, M, C, gamma, beta, eps, momentum, run_mean, run_var, save, \
+                                     nvec, y, mask)))
+  if (km <= 1) { TFX_FIN_LAUNCH(1); }
+  else if (km <= 2) { TFX_FIN_LAUNCH(2); }
+  else if (km <= 4) { TFX_FIN_LAUNCH(4); }
+  else if (km <= 8) { TFX_FIN_LAUNCH(8); }
+  else { TFX_FIN_LAUNCH(16); }
+#undef TFX_FIN_LAUNCH
 }
 
 void bn_apply_res_bn(const uint16_t* x, const uint16_t* res_x, const float* save, const float* res_save, int64_t M,

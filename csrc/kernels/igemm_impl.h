@@ -1184,7 +1184,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
         if (t < BN) {
           const int nn = n0 + t;
           if (nn < a.N) {
-            float* slot = (bnb ? a.bnb_slots : a.stats) + (size_t)(tm % NSLOT) * 2 * a.N;
+            float* slot = (bnb ? a.bnb_slots : a.stats) + (size_t)(tm % (bnb ? NSLOT : a.stat_slots)) * 2 * a.N;
             atomicAdd(&slot[nn], red[t * 2] + red[(BN + t) * 2]);
             atomicAdd(&slot[a.N + nn], red[t * 2 + 1] + red[(BN + t) * 2 + 1]);
           }

@@ -271,6 +271,67 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   return {y, save};
 }
 
+// conv_fwd_bn without the finalize: the epilogue adds the statistics into the first stat_slots rows of
+// ws and the BN's apply finalizes them itself (bn_apply_fin_into), or bn_finalize_into does when the
+// consumer cannot.  Always the implicit GEMM (never the stem route).  Returns y.
+Tensor conv_fwd_bn_nofin(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor ws, int64_t stat_slots) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
+  TORCH_CHECK(stat_slots >= 1 && stat_slots <= 16, "conv_fwd_bn_nofin: 1..16 statistics rows");
+  auto g = geom(x.sizes().vec(), w.sizes().vec(), stride, pad, dil);
+  auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
+  auto a = conv_args(g, stride, pad, dil);
+  a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
+  a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
+  a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
+  a.out_mode = tfx::OUT_BF16;
+  check_bn_ws(ws, g.Ko);
+  a.stats = ws.data_ptr<float>();
+  a.stat_slots = (int)stat_slots;
+  tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
+  return y;
+}
+
+// the finalize of a conv_fwd_bn_nofin (its statistics rows re-zeroed): fills save = [mean|invstd|scale|shift]
+void bn_finalize_into(Tensor ws, int64_t M, optional<Tensor> gamma, optional<Tensor> beta, optional<Tensor> run_mean,
+                      optional<Tensor> run_var, double momentum, double eps, Tensor save) {
+  CHECK_F32(save); CHECK_CONTIG(save);
+  const int64_t C = save.numel() / 4;
+  check_bn_ws(ws, C);
+  tfx::bn_finalize(ws.data_ptr<float>(), M, (int)C, fp(gamma), fp(beta), (float)eps, (float)momentum,
+                   fpm(run_mean), fpm(run_var), save.data_ptr<float>(), cur_stream());
+}
+
+// BN apply (out = relu?(x sc + sh (+ res)), mask bits with res) with the finalize folded in: scale /
+// shift from the first nsl statistics rows of ws (conv_fwd_bn_nofin), save and the running stats
+// written by block 0, the rows and the counter after [NSLOT][2][C] re-zeroed by the last block.
+bool bn_apply_fin_supported(int64_t C) { return tfx::bn_apply_fin_ok((int)C); }
+
+void bn_apply_fin_into(Tensor x, optional<Tensor> res, Tensor ws, int64_t nsl, optional<Tensor> gamma,
+                       optional<Tensor> beta, optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
+                       double eps, bool relu, Tensor save, Tensor out, optional<Tensor> mask) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(out); CHECK_CONTIG(out);
+  CHECK_F32(ws); CHECK_CONTIG(ws); CHECK_F32(save); CHECK_CONTIG(save);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(tfx::bn_apply_fin_ok((int)C) && out.numel() == x.numel() && save.numel() == 4 * C,
+              "bn_apply_fin_into: shapes");
+  TORCH_CHECK(nsl >= 1 && nsl <= 16, "bn_apply_fin_into: 1..16 statistics rows");
+  TORCH_CHECK(ws.numel() >= tfx::NSLOT * 2 * C + 4, "bn_apply_fin_into: workspace lacks the counter word");
+  const uint16_t* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    CHECK_BF16(*res); CHECK_CONTIG(*res);
+    TORCH_CHECK(res->numel() == x.numel(), "bn_apply_fin_into: residual");
+    r = bf(*res);
+  }
+  uint8_t* mk = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(r && relu && mask->numel() * 8 == x.numel(), "bn_apply_fin_into: mask");
+    mk = mask->data_ptr<uint8_t>();
+  }
+  tfx::bn_apply_fin(bf(x), r, ws.data_ptr<float>(), (int)nsl, M, (int)C, fp(gamma), fp(beta), (float)eps,
+                    (float)momentum, fpm(run_mean), fpm(run_var), save.data_ptr<float>(), relu, bfm(out), mk,
+                    cur_stream());
+}
+
 // A/B hook for the stem forward kernel; returns the previous setting
 bool conv_stem_fwd(bool on) {
   const bool prev = g_stem_fwd;
@@ -1782,6 +1843,10 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);
+  m.def("conv_fwd_bn_nofin", &conv_fwd_bn_nofin);
+  m.def("bn_finalize_into", &bn_finalize_into);
+  m.def("bn_apply_fin_supported", &bn_apply_fin_supported);
+  m.def("bn_apply_fin_into", &bn_apply_fin_into);
   m.def("conv_fwd_bn_in", &conv_fwd_bn_in);
   m.def("stem_wgrad", &stem_wgrad);
   m.def("conv_stem_fwd", &conv_stem_fwd);

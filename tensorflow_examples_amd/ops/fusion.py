@@ -25,6 +25,9 @@ conv3_fused_bwd        stage-1 3x3 conv backward in one launch (conv3x3_bwd_fuse
 stem_kernels           CIFAR stem forward / weight gradient (stem.hip)              generic implicit GEMM
 fused_head             pool + FC + softmax-xent + input gradient (head.hip)         three composed ops
 head_tail              last tail BN applied inside the fused head (TAIL mode)       bn_apply before the head
+bn_finalize_fold       stage 2-4 BN finalize inside the layer-wise apply: every     bn_finalize launch after the
+                       block reduces the conv epilogue's few statistics rows         conv (conv_fwd_bn)
+                       itself, the last one re-zeroes them (bn_apply_fin)
 =====================  ==========================================================  ===============================
 
 ``TFX_FUSION`` selects a profile at import: ``all`` (default), ``r2`` (the round-2 level: epilogue
@@ -39,7 +42,8 @@ from collections import Counter, OrderedDict
 from typing import Dict, Iterable, List, Optional, Tuple
 
 GROUPS = ("bn_epilogue", "grad_sink", "masked_res", "s2_addend", "deferred_slot_reduce", "block_boundary_fwd",
-          "bn_on_load", "lazy_bn_bwd", "conv3_fused_bwd", "stem_kernels", "fused_head", "head_tail")
+          "bn_on_load", "lazy_bn_bwd", "conv3_fused_bwd", "stem_kernels", "fused_head", "head_tail",
+          "bn_finalize_fold")
 PROFILES = {
     "all": set(GROUPS),
     "r2": {"bn_epilogue", "grad_sink", "masked_res", "s2_addend", "deferred_slot_reduce", "fused_head"},
@@ -64,6 +68,7 @@ def _bind() -> Dict[str, List[Tuple[object, str]]]:
         "stem_kernels": [(nn, "_STEM_WGRAD")],
         "fused_head": [(nn, "_FUSE_HEAD")],
         "head_tail": [(nn, "_HEAD_TAIL")],
+        "bn_finalize_fold": [(nn, "_FOLD_FIN")],
     }
 
 

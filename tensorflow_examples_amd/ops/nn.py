@@ -133,6 +133,10 @@ _DEFER_TAIL = True
 _DEFER_BN_IN = True
 _FUSE_CONV3_BWD = True  # False: the stage-1 3x3 conv's backward runs layer-wise (forward still fused)
 PW_SQUEEZE_CALLS = [0]  # fused tail + conv1 forward launches (tests)
+# finalize folded into the layer-wise apply (bn_apply_fin): stage 2-4 BN layers (M <= 65536 rows)
+_FOLD_FIN = True
+FOLD_FIN_CALLS = [0]  # applies that finalized their own statistics (tests)
+_FOLD_FIN_MAX_ROWS = 65536
 
 
 class TailPending:
@@ -143,15 +147,32 @@ class TailPending:
     on load WITHOUT writing it (conv3x3_fwd_fused) -- whatever reads ``out`` later (that conv's
     weight gradient) calls :meth:`materialize` (bn_apply_into), as does any consumer that cannot fuse.
     Everything that reads ``out`` runs after that conv in the block's forward order."""
-    __slots__ = ("x", "save", "res", "res_save", "out", "mask", "done")
+    __slots__ = ("x", "save", "res", "res_save", "out", "mask", "done", "fin")
 
-    def __init__(self, x, save, res, res_save, out, mask):
+    def __init__(self, x, save, res, res_save, out, mask, fin=None):
         self.x, self.save, self.res, self.res_save, self.out, self.mask = x, save, res, res_save, out, mask
         self.done = False
+        # the BNWorkspace whose finalize is still owed (conv_fwd_bn_nofin): ``save`` is unwritten until
+        # the apply runs it in-kernel (materialize) or a fused consumer calls ensure_fin first
+        self.fin = fin
+
+    def ensure_fin(self) -> None:
+        if self.fin is not None:
+            self.fin.settle_fin(self.save)
+            self.fin = None
 
     def materialize(self) -> None:
         if not self.done:
-            torch.ops.tfx.bn_apply_into(self.x, self.res, self.save, self.res_save, self.out, self.mask)
+            ws = self.fin
+            if ws is not None and ws.fin is not None and self.res_save is None:
+                torch.ops.tfx.bn_apply_fin_into(self.x, self.res, ws.buf, ws.fin[1], *ws.finalize_args,
+                                                True, self.save, self.out, self.mask)
+                ws.fin = None
+                self.fin = None
+                FOLD_FIN_CALLS[0] += 1
+            else:
+                self.ensure_fin()
+                torch.ops.tfx.bn_apply_into(self.x, self.res, self.save, self.res_save, self.out, self.mask)
             self.done = True
 
 
@@ -272,6 +293,15 @@ def _pw_squeeze_bwd_ok(x, w, stride, pad, dil, lazy, sink, bnb) -> bool:
     return bool(torch.ops.tfx.pw_bwd_squeeze_supported(sh[3], sh[0], x.numel() // sh[3]))
 
 
+def _conv_rows(x, w, stride, pad, dil) -> int:
+    """Output pixels N*P*Q of an NHWC conv (the GEMM's M)."""
+    n, h, wd = x.shape[0], x.shape[1], x.shape[2]
+    r, s_ = w.shape[1], w.shape[2]
+    p = (h + 2 * pad - dil * (r - 1) - 1) // stride + 1
+    q = (wd + 2 * pad - dil * (s_ - 1) - 1) // stride + 1
+    return n * p * q
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, w: Variable, stride, pad, dil, stats_into, sink, bnb):
@@ -287,6 +317,7 @@ class _Conv2d(torch.autograd.Function):
                     # BN + ReLU of the input applied on load, 3x3 conv from a halo tile, the output
                     # BN's statistics (conv3x3_fused.hip); x stays unwritten until something reads it
                     ws = stats_into
+                    tp.ensure_fin()
                     y, ws.pending_save = torch.ops.tfx.conv3x3_fwd_fused(tp.x, tp.save, w.value, ws.get(x.device),
                                                                          *ws.finalize_args)
                     ctx.pending_in = tp
@@ -297,6 +328,7 @@ class _Conv2d(torch.autograd.Function):
                     # a plain ReLU BN applied on load by this single-k-tile 1x1 conv (igemm a_scale):
                     # x stays unwritten (the fused backward forms it on load too)
                     ws = stats_into
+                    tp.ensure_fin()
                     y, ws.pending_save = torch.ops.tfx.conv_fwd_bn_in(tp.x, tp.save, w.value, ws.get(x.device),
                                                                       *ws.finalize_args)
                     ctx.pending_in = tp
@@ -307,21 +339,36 @@ class _Conv2d(torch.autograd.Function):
                     # the previous block's tail apply + this conv + its BN statistics in one launch:
                     # x (and the tail's mask bits) are written here (pw_fwd.hip)
                     ws = stats_into
+                    tp.ensure_fin()
                     y, ws.pending_save = torch.ops.tfx.pw_fwd_squeeze(
                         tp.x, tp.save, tp.res, tp.res_save, w.value, x, tp.mask, ws.get(x.device), *ws.finalize_args)
                     tp.done = True
                     PW_SQUEEZE_CALLS[0] += 1
                     fusion.note("block_boundary_fwd", w.name, "pw_fwd_squeeze")
                     return y
-                fusion.note("layerwise", w.name, "bn_apply_into")
+                if tp.fin is not None and tp.res_save is None:
+                    fusion.note("bn_finalize_fold", w.name, "bn_apply_fin")
+                else:
+                    fusion.note("layerwise", w.name, "bn_apply_into")
                 tp.materialize()
             if isinstance(stats_into, BNWorkspace):
                 ws = stats_into
+                stem = _STEM_WGRAD and _stem_ok(x, w, stride, pad, dil)
+                m_out = _conv_rows(x, w, stride, pad, dil)
+                if _FOLD_FIN and not stem and m_out <= _FOLD_FIN_MAX_ROWS and \
+                        torch.ops.tfx.bn_apply_fin_supported(w.shape[0]):
+                    # epilogue statistics into a few slot rows; the finalize is owed (ws.fin) -- the
+                    # BN's apply runs it in-kernel, or ws.settle_fin launches it for other consumers
+                    nsl = max(1, min(16, m_out // 4096))
+                    y = torch.ops.tfx.conv_fwd_bn_nofin(x.contiguous(), w.value, stride, pad, dil, ws.get(x.device), nsl)
+                    ws.pending_save = torch.empty(4 * w.shape[0], dtype=torch.float32, device=x.device)
+                    ws.fin = (m_out, nsl)
+                    fusion.note("bn_epilogue", w.name, "igemm_fwd_stats")
+                    return y
                 # epilogue statistics, then the finalize: the BN only applies
                 y, ws.pending_save = torch.ops.tfx.conv_fwd_bn(x.contiguous(), w.value, stride, pad, dil,
                                                                ws.get(x.device), *ws.finalize_args)
-                fusion.note("bn_epilogue", w.name, "stem_fwd" if (_STEM_WGRAD and _stem_ok(x, w, stride, pad, dil))
-                            else "igemm_fwd_stats")
+                fusion.note("bn_epilogue", w.name, "stem_fwd" if stem else "igemm_fwd_stats")
                 return y
             if stats_into is not None:
                 fusion.note("bn_epilogue", w.name, "igemm_fwd_stats_only")
@@ -562,13 +609,22 @@ class BNWorkspace:
         self.buf = None
         self.finalize_args = None
         self.pending_save = None
+        # (rows M, statistics rows nsl) while the finalize of a conv_fwd_bn_nofin is owed
+        self.fin = None
 
     def get(self, device) -> torch.Tensor:
         if self.buf is None or self.buf.device != device:
             if device.type == "cuda" and _native.use_native_device(device):
                 assert int(torch.ops.tfx.bn_nslot()) == self.NSLOT, "BNWorkspace.NSLOT != tfx::NSLOT"
-            self.buf = torch.zeros(self.NSLOT * 2 * self.c, dtype=torch.float32, device=device)
+            # + the folded apply's last-reader counter word (and padding), zero between uses too
+            self.buf = torch.zeros(self.NSLOT * 2 * self.c + 64, dtype=torch.float32, device=device)
         return self.buf
+
+    def settle_fin(self, save: torch.Tensor) -> None:
+        """Run the owed finalize (bn_finalize_into) into ``save``, if any."""
+        if self.fin is not None:
+            torch.ops.tfx.bn_finalize_into(self.buf, self.fin[0], *self.finalize_args, save)
+            self.fin = None
 
 
 class BNBackwardFusion:
@@ -717,16 +773,21 @@ class _BatchNorm(torch.autograd.Function):
                 res = torch.ops.tfx.bn_apply_train(res_bnb.x, None, res_bnb.save, False)[0]
             defer_out = defer and pending and res is None and bnb_out is not None and _vec_ok(x.shape[-1])
             if pending:
-                # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
+                # the producing conv's epilogue already finalized the statistics (conv_fwd_bn) -- or
+                # owes the finalize (wsobj.fin): a deferred apply takes it along, anything else runs it
                 save, wsobj.pending_save = wsobj.pending_save, None
+                owed = wsobj if wsobj.fin is not None else None
+                if owed is not None and not (defer_plain or (defer_tail and not fuse_res)):
+                    owed.settle_fin(save)
+                    owed = None
                 if defer_plain:
                     y = torch.empty_like(x)
-                    y._tfx_tail = TailPending(x, save, None, None, y, None)
+                    y._tfx_tail = TailPending(x, save, None, None, y, None, fin=owed)
                 elif defer_tail:
                     y = torch.empty_like(x)
                     mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
                     y._tfx_tail = TailPending(x, save, res_bnb.x if fuse_res else res.contiguous(),
-                                              res_bnb.save if fuse_res else None, y, mask)
+                                              res_bnb.save if fuse_res else None, y, mask, fin=owed)
                 elif fuse_res:
                     y, mask = torch.ops.tfx.bn_apply_res_bn(x, res_bnb.x, save, res_bnb.save, relu)
                 elif defer_out:
@@ -743,6 +804,7 @@ class _BatchNorm(torch.autograd.Function):
             # residual + ReLU: the backward needs only the 1-bit ReLU mask, not the residual tensor
             assert not fuse_res or mask is not None
             ctx.save_for_backward(x, None if mask is not None else res, save, mask)
+            ctx.tp = getattr(y, "_tfx_tail", None) if (defer_plain or defer_tail) and pending else None
             if training and bnb_out is not None and (res is None or not relu or mask is not None) \
                     and x.shape[-1] % 8 == 0:
                 train_p = gamma is not None and gamma.trainable
@@ -763,6 +825,8 @@ class _BatchNorm(torch.autograd.Function):
             x, res, save, mask = ctx.saved_tensors
             if not training:
                 raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
+            if ctx.tp is not None:  # a deferred apply nobody consumed still owes the finalize
+                ctx.tp.ensure_fin()
             if ctx.bnb is not None:
                 if ctx.bnb.sec_lazy is not None:  # the tail's conv3 has not run yet: reduce here
                     ctx.bnb.sec_lazy.materialize()
@@ -1227,6 +1291,7 @@ def _head_tail(feat):
         return None
     if bnb.deferred or bnb.red is not None or bnb.sr_pending or bnb.x is not tp.x:
         return None
+    tp.ensure_fin()  # the head reads save
     return tp, bnb
 
 

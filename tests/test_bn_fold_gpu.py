@@ -1,0 +1,115 @@
+"""The BN finalize folded into the layer-wise apply (bn_apply_fin_kernel, fusion group
+``bn_finalize_fold``): the conv epilogue adds its statistics into a few slot rows, every apply block
+reduces them itself, block 0 writes save + running statistics, the last block re-zeroes the rows and
+its counter.  Checked against the separate-finalize path (conv_fwd_bn + bn_apply_into) and an fp32
+reference of the BN, at stage 2-4 shapes, twice in a row (the counter and rows must be back to zero)."""
+import pytest
+import torch
+
+from tensorflow_examples_amd.models.resnet import _BN, build_resnet_cifar, to_model_input
+from tensorflow_examples_amd.ops import nn as tnn
+from tensorflow_examples_amd.optim import MomentumOptimizer
+from tensorflow_examples_amd.train import ClassifierTrainer
+
+pytestmark = pytest.mark.gpu
+
+NSLOT = 64
+
+
+@pytest.mark.parametrize("m,c,nsl,res", [(65536, 128, 16, False), (65536, 512, 16, True), (16384, 256, 4, False),
+                                         (16384, 1024, 4, True), (4096, 2048, 1, True), (4096, 512, 1, False),
+                                         (16384, 64, 16, False)])
+def test_bn_apply_fin_matches_finalize_then_apply(gpu, m, c, nsl, res):
+    g = torch.Generator().manual_seed(m + c)
+    k = 64
+    x = (torch.randn(m // 64, 8, 8, k, generator=g) * 2).to(gpu).bfloat16()
+    w = (torch.randn(c, 1, 1, k, generator=g) * 0.1).to(gpu).bfloat16()
+    r = torch.randn(m, c, generator=g).to(gpu).bfloat16() if res else None
+    gamma = (torch.rand(c, generator=g) + 0.5).to(gpu)
+    beta = (torch.randn(c, generator=g) * 0.1).to(gpu)
+    ref_rm, ref_rv = torch.zeros(c, device=gpu), torch.ones(c, device=gpu)
+    ws_ref = torch.zeros(NSLOT * 2 * c + 64, device=gpu)
+    y, save_ref = torch.ops.tfx.conv_fwd_bn(x, w, 1, 0, 1, ws_ref, gamma, beta, ref_rm, ref_rv, 0.1, 1e-5)
+    out_ref = torch.empty(m, c, device=gpu, dtype=torch.bfloat16)
+    mask_ref = torch.empty(m * c // 8, device=gpu, dtype=torch.uint8) if res else None
+    torch.ops.tfx.bn_apply_into(y.view(m, c), r, save_ref, None, out_ref, mask_ref)
+
+    ws = torch.zeros(NSLOT * 2 * c + 64, device=gpu)
+    rm, rv = torch.zeros(c, device=gpu), torch.ones(c, device=gpu)
+    for it in range(2):  # the second round checks the rows and the counter were left at zero
+        y2 = torch.ops.tfx.conv_fwd_bn_nofin(x, w, 1, 0, 1, ws, nsl)
+        assert torch.equal(y2, y)
+        save = torch.full((4 * c,), float("nan"), device=gpu)
+        out = torch.empty(m, c, device=gpu, dtype=torch.bfloat16)
+        mask = torch.empty(m * c // 8, device=gpu, dtype=torch.uint8) if res else None
+        torch.ops.tfx.bn_apply_fin_into(y2.view(m, c), r, ws, nsl, gamma, beta, rm, rv, 0.1, 1e-5, True, save, out,
+                                        mask)
+        torch.cuda.synchronize()
+        assert float(ws.abs().max()) == 0.0, "statistics rows / counter not re-zeroed"
+        torch.testing.assert_close(save, save_ref, rtol=2e-5, atol=2e-5)
+        # bf16 outputs: the same scale/shift up to f32 summation order -> at most 1 bf16 ulp apart
+        d = (out.float() - out_ref.float()).abs()
+        assert float((d > 1e-2 * (1 + out_ref.float().abs())).float().mean()) < 1e-4
+        if res:
+            assert float((mask != mask_ref).float().mean()) < 1e-4
+    # running statistics after two updates vs the fp32 BN of y
+    yf = y.view(m, c).float()
+    mean, var = yf.mean(0), yf.var(0, unbiased=True)
+    exp_rm = 0.1 * mean * (1 + 0.9)
+    exp_rv = 0.81 + 0.1 * var * (1 + 0.9)
+    torch.testing.assert_close(rm, exp_rm, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rv, exp_rv, rtol=1e-3, atol=1e-4)
+
+
+def test_resnet50_fold_matches_separate_finalize(gpu):
+    """One batch-256 ResNet-50 training step with the folded finalize vs with separate finalize
+    launches: same loss, same BN running statistics (f32 summation order only), every BN workspace zero
+    afterwards, and the folded apply actually ran for the stage 2-4 layers."""
+    img = torch.randint(0, 256, (256, 32, 32, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
+    lab = torch.randint(0, 10, (256,), generator=torch.Generator().manual_seed(6)).to(gpu)
+    out = {}
+    prev = tnn._FOLD_FIN
+    try:
+        for fold in (True, False):
+            tnn._FOLD_FIN = fold
+            st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=3)
+            tr = ClassifierTrainer(st, m, MomentumOptimizer(st, 0.0, momentum=0.9))
+            n0 = tnn.FOLD_FIN_CALLS[0]
+            loss = float(tr.step(to_model_input(img.to(gpu)), lab))
+            torch.cuda.synchronize()
+            calls = tnn.FOLD_FIN_CALLS[0] - n0
+            bns = _bns(m)
+            stats = {b.gamma.name: (b.mean.detach().clone(), b.var.detach().clone()) for b in bns}
+            dirty = [b.gamma.name for b in bns if b.ws.buf is not None and float(b.ws.buf.abs().max()) != 0.0]
+            out[fold] = (loss, calls, stats, dirty)
+    finally:
+        tnn._FOLD_FIN = prev
+    (l1, c1, s1, d1), (l0, c0, s0, d0) = out[True], out[False]
+    assert c0 == 0 and c1 >= 20, (c1, c0)
+    assert not d1 and not d0, (d1, d0)
+    assert abs(l1 - l0) <= 2e-3 * abs(l0), (l1, l0)
+    assert s1.keys() == s0.keys() and len(s1) > 0
+    for k in s1:
+        for a, b in zip(s1[k], s0[k]):
+            torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4, msg=k)
+
+
+def _bns(model):
+    seen, out = set(), []
+
+    def walk(o):
+        if id(o) in seen:
+            return
+        seen.add(id(o))
+        if isinstance(o, _BN):
+            out.append(o)
+            return
+        for v in list(getattr(o, "__dict__", {}).values()):
+            if isinstance(v, list):
+                for e in v:
+                    if hasattr(e, "__dict__"):
+                        walk(e)
+            elif hasattr(v, "__dict__") and type(v).__module__.startswith("tensorflow_examples_amd.models"):
+                walk(v)
+    walk(model)
+    return out
