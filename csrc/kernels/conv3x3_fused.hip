@@ -10,8 +10,13 @@
 // (igemm.hip EPI_STATS math); the op finalizes them.
 // Pipeline: 512 threads (8 waves), one block per CU, a register staging ring of two tiles' halos, LDS
 // halo images double-buffered, one barrier per tile.
-// Reference: the conv2 / BN layers of the R/cnn ResNet bottleneck; north-star ResNet-50
-// (BASELINE.json config 3).
+// Reference: the reference has no ResNet; this is the north-star ResNet-50 config (BASELINE.json config 3,
+// SURVEY §2.7's "fuse the unfused op chain" of /root/reference/distributed/distributed.py:96-102).
+// Why stage 1 only (C = K = 64, width 32): the kernel's premise is the whole 9 x C x K filter resident
+// in LDS for the launch (9 x 64 x 64 x 2 B = 72 KB beside two 26 KB halo images).  Stage 2's 128 x 128
+// filter is 288 KB and stage 3's 1.2 MB -- more than the 160 KB LDS -- so those convs must stream their
+// weights per k-tile, which is the generic implicit GEMM (igemm_impl.h, KM_FWD_XT tap-uniform operand);
+// their halo-operand variant inside the igemm was measured ~2x slower (profiles/r03_halo/README.md).
 #include "pw_common.h"
 
 namespace tfx {

@@ -15,8 +15,9 @@
 // BN1's slot workspace; the op runs bn_finalize after it, as conv_fwd_bn does.
 // Pipeline: as pw_bwd.hip -- 512 threads, one block per CU, a register staging ring of two 32-row
 // m-tiles, one barrier per step.
-// Reference: the per-layer chain of R/cnn ResNet blocks that SURVEY §2.7 says the framework fuses;
-// north-star ResNet-50 (BASELINE.json config 3).
+// Reference: no ResNet in the reference; SURVEY §2.7 asks the framework to fuse the reference's
+// unfused per-op chain (/root/reference/distributed/distributed.py:96-102) -- here at the north-star
+// ResNet-50 scale (BASELINE.json config 3).
 #include "pw_common.h"
 
 namespace tfx {

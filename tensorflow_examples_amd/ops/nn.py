@@ -363,6 +363,7 @@ class _Conv2d(torch.autograd.Function):
                     y = torch.ops.tfx.conv_fwd_bn_nofin(x.contiguous(), w.value, stride, pad, dil, ws.get(x.device), nsl)
                     ws.pending_save = torch.empty(4 * w.shape[0], dtype=torch.float32, device=x.device)
                     ws.fin = (m_out, nsl)
+                    _OWED_FIN.append(ws)
                     fusion.note("bn_epilogue", w.name, "igemm_fwd_stats")
                     return y
                 # epilogue statistics, then the finalize: the BN only applies
@@ -685,11 +686,20 @@ _PENDING_SR: List["BNBackwardFusion"] = []
 _XENT_MEAN_MAX = 1024
 
 
+# BN workspaces whose conv epilogue owed a folded finalize this step (conv_fwd_bn_nofin)
+_OWED_FIN: List["BNWorkspace"] = []
+
+
 def reset_pending_slot_reductions() -> None:
     """Forget deferred reductions / finalizes of an abandoned step (an exception part-way through)."""
     for b in _PENDING_SR:
         b.sr_pending = False
     _PENDING_SR.clear()
+    for ws in _OWED_FIN:
+        if ws.fin is not None:  # never finalized: its statistics rows are dirty
+            ws.buf.zero_()
+            ws.fin = None
+    _OWED_FIN.clear()
 
 
 def _resolve_pending(b: "BNBackwardFusion") -> None:
