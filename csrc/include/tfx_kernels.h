@@ -248,12 +248,13 @@ void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float
 void bn_slot_reduce(float* slots, int C, float* red, float* dgamma, float* dbeta, hipStream_t s);
 void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
                   const float* run_var, float* save, hipStream_t s);
-// the apply with the finalize folded in (bn_apply_fin_kernel): statistics in the first nsl (<= 16)
-// rows of slots ([NSLOT][2][C] + an int counter after them), re-zeroed by the last block
+// the apply with the finalize folded in (bn_apply_fin_kernel): statistics in nsl (<= 16) rows
+// [nsl][2][C] that the caller zeroes between uses; y == nullptr: the finalize alone (one block)
 bool bn_apply_fin_ok(int C);
-void bn_apply_fin(const uint16_t* x, const uint16_t* res, float* slots, int nsl, int64_t M, int C, const float* gamma,
-                  const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* save,
-                  bool relu, uint16_t* y, uint8_t* mask, hipStream_t s);
+bool igemm_xt_enabled();  // TFX_IGEMM_XT (igemm.hip)
+void bn_apply_fin(const uint16_t* x, const uint16_t* res, const float* slots, int nsl, int64_t M, int C,
+                  const float* gamma, const float* beta, float eps, float momentum, float* run_mean, float* run_var,
+                  float* save, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s);
 // mask (optional, residual + ReLU on the C % 8 == 0 path): 1 bit per element, the ReLU mask of y
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
               uint16_t* y, uint8_t* mask, hipStream_t s);

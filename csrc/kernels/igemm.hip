@@ -12,6 +12,16 @@
 #include <vector>
 
 namespace tfx {
+// TFX_IGEMM_XT=0 routes the 3x3 convs to the round-3 per-element-decode operands (KM_FWD_X /
+// MN_WGRAD_X) instead of the tap-uniform ones (A/B and numerics bisection hook; read once)
+bool igemm_xt_enabled() {
+  static const int on = [] {
+    const char* e = getenv("TFX_IGEMM_XT");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 
 constexpr int BKT_HOST = 64;  // k-tile depth of igemm_impl.h (BKT)
 
@@ -158,7 +168,8 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
     }
   }
   // im2col operand (forward, flipped-filter data gradient) whose k-tiles each lie in one filter tap
-  if ((mode == MODE_FWD || mode == MODE_DGRAD_FLIP) && a.C % BKT_HOST == 0 && a.R * a.S <= 32 && !a.a_scale)
+  if ((mode == MODE_FWD || mode == MODE_DGRAD_FLIP) && a.C % BKT_HOST == 0 && a.R * a.S <= 32 && !a.a_scale &&
+      igemm_xt_enabled())
     a.tapmask = 1;
   switch (mode) {
     case MODE_FWD: igemm_fwd_im2col(a, s); break;

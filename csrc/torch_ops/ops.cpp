@@ -271,9 +271,9 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   return {y, save};
 }
 
-// conv_fwd_bn without the finalize: the epilogue adds the statistics into the first stat_slots rows of
-// ws and the BN's apply finalizes them itself (bn_apply_fin_into), or bn_finalize_into does when the
-// consumer cannot.  Always the implicit GEMM (never the stem route).  Returns y.
+// conv_fwd_bn without the finalize: the epilogue adds the statistics into the stat_slots zeroed rows
+// ws = [stat_slots][2][Ko] and the BN's apply finalizes them itself (bn_apply_fin_into), or
+// bn_finalize_rows does when the consumer cannot.  Always the implicit GEMM (never the stem route).
 Tensor conv_fwd_bn_nofin(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor ws, int64_t stat_slots) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
   TORCH_CHECK(stat_slots >= 1 && stat_slots <= 16, "conv_fwd_bn_nofin: 1..16 statistics rows");
@@ -284,26 +284,30 @@ Tensor conv_fwd_bn_nofin(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_
   a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
   a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
   a.out_mode = tfx::OUT_BF16;
-  check_bn_ws(ws, g.Ko);
+  CHECK_F32(ws); CHECK_CONTIG(ws);
+  TORCH_CHECK(ws.numel() >= stat_slots * 2 * g.Ko, "conv_fwd_bn_nofin: statistics rows too small");
   a.stats = ws.data_ptr<float>();
   a.stat_slots = (int)stat_slots;
   tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
   return y;
 }
 
-// the finalize of a conv_fwd_bn_nofin (its statistics rows re-zeroed): fills save = [mean|invstd|scale|shift]
-void bn_finalize_into(Tensor ws, int64_t M, optional<Tensor> gamma, optional<Tensor> beta, optional<Tensor> run_mean,
-                      optional<Tensor> run_var, double momentum, double eps, Tensor save) {
-  CHECK_F32(save); CHECK_CONTIG(save);
+// the finalize of a conv_fwd_bn_nofin's rows alone (one block of bn_apply_fin_kernel): save =
+// [mean|invstd|scale|shift], running statistics updated; the rows stay (zeroed with the gradients)
+void bn_finalize_rows(Tensor rows, int64_t nsl, int64_t M, optional<Tensor> gamma, optional<Tensor> beta,
+                      optional<Tensor> run_mean, optional<Tensor> run_var, double momentum, double eps, Tensor save) {
+  CHECK_F32(rows); CHECK_CONTIG(rows); CHECK_F32(save); CHECK_CONTIG(save);
   const int64_t C = save.numel() / 4;
-  check_bn_ws(ws, C);
-  tfx::bn_finalize(ws.data_ptr<float>(), M, (int)C, fp(gamma), fp(beta), (float)eps, (float)momentum,
-                   fpm(run_mean), fpm(run_var), save.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(tfx::bn_apply_fin_ok((int)C) && nsl >= 1 && nsl <= 16 && rows.numel() >= nsl * 2 * C,
+              "bn_finalize_rows: shapes");
+  tfx::bn_apply_fin(nullptr, nullptr, rows.data_ptr<float>(), (int)nsl, M, (int)C, fp(gamma), fp(beta), (float)eps,
+                    (float)momentum, fpm(run_mean), fpm(run_var), save.data_ptr<float>(), false, nullptr, nullptr,
+                    cur_stream());
 }
 
 // BN apply (out = relu?(x sc + sh (+ res)), mask bits with res) with the finalize folded in: scale /
-// shift from the first nsl statistics rows of ws (conv_fwd_bn_nofin), save and the running stats
-// written by block 0, the rows and the counter after [NSLOT][2][C] re-zeroed by the last block.
+// shift from the nsl statistics rows ws = [nsl][2][C] (conv_fwd_bn_nofin), save and the running stats
+// written by block 0; the rows are left for the caller to zero (the gradient fill of the next step).
 bool bn_apply_fin_supported(int64_t C) { return tfx::bn_apply_fin_ok((int)C); }
 
 void bn_apply_fin_into(Tensor x, optional<Tensor> res, Tensor ws, int64_t nsl, optional<Tensor> gamma,
@@ -315,7 +319,7 @@ void bn_apply_fin_into(Tensor x, optional<Tensor> res, Tensor ws, int64_t nsl, o
   TORCH_CHECK(tfx::bn_apply_fin_ok((int)C) && out.numel() == x.numel() && save.numel() == 4 * C,
               "bn_apply_fin_into: shapes");
   TORCH_CHECK(nsl >= 1 && nsl <= 16, "bn_apply_fin_into: 1..16 statistics rows");
-  TORCH_CHECK(ws.numel() >= tfx::NSLOT * 2 * C + 4, "bn_apply_fin_into: workspace lacks the counter word");
+  TORCH_CHECK(ws.numel() >= nsl * 2 * C, "bn_apply_fin_into: statistics rows too small");
   const uint16_t* r = nullptr;
   if (res.has_value() && res->defined()) {
     CHECK_BF16(*res); CHECK_CONTIG(*res);
@@ -1844,7 +1848,7 @@ TORCH_LIBRARY(tfx, m) {
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_fwd_bn_nofin", &conv_fwd_bn_nofin);
-  m.def("bn_finalize_into", &bn_finalize_into);
+  m.def("bn_finalize_rows", &bn_finalize_rows);
   m.def("bn_apply_fin_supported", &bn_apply_fin_supported);
   m.def("bn_apply_fin_into", &bn_apply_fin_into);
   m.def("conv_fwd_bn_in", &conv_fwd_bn_in);

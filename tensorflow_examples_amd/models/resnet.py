@@ -47,7 +47,7 @@ class _BN:
             self.beta = store.variable([c], Zeros(), name="beta")
             self.mean = store.add_state("moving_mean", torch.zeros(c))
             self.var = store.add_state("moving_variance", torch.ones(c))
-        self.ws = BNWorkspace(c)
+        self.ws = BNWorkspace(c, store)
 
     def __call__(self, x, training, relu=False, residual=None, stats_ready=False, residual_sink=None, ws_obj=False,
                  residual_is_bn=False, defer_output=False, lazy_backward=False, defer_apply=False):

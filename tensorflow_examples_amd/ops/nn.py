@@ -133,10 +133,11 @@ _DEFER_TAIL = True
 _DEFER_BN_IN = True
 _FUSE_CONV3_BWD = True  # False: the stage-1 3x3 conv's backward runs layer-wise (forward still fused)
 PW_SQUEEZE_CALLS = [0]  # fused tail + conv1 forward launches (tests)
-# finalize folded into the layer-wise apply (bn_apply_fin): stage 2-4 BN layers (M <= 65536 rows)
+# finalize folded into the layer-wise apply (bn_apply_fin): stage 3-4 BN layers (M <= 16384 rows: few
+# statistics rows, so every apply block can afford to reduce them; profiles/r04_fold)
 _FOLD_FIN = True
 FOLD_FIN_CALLS = [0]  # applies that finalized their own statistics (tests)
-_FOLD_FIN_MAX_ROWS = 65536
+_FOLD_FIN_MAX_ROWS = 16384
 
 
 class TailPending:
@@ -165,7 +166,7 @@ class TailPending:
         if not self.done:
             ws = self.fin
             if ws is not None and ws.fin is not None and self.res_save is None:
-                torch.ops.tfx.bn_apply_fin_into(self.x, self.res, ws.buf, ws.fin[1], *ws.finalize_args,
+                torch.ops.tfx.bn_apply_fin_into(self.x, self.res, ws.fin[2], ws.fin[1], *ws.finalize_args,
                                                 True, self.save, self.out, self.mask)
                 ws.fin = None
                 self.fin = None
@@ -355,14 +356,15 @@ class _Conv2d(torch.autograd.Function):
                 ws = stats_into
                 stem = _STEM_WGRAD and _stem_ok(x, w, stride, pad, dil)
                 m_out = _conv_rows(x, w, stride, pad, dil)
-                if _FOLD_FIN and not stem and m_out <= _FOLD_FIN_MAX_ROWS and \
-                        torch.ops.tfx.bn_apply_fin_supported(w.shape[0]):
-                    # epilogue statistics into a few slot rows; the finalize is owed (ws.fin) -- the
-                    # BN's apply runs it in-kernel, or ws.settle_fin launches it for other consumers
-                    nsl = max(1, min(16, m_out // 4096))
-                    y = torch.ops.tfx.conv_fwd_bn_nofin(x.contiguous(), w.value, stride, pad, dil, ws.get(x.device), nsl)
+                rows = ws.fin_rows() if (_FOLD_FIN and not stem and m_out <= _FOLD_FIN_MAX_ROWS and
+                                         torch.ops.tfx.bn_apply_fin_supported(w.shape[0])) else None
+                if rows is not None:
+                    # epilogue statistics into a few zeroed scratch rows; the finalize is owed (ws.fin) --
+                    # the BN's apply runs it in-kernel, or ws.settle_fin launches it for other consumers
+                    nsl = max(1, min(BNWorkspace.FIN_ROWS, m_out // 4096))
+                    y = torch.ops.tfx.conv_fwd_bn_nofin(x.contiguous(), w.value, stride, pad, dil, rows, nsl)
                     ws.pending_save = torch.empty(4 * w.shape[0], dtype=torch.float32, device=x.device)
-                    ws.fin = (m_out, nsl)
+                    ws.fin = (m_out, nsl, rows)
                     _OWED_FIN.append(ws)
                     fusion.note("bn_epilogue", w.name, "igemm_fwd_stats")
                     return y
@@ -605,26 +607,44 @@ class BNWorkspace:
     statistics and leaves [mean | invstd | scale | shift] in ``pending_save``."""
     NSLOT = 64  # = tfx::NSLOT (csrc/include/tfx_kernels.h), checked on first GPU use
 
-    def __init__(self, channels: int):
+    FIN_ROWS = 16  # forward statistics rows of a folded finalize (conv_fwd_bn_nofin), at most
+
+    def __init__(self, channels: int, store=None):
         self.c = channels
         self.buf = None
         self.finalize_args = None
         self.pending_save = None
         # (rows M, statistics rows nsl) while the finalize of a conv_fwd_bn_nofin is owed
         self.fin = None
+        # the folded finalize's forward statistics rows live in the store's gradient-zeroed scratch
+        # (VariableStore.reserve_scratch): zeroed with the gradients once per step, so the apply that
+        # reads them never has to re-zero them (no cross-block "last reader" round trip)
+        self.store = store
+        self.rows_off = store.reserve_scratch(self.FIN_ROWS * 2 * channels) if store is not None else None
+        self.rows_epoch = -1
+
+    def fin_rows(self) -> Optional[torch.Tensor]:
+        """This step's zeroed statistics rows for a folded finalize, or None (no store scratch, or the
+        rows were already used since the last VariableStore.zero_grad)."""
+        st = self.store
+        if st is None or st.scratch is None or self.rows_epoch == st.grad_epoch:
+            return None
+        self.rows_epoch = st.grad_epoch
+        n = self.FIN_ROWS * 2 * self.c
+        return st.scratch[self.rows_off:self.rows_off + n]
 
     def get(self, device) -> torch.Tensor:
         if self.buf is None or self.buf.device != device:
             if device.type == "cuda" and _native.use_native_device(device):
                 assert int(torch.ops.tfx.bn_nslot()) == self.NSLOT, "BNWorkspace.NSLOT != tfx::NSLOT"
-            # + the folded apply's last-reader counter word (and padding), zero between uses too
-            self.buf = torch.zeros(self.NSLOT * 2 * self.c + 64, dtype=torch.float32, device=device)
+            self.buf = torch.zeros(self.NSLOT * 2 * self.c, dtype=torch.float32, device=device)
         return self.buf
 
     def settle_fin(self, save: torch.Tensor) -> None:
-        """Run the owed finalize (bn_finalize_into) into ``save``, if any."""
+        """Run the owed finalize (bn_finalize_rows: one block) into ``save``, if any."""
         if self.fin is not None:
-            torch.ops.tfx.bn_finalize_into(self.buf, self.fin[0], *self.finalize_args, save)
+            m, nsl, rows = self.fin
+            torch.ops.tfx.bn_finalize_rows(rows, nsl, m, *self.finalize_args, save)
             self.fin = None
 
 
@@ -696,9 +716,7 @@ def reset_pending_slot_reductions() -> None:
         b.sr_pending = False
     _PENDING_SR.clear()
     for ws in _OWED_FIN:
-        if ws.fin is not None:  # never finalized: its statistics rows are dirty
-            ws.buf.zero_()
-            ws.fin = None
+        ws.fin = None  # never finalized: its rows are re-zeroed with the gradients (zero_grad)
     _OWED_FIN.clear()
 
 

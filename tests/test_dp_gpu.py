@@ -129,7 +129,10 @@ lab = torch.randint(0, 10, (BATCH,), generator=g).to(dev)
 x = to_model_input(img)
 runs = {}
 for mode in ("ref", "eager", "graphed"):
-    store, model = build_resnet_cifar(device=dev, depth=DEPTH, dtype=torch.bfloat16, seed=0)
+    # zero-init residual gammas: from a random-init start one step of this model is chaotic in f32
+    # rounding order (a 1e-6 nudge of one BN gamma moves the step by 20-100 %, profiles/r04_determinism),
+    # so two runs could only be compared bit-exactly; from the identity-block start they agree to ~0.3 %
+    store, model = build_resnet_cifar(device=dev, depth=DEPTH, dtype=torch.bfloat16, seed=0, zero_init_residual=True)
     w0 = store.master.clone()
     dp = None
     if mode != "ref":
@@ -159,8 +162,9 @@ for mode in ("eager", "graphed"):
     worst = max(((d[lo:hi] - ref[lo:hi]).norm() / ref[lo:hi].norm()).item() for lo, hi in buckets
                 if ref[lo:hi].norm() > 0)
     print("REL", mode, rel, "worst_bucket", worst, "buckets", len(buckets), flush=True)
-    # bf16 on the wire rounds every gradient to 8 significant bits (rel ~ 2^-9 per element)
-    lim = (1e-2, 3e-2) if BF16 else (2e-3, 1e-2)
+    # run-to-run floor ~3e-3 (f32 atomic order); bf16 on the wire adds 8-bit rounding (rel ~ 2^-9 per
+    # element).  A dropped or early collective leaves its bucket at half the update: rel ~0.5
+    lim = (2e-2, 5e-2) if BF16 else (1e-2, 3e-2)
     assert rel < lim[0] and worst < lim[1], (mode, rel, worst)
 dist.destroy_process_group()
 """
