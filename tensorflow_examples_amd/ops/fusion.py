@@ -30,7 +30,8 @@ bn_finalize_fold       stage 2-4 BN finalize inside the layer-wise apply: every 
                        itself, the last one re-zeroes them (bn_apply_fin)
 =====================  ==========================================================  ===============================
 
-``TFX_FUSION`` selects a profile at import: ``all`` (default), ``r2`` (the round-2 level: epilogue
+``TFX_FUSION`` selects a profile at import: ``all`` (default: every group but the opt-in
+``bn_finalize_fold``), ``r2`` (the round-2 level: epilogue
 fusions only, no cross-layer kernels), ``none`` (layer-wise), or a comma list of ``-group`` /
 ``+group`` edits applied to ``all`` (e.g. ``-head_tail,-bn_on_load``).  :func:`set_groups` switches
 them at run time (tests, A/B runs); :class:`record` collects what one traced step actually ran.
@@ -44,8 +45,9 @@ from typing import Dict, Iterable, List, Optional, Tuple
 GROUPS = ("bn_epilogue", "grad_sink", "masked_res", "s2_addend", "deferred_slot_reduce", "block_boundary_fwd",
           "bn_on_load", "lazy_bn_bwd", "conv3_fused_bwd", "stem_kernels", "fused_head", "head_tail",
           "bn_finalize_fold")
+# bn_finalize_fold is opt-in (``TFX_FUSION=+bn_finalize_fold``): measured neutral, profiles/r04_fold
 PROFILES = {
-    "all": set(GROUPS),
+    "all": set(GROUPS) - {"bn_finalize_fold"},
     "r2": {"bn_epilogue", "grad_sink", "masked_res", "s2_addend", "deferred_slot_reduce", "fused_head"},
     "none": set(),
 }

@@ -134,8 +134,10 @@ _DEFER_BN_IN = True
 _FUSE_CONV3_BWD = True  # False: the stage-1 3x3 conv's backward runs layer-wise (forward still fused)
 PW_SQUEEZE_CALLS = [0]  # fused tail + conv1 forward launches (tests)
 # finalize folded into the layer-wise apply (bn_apply_fin): stage 3-4 BN layers (M <= 16384 rows: few
-# statistics rows, so every apply block can afford to reduce them; profiles/r04_fold)
-_FOLD_FIN = True
+# statistics rows, so every apply block can afford to reduce them).  Off by default: measured neutral
+# to +9 us/step in the bench (the ~5 us a finalize shows in a step trace is mostly the producer conv's
+# drain, which the next launch pays either way; profiles/r04_fold/README.md).  TFX_FUSION=+bn_finalize_fold
+_FOLD_FIN = False
 FOLD_FIN_CALLS = [0]  # applies that finalized their own statistics (tests)
 _FOLD_FIN_MAX_ROWS = 16384
 
