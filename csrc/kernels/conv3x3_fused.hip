@@ -391,13 +391,23 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
 #pragma unroll
       for (int m = 0; m < 2; ++m)
         fa[m] = pw_frag_tr(timg, 0, wco + 16 * m, lane, [hp0](int kr, int c) { return pw_kmaj(hp0 + kr, c); });
-#pragma unroll
-      for (int nn = 0; nn < 9; ++nn) {
+      // B fragments two column tiles ahead (a 3-slot register ring): each transposed LDS read has two
+      // iterations of MFMAs to land behind instead of stalling the one right after it
+      auto fbld = [&](int nn) {
         const int idx = wng + nn, tap = idx >> 2, cit = idx & 3, ky = tap / 3, kx = tap % 3;
         const int hb0 = (r + ky) * C3_HW + kx;
-        const bf16x8_t fb = pw_frag_tr(aimg, 0, 16 * cit, lane, [hb0](int kr, int c) { return pw_kmaj(hb0 + kr, c); });
+        return pw_frag_tr(aimg, 0, 16 * cit, lane, [hb0](int kr, int c) { return pw_kmaj(hb0 + kr, c); });
+      };
+      bf16x8_t fbq[3];
+      fbq[0] = fbld(0);
+      fbq[1] = fbld(1);
 #pragma unroll
-        for (int m = 0; m < 2; ++m) accw[m][nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb, accw[m][nn], 0, 0, 0);
+      for (int nn = 0; nn < 9; ++nn) {
+        if (nn + 2 < 9) fbq[(nn + 2) % 3] = fbld(nn + 2);
+        __builtin_amdgcn_sched_barrier(0);  // the prefetch issues before this step's MFMAs
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          accw[m][nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fbq[nn % 3], accw[m][nn], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);  // bound the fragment reads hoisted ahead
       }
     }
