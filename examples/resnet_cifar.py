@@ -18,7 +18,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from tensorflow_examples_amd import app, ops  # noqa: E402
-from tensorflow_examples_amd.ckpt import Saver, latest_checkpoint, store_graph_nodes, write_graph  # noqa: E402
+from tensorflow_examples_amd.ckpt import (Saver, export_saved_model, latest_checkpoint, store_graph_nodes,  # noqa: E402
+                                          write_graph)
 from tensorflow_examples_amd.data.cifar import augment_model_input, load_cifar10  # noqa: E402
 from tensorflow_examples_amd.data.pipeline import DevicePrefetcher, batches  # noqa: E402
 from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
@@ -38,6 +39,7 @@ flags.DEFINE_float("weight_decay", 5e-4, "L2 weight decay")
 flags.DEFINE_string("lr_boundaries", "0.5,0.75", "fractions of training where the LR drops 10x")
 flags.DEFINE_float("bucket_mb", 32.0, "all-reduce bucket size (MB)")
 flags.DEFINE_string("logdir", "", "checkpoint directory (resume from the latest checkpoint in it)")
+flags.DEFINE_string("export_dir", "", "after training, export a SavedModel (saved_model.pb + variables/) here")
 flags.DEFINE_integer("synthetic_train", 50000, "synthetic training-set size when no data is found")
 flags.DEFINE_integer("eval_examples", 0, "evaluate on the first N test images (0 = all)")
 flags.DEFINE_integer("seed", 0, "weight-initialisation seed (also offsets the data shuffle)")
@@ -134,6 +136,11 @@ def main(_):
         print("images/sec (all GPUs) %.1f" % float(ips))
         if FLAGS.logdir:
             print("saved", Saver().save(store, os.path.join(FLAGS.logdir, "model.ckpt"), global_step=step))
+        if FLAGS.export_dir:
+            sig = {"serving_default": {"inputs": {"images": ("images:0", "uint8", [-1, 32, 32, 3])},
+                                       "outputs": {"logits": ("logits:0", "float32", [-1, 10])}}}
+            print("exported", export_saved_model(store, FLAGS.export_dir, {"model": "resnet%d" % FLAGS.depth},
+                                                 signature_defs=sig))
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

@@ -14,8 +14,9 @@ tensor is verified on restore.  ``.meta`` is a binary MetaGraphDef encoded by ``
 the graph (one ``VariableV2`` node per variable unless the caller passes the model's nodes), TF1's
 default SaverDef, the ``variables`` / ``trainable_variables`` collections (serialized VariableDefs)
 and a ``tfx_meta`` collection holding the caller's metadata as JSON; ``read_meta_graph`` parses it.  ``export_saved_model`` writes the SavedModel-shaped directory
-``saved_model.pb`` + ``variables/variables.{index,data-00000-of-00001}``; ``saved_model.pb`` here is
-our container (magic ``TFXSM001`` + JSON signature/meta), not a TF protobuf.
+``saved_model.pb`` + ``variables/variables.{index,data-00000-of-00001}``; ``saved_model.pb`` is a SavedModel
+protobuf (one MetaGraphDef tagged ``serve`` with the graph, SaverDef, variable collections and the serving
+SignatureDefs; ``read_saved_model`` parses it).
 The reference's Supervisor builds a default Saver but never saves without ``logdir``
 (R/distributed/distributed.py:129-131); ``--logdir`` turns it on in this framework.
 """
@@ -192,26 +193,72 @@ def latest_checkpoint(checkpoint_dir: str) -> Optional[str]:
     return None
 
 
-def export_saved_model(store, export_dir: str, signature: Optional[dict] = None) -> str:
+def export_saved_model(store, export_dir: str, signature: Optional[dict] = None,
+                       signature_defs: Optional[Dict[str, dict]] = None, graph_nodes: Optional[List[Dict]] = None,
+                       tags=("serve",)) -> str:
+    """The SavedModel directory layout: ``saved_model.pb`` -- a SavedModel protobuf (schema version 1, one
+    MetaGraphDef tagged ``tags`` with the graph, TF1's default SaverDef, the variable collections and the
+    serving ``signature_defs``) -- and ``variables/variables.{index,data-00000-of-00001}`` (our container).
+    ``signature_defs``: {key: {"inputs": {name: (tensor, dtype, shape)}, "outputs": {...},
+    "method_name": ...}}; ``signature`` is free-form caller metadata kept in the ``tfx_meta`` collection."""
     os.makedirs(os.path.join(export_dir, "variables"), exist_ok=True)
-    _write_tensors(os.path.join(export_dir, "variables", "variables"), store.named_values(), {"saved_model": True})
-    body = json.dumps({"format": FORMAT, "signature": signature or {},
-                       "variables": [{"name": v.name, "shape": list(v.shape)} for v in store.vars]}).encode()
-    with open(os.path.join(export_dir, "saved_model.pb"), "wb") as f:
-        f.write(SM_MAGIC + body)
+    values = store.named_values()
+    _write_tensors(os.path.join(export_dir, "variables", "variables"), values, {"saved_model": True})
+    trainable = {v.name: bool(v.trainable) for v in store.vars}
+    names = sorted(values)
+    nodes = graph_nodes if graph_nodes is not None else store_graph_nodes(store)
+    sigs = {}
+    for key, d in (signature_defs or {}).items():
+        ins = {k: summary.tensor_info(*spec) for k, spec in d.get("inputs", {}).items()}
+        outs = {k: summary.tensor_info(*spec) for k, spec in d.get("outputs", {}).items()}
+        sigs[key] = summary.signature_def(ins, outs, d.get("method_name", "tensorflow/serving/predict"))
+    meta = {"format": FORMAT, "signature": signature or {},
+            "variables": [{"name": v.name, "shape": list(v.shape)} for v in store.vars]}
+    mg = summary.meta_graph_def(
+        summary.graph_def(nodes), tags=tags, saver=summary.saver_def(),
+        collections={"variables": [summary.variable_def(n, trainable.get(n, False)) for n in names],
+                     "trainable_variables": [summary.variable_def(n, True) for n in names if trainable.get(n)],
+                     "tfx_meta": [json.dumps(meta).encode()]},
+        signatures=sigs)
+    tmp = os.path.join(export_dir, "saved_model.pb.tmp")
+    with open(tmp, "wb") as f:
+        f.write(summary.saved_model([mg]))
+    os.replace(tmp, os.path.join(export_dir, "saved_model.pb"))
     return export_dir
 
 
-def load_saved_model(store, export_dir: str) -> dict:
+def read_saved_model(export_dir: str) -> dict:
+    """Parse ``saved_model.pb``: schema version, tags, graph nodes, saver, signature_defs, variables and the
+    caller metadata (``meta``).  Round-1..3 exports (magic ``TFXSM001`` + JSON) read too."""
     with open(os.path.join(export_dir, "saved_model.pb"), "rb") as f:
         raw = f.read()
-    if not raw.startswith(SM_MAGIC):
-        raise ValueError("not a tensorflow_examples_amd SavedModel")
-    meta = json.loads(raw[len(SM_MAGIC):])
+    if raw.startswith(SM_MAGIC):  # the pre-protobuf container
+        meta = json.loads(raw[len(SM_MAGIC):])
+        return {"schema_version": 0, "tags": [], "nodes": [], "saver": None, "signature_defs": {}, "meta": meta,
+                "variables": [v["name"] for v in meta.get("variables", [])]}
+    sm = summary.parse_saved_model(raw)
+    if not sm["meta_graphs"]:
+        raise ValueError(f"{export_dir}/saved_model.pb: no MetaGraphDef")
+    mg = sm["meta_graphs"][0]
+    colls = mg["collections"]
+    tm = colls.get("tfx_meta")
+    return {"schema_version": sm["schema_version"], "tags": mg["meta_info"]["tags"], "nodes": mg["nodes"],
+            "saver": mg["saver"], "signature_defs": mg["signature_defs"],
+            "meta": json.loads(tm[0]) if tm else {},
+            "variables": [summary.parse_variable_def(b)["variable_name"].rsplit(":", 1)[0]
+                          for b in colls.get("variables", [])]}
+
+
+def load_saved_model(store, export_dir: str) -> dict:
+    """Restore a SavedModel export into ``store``; returns its caller metadata (format, signature,
+    variables) plus the parsed ``tags`` and ``signature_defs``."""
+    sm = read_saved_model(export_dir)
     tensors = read_checkpoint(os.path.join(export_dir, "variables", "variables"))
     store.load_named(tensors, strict=False)
+    meta = dict(sm["meta"])
+    meta["tags"], meta["signature_defs"] = sm["tags"], sm["signature_defs"]
     return meta
 
 
-__all__ = ["Saver", "latest_checkpoint", "read_checkpoint", "export_saved_model", "load_saved_model",
+__all__ = ["Saver", "latest_checkpoint", "read_checkpoint", "export_saved_model", "load_saved_model", "read_saved_model",
            "read_meta_graph", "write_graph", "read_graph", "store_graph_nodes"]

@@ -105,8 +105,38 @@ def variable_def(name: str, trainable: bool = True) -> bytes:
             _bytes_field(3, f"{name}/read:0".encode()) + _varint_field(7, 1 if trainable else 0))
 
 
+# tensorflow DataType enum values of the dtypes a signature names
+_DT = {"float32": 1, "float64": 2, "int32": 3, "uint8": 4, "int64": 9, "bool": 10, "float16": 19, "bfloat16": 14}
+_DT_NAME = {v: k for k, v in _DT.items()}
+
+
+def tensor_info(name: str, dtype: str = "float32", shape: Optional[Sequence[int]] = None) -> bytes:
+    """TensorInfo { name, dtype, tensor_shape { dim { size }* } } (-1 = unknown dimension)."""
+    out = _bytes_field(1, name.encode()) + _varint_field(2, _DT[dtype])
+    if shape is not None:
+        dims = b"".join(_bytes_field(2, _varint_field(1, int(d) & 0xFFFFFFFFFFFFFFFF)) for d in shape)
+        out += _bytes_field(3, dims)
+    return out
+
+
+def signature_def(inputs: Dict[str, bytes], outputs: Dict[str, bytes],
+                  method_name: str = "tensorflow/serving/predict") -> bytes:
+    """SignatureDef { inputs map, outputs map, method_name } from TensorInfo bytes (tensor_info)."""
+    out = b""
+    for field, m in ((1, inputs), (2, outputs)):
+        for k, ti in m.items():
+            out += _bytes_field(field, _bytes_field(1, k.encode()) + _bytes_field(2, ti))
+    return out + _bytes_field(3, method_name.encode())
+
+
+def saved_model(meta_graphs: Sequence[bytes]) -> bytes:
+    """SavedModel { saved_model_schema_version = 1, meta_graphs* } (the saved_model.pb message)."""
+    return _varint_field(1, 1) + b"".join(_bytes_field(2, bytes(m)) for m in meta_graphs)
+
+
 def meta_graph_def(graph: bytes, tags: Sequence[str] = (), saver: Optional[bytes] = None,
-                   collections: Optional[Dict[str, Sequence[bytes]]] = None) -> bytes:
+                   collections: Optional[Dict[str, Sequence[bytes]]] = None,
+                   signatures: Optional[Dict[str, bytes]] = None) -> bytes:
     """MetaGraphDef: meta_info_def { meta_graph_version, tags*, tensorflow_version,
     tensorflow_git_version } + graph_def (what TF1's FileWriter(graph=...) writes after the GraphDef
     event, R/distributed/distributed.py:138), plus -- for a checkpoint's ``.meta`` (what TF1's
@@ -123,7 +153,36 @@ def meta_graph_def(graph: bytes, tags: Sequence[str] = (), saver: Optional[bytes
         blist = b"".join(_bytes_field(1, bytes(v)) for v in values)
         entry = _bytes_field(1, key.encode()) + _bytes_field(2, _bytes_field(2, blist))
         out += _bytes_field(4, entry)
+    for key, sig in (signatures or {}).items():  # signature_def map (a SavedModel's serving signatures)
+        out += _bytes_field(5, _bytes_field(1, key.encode()) + _bytes_field(2, bytes(sig)))
     return out
+
+
+def parse_tensor_info(b: bytes) -> Dict:
+    f = _parse(bytes(b))
+    shape = None
+    if 3 in f:
+        shape = []
+        for db in _parse(f[3][0]).get(2, []):
+            v = _parse(db).get(1, [0])[0]
+            shape.append(v - (1 << 64) if v >= (1 << 63) else v)
+    return {"name": f[1][0].decode(), "dtype": _DT_NAME.get(f.get(2, [0])[0], "invalid"), "shape": shape}
+
+
+def parse_signature_def(b: bytes) -> Dict:
+    f = _parse(bytes(b))
+    out = {"inputs": {}, "outputs": {}, "method_name": f.get(3, [b""])[0].decode()}
+    for field, key in ((1, "inputs"), (2, "outputs")):
+        for eb in f.get(field, []):
+            e = _parse(eb)
+            out[key][e[1][0].decode()] = parse_tensor_info(e[2][0])
+    return out
+
+
+def parse_saved_model(b: bytes) -> Dict:
+    """A SavedModel as {"schema_version", "meta_graphs": [parse_meta_graph_def(...)]}."""
+    f = _parse(bytes(b))
+    return {"schema_version": f.get(1, [0])[0], "meta_graphs": [parse_meta_graph_def(m) for m in f.get(2, [])]}
 
 
 def parse_graph_def(b: bytes) -> List[Dict]:
@@ -155,6 +214,10 @@ def parse_meta_graph_def(b: bytes) -> Dict:
         coll = _parse(e[2][0])
         vals = _parse(coll[2][0]).get(1, []) if 2 in coll else []
         out["collections"][e[1][0].decode()] = [bytes(v) for v in vals]
+    out["signature_defs"] = {}
+    for eb in f.get(5, []):
+        e = _parse(eb)
+        out["signature_defs"][e[1][0].decode()] = parse_signature_def(e[2][0])
     return out
 
 

@@ -48,12 +48,36 @@ def test_crc_detects_corruption(tmp_path):
 
 def test_saved_model_export(tmp_path):
     a = _store(3)
-    ckpt.export_saved_model(a, str(tmp_path / "export"), {"inputs": "x"})
+    sig = {"serving_default": {"inputs": {"x": ("input/x-input:0", "float32", [-1, 784])},
+                               "outputs": {"probs": ("softmax/Softmax:0", "float32", [-1, 10])}}}
+    ckpt.export_saved_model(a, str(tmp_path / "export"), {"inputs": "x"}, signature_defs=sig)
     assert os.path.exists(tmp_path / "export" / "saved_model.pb")
     assert os.path.exists(tmp_path / "export" / "variables" / "variables.index")
+    raw = open(tmp_path / "export" / "saved_model.pb", "rb").read()
+    assert raw[:2] == b"\x08\x01"  # SavedModel.saved_model_schema_version = 1: a protobuf, not our old container
+    sm = ckpt.read_saved_model(str(tmp_path / "export"))
+    assert sm["schema_version"] == 1 and sm["tags"] == ["serve"]
+    assert sm["saver"]["restore_op_name"] == "save/restore_all"
+    sd = sm["signature_defs"]["serving_default"]
+    assert sd["method_name"] == "tensorflow/serving/predict"
+    assert sd["inputs"]["x"] == {"name": "input/x-input:0", "dtype": "float32", "shape": [-1, 784]}
+    assert sd["outputs"]["probs"]["shape"] == [-1, 10]
+    assert set(sm["variables"]) >= {v.name for v in a.vars}
+    assert {n["name"] for n in sm["nodes"]} >= {v.name for v in a.vars}
     b = _store(4)
     meta = ckpt.load_saved_model(b, str(tmp_path / "export"))
     assert meta["signature"] == {"inputs": "x"} and torch.equal(a.master, b.master)
+    assert meta["signature_defs"]["serving_default"]["inputs"]["x"]["name"] == "input/x-input:0"
+
+
+def test_saved_model_reads_legacy_container(tmp_path):
+    a = _store(6)
+    d = tmp_path / "old"
+    ckpt.export_saved_model(a, str(d))
+    with open(d / "saved_model.pb", "wb") as f:  # what rounds 1-3 wrote
+        f.write(ckpt.SM_MAGIC + b'{"format": "tfx-ckpt-v1", "signature": {"k": 1}, "variables": []}')
+    b = _store(7)
+    assert ckpt.load_saved_model(b, str(d))["signature"] == {"k": 1} and torch.equal(a.master, b.master)
 
 
 def test_meta_is_metagraphdef_and_graph_pbtxt(tmp_path):

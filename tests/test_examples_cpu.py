@@ -59,9 +59,14 @@ def test_resnet_cifar_example_dp2(tmp_path):
     assert len(mg["trainable_variables"]) > 50 and mg["saver"]["version"] == 2
     # resume: the second run restores the checkpoint and continues from its global step
     out2 = _torchrun("resnet_cifar.py", 2, "--depth=18", "--batch_size=8", "--max_steps=2", "--synthetic_train=256",
-                     "--eval_examples=100", f"--logdir={tmp_path}")
+                     "--eval_examples=100", f"--logdir={tmp_path}", f"--export_dir={tmp_path / 'export'}")
     second = ckpt.latest_checkpoint(str(tmp_path))
     assert int(first.rsplit("-", 1)[1]) == 2 and int(second.rsplit("-", 1)[1]) == 4, (first, second, out2[-500:])
+    # SavedModel export: a SavedModel protobuf with the serving signature + the variables directory
+    sm = ckpt.read_saved_model(str(tmp_path / "export"))
+    assert sm["tags"] == ["serve"] and sm["schema_version"] == 1
+    assert sm["signature_defs"]["serving_default"]["inputs"]["images"]["shape"] == [-1, 32, 32, 3]
+    assert os.path.exists(tmp_path / "export" / "variables" / "variables.data-00000-of-00001")
 
 
 def test_word2vec_example():
