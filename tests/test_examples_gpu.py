@@ -28,7 +28,9 @@ def _field(out, prefix):
 def test_resnet_cifar_example_graph_vs_eager():
     common = ["--depth=18", "--batch_size=64", "--max_steps=60", "--synthetic_train=4096", "--learning_rate=0.02",
               "--eval_examples=1000", "--data_dir=/nonexistent", "--lr_boundaries=0.5",
-              "--warmup_steps=0"]  # a 60-step run: no lr warm-up (the example's default ramps over 50 steps)
+              "--warmup_steps=0", "--nozero_init_residual"]
+    # a 60-step run at lr 0.02: no lr warm-up (the example's default ramps over 50 steps) and full-scale
+    # residual branches (zero-init branches grow too slowly to learn anything in 30 steps at this lr)
     g = _run(*common, "--graph")
     e = _run(*common, "--nograph")
     assert "hip graph: replaying the captured step" in g
