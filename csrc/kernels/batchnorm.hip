@@ -20,6 +20,8 @@
 #include "tfx_common.h"
 #include "tfx_kernels.h"
 
+#include <cstdlib>
+
 namespace tfx {
 
 namespace {
@@ -661,11 +663,20 @@ int grid_for(int64_t work, int per_block, int cap = 2048) {
   return (int)(g < 1 ? 1 : g);
 }
 int gcd(int a, int b) { return b ? gcd(b, a % b) : a; }
+// vectors per thread of the fixed-channel elementwise passes (TFX_BN_VPT, read once; A/B hook)
+static int bn_vpt() {
+  static const int v = [] {
+    const char* e = getenv("TFX_BN_VPT");
+    const int x = e ? atoi(e) : 4;
+    return x >= 1 && x <= 64 ? x : 4;
+  }();
+  return v;
+}
 // elementwise grid whose stride (grid*256 vectors) is a multiple of C/8
 int fixed_channel_grid(int64_t nvec, int C) {
   const int cv = C / 8;
   const int mult = cv / gcd(cv, 256);  // blocks per channel period
-  int g = grid_for(nvec, 256 * 4, 4096);
+  int g = grid_for(nvec, 256 * bn_vpt(), 4096);
   g = (g + mult - 1) / mult * mult;
   return g;
 }
