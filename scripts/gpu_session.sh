@@ -7,7 +7,7 @@
 #   prof     rocprofv3 --kernel-trace --stats over a short bench, summarised by scripts/kstats.py
 #   pmc      PMC passes (MFMA busy, LDS conflicts, HBM bytes) over an eager bench, one run per pass
 #   convs    scripts/conv_bench.py (every ResNet-50 conv pass in isolation)
-#   models   scripts/bench_models.py (LeNet-5, word2vec, char-LSTM)
+#   models   scripts/bench_models.py (LeNet-5, word2vec, char-LSTM; native graphed and stock PyTorch)
 #   dpforce  the DP step on a 1-rank RCCL group under torch.distributed.run, graphed and eager
 set -u
 # R = the tree to run (cwd: the repo root, or the frozen .snap copy of scripts/snap_submit.sh);
@@ -53,9 +53,14 @@ for s in $STEPS; do
       timeout -k 10 400 python scripts/conv_bench.py --out $O/conv_bench.json > $O/conv_bench.log 2>&1
       rc=$?; echo "convs rc=$rc"; tail -3 $O/conv_bench.log; [ $rc -eq 0 ] || exit $rc ;;
     models)
-      timeout -k 10 600 python scripts/bench_models.py > $O/bench_models.jsonl 2> $O/bench_models.err
-      rc=$?; echo "models rc=$rc"; cat $O/bench_models.jsonl; [ $rc -eq 0 ] || { tail -5 $O/bench_models.err; exit $rc; }
-      ;;
+      : > $O/bench_models.jsonl
+      for spec in "lenet5 --graph" "lenet5 --graph --impl torch" "word2vec --graph --batch 128" \
+                  "word2vec --graph --batch 4096" "word2vec --impl torch --batch 4096" "char_lstm --graph" \
+                  "char_lstm --impl torch"; do
+        timeout -k 10 300 python scripts/bench_models.py --model $spec >> $O/bench_models.jsonl 2>> $O/bench_models.err
+        rc=$?; echo "models [$spec] rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/bench_models.err; exit $rc; }
+      done
+      cat $O/bench_models.jsonl ;;
     dpforce)
       for v in 1 0; do
         TFX_DP_FORCE_COLLECTIVE=1 TFX_DP_GRAPH=$v timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
