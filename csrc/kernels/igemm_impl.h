@@ -1297,13 +1297,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
           const int row = q * RPI + lane / WN, col = lane % WN;
           const float v = T[row * WN + (col ^ (((row >> 2) & 1) << 4))];
           const int m = mb + row, n = nb + col;
-#ifdef TFX_PROBE_SPLITK_STORE
-          // cost probe only (csrc/probes/igemm_splitk_probe_store.hip; never in libtfx_ops.so): a plain
-          // store in place of the split-K atomic, to time the atomic epilogue -- results are wrong
-          if (m < a.M && n < a.N) Cf[(int64_t)m * a.ldc + n] = v;
-#else
           if (m < a.M && n < a.N) atomicAdd(Cf + (int64_t)m * a.ldc + n, v);
-#endif
         }
       } else {
 #pragma unroll

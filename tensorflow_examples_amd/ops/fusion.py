@@ -27,7 +27,8 @@ fused_head             pool + FC + softmax-xent + input gradient (head.hip)     
 head_tail              last tail BN applied inside the fused head (TAIL mode)       bn_apply before the head
 bn_finalize_fold       stage 2-4 BN finalize inside the layer-wise apply: every     bn_finalize launch after the
                        block reduces the conv epilogue's few statistics rows         conv (conv_fwd_bn)
-                       itself, the last one re-zeroes them (bn_apply_fin)
+                       itself (bn_apply_fin); the rows live in the store's
+                       gradient scratch, re-zeroed by VariableStore.zero_grad
 =====================  ==========================================================  ===============================
 
 ``TFX_FUSION`` selects a profile at import: ``all`` (default: every group but the opt-in

@@ -171,6 +171,7 @@ class TailPending:
                 torch.ops.tfx.bn_apply_fin_into(self.x, self.res, ws.fin[2], ws.fin[1], *ws.finalize_args,
                                                 True, self.save, self.out, self.mask)
                 ws.fin = None
+                _owed_done(ws)
                 self.fin = None
                 FOLD_FIN_CALLS[0] += 1
             else:
@@ -648,6 +649,7 @@ class BNWorkspace:
             m, nsl, rows = self.fin
             torch.ops.tfx.bn_finalize_rows(rows, nsl, m, *self.finalize_args, save)
             self.fin = None
+            _owed_done(self)
 
 
 class BNBackwardFusion:
@@ -708,8 +710,17 @@ _PENDING_SR: List["BNBackwardFusion"] = []
 _XENT_MEAN_MAX = 1024
 
 
-# BN workspaces whose conv epilogue owed a folded finalize this step (conv_fwd_bn_nofin)
+# BN workspaces whose conv epilogue owed a folded finalize this step (conv_fwd_bn_nofin); an entry
+# leaves the list when its finalize runs (settle_fin / the folded apply), so any training loop that
+# enables the group keeps it bounded, not only ClassifierTrainer's reset
 _OWED_FIN: List["BNWorkspace"] = []
+
+
+def _owed_done(ws: "BNWorkspace") -> None:
+    for i, w in enumerate(_OWED_FIN):
+        if w is ws:
+            del _OWED_FIN[i]
+            return
 
 
 def reset_pending_slot_reductions() -> None:

@@ -63,13 +63,23 @@ class Optimizer:
         """p <- update(p, grad_scale * g); refreshes the bf16 shadow. ``sumsq`` (device scalar
         ||g||^2) enables clip-by-global-norm at ``max_norm``.  ``skip_if`` (a device int32 word, GPU):
         when it is nonzero at execution time the update is skipped ON THE DEVICE -- parameters,
-        moments and shadow unchanged (the persistent LSTM's health word guards its steps this way).
+        moments, shadow and Adam's bias-correction step unchanged (the persistent LSTM's health word guards
+        its steps this way); only the native dense path has that guard, so ``skip_if`` with sparse
+        variables or a CPU store raises.  ``iterations`` (host count of calls) still advances.
         ``grad``: the flat gradient buffer to apply instead of the store's f32 one (same layout; f32 or
         bf16 -- the DP bf16 wire format hands its all-reduced bf16 buffer straight to the kernel)."""
         st = self.store
+        if skip_if is not None and (st.sparse or not _native.use_native(st.master)):
+            # the device-side skip is honoured only by the native dense kernel: refuse rather than apply
+            # an update the caller asked to be skipped (sparse tables / the CPU path have no such guard)
+            raise ValueError("skip_if needs the native dense optimizer (no sparse variables, GPU store)")
         self.iterations += 1
         if self.kind >= ADAM:  # only the bias corrections read the device step counter (one launch less)
-            self.step_t.add_(1.0)
+            if skip_if is not None:
+                # a skipped step must not advance the bias-correction step either: += (skip == 0)
+                self.step_t.add_((skip_if.reshape(-1)[:1] == 0).to(self.step_t.dtype))
+            else:
+                self.step_t.add_(1.0)
         if st.sparse:
             self.apply_sparse(grad_scale)
         if not st.vars:

@@ -37,6 +37,22 @@ import torch.distributed as dist
 from ..variables import ALIGN, Variable, VariableStore
 
 
+def premul_scalar(factor: float, dtype: torch.dtype) -> float:
+    """The Python float to hand ``dist._make_nccl_premul_sum`` so RCCL scales a ``dtype`` buffer by ``factor``.
+
+    On this image (torch 2.10 + RCCL 2.26.6) the pre-multiplied sum of a bf16 buffer reads the LOW 16 bits
+    of the 4-byte float scalar torch passes as the bf16 factor: 2.0f = 0x40000000 becomes bf16 0x0000, so
+    the collective returned zeros (round 4); a float whose low half is bf16 0x4000 scales by exactly 2
+    (measured, ``scripts/diag_premul_bf16.py`` -> ``profiles/r05_dp/diag_premul_bf16.txt``).  For bf16 the
+    scalar is therefore built with the factor's bf16 bits in BOTH halves: read as a float it is the
+    factor to within 2^-7, read as its low half it is exactly bf16(factor) -- right under either
+    interpretation.  Other dtypes get the factor unchanged."""
+    if dtype != torch.bfloat16:
+        return float(factor)
+    b = int(torch.tensor([factor], dtype=torch.bfloat16).view(torch.int16).item()) & 0xFFFF
+    return float(torch.tensor([(b << 16) | b], dtype=torch.int64).to(torch.int32).view(torch.float32).item())
+
+
 class GradAllReduce:
     def __init__(self, store: VariableStore, bucket_bytes: int = 32 << 20, group=None, overlap: bool = True,
                  compress_bf16: bool = False, tail_bytes: int = 2 << 20, force_collective: Optional[bool] = None,
@@ -46,7 +62,8 @@ class GradAllReduce:
         # premul: RCCL pre-multiplied sum (each rank's bucket scaled by `premul` inside the
         # collective).  Used by the GPU tests to make a 1-rank collective observable: a bucket whose
         # all-reduce was dropped, or ran before its gradient was written, then shows up as a wrong
-        # (unscaled) gradient.
+        # (unscaled) gradient.  With the bf16 wire the scalar is encoded by premul_scalar (RCCL reads a
+        # bf16 factor from the float's low half on this image).
         self.premul = premul
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         # issue the collectives even at world size 1 (TFX_DP_FORCE_COLLECTIVE=1): lets a one-GPU box
@@ -144,7 +161,8 @@ class GradAllReduce:
             # before forking the launch stream (a forked, never-joined stream would stay capturing)
             raise RuntimeError("HIP graph capture of the DP step needs the nccl (RCCL) backend, not %s"
                                % dist.get_backend(self.group))
-        op = dist.ReduceOp.SUM if self.premul is None else dist._make_nccl_premul_sum(float(self.premul))
+        op = dist.ReduceOp.SUM if self.premul is None else \
+            dist._make_nccl_premul_sum(premul_scalar(self.premul, torch.bfloat16 if self.compress else view.dtype))
         # issued from the compute stream right after the bucket's last gradient kernel: RCCL runs it
         # on its own stream, ordered after that kernel, beside the rest of backward
         if self.compress:

@@ -91,12 +91,17 @@ def _varint_field(field: int, v: int) -> bytes:
     return _varint(field << 3) + _varint(int(v))
 
 
-def saver_def(max_to_keep: int = 5) -> bytes:
-    """SaverDef { filename_tensor_name, save_tensor_name, restore_op_name, max_to_keep, sharded,
-    keep_checkpoint_every_n_hours, version: V2 } with the names TF1's default Saver uses."""
+def saver_def(max_to_keep: int = 5, sharded: bool = False) -> bytes:
+    """SaverDef { filename_tensor_name, save_tensor_name, restore_op_name, max_to_keep, [sharded],
+    keep_checkpoint_every_n_hours, version: V2 } with the names TF1's default (non-sharded) Saver uses --
+    the one the Supervisor builds; ``sharded`` is written only when set (proto3 default false).
+
+    The ``.meta`` / ``saved_model.pb`` these go into are STRUCTURAL protobufs (field numbers and names of
+    TF1's MetaGraphDef / SavedModel, read back by this package's own parsers): their GraphDef nodes carry
+    no dtype/shape attrs and no ``save/*`` ops, so TensorFlow itself could not import them as graphs."""
     return (_bytes_field(1, b"save/Const:0") + _bytes_field(2, b"save/control_dependency:0") +
-            _bytes_field(3, b"save/restore_all") + _varint_field(4, max_to_keep) + _varint_field(5, 1) +
-            b"\x35" + struct.pack("<f", 10000.0) + _varint_field(7, 2))
+            _bytes_field(3, b"save/restore_all") + _varint_field(4, max_to_keep) +
+            (_varint_field(5, 1) if sharded else b"") + b"\x35" + struct.pack("<f", 10000.0) + _varint_field(7, 2))
 
 
 def variable_def(name: str, trainable: bool = True) -> bytes:

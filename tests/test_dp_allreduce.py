@@ -168,3 +168,18 @@ def test_dp_bf16_wire_format_vs_f32_reduce():
     d32, d16 = res[False] - st.master, res[True] - st.master
     rel = ((d16 - d32).norm() / d32.norm()).item()
     assert 0 < rel < 2e-2, rel
+
+
+def test_premul_scalar_encoding():
+    """premul_scalar: f32 buffers get the factor as is; for bf16 the float carries bf16(factor) in both
+    16-bit halves, so RCCL's low-half read (this image) and a float read both give the factor."""
+    import struct
+
+    from tensorflow_examples_amd.parallel.allreduce import premul_scalar
+    assert premul_scalar(2.0, torch.float32) == 2.0
+    for f in (2.0, 0.5, 3.0, 1.0, 0.125):
+        v = premul_scalar(f, torch.bfloat16)
+        bits = struct.unpack("<I", struct.pack("<f", v))[0]
+        lo = torch.tensor([bits & 0xFFFF], dtype=torch.int32).to(torch.int16).view(torch.bfloat16).item()
+        assert lo == f and (bits >> 16) == (bits & 0xFFFF), (f, hex(bits))
+        assert abs(v - f) <= f * 2 ** -7, (f, v)

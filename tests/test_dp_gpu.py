@@ -136,11 +136,12 @@ for mode in ("ref", "eager", "graphed"):
     w0 = store.master.clone()
     dp = None
     if mode != "ref":
-        # bf16 wire: a plain SUM (RCCL's pre-multiplied sum on a bf16 buffer returned zeros here), so the
-        # 1-rank collective is the identity and a dropped / early bucket shows as a stale (zero) cast
-        dp = GradAllReduce(store, bucket_bytes=BUCKET, premul=None if BF16 else 2.0, compress_bf16=BF16)
+        # bf16 wire too: a pre-multiplied sum by 2 (its scalar encoded by premul_scalar -- RCCL reads a bf16
+        # factor from the float's low half), so every 1-rank collective doubles its bucket and a dropped,
+        # early or un-cast bucket shows as half the update
+        dp = GradAllReduce(store, bucket_bytes=BUCKET, premul=2.0, compress_bf16=BF16)
         assert dp.force and len(dp.buckets) > 2
-    lr = 0.02 if (mode == "ref" or BF16) else 0.01
+    lr = 0.02 if mode == "ref" else 0.01
     opt = MomentumOptimizer(store, lr, momentum=0.9)
     tr = ClassifierTrainer(store, model, opt, dp)
     if mode == "graphed":
@@ -164,9 +165,10 @@ for mode in ("eager", "graphed"):
     worst = max(((d[lo:hi] - ref[lo:hi]).norm() / ref[lo:hi].norm()).item() for lo, hi in buckets
                 if ref[lo:hi].norm() > 0)
     print("REL", mode, rel, "worst_bucket", worst, "buckets", len(buckets), flush=True)
-    # run-to-run floor ~3e-3 (f32 atomic order); bf16 on the wire adds 8-bit rounding (rel ~ 2^-9 per
-    # element).  A dropped or early collective leaves its bucket at half the update: rel ~0.5
-    lim = (2e-2, 5e-2) if BF16 else (1e-2, 3e-2)
+    # run-to-run floor (f32 atomic order) grows with depth and batch; bf16 on the wire adds 8-bit rounding
+    # (rel ~ 2^-9 per element).  A dropped or early collective leaves its bucket at half the update: rel ~0.5.
+    # The depth-18 / batch-16 f32 case keeps the tight bounds a partly stale bucket would break.
+    lim = (2e-2, 5e-2) if BF16 else ((1e-2, 3e-2) if DEPTH >= 50 else (2e-3, 1e-2))
     assert rel < lim[0] and worst < lim[1], (mode, rel, worst)
 dist.destroy_process_group()
 """
@@ -195,3 +197,37 @@ def test_dp_graph_capture_rccl_one_rank(gpu, tmp_path, depth, batch, bf16, bucke
     print(p.stdout, p.stderr[-3000:])
     assert p.returncode == 0, p.stderr[-3000:]
     assert "REL" in p.stdout
+
+
+PREMUL_WORKER = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"])
+from tensorflow_examples_amd.parallel.allreduce import premul_scalar
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+for dt in (torch.float32, torch.bfloat16):
+    for f in (2.0, 0.5, 3.0):
+        x = torch.ones(4096, dtype=dt, device="cuda")
+        dist.all_reduce(x, op=dist._make_nccl_premul_sum(premul_scalar(f, dt)))
+        torch.cuda.synchronize()
+        vals = x.float().unique().tolist()
+        print("PREMUL", dt, f, vals, flush=True)
+        assert vals == [f], (dt, f, vals)
+dist.destroy_process_group()
+"""
+
+
+def test_premul_bf16_scalar_encoding_rccl(gpu, tmp_path):
+    """RCCL's pre-multiplied sum on f32 and bf16 buffers scales by exactly the requested factor through
+    premul_scalar (a plain float factor on a bf16 buffer is read from its low 16 bits: 2.0 -> zeros)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    script = tmp_path / "p.py"
+    script.write_text(PREMUL_WORKER)
+    env = dict(os.environ, ROOT=ROOT, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port))
+    p = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=200)
+    print(p.stdout, p.stderr[-2000:])
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.stdout.count("PREMUL") == 6
