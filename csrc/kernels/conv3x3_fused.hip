@@ -30,6 +30,16 @@ constexpr int C3_WTAP = C3_C * 128;                                         // o
 constexpr int C3_PIECES = C3_HP * 8;                                        // 16-B halo pieces
 constexpr int C3_PPT = (C3_PIECES + PW_NT - 1) / PW_NT;                     // per thread (4)
 
+// v zeroed where !keep, as a bit mask on the packed words: a per-element `keep ? x : 0` on the staged
+// halo compiles to one exec-masked branch per element, and every such branch makes the waitcnt pass
+// wait for the loads at its join (the next tile's halo included) -- padding pixels are zeroed after
+// the BN transform (relu(0 sc + sh) is not 0) with straight-line code instead
+__device__ __forceinline__ U4 mask_u4(U4 v, bool keep) {
+  const uint32_t m = 0u - (uint32_t)keep;
+  v.x &= m; v.y &= m; v.z &= m; v.w &= m;
+  return v;
+}
+
 // PROBE (cost probes only, csrc/probes/conv3x3_probe.hip; production = 0): bit 0 skips the MFMAs, bit 1 the
 // BN transform of the staged halo (raw copy), bit 2 the epilogue stores / statistics
 template <int PROBE = 0>
@@ -84,20 +94,19 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
       float f[8];
       unpack8(__builtin_bit_cast(U4, s.v[i]), f);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) f[k] = in ? fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f) : 0.f;
+      for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f);
       if constexpr (PROBE & 2) *reinterpret_cast<pw_u32x4*>(img + pw_kmaj(hp, hch)) = s.v[i];
-      else *reinterpret_cast<U4*>(img + pw_kmaj(hp, hch)) = pack8(f);
+      else *reinterpret_cast<U4*>(img + pw_kmaj(hp, hch)) = mask_u4(pack8(f), in);
     }
   };
   // wave tile: output row r = wv & 3 of the tile (32 pixels = 2 m-tiles), 32 output channels (wv >> 2)
   const int wr = wv & 3, wcb = 32 * (wv >> 2);
-  float bs[2][4], bq[2][4];
+  // BN statistics of the lane's 8 output channels (after the epilogue's lane pairing, below)
+  float bs[8], bq[8];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bs[j][r] = bq[j][r] = 0.f;
-  auto compute = [&](const char* img, int tile) {
-    f32x4_t acc[2][2];
+  for (int k = 0; k < 8; ++k) bs[k] = bq[k] = 0.f;
+  const int ecol = wcb + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5);
+  auto mfma = [&](const char* img, f32x4_t (&acc)[2][2]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -126,29 +135,45 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
         }
       }
     }
+  };
+  // epilogue: y (bf16) + BN statistics of the stored values.  v_permlane16_swap pairs the lane's two
+  // 16-column tiles so each lane holds 8 consecutive channels of one pixel: one 16-byte store per pixel
+  // group (16 pixels x 64 contiguous bytes per wave-instruction) instead of two 8-byte ones
+  auto epi = [&](const f32x4_t (&acc)[2][2], int tile) {
     if constexpr (PROBE & 4) {
-      if (acc[0][0][0] == 12345.f) bs[0][0] += 1.f;  // keep the loop live
+      if (acc[0][0][0] == 12345.f) bs[0] += 1.f;  // keep the loop live
       return;
     }
-    // epilogue: y (bf16, 8-byte stores) + BN statistics of the stored values
     const int n = tile / tiles_img, y0 = (tile % tiles_img) * C3_TR;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int pix = (n * a.H + y0 + wr) * C3_IW + 16 * i + (lane & 15);
+      float o[8];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wcb + 16 * j + (lane >> 4) * 4;
-        const uint32_t lo = pack_bf16x2(acc[i][j][0], acc[i][j][1]), hi = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-        __builtin_amdgcn_raw_buffer_store_b64((pw_u32x2){lo, hi}, ry, (uint32_t)(pix * C3_C + col) * 2u, 0, 0);
-        const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u), __uint_as_float(hi << 16),
-                            __uint_as_float(hi & 0xffff0000u)};
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][0][r]), __float_as_uint(acc[i][1][r]),
+                                                         false, false);
+        o[r] = __uint_as_float(sw[0]);
+        o[4 + r] = __uint_as_float(sw[1]);
+      }
+      const U4 packed = pack8(o);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pw_u32x4, packed), ry,
+                                             (uint32_t)(pix * C3_C + ecol) * 2u, 0, 0);
+      float v[8];
+      unpack8(packed, v);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          bs[j][r] += v[r];
-          bq[j][r] = fmaf(v[r], v[r], bq[j][r]);
-        }
+      for (int k = 0; k < 8; ++k) {
+        bs[k] += v[k];
+        bq[k] = fmaf(v[k], v[k], bq[k]);
       }
     }
+  };
+  // (measured: waves 4-7 running each tile's epilogue one tile late, beside their partners' MFMAs, was
+  // 4 % slower than this lockstep order -- profiles/r05_conv3)
+  auto compute = [&](const char* img, int tile) {
+    f32x4_t acc[2][2];
+    mfma(img, acc);
+    epi(acc, tile);
   };
   auto sync = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -174,16 +199,13 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
   // ---- BN statistics: sum the 16 rows of each DPP row, one atomic pair per column per wave
   float* slots = a.slots + (size_t)(blockIdx.x % NSLOT) * 2 * C3_C;
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float s = row16_sum(bs[j][r]), q = row16_sum(bq[j][r]);
-      if ((lane & 15) == 0) {
-        const int c = wcb + 16 * j + (lane >> 4) * 4 + r;
-        atomicAdd(slots + c, s);
-        atomicAdd(slots + C3_C + c, q);
-      }
+  for (int k = 0; k < 8; ++k) {
+    const float s = row16_sum(bs[k]), q = row16_sum(bq[k]);
+    if ((lane & 15) == 0) {
+      atomicAdd(slots + ecol + k, s);
+      atomicAdd(slots + C3_C + ecol + k, q);
     }
+  }
 }
 
 // ---------------------------------------------------------------------------------------- backward
@@ -285,10 +307,10 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float gg = fmaf(y2[k], s2[k], h2[k]) > 0.f ? g[k] : 0.f;
-          g[k] = in ? fmaf(cA[k], gg, fmaf(cB[k], y2[k], cD[k])) : 0.f;
+          g[k] = fmaf(cA[k], gg, fmaf(cB[k], y2[k], cD[k]));
         }
         if constexpr (PROBE & 4) *reinterpret_cast<pw_u32x4*>(timg + pw_kmaj(hp, hch)) = st.g[i];
-        else *reinterpret_cast<U4*>(timg + pw_kmaj(hp, hch)) = pack8(g);
+        else *reinterpret_cast<U4*>(timg + pw_kmaj(hp, hch)) = mask_u4(pack8(g), in);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -306,9 +328,9 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
         float y1[8];
         unpack8(__builtin_bit_cast(U4, st.y1[i]), y1);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) y1[k] = in ? fmaxf(fmaf(y1[k], s1[k], h1[k]), 0.f) : 0.f;
+        for (int k = 0; k < 8; ++k) y1[k] = fmaxf(fmaf(y1[k], s1[k], h1[k]), 0.f);
         if constexpr (PROBE & 4) *reinterpret_cast<pw_u32x4*>(aimg + pw_kmaj(hp, hch)) = st.y1[i];
-        else *reinterpret_cast<U4*>(aimg + pw_kmaj(hp, hch)) = pack8(y1);
+        else *reinterpret_cast<U4*>(aimg + pw_kmaj(hp, hch)) = mask_u4(pack8(y1), in);
         // raw y1 of the tile interior; border pixels go to a trash slot past the image (no branch)
         const bool inner = ((unsigned)(hy - 1) < (unsigned)C3_TR) & ((unsigned)(hx - 1) < (unsigned)C3_IW);
         *reinterpret_cast<pw_u32x4*>(yimg + (inner ? pw_kmaj((hy - 1) * C3_IW + hx - 1, hch) : C3_YBYTES)) = st.y1[i];
@@ -327,89 +349,93 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
 #pragma unroll
     for (int nn = 0; nn < 9; ++nn) accw[m][nn] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int tile) {
-    // ---- data gradient: dA1[px][ci] = sum over taps of dy2(px + (1 - ky, 1 - kx)) . W[:, tap, ci]
-    {
-      f32x4_t acc[2][2];
+  // ---- data gradient: dA1[px][ci] = sum over taps of dy2(px + (1 - ky, 1 - kx)) . W[:, tap, ci]
+  auto dgrad_mfma = [&](f32x4_t (&acc)[2][2]) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-      for (int ky = 0; ky < 3; ++ky)
+    for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int tap = 3 * ky + kx;
+    for (int kx = 0; kx < 3; ++kx) {
+      const int tap = 3 * ky + kx;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          bf16x8_t fa[2], fb[2];
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8_t fa[2], fb[2];
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int hp = (wr + 2 - ky) * C3_HW + 16 * i + (lane & 15) + 2 - kx;
-            fa[i] = *(const pw_lds_bf16x8*)((pw_lds_char*)timg + pw_kmaj(hp, 4 * kk + (lane >> 4)));
-          }
+        for (int i = 0; i < 2; ++i) {
+          const int hp = (wr + 2 - ky) * C3_HW + 16 * i + (lane & 15) + 2 - kx;
+          fa[i] = *(const pw_lds_bf16x8*)((pw_lds_char*)timg + pw_kmaj(hp, 4 * kk + (lane >> 4)));
+        }
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            fb[j] = pw_frag_tr(wimg, tap * C3_WTAP + 32 * kk * 128, dcb + 16 * j, lane,
-                               [](int r, int c) { return pw_mn<64>(r, c); });
-          if constexpr (!(PROBE & 1)) {
+        for (int j = 0; j < 2; ++j)
+          fb[j] = pw_frag_tr(wimg, tap * C3_WTAP + 32 * kk * 128, dcb + 16 * j, lane,
+                             [](int r, int c) { return pw_mn<64>(r, c); });
+        if constexpr (!(PROBE & 1)) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-              for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-          } else {
-            acc[0][0][0] += (float)fa[0][0] + (float)fb[0][0] + (float)fa[1][0] + (float)fb[1][0];
-          }
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        } else {
+          acc[0][0][0] += (float)fa[0][0] + (float)fb[0][0] + (float)fa[1][0] + (float)fb[1][0];
         }
       }
-      if constexpr (PROBE & 8) {
-        if (acc[0][0][0] == 12345.f) bnacc[0] = 1.f;  // keep the loop live
-      } else {
-      // epilogue: dA1 (bf16, 8-byte stores) + BN1 backward partials (ReLU mask from y1 sc1 + sh1 > 0)
+    }
+  };
+  // epilogue: dA1 (bf16) + BN1 backward partials (ReLU mask from y1 sc1 + sh1 > 0).  v_permlane16_swap
+  // pairs the lane's two 16-column tiles so each lane holds 8 CONSECUTIVE channels of one pixel: one
+  // 16-byte store per pixel group (a wave-instruction writes 16 pixels x 64 contiguous bytes) instead of
+  // two 8-byte ones.  The partials are sum g' and sum g' y1 (xhat is affine in y1: centred and scaled
+  // once per block, below) -- two coefficients per channel live here instead of four.
+  auto dgrad_epi = [&](const f32x4_t (&acc)[2][2], int tile) {
+    if constexpr (PROBE & 8) {
+      if (acc[0][0][0] == 12345.f) bnacc[0] = 1.f;  // keep the loop live
+    } else {
       const int n = tile / tiles_img, y0 = (tile % tiles_img) * C3_TR;
-      float bs[2][4], bq[2][4];  // this tile's BN1 partials of the lane's 8 columns
+      const int g = lane >> 4, col = dcb + 16 * (g & 1) + 8 * (g >> 1);
+      float bs[8], bq[8];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bs[j][r] = bq[j][r] = 0.f;
+      for (int k = 0; k < 8; ++k) bs[k] = bq[k] = 0.f;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int lpx = wr * C3_IW + 16 * i + (lane & 15);
         const int pix = (n * a.H + y0 + wr) * C3_IW + 16 * i + (lane & 15);
+        float o[8];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = dcb + 16 * j + (lane >> 4) * 4;
-          const uint32_t lo = pack_bf16x2(acc[i][j][0], acc[i][j][1]), hi = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-          __builtin_amdgcn_raw_buffer_store_b64((pw_u32x2){lo, hi}, rdx, (uint32_t)(pix * C3_C + col) * 2u, 0, 0);
-          const pw_u32x2 yv = *reinterpret_cast<const pw_u32x2*>(yimg + pw_kmaj(lpx, col >> 3) + ((col >> 2) & 1) * 8);
-          const float y1[4] = {__uint_as_float(yv[0] << 16), __uint_as_float(yv[0] & 0xffff0000u),
-                               __uint_as_float(yv[1] << 16), __uint_as_float(yv[1] & 0xffff0000u)};
-          const float gv[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u), __uint_as_float(hi << 16),
-                               __uint_as_float(hi & 0xffff0000u)};
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][0][r]), __float_as_uint(acc[i][1][r]),
+                                                           false, false);
+          o[r] = __uint_as_float(sw[0]);
+          o[4 + r] = __uint_as_float(sw[1]);
+        }
+        const U4 packed = pack8(o);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pw_u32x4, packed), rdx,
+                                               (uint32_t)(pix * C3_C + col) * 2u, 0, 0);
+        float y1[8], gv[8];
+        unpack8(*reinterpret_cast<const U4*>(yimg + pw_kmaj(lpx, col >> 3)), y1);
+        unpack8(packed, gv);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int c = col + r;
-            const float gp = fmaf(y1[r], coef[5 * C3_C + c], coef[6 * C3_C + c]) > 0.f ? gv[r] : 0.f;
-            bs[j][r] += gp;
-            bq[j][r] = fmaf(gp, fmaf(y1[r], coef[7 * C3_C + c], coef[8 * C3_C + c]), bq[j][r]);
-          }
+        for (int k = 0; k < 8; ++k) {
+          const int c = col + k;
+          const float gp = fmaf(y1[k], coef[5 * C3_C + c], coef[6 * C3_C + c]) > 0.f ? gv[k] : 0.f;
+          bs[k] += gp;
+          bq[k] = fmaf(gp, y1[k], bq[k]);
         }
       }
       // the 16 rows of each DPP row share columns: reduce, one LDS float atomic per column and wave
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float sv = row16_sum(bs[j][r]), qv = row16_sum(bq[j][r]);
-          if ((lane & 15) == 0) {
-            const int c = dcb + 16 * j + (lane >> 4) * 4 + r;
-            atomicAdd(&bnacc[c], sv);
-            atomicAdd(&bnacc[C3_C + c], qv);
-          }
+      for (int k = 0; k < 8; ++k) {
+        const float sv = row16_sum(bs[k]), qv = row16_sum(bq[k]);
+        if ((lane & 15) == 0) {
+          atomicAdd(&bnacc[col + k], sv);
+          atomicAdd(&bnacc[C3_C + col + k], qv);
         }
       }
     }
-    // ---- weight gradient: dW[co][tap][ci] += sum over the tile's pixels of dy2[px][co] a1[px + tap - 1][ci]
+  };
+  // ---- weight gradient: dW[co][tap][ci] += sum over the tile's pixels of dy2[px][co] a1[px + tap - 1][ci]
+  auto wgrad = [&]() {
 #pragma unroll 1
     for (int r = 0; r < C3_TR; ++r) {  // k-step = one output row (32 pixels)
       const int hp0 = (r + 1) * C3_HW + 1;
@@ -441,6 +467,14 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
         __builtin_amdgcn_sched_barrier(0);  // bound the fragment reads hoisted ahead
       }
     }
+  };
+  // (measured: placing the epilogue of waves 4-7 after half the weight-gradient k-steps, so SIMD partners
+  // reach it at different times, was 3 % slower than this lockstep order -- profiles/r05_conv3)
+  auto compute = [&](int tile) {
+    f32x4_t acc[2][2];
+    dgrad_mfma(acc);
+    dgrad_epi(acc, tile);
+    wgrad();
   };
   auto sync = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -476,9 +510,14 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
       for (int nn = 0; nn < 9; ++nn)
         *reinterpret_cast<f32x4_t*>(slab + ((size_t)(m * 9 + nn) * PW_NT + t) * 4) = accw[m][nn];
   }
-  // ---- BN1 partials of the block -> its slot (one global atomic per value)
+  // ---- BN1 partials of the block -> its slot (one global atomic per value); the block summed g' and
+  // g' y1, so sum g' xhat = is1 (sum g' y1) - mu1 is1 (sum g')
   __syncthreads();
-  if (t < 2 * C3_C) atomicAdd(a.slots1 + (size_t)(blockIdx.x % NSLOT) * 2 * C3_C + t, bnacc[t]);
+  if (t < 2 * C3_C) {
+    const int c = t & (C3_C - 1);
+    const float v = t < C3_C ? bnacc[t] : fmaf(coef[7 * C3_C + c], bnacc[t], coef[8 * C3_C + c] * bnacc[c]);
+    atomicAdd(a.slots1 + (size_t)(blockIdx.x % NSLOT) * 2 * C3_C + t, v);
+  }
 }
 
 }  // namespace

@@ -4,6 +4,7 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 timeout -k 10 300 python -u scripts/dev/conv3x3_probe.py > gpurun_out/conv3x3_probe.txt 2>&1
 rc=$?; echo "probe rc=$rc"; cat gpurun_out/conv3x3_probe.txt; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29611 \
-  scripts/diag_premul_bf16.py > gpurun_out/diag_premul_bf16.txt 2>&1
-rc=$?; echo "premul rc=$rc"; grep '{' gpurun_out/diag_premul_bf16.txt; exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_conv3_fused_gpu.py tests/test_resnet50_train_gpu.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/pytest_c3.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_c3.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench.log; exit $rc
