@@ -1707,9 +1707,26 @@ Tensor image_normalize(Tensor x, std::vector<double> mean, std::vector<double> s
 // (data/pipeline.py PinnedRing(zero_copy=True) orders that with an event per slot).
 // Training augmentation (pad-`pad` random crop + flip; offsets [N][3] int32 = ox, oy, flip on the
 // device) fused with the uint8 -> normalised bf16 conversion: returns [N][H][W][cout]
+void augment_normalize_into(Tensor x, Tensor offsets, std::vector<double> mean, std::vector<double> stdv, int64_t pad,
+                            Tensor y);
+
 Tensor augment_normalize(Tensor x, Tensor offsets, std::vector<double> mean, std::vector<double> stdv, int64_t cout,
                          int64_t pad) {
-  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_DEV(offsets); CHECK_CONTIG(offsets);
+  CHECK_DEV(x);
+  auto y = at::empty({x.size(0), x.size(1), x.size(2), cout}, x.options().dtype(at::kBFloat16));
+  augment_normalize_into(x, offsets, mean, stdv, pad, y);
+  return y;
+}
+
+// the same into a preallocated bf16 NHWC tensor (e.g. a captured training graph's static input: the batch
+// is written where the graph reads it, no copy)
+void augment_normalize_into(Tensor x, Tensor offsets, std::vector<double> mean, std::vector<double> stdv, int64_t pad,
+                            Tensor y) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_DEV(offsets); CHECK_CONTIG(offsets); CHECK_DEV(y); CHECK_CONTIG(y);
+  CHECK_BF16(y);
+  const int64_t cout = y.dim() == 4 ? y.size(3) : 0;
+  TORCH_CHECK(y.dim() == 4 && x.dim() == 4 && y.size(0) == x.size(0) && y.size(1) == x.size(1) && y.size(2) == x.size(2),
+              "augment_normalize: output [N][H][W][cout] of the image batch's size");
   TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4, "augment_normalize: uint8 NHWC images");
   TORCH_CHECK(offsets.scalar_type() == at::kInt && offsets.dim() == 2 && offsets.size(0) == x.size(0) &&
                   offsets.size(1) == 3, "augment_normalize: offsets [N][3] int32");
@@ -1718,7 +1735,6 @@ Tensor augment_normalize(Tensor x, Tensor offsets, std::vector<double> mean, std
               "augment_normalize: 1..4 channels with per-channel mean/std");
   TORCH_CHECK(cout == 4 || cout == 8, "augment_normalize: cout 4 or 8");
   TORCH_CHECK(pad >= 0 && pad < 64, "augment_normalize: pad");
-  auto y = at::empty({x.size(0), x.size(1), x.size(2), cout}, x.options().dtype(at::kBFloat16));
   float m[4] = {0, 0, 0, 0}, sd[4] = {1, 1, 1, 1};
   for (int64_t c = 0; c < cin; ++c) {
     m[c] = (float)mean[c];
@@ -1726,7 +1742,6 @@ Tensor augment_normalize(Tensor x, Tensor offsets, std::vector<double> mean, std
   }
   tfx::augment_normalize(x.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)cin, (int)cout,
                          (int)pad, offsets.data_ptr<int32_t>(), m, sd, bfm(y), cur_stream());
-  return y;
 }
 
 // End a capture left open on `stream` (a side stream forked into a HIP-graph capture that failed
@@ -1797,6 +1812,8 @@ TORCH_LIBRARY(tfx, m) {
   m.def("image_normalize", &image_normalize);
   m.def("image_normalize_into", &image_normalize_into);
   m.def("augment_normalize", &augment_normalize);
+  m.def("augment_normalize_into(Tensor x, Tensor offsets, float[] mean, float[] stdv, int pad, Tensor(a!) y) -> ()",
+        &augment_normalize_into);
   m.def("end_stream_capture", &end_stream_capture);
   m.def("philox_fill", &philox_fill);
   m.def("maxpool_fwd", &maxpool_fwd);

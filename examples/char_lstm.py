@@ -6,7 +6,9 @@ across windows (truncated BPTT), stacked LSTM layers with the four gates in one 
 softmax projection, SGD with clip_by_global_norm and LR decay after ``--max_epoch`` epochs.  One
 process per GPU under torchrun: each rank takes its own slice of the batch rows; gradients are
 all-reduced in buckets overlapped with backward.  Text from ``--data_path`` when present, else a
-synthetic order-2 Markov character stream.
+synthetic order-2 Markov character stream.  ``--logs_path`` writes cost / perplexity scalars and the
+graph to an event file, ``--logdir`` checkpoints periodically and resumes (utils/runlog.py; the
+reference's conventions, R/distributed/distributed.py:120-138).
 
     torchrun --nproc-per-node 4 --master-addr 127.0.0.1 examples/char_lstm.py --batch_size=64
 """
@@ -22,12 +24,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from tensorflow_examples_amd import app  # noqa: E402
-from tensorflow_examples_amd.ckpt import Saver  # noqa: E402
 from tensorflow_examples_amd.data.text import CharCorpus, ptb_batches, synthetic_char_ids  # noqa: E402
 from tensorflow_examples_amd.data.pipeline import DevicePrefetcher  # noqa: E402
 from tensorflow_examples_amd.models.char_lstm import LMTrainer, build_char_lstm  # noqa: E402
 from tensorflow_examples_amd.optim import GradientDescentOptimizer  # noqa: E402
 from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed  # noqa: E402
+from tensorflow_examples_amd.utils import runlog  # noqa: E402
 
 flags = app.flags
 flags.DEFINE_string("data_path", "", "text file to model (synthetic character stream if absent)")
@@ -43,7 +45,8 @@ flags.DEFINE_integer("max_max_epoch", 6, "total epochs")
 flags.DEFINE_float("max_grad_norm", 5.0, "clip_by_global_norm bound")
 flags.DEFINE_integer("max_steps", 0, "stop after N steps (0 = full epochs)")
 flags.DEFINE_integer("synthetic_chars", 2000000, "synthetic stream length")
-flags.DEFINE_string("logdir", "", "checkpoint directory")
+flags.DEFINE_integer("log_every", 50, "print / log scalars every N steps")
+runlog.define_flags(flags)
 FLAGS = flags.FLAGS
 
 
@@ -63,33 +66,40 @@ def main(_):
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     store, model = build_char_lstm(dev, vocab_size=vocab, embed=FLAGS.embed_size, hidden=FLAGS.hidden_size,
                                    layers=FLAGS.num_layers, dtype=dtype, seed=0)
-    broadcast_variables(store)
     opt = GradientDescentOptimizer(store, FLAGS.learning_rate)
+    log = runlog.RunLog(store, opt, FLAGS.logs_path, FLAGS.logdir, FLAGS.save_checkpoint_steps, rank=rank)
+    start = log.restore()  # every rank restores; the broadcast below keeps them identical
+    broadcast_variables(store)
     dp = GradAllReduce(store) if world > 1 else None
     trainer = LMTrainer(model, opt, dp, FLAGS.max_grad_norm)
     if rank == 0:
         print("char-LSTM: vocab %d, %d x %d LSTM, %d params, %d GPU(s)" %
               (vocab, FLAGS.num_layers, FLAGS.hidden_size, store.num_params(), world))
     B, T = FLAGS.batch_size, FLAGS.num_steps
-    step, tokens, t0 = 0, 0, time.time()
-    for ep in range(FLAGS.max_max_epoch):
+    steps_per_epoch = max(1, (len(train) // (B * world) - 1) // T)
+    step, tokens, t0 = start, 0, time.time()
+    for ep in range(start // steps_per_epoch, FLAGS.max_max_epoch):
         opt.set_learning_rate(FLAGS.learning_rate * FLAGS.lr_decay ** max(ep + 1 - FLAGS.max_epoch, 0))
         state, costs, iters = None, 0.0, 0
         # global batch = B * world rows; rank r trains rows [r*B, (r+1)*B).  Windows reach the GPU
-        # through the pinned ring (async H2D on a copy stream, two windows ahead of the step)
+        # through the pinned ring (async H2D on a copy stream, two windows ahead of the step).  A resumed
+        # run skips the windows of the epoch its checkpoint had already trained on
+        skip = step - ep * steps_per_epoch
         shard = ((x[:, rank * B:(rank + 1) * B], y[:, rank * B:(rank + 1) * B])
-                 for x, y in ptb_batches(train, B * world, T))
+                 for k, (x, y) in enumerate(ptb_batches(train, B * world, T)) if k >= skip)
         for xs, ys in DevicePrefetcher(shard, dev, depth=2):
             loss, state = trainer.step(xs, ys, state)
             step += 1
             tokens += B * T * world
-            if step % 50 == 0:
+            if step % FLAGS.log_every == 0:
                 costs += float(loss)
                 iters += 1
                 trainer.check()  # a timed-out persistent-LSTM hand-off: steps skipped, per-step kernels from here
                 if rank == 0:
                     print("epoch %d step %d perplexity %.3f  %.0f tokens/sec" %
                           (ep + 1, step, math.exp(costs / iters), tokens / (time.time() - t0)), flush=True)
+                    log.scalars(step, cost=float(loss), perplexity=math.exp(float(loss)))
+            log.maybe_save(step)
             if FLAGS.max_steps and step >= FLAGS.max_steps:
                 break
         if FLAGS.max_steps and step >= FLAGS.max_steps:
@@ -108,9 +118,11 @@ def main(_):
             vn += 1
     if rank == 0:
         print("valid perplexity %.3f" % math.exp(vcost / max(vn, 1)))
-        print("tokens/sec (all GPUs) %.1f" % (tokens / dt))
-        if FLAGS.logdir:
-            print("saved", Saver().save(store, os.path.join(FLAGS.logdir, "model.ckpt"), global_step=step))
+        print("tokens/sec (all GPUs) %.1f" % (tokens / max(dt, 1e-9)))
+        log.scalars(step, valid_perplexity=math.exp(vcost / max(vn, 1)))
+    saved = log.close(step)
+    if saved:
+        print("saved", saved)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

@@ -2,8 +2,13 @@
 
 One process per GPU (launch with torchrun), RCCL bucketed all-reduce overlapped with backward,
 fused momentum SGD with weight decay and a step-wise LR schedule, on-device augmentation
-(pad-4 random crop + flip), host->HBM double-buffered prefetch, per-epoch test accuracy and
-checkpoints (rank 0).  CIFAR-10 binary files from ``--data_dir`` when present, else synthetic.
+(pad-4 random crop + flip, written straight into the captured graph's static input), host->HBM
+double-buffered prefetch, per-epoch test accuracy, TensorBoard scalars (``--logs_path``: cost,
+accuracy, learning rate, test accuracy) and periodic checkpoints with resume (``--logdir``,
+``--save_checkpoint_steps``; rank 0 writes) -- the reference's conventions
+(R/distributed/distributed.py:120-138, Supervisor :129-131; utils/runlog.py).  CIFAR-10 binary files
+from ``--data_dir`` when present, else synthetic.  The reported images/sec is the steady state: the
+graph-capture step (with its warm-up) and the evaluations are timed apart.
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/resnet_cifar.py --depth=50 --batch_size=256
 """
@@ -18,15 +23,15 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from tensorflow_examples_amd import app, ops  # noqa: E402
-from tensorflow_examples_amd.ckpt import (Saver, export_saved_model, latest_checkpoint, store_graph_nodes,  # noqa: E402
-                                          write_graph)
-from tensorflow_examples_amd.data.cifar import augment_model_input, load_cifar10  # noqa: E402
+from tensorflow_examples_amd.ckpt import export_saved_model  # noqa: E402
+from tensorflow_examples_amd.data.cifar import augment_model_input, hard_synthetic_cifar, load_cifar10  # noqa: E402
 from tensorflow_examples_amd.data.pipeline import DevicePrefetcher, batches  # noqa: E402
 from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
 from tensorflow_examples_amd.optim import MomentumOptimizer  # noqa: E402
 from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed  # noqa: E402
 from tensorflow_examples_amd.parallel.launch import control_device, control_group as _control_group  # noqa: E402
 from tensorflow_examples_amd.train import ClassifierTrainer  # noqa: E402
+from tensorflow_examples_amd.utils import runlog  # noqa: E402
 
 flags = app.flags
 flags.DEFINE_string("data_dir", "", "directory with the CIFAR-10 binary batches (synthetic if absent)")
@@ -38,7 +43,6 @@ flags.DEFINE_float("learning_rate", 0.1, "base LR (scaled by the number of GPUs)
 flags.DEFINE_float("weight_decay", 5e-4, "L2 weight decay")
 flags.DEFINE_string("lr_boundaries", "0.5,0.75", "fractions of training where the LR drops 10x")
 flags.DEFINE_float("bucket_mb", 32.0, "all-reduce bucket size (MB)")
-flags.DEFINE_string("logdir", "", "checkpoint directory (resume from the latest checkpoint in it)")
 flags.DEFINE_string("export_dir", "", "after training, export a SavedModel (saved_model.pb + variables/) here")
 flags.DEFINE_integer("synthetic_train", 50000, "synthetic training-set size when no data is found")
 flags.DEFINE_integer("eval_examples", 0, "evaluate on the first N test images (0 = all)")
@@ -49,7 +53,21 @@ flags.DEFINE_integer("warmup_steps", 50, "linear learning-rate warm-up over the 
 flags.DEFINE_boolean("graph", True, "GPU: capture the training step (forward, backward with the bucketed RCCL "
                      "all-reduces, optimizer) in a HIP graph on the first batch and replay it (the capture's "
                      "warm-up trains on that batch 3 extra times); --nograph runs eager launches")
+flags.DEFINE_integer("log_every", 50, "print / log scalars every N steps")
+flags.DEFINE_string("data", "auto", "auto (CIFAR-10 files, else synthetic) | synthetic | hard: the overlapping "
+                    "class-conditional texture task of data/cifar.py (not solved perfectly)")
+runlog.define_flags(flags)
 FLAGS = flags.FLAGS
+
+
+def evaluate(model, xte, yte, dev, dtype):
+    correct = 0.0
+    with torch.no_grad():
+        for i in range(0, len(xte), 500):
+            x = to_model_input(torch.as_tensor(xte[i:i + 500], device=dev), dtype)
+            y = torch.as_tensor(yte[i:i + 500], device=dev)
+            correct += float(ops.accuracy(model(x, training=False), y)) * len(y)
+    return correct / len(xte)
 
 
 def main(_):
@@ -61,18 +79,23 @@ def main(_):
     ctl = _control_group() if dist.is_initialized() else None
     cdev = control_device(ctl, dev)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
-    xtr, ytr, xte, yte, synth = load_cifar10(FLAGS.data_dir or None, synthetic_train=FLAGS.synthetic_train)
+    if FLAGS.data == "hard":
+        xtr, ytr = hard_synthetic_cifar(FLAGS.synthetic_train, 0)
+        xte, yte = hard_synthetic_cifar(10000, 1)
+        synth = "hard synthetic"
+    else:
+        xtr, ytr, xte, yte, synth = load_cifar10(None if FLAGS.data == "synthetic" else (FLAGS.data_dir or None),
+                                                 synthetic_train=FLAGS.synthetic_train)
+        synth = "synthetic" if synth else "binary"
+    if FLAGS.eval_examples:
+        xte, yte = xte[:FLAGS.eval_examples], yte[:FLAGS.eval_examples]
     if rank == 0:
-        print("CIFAR-10 %s: %d train / %d test" % ("synthetic" if synth else "binary", len(xtr), len(xte)))
+        print("CIFAR-10 %s: %d train / %d test" % (synth, len(xtr), len(xte)))
     store, model = build_resnet_cifar(device=dev, depth=FLAGS.depth, dtype=dtype, seed=FLAGS.seed,
                                       zero_init_residual=FLAGS.zero_init_residual)
     opt = MomentumOptimizer(store, FLAGS.learning_rate * world, momentum=0.9, weight_decay=FLAGS.weight_decay)
-    start_step = 0
-    if FLAGS.logdir and latest_checkpoint(FLAGS.logdir):
-        tensors = Saver().restore(store, latest_checkpoint(FLAGS.logdir))
-        start_step = int(float(tensors["global_step"])) if "global_step" in tensors else 0
-    if FLAGS.logdir and rank == 0:
-        write_graph(FLAGS.logdir, store_graph_nodes(store))  # graph.pbtxt, as TF1's Supervisor writes it
+    log = runlog.RunLog(store, opt, FLAGS.logs_path, FLAGS.logdir, FLAGS.save_checkpoint_steps, rank=rank)
+    start_step = log.restore()  # every rank restores the same checkpoint (then broadcast keeps them equal)
     broadcast_variables(store)
     dp = GradAllReduce(store, bucket_bytes=int(FLAGS.bucket_mb * (1 << 20))) if world > 1 else None
     trainer = ClassifierTrainer(store, model, opt, dp)
@@ -80,18 +103,25 @@ def main(_):
     steps_per_epoch = len(shard) // FLAGS.batch_size
     total = FLAGS.max_steps or steps_per_epoch * FLAGS.epochs
     bounds = [int(float(f) * total) for f in FLAGS.lr_boundaries.split(",") if f]
-    step, t0, seen = start_step, time.time(), 0
+    step, seen = start_step, 0
     want_graph = FLAGS.graph and dev.type == "cuda"
+    sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)
+    t_start = time.time()
+    t0, t_eval, t_capture = None, 0.0, 0.0  # steady-state timer starts after the first (capture) step
+    test_acc = None
     for ep in range(FLAGS.epochs):
+        if step - start_step >= total:
+            break
         src = batches([xtr[shard], ytr[shard]], FLAGS.batch_size, seed=ep * 1000 + rank + 7919 * FLAGS.seed)
         for img, lab in DevicePrefetcher(src, dev):
             lr = FLAGS.learning_rate * world * (0.1 ** sum(step >= b for b in bounds))
             if FLAGS.warmup_steps and step < FLAGS.warmup_steps:
                 lr *= (step + 1) / FLAGS.warmup_steps
             opt.set_learning_rate(lr)  # a device scalar: a replayed graph reads the new value
-            x = augment_model_input(img, dtype)  # crop + flip + normalise: one fused kernel on the GPU
             if want_graph:
                 want_graph = False
+                tc = time.time()
+                x = augment_model_input(img, dtype)
                 ok = True
                 try:
                     trainer.capture(x, lab)
@@ -104,38 +134,61 @@ def main(_):
                     ok = bool(agree.item())
                 if not ok:
                     trainer.graph = None
+                sync()
+                t_capture = time.time() - tc
                 if rank == 0:
-                    print("hip graph: %s" % ("replaying the captured step" if ok else "eager launches"), flush=True)
+                    print("hip graph: %s (capture + warm-up %.2f s, timed apart)" %
+                          ("replaying the captured step" if ok else "eager launches", t_capture), flush=True)
+            # graphed: crop + flip + normalise written straight into the graph's static input (one fused
+            # kernel, no copy), the labels into its static label buffer
+            xbuf, ybuf = trainer.input_buffer(), trainer.label_buffer()
+            x = augment_model_input(img, dtype, out=xbuf)
+            if ybuf is not None:
+                ybuf.copy_(lab, non_blocking=True)
+                lab = ybuf
             loss = trainer.step(x, lab)
             if rank == 0 and step == start_step and trainer.plan is not None:
                 print(trainer.plan.table(), flush=True)  # which fusion group ran which layer (ops/fusion.py)
             step += 1
-            seen += img.shape[0]
-            if rank == 0 and step % 50 == 0:
-                print("epoch %d step %d lr %.4f loss %.4f" % (ep + 1, step, lr, float(loss)), flush=True)
+            if t0 is None:  # the first step (graph capture + its warm-up + first replay) is not steady state
+                sync()
+                t0 = time.time()
+            else:
+                seen += img.shape[0]
+            if step % FLAGS.log_every == 0:
+                if rank == 0:
+                    with torch.no_grad():  # training-batch accuracy (the reference's summary op), eval-mode forward
+                        acc = float(ops.accuracy(model(x, training=False), lab))
+                    print("epoch %d step %d lr %.4f loss %.4f" % (ep + 1, step, lr, float(loss)), flush=True)
+                    log.scalars(step, cost=float(loss), accuracy=acc, learning_rate=lr)
+            log.maybe_save(step)
             if step - start_step >= total:
                 break
-        if step - start_step >= total:
-            break
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    dt = time.time() - t0
+        # per-epoch test accuracy (rank 0; the other ranks wait at the next collective), timed apart
+        sync()
+        te = time.time()
+        if rank == 0:
+            test_acc = evaluate(model, xte, yte, dev, dtype)
+            print("epoch %d test accuracy %.4f" % (ep + 1, test_acc), flush=True)
+            log.scalars(step, test_accuracy=test_acc)
+        t_eval += time.time() - te
+    sync()
+    t_end = time.time()
+    dt = max((t_end - t0) - t_eval, 1e-9) if t0 is not None else 1e-9
     ips = torch.tensor([seen / dt], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(ips, group=ctl)
-    if FLAGS.eval_examples:
-        xte, yte = xte[:FLAGS.eval_examples], yte[:FLAGS.eval_examples]
-    correct = 0.0
-    with torch.no_grad():
-        for i in range(0, len(xte), 500):
-            x = to_model_input(torch.as_tensor(xte[i:i + 500], device=dev), dtype)
-            y = torch.as_tensor(yte[i:i + 500], device=dev)
-            correct += float(ops.accuracy(model(x, training=False), y)) * len(y)
+    if test_acc is None and rank == 0:
+        test_acc = evaluate(model, xte, yte, dev, dtype)
     if rank == 0:
-        print("test accuracy %.4f" % (correct / len(xte)))
+        print("test accuracy %.4f" % test_acc)
         print("images/sec (all GPUs) %.1f" % float(ips))
-        if FLAGS.logdir:
-            print("saved", Saver().save(store, os.path.join(FLAGS.logdir, "model.ckpt"), global_step=step))
+        print("end-to-end %.1f s: steady-state training %.1f s, graph capture %.1f s, evaluation %.1f s" %
+              (t_end - t_start, dt, t_capture, t_eval))
+    saved = log.close(step)
+    if rank == 0:
+        if saved:
+            print("saved", saved)
         if FLAGS.export_dir:
             sig = {"serving_default": {"inputs": {"images": ("images:0", "uint8", [-1, 32, 32, 3])},
                                        "outputs": {"logits": ("logits:0", "float32", [-1, 10])}}}

@@ -6,7 +6,9 @@ sparse variables, log-uniform negatives (64 per batch), fused loss/gradient kern
 (scatter-add) updates.  The corpus is a text file (``--train_data``, e.g. text8) when present, else a
 synthetic Zipfian corpus; batches are drawn on the GPU by one kernel (random center + in-window
 context).  ``--graph`` captures the whole step (batch generation, sampling, forward, backward,
-update) in a HIP graph and replays it.
+update) in a HIP graph and replays it.  ``--logs_path`` writes the average-loss scalar and the graph to
+an event file, ``--logdir`` checkpoints the tables (and the batch-generator counter) periodically and
+resumes (utils/runlog.py; the reference's conventions, R/distributed/distributed.py:120-138).
 
     python examples/word2vec.py --vocabulary_size=1000000 --batch_size=128 --num_steps=100001
 """
@@ -22,6 +24,7 @@ import torch  # noqa: E402
 from tensorflow_examples_amd import app  # noqa: E402
 from tensorflow_examples_amd.data.text import build_dataset, device_skipgram_batch, synthetic_zipf_corpus  # noqa: E402
 from tensorflow_examples_amd.models.word2vec import build_skipgram  # noqa: E402
+from tensorflow_examples_amd.utils import runlog  # noqa: E402
 
 flags = app.flags
 flags.DEFINE_string("train_data", "", "whitespace-tokenised text corpus (synthetic Zipf corpus if absent)")
@@ -36,6 +39,7 @@ flags.DEFINE_string("loss", "nce", "nce | sampled_softmax")
 flags.DEFINE_integer("corpus_words", 20000000, "synthetic corpus length")
 flags.DEFINE_boolean("graph", False, "capture the training step in a HIP graph")
 flags.DEFINE_integer("log_every", 2000, "print the average loss every N steps")
+runlog.define_flags(flags, save_steps_default=10000)
 FLAGS = flags.FLAGS
 
 
@@ -56,6 +60,11 @@ def main(_):
     store, model = build_skipgram(dev, V, FLAGS.embedding_size, FLAGS.num_sampled, FLAGS.loss, seed=0)
     counter = torch.zeros(1, dtype=torch.long, device=dev)
     lr, B = FLAGS.learning_rate, FLAGS.batch_size
+    # the device counter seeds the batch generator and the sampler: checkpointed with the tables, so a
+    # resumed run continues the same stream
+    log = runlog.RunLog(store, None, FLAGS.logs_path, FLAGS.logdir, FLAGS.save_checkpoint_steps,
+                        extra_state={"skipgram/step_counter": counter})
+    start = log.restore()
 
     def step():
         c, l = device_skipgram_batch(corpus, B, FLAGS.skip_window, seed=1, seed_tensor=counter)
@@ -79,15 +88,17 @@ def main(_):
     avg = torch.zeros((), device=dev)
     t0 = time.time()
     t_last = t0
-    for i in range(FLAGS.num_steps):
+    for i in range(start, FLAGS.num_steps):
         avg += run()
         if (i + 1) % FLAGS.log_every == 0:
             a = float(avg) / FLAGS.log_every
             now = time.time()
             print("Average loss at step %d: %.4f  (%.0f examples/sec)" %
                   (i + 1, a, FLAGS.log_every * B / (now - t_last)), flush=True)
+            log.scalars(i + 1, loss=a)
             avg.zero_()
             t_last = now
+        log.maybe_save(i + 1)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.time() - t0
@@ -96,7 +107,10 @@ def main(_):
     for r, w in enumerate(valid.tolist()[:4]):
         name = (lambda k: rev.get(k, str(k))) if rev else str
         print("Nearest to %s: %s" % (name(w), ", ".join(name(int(k)) for k in near[r])))
-    print("examples/sec %.1f" % (FLAGS.num_steps * B / dt))
+    print("examples/sec %.1f" % (max(FLAGS.num_steps - start, 0) * B / max(dt, 1e-9)))
+    saved = log.close(max(FLAGS.num_steps, start))
+    if saved:
+        print("saved", saved)
     return 0
 
 
