@@ -1,0 +1,152 @@
+"""Convergence parity of the fused bf16 ResNet training step against the same model in fp32 reference ops.
+
+Both runs start from the same weights (bf16-representable), see the same batches of the hard synthetic
+CIFAR task (data/cifar.py hard_synthetic_cifar: overlapping class textures, shifts, label noise -- no
+path reaches 100 %) in the same order, with the same momentum-SGD recipe (linear lr warm-up, weight
+decay, zero-init residual gammas).  Reported per run: the loss averaged over each 50-step window and the
+final test accuracy.  ``--negctl group:factor`` adds a run whose named fused backward group has its
+gradients scaled (ops/nn.py NEG_CONTROL): the deliberately wrong fused gradient the comparison must
+catch.  Reference: the reference judges a run by its final accuracy line
+(R/distributed/distributed.py:164).
+
+    python scripts/convergence_parity.py --steps 300 --batch 128 --negctl lazy_bn_bwd:0.8 --out conv.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tensorflow_examples_amd import ops  # noqa: E402
+from tensorflow_examples_amd.data.cifar import hard_synthetic_cifar  # noqa: E402
+from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input  # noqa: E402
+from tensorflow_examples_amd.ops import _native  # noqa: E402
+from tensorflow_examples_amd.ops import nn as nnops  # noqa: E402
+from tensorflow_examples_amd.optim import MomentumOptimizer  # noqa: E402
+from tensorflow_examples_amd.train import ClassifierTrainer  # noqa: E402
+
+WINDOW = 50
+
+
+def window_means(losses):
+    return [float(np.mean(losses[i:i + WINDOW])) for i in range(0, len(losses) - WINDOW + 1, WINDOW)]
+
+
+def run(mode, a, data, w0, negctl=None):
+    dev = torch.device("cuda", 0)
+    xtr, ytr, xte, yte = data
+    dt = torch.float32 if mode == "ref32" else torch.bfloat16
+    st, m = build_resnet_cifar(device=dev, depth=a.depth, dtype=dt, seed=a.seed, zero_init_residual=True)
+    st.master.copy_(w0)
+    st.refresh_shadow()
+    opt = MomentumOptimizer(st, a.lr, momentum=0.9, weight_decay=a.wd)
+    tr = ClassifierTrainer(st, m, opt) if mode != "ref32" else None
+    nnops.NEG_CONTROL.clear()
+    if negctl:
+        g, f = negctl.split(":")
+        nnops.NEG_CONTROL[g] = float(f)
+    losses = []
+    t0 = time.time()
+    try:
+        for i in range(a.steps):
+            opt.set_learning_rate(a.lr * min(1.0, (i + 1) / a.warmup))
+            sl = slice(a.batch * i, a.batch * (i + 1))
+            x = to_model_input(xtr[sl], dtype=dt)
+            y = ytr[sl]
+            if tr is not None:
+                loss = tr.step(x, y)
+            else:
+                with _native.reference_mode():
+                    st.zero_grad()
+                    loss = ops.softmax_cross_entropy(m(x, training=True), y)
+                    loss.backward()
+                    opt.apply_gradients()
+            losses.append(loss)
+        losses = [float(v) for v in losses]
+        correct = 0.0
+        with torch.no_grad():
+            for i in range(0, len(xte), 500):
+                xe = to_model_input(xte[i:i + 500], dtype=dt)
+                if tr is None:
+                    with _native.reference_mode():
+                        correct += float(ops.accuracy(m(xe, training=False), yte[i:i + 500])) * len(xe)
+                else:
+                    correct += float(ops.accuracy(m(xe, training=False), yte[i:i + 500])) * len(xe)
+    finally:
+        nnops.NEG_CONTROL.clear()
+    torch.cuda.synchronize()
+    return {"mode": mode if not negctl else "%s[negctl %s]" % (mode, negctl), "window_loss": window_means(losses),
+            "final_loss50": float(np.mean(losses[-WINDOW:])), "test_accuracy": correct / len(xte),
+            "nan": any(v != v for v in losses), "seconds": time.time() - t0}
+
+
+def compare(ref, other, rel_tol, acc_tol):
+    rel = [abs(o - r) / r for r, o in zip(ref["window_loss"], other["window_loss"])]
+    dacc = abs(other["test_accuracy"] - ref["test_accuracy"])
+    return {"max_rel_window_loss": max(rel), "rel_window_loss": rel, "accuracy_delta": dacc,
+            "pass": (max(rel) <= rel_tol and dacc <= acc_tol and not other["nan"])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--wd", type=float, default=5e-4)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--test", type=int, default=2000)
+    ap.add_argument("--modes", default="ref32,fused")
+    ap.add_argument("--repeat", type=int, default=1, help="fused runs (the run-to-run spread of the bf16 path)")
+    ap.add_argument("--negctl", default="", help="comma list of group:factor negative-control fused runs")
+    ap.add_argument("--rel_tol", type=float, default=0.05)
+    ap.add_argument("--acc_tol", type=float, default=0.02)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    t = time.time()
+    xtr, ytr = hard_synthetic_cifar(a.steps * a.batch, 0)
+    xte, yte = hard_synthetic_cifar(a.test, 1)
+    data = (torch.as_tensor(xtr, device=dev), torch.as_tensor(ytr, device=dev), torch.as_tensor(xte, device=dev),
+            torch.as_tensor(yte, device=dev))
+    print("data %.1f s" % (time.time() - t), flush=True)
+    st0, _ = build_resnet_cifar(device=dev, depth=a.depth, dtype=torch.bfloat16, seed=a.seed, zero_init_residual=True)
+    w0 = st0.master.bfloat16().float()
+    del st0
+    runs = []
+    for mode in a.modes.split(","):
+        for _ in range(a.repeat if mode == "fused" else 1):
+            r = run(mode, a, data, w0)
+            runs.append(r)
+            print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
+    for neg in [n for n in a.negctl.split(",") if n]:
+        r = run("fused", a, data, w0, negctl=neg)
+        runs.append(r)
+        print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
+    ref = [r for r in runs if r["mode"] == "ref32"]
+    res = {"config": vars(a), "runs": runs, "comparisons": []}
+    if ref:
+        for r in runs:
+            if r is ref[0]:
+                continue
+            c = compare(ref[0], r, a.rel_tol, a.acc_tol)
+            c["mode"] = r["mode"]
+            res["comparisons"].append(c)
+            print("COMPARE %-32s max rel window loss %.4f  accuracy delta %.4f  -> %s" %
+                  (r["mode"], c["max_rel_window_loss"], c["accuracy_delta"], "PASS" if c["pass"] else "FAIL"),
+                  flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    return res
+
+
+if __name__ == "__main__":
+    main()
