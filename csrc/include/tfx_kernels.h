@@ -415,6 +415,11 @@ int ipc_get_handle(void* ptr, uint8_t* out64);
 int ipc_open(int device, const uint8_t* handle64, void** ptr);
 int ipc_close(void* ptr);
 
+// ---------------------------------------------------------------- one-GPU stand-in for an 8-rank ring all-reduce
+// nblocks workgroups stream buf (read + write back the same bytes) for duration_us (<= 10 ms), holding
+// their CUs like RCCL's channel blocks (dp_sim.hip; scripts/dp_contention.py)
+void dp_ring_sim(void* buf, int64_t nbytes, int nblocks, double duration_us, int passes, hipStream_t s);
+
 // ---------------------------------------------------------------- Philox4x32-10 init (dist 0 uniform [a,b),
 // 1 normal(a, b), 2 normal(a, b) truncated at 2 sigma)
 void philox_fill(float* out, int64_t n, uint64_t seed, uint64_t subseq, int dist, float a, float b, hipStream_t s);

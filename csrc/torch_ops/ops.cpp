@@ -1808,10 +1808,17 @@ void image_normalize_into(Tensor x, std::vector<double> mean, std::vector<double
 
 }  // namespace
 
+// the CU / memory footprint of one bucket's 8-rank ring all-reduce on the current stream (dp_sim.hip)
+void dp_ring_sim(Tensor buf, int64_t nblocks, double duration_us, int64_t passes) {
+  CHECK_DEV(buf); CHECK_CONTIG(buf);
+  tfx::dp_ring_sim(buf.data_ptr(), buf.nbytes(), (int)nblocks, duration_us, (int)passes, cur_stream());
+}
+
 TORCH_LIBRARY(tfx, m) {
   m.def("image_normalize", &image_normalize);
   m.def("image_normalize_into", &image_normalize_into);
   m.def("augment_normalize", &augment_normalize);
+  m.def("dp_ring_sim(Tensor(a!) buf, int nblocks, float duration_us, int passes) -> ()", &dp_ring_sim);
   m.def("augment_normalize_into(Tensor x, Tensor offsets, float[] mean, float[] stdv, int pad, Tensor(a!) y) -> ()",
         &augment_normalize_into);
   m.def("end_stream_capture", &end_stream_capture);

@@ -107,7 +107,7 @@ def main(_):
     want_graph = FLAGS.graph and dev.type == "cuda"
     sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)
     t_start = time.time()
-    t0, t_eval, t_capture = None, 0.0, 0.0  # steady-state timer starts after the first (capture) step
+    t0, t_eval, t_capture, t_save = None, 0.0, 0.0, 0.0  # steady state starts after the first (capture) step
     test_acc = None
     for ep in range(FLAGS.epochs):
         if step - start_step >= total:
@@ -161,7 +161,11 @@ def main(_):
                         acc = float(ops.accuracy(model(x, training=False), lab))
                     print("epoch %d step %d lr %.4f loss %.4f" % (ep + 1, step, lr, float(loss)), flush=True)
                     log.scalars(step, cost=float(loss), accuracy=acc, learning_rate=lr)
-            log.maybe_save(step)
+            if log.save_steps > 0 and step % log.save_steps == 0 and FLAGS.logdir:
+                sync()
+                ts = time.time()
+                log.maybe_save(step)  # device -> host copy + file write, timed apart like the evaluations
+                t_save += time.time() - ts
             if step - start_step >= total:
                 break
         # per-epoch test accuracy (rank 0; the other ranks wait at the next collective), timed apart
@@ -174,7 +178,7 @@ def main(_):
         t_eval += time.time() - te
     sync()
     t_end = time.time()
-    dt = max((t_end - t0) - t_eval, 1e-9) if t0 is not None else 1e-9
+    dt = max((t_end - t0) - t_eval - t_save, 1e-9) if t0 is not None else 1e-9
     ips = torch.tensor([seen / dt], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(ips, group=ctl)
@@ -183,8 +187,8 @@ def main(_):
     if rank == 0:
         print("test accuracy %.4f" % test_acc)
         print("images/sec (all GPUs) %.1f" % float(ips))
-        print("end-to-end %.1f s: steady-state training %.1f s, graph capture %.1f s, evaluation %.1f s" %
-              (t_end - t_start, dt, t_capture, t_eval))
+        print("end-to-end %.1f s: steady-state training %.1f s, graph capture %.1f s, evaluation %.1f s, "
+              "checkpoints %.1f s" % (t_end - t_start, dt, t_capture, t_eval, t_save))
     saved = log.close(step)
     if rank == 0:
         if saved:

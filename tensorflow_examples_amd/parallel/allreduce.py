@@ -56,8 +56,15 @@ def premul_scalar(factor: float, dtype: torch.dtype) -> float:
 class GradAllReduce:
     def __init__(self, store: VariableStore, bucket_bytes: int = 32 << 20, group=None, overlap: bool = True,
                  compress_bf16: bool = False, tail_bytes: int = 2 << 20, force_collective: Optional[bool] = None,
-                 premul: Optional[float] = None):
+                 premul: Optional[float] = None, simulate_ring: Optional[dict] = None):
         self.store = store
+        # simulate_ring = {"blocks": B, "ranks": N, "link_gbps": G, "latency_us": L}: one-GPU contention
+        # rehearsal of an N-rank node (scripts/dp_contention.py) -- each bucket's collective is replaced by
+        # dp_ring_sim: B workgroups streaming the bucket on a side stream for the ring's modelled time
+        # 2 (N-1)/N S / G + L, forked at the bucket's ready point and joined before the optimizer
+        self.sim = dict(simulate_ring) if simulate_ring else None
+        self._sim_stream = None
+        self._sim_events = []
         self.group = group
         # premul: RCCL pre-multiplied sum (each rank's bucket scaled by `premul` inside the
         # collective).  Used by the GPU tests to make a 1-rank collective observable: a bucket whose
@@ -112,7 +119,7 @@ class GradAllReduce:
         self._pending: List[int] = []
         self._launched: List[bool] = []
         self._works = []
-        if overlap and (self.world > 1 or self.force):
+        if overlap and (self.world > 1 or self.force or self.sim):
             store.grad_ready_hook = self._on_ready
         self.start_step()
 
@@ -148,7 +155,35 @@ class GradAllReduce:
         if self._pending[b] == 0:
             self._launch(b)
 
+    def sim_ring_us(self, nbytes: int) -> float:
+        n, g = self.sim.get("ranks", 8), self.sim.get("link_gbps", 153.0)
+        return 2.0 * (n - 1) / n * nbytes / (g * 1e3) + self.sim.get("latency_us", 0.0)
+
+    def _launch_sim(self, b: int) -> None:
+        lo, hi = self.buckets[b]
+        view = self.store.grad[lo:hi]
+        if self.compress:  # the bf16 wire: the cast runs on the compute stream as in the real path
+            g16 = self.grad16[lo:hi]
+            torch.ops.tfx.cast_f32_bf16(view, g16)
+            self._used16 = True
+            view = g16
+        if self._sim_stream is None:
+            self._sim_stream = torch.cuda.Stream()
+        cur = torch.cuda.current_stream()
+        self._sim_stream.wait_stream(cur)
+        with torch.cuda.stream(self._sim_stream):
+            torch.ops.tfx.dp_ring_sim(view, int(self.sim.get("blocks", 16)),
+                                      float(self.sim_ring_us(view.numel() * view.element_size())),
+                                      int(self.sim.get("passes", 2)))
+            e = torch.cuda.Event()
+            e.record()
+        self._sim_events.append(e)
+
     def _launch(self, b: int) -> None:
+        if self.sim is not None and not self._launched[b]:
+            self._launched[b] = True
+            self._launch_sim(b)
+            return
         if self._launched[b] or (self.world == 1 and not self.force):
             self._launched[b] = True
             return
@@ -185,6 +220,9 @@ class GradAllReduce:
             work.wait()
             if view is not None:
                 view.copy_(tmp)
+        for e in self._sim_events:
+            torch.cuda.current_stream().wait_event(e)
+        self._sim_events = []
         self._pending = [len(m) for m in self.members]
         self._launched = [False] * len(self.buckets)
         self._works = []
@@ -193,6 +231,7 @@ class GradAllReduce:
         self._pending = [len(m) for m in self.members]
         self._launched = [False] * len(self.buckets)
         self._works = []
+        self._sim_events = []
         self._used16 = False
 
     @property

@@ -231,3 +231,34 @@ def test_premul_bf16_scalar_encoding_rccl(gpu, tmp_path):
     print(p.stdout, p.stderr[-2000:])
     assert p.returncode == 0, p.stderr[-3000:]
     assert p.stdout.count("PREMUL") == 6
+
+
+def test_dp_ring_simulation_leaves_gradients_unchanged(gpu):
+    """GradAllReduce(simulate_ring=...) (the one-GPU contention rehearsal of scripts/dp_contention.py): the
+    stand-in kernels stream every bucket and write the same bytes back, forked and joined inside the captured
+    step -- one graphed step must equal the no-DP step (f32 and bf16 wire)."""
+    import torch
+    from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
+    from tensorflow_examples_amd.optim import MomentumOptimizer
+    from tensorflow_examples_amd.parallel import GradAllReduce
+    from tensorflow_examples_amd.train import ClassifierTrainer
+    g = torch.Generator().manual_seed(1)
+    x = to_model_input(torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, generator=g).to(gpu))
+    y = torch.randint(0, 10, (16,), generator=g).to(gpu)
+    upd = {}
+    for mode in ("none", "f32", "bf16"):
+        st, m = build_resnet_cifar(device=gpu, depth=18, dtype=torch.bfloat16, seed=0, zero_init_residual=True)
+        w0 = st.master.clone()
+        dp = None if mode == "none" else GradAllReduce(st, bucket_bytes=2 << 20, compress_bf16=mode == "bf16",
+                                                        simulate_ring={"blocks": 8, "passes": 2})
+        opt = MomentumOptimizer(st, 0.0, momentum=0.9)
+        tr = ClassifierTrainer(st, m, opt, dp)
+        tr.capture(x, y, warmup=2)
+        opt.set_learning_rate(0.01)
+        tr.step(x, y)
+        torch.cuda.synchronize()
+        upd[mode] = st.master - w0
+    ref = upd["none"]
+    for mode, lim in (("f32", 1e-2), ("bf16", 2e-2)):
+        rel = ((upd[mode] - ref).norm() / ref.norm()).item()
+        assert rel < lim, (mode, rel)
