@@ -139,7 +139,8 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
     switch (mode) {
       case MODE_FWD:  // X[M][C] . W[Ko][C]^T
         a.lda = a.C; a.ldb = a.C;
-        igemm_fwd_pointwise(a, s);
+        if (igemm_fwd_persist_ok(a)) igemm_fwd_persist(a, s);  // one ring over all of a block's tiles
+        else igemm_fwd_pointwise(a, s);
         return;
       case MODE_DGRAD:  // dY[M][Ko] . W[Ko][C]
         a.lda = a.Ko; a.ldb = a.C;

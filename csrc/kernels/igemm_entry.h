@@ -16,6 +16,9 @@ void igemm_wgrad_dense(IgemmArgs& a, hipStream_t s);     // dY^T . X (1x1) -- f3
 void igemm_wgrad_x(IgemmArgs& a, hipStream_t s);         // dY^T . im2col(X)
 void igemm_wgrad_t_x(IgemmArgs& a, hipStream_t s);       // im2col(X)^T . dY (transposed store)
 void igemm_gemm(IgemmArgs& a, hipStream_t s);            // plain GEMMs (FC layers, LSTM)
+// persistent 1x1 forward (igemm_persist.hip): one continuous LDS-DMA ring over all of a block's tiles
+bool igemm_fwd_persist_ok(const IgemmArgs& a);
+void igemm_fwd_persist(IgemmArgs& a, hipStream_t s);
 
 // ---- measured launch configurations (igemm.hip; table from scripts/tune_convs.py)
 // family = which entry above launched; a config overrides the built-in heuristics of launch_shape /

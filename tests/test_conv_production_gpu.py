@@ -96,3 +96,41 @@ def test_conv_production_shape(gpu, shape):
         _, _, red_ref = torch.ops.tfx.bn_bwd(dx2, xb, None, sv, True, torch.zeros_like(wsb), None, None, None)
         assert _rel(red, red_ref) < 2e-3
         assert wsb.abs().max().item() == 0.0
+
+
+PW_FWD = [s for s in SHAPES if s[5] == 1 and s[6] == 1 and s[0] == 256]
+
+
+@pytest.mark.parametrize("shape", PW_FWD, ids=[_ids(s) for s in PW_FWD])
+def test_persistent_pointwise_forward_matches_per_tile_kernel(gpu, shape):
+    """The persistent 1x1 forward (igemm_persist.hip: one LDS-DMA ring over all of a block's tiles, ring
+    depth 2 or 3) against the one-tile-per-block kernel and fp32: output and the fused BN statistics
+    (saved mean / invstd) at every production 1x1 shape."""
+    N, H, W, C, Ko, R, st = shape
+    g = torch.Generator(device=gpu).manual_seed(7 + C + Ko)
+    x = _bf(torch.randn(N, H, W, C, device=gpu, generator=g))
+    w = _bf(torch.randn(Ko, 1, 1, C, device=gpu, generator=g) * (1.0 / math.sqrt(C)))
+    yr = torch.einsum("nhwc,kc->nhwk", x.float(), w.float().reshape(Ko, C))
+    gamma = torch.rand(Ko, device=gpu, generator=g) + 0.5
+    beta = torch.randn(Ko, device=gpu, generator=g)
+    res = {}
+    prev = torch.ops.tfx.igemm_persist_mode(0)
+    try:
+        for mode in (0, 2, 3):
+            torch.ops.tfx.igemm_persist_mode(mode)
+            ws = torch.zeros(64 * 2 * Ko + 64, device=gpu)
+            yb, save = torch.ops.tfx.conv_fwd_bn(x, w, 1, 0, 1, ws, gamma, beta, None, None, 0.1, 1e-5)
+            y = torch.ops.tfx.conv_fwd(x, w, 1, 0, 1)
+            torch.cuda.synchronize()
+            assert float(ws[:64 * 2 * Ko].abs().max()) == 0.0, "statistics slots left dirty"
+            res[mode] = (yb, save.clone(), y)
+    finally:
+        torch.ops.tfx.igemm_persist_mode(prev)
+    mean_r = yr.reshape(-1, Ko).mean(0)
+    for mode in (2, 3):
+        yb, save, y = res[mode]
+        assert _rel(yb, yr) < 1e-2 and _rel(y, yr) < 1e-2
+        # (the per-tile kernel splits K over two wave groups at some shapes: summation order differs)
+        assert _rel(yb, res[0][0]) < 2e-3 and _rel(y, res[0][2]) < 2e-3
+        assert _rel(save[:Ko], res[0][1][:Ko]) < 1e-4 and _rel(save[Ko:2 * Ko], res[0][1][Ko:2 * Ko]) < 1e-4
+        assert _rel(save[:Ko], mean_r) < 2e-2
