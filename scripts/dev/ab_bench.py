@@ -1,8 +1,8 @@
-"""Same-process A/B of bench.py's training step under fusion hooks (ops.nn module globals): the configs
+"""Same-process A/B of bench.py's training step under fusion knobs (ops/fusion.py KNOBS): the configs
 run interleaved (A B C A B C ...) on ONE GPU so box-to-box variance (~4 % on this pool) cancels.
 
 usage: PYTHONPATH=. python scripts/dev/ab_bench.py [--reps 3] [--steps 30] [--warmup 10]
-       --config name:HOOK=0,HOOK=1 ...   (default: all fusions on vs each fused 3x3 path off)"""
+       --config name:knob=0,knob=1 ...   (default: all fusions on vs each fused 3x3 path off)"""
 import argparse
 import contextlib
 import io
@@ -13,12 +13,12 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import bench  # noqa: E402
-from tensorflow_examples_amd.ops import nn as nnops  # noqa: E402
+from tensorflow_examples_amd.ops import fusion  # noqa: E402
 
 DEFAULT = [
     "fused:",
-    "no_c3bwd:_FUSE_CONV3_BWD=0",
-    "no_bn_in:_DEFER_BN_IN=0",
+    "no_c3bwd:fuse_conv3_bwd=0",
+    "no_bn_in:defer_bn_in=0",
 ]
 
 
@@ -39,14 +39,14 @@ def main():
     ap.add_argument("--config", action="append")
     a = ap.parse_args()
     cfgs = [parse_cfg(c) for c in (a.config or DEFAULT)]
-    base = {k: getattr(nnops, k) for _, kv in cfgs for k in kv}
+    base = {k: fusion.knob(k) for _, kv in cfgs for k in kv}
     res = {name: [] for name, _ in cfgs}
     for rep in range(a.reps):
         for name, kv in cfgs:
             for k, v in base.items():
-                setattr(nnops, k, v)
+                fusion.CONFIG.set(k, v)
             for k, v in kv.items():
-                setattr(nnops, k, v)
+                fusion.CONFIG.set(k, v)
             buf = io.StringIO()
             with contextlib.redirect_stdout(buf):
                 bench.run(bench.parse(["--steps", str(a.steps), "--warmup", str(a.warmup)]))

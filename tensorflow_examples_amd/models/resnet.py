@@ -17,7 +17,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from .. import ops
-from ..ops import _native
+from ..ops import _native, fusion
 from ..ops.nn import BNWorkspace
 from ..variables import Constant, HeNormal, VariableStore, Zeros
 
@@ -31,13 +31,14 @@ STAGES = {
 IN_CH_PAD = 8
 _MEAN = (0.4914, 0.4822, 0.4465)  # CIFAR-10 per-channel statistics
 _STD = (0.2470, 0.2435, 0.2616)
-# GPU training fusions (each measured as an interleaved A/B when introduced, README ledger):
-# the residual-gradient sum in conv1's data-gradient epilogue (GradSink); the conv<->BN epilogue
-# fusions (BN statistics in the producing conv's epilogue, BN backward reduction in the consuming
-# conv's data-gradient epilogue: igemm.hip EPI_STATS / EPI_BNB); identity blocks hand conv1 the
-# residual BN's (gradient, ReLU mask) instead of the masked gradient tensor; a 1x1 stride-2
-# projection parks its input gradient compact (even pixels only) for conv1's epilogue to add.
-_SINK = _FUSE_BN = _MASKED_RES = _S2_ADDEND = True
+# GPU training fusions (each measured as an interleaved A/B when introduced, README ledger), read
+# from the fusion config (ops/fusion.py knobs): the residual-gradient sum in conv1's data-gradient
+# epilogue (GradSink, "sink"); the conv<->BN epilogue fusions (BN statistics in the producing conv's
+# epilogue, BN backward reduction in the consuming conv's data-gradient epilogue: igemm.hip
+# EPI_STATS / EPI_BNB, "fuse_bn"); identity blocks hand conv1 the residual BN's (gradient, ReLU mask)
+# instead of the masked gradient tensor ("masked_res"); a 1x1 stride-2 projection parks its input
+# gradient compact (even pixels only) for conv1's epilogue to add ("s2_addend").  Which kernel each
+# layer runs is the model's fusion plan (ResNetCifar.plan_for, fusion.plan_resnet).
 
 
 class _BN:
@@ -59,16 +60,16 @@ class _BN:
 
     def after_conv(self, conv, x, training, relu=False, residual=None, sink=None, residual_sink=None,
                    fuse_input_bn_backward=False, residual_is_bn=False, defer_output=False, defer_apply=False):
-        """conv -> BN with the BN statistics produced (and, with _FUSE_BN, finalized) by the conv's
+        """conv -> BN with the BN statistics produced (and, with knob fuse_bn, finalized) by the conv's
         epilogue (GPU, training).  ``fuse_input_bn_backward``: the conv's data gradient is the
         complete gradient of ``x`` -- reduce x's producing BN's backward in its epilogue.  The BN's
         input gradient may reach ``conv`` unmaterialised (ops.nn.LazyBNGrad): it is its only producer.
         ``defer_apply``: the output's first reader is the next bottleneck's conv1, which applies this
         (tail) BN while loading it (ops.nn.TailPending)."""
         fused = training and x.device.type == "cuda"
-        if fused and _FUSE_BN:
+        if fused and fusion.knob("fuse_bn"):
             self.ws.finalize_args = (self.gamma.master, self.beta.master, self.mean, self.var, 0.1, 1e-5)
-            y = conv(x, self.ws, sink, fuse_input_bn_backward and _FUSE_BN)
+            y = conv(x, self.ws, sink, fuse_input_bn_backward and fusion.knob("fuse_bn"))
             return self(y, training, relu=relu, residual=residual, stats_ready=True, residual_sink=residual_sink,
                         ws_obj=True, residual_is_bn=residual_is_bn, defer_output=defer_output, lazy_backward=True,
                         defer_apply=defer_apply)
@@ -109,10 +110,11 @@ class Bottleneck:
         # this block's tail BN while loading its input (pw_fwd.hip)
         # x feeds conv1 and the shortcut: the shortcut's input-gradient is folded into conv1's
         # dgrad epilogue (GradSink) instead of an autograd add kernel
-        prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
-        if prod is not None and _MASKED_RES:
+        gpu_train = training and x.device.type == "cuda"
+        prod, cons = ops.GradSink.pair() if (gpu_train and fusion.knob("sink")) else (None, None)
+        if prod is not None and fusion.knob("masked_res"):
             prod.accept_masked = True  # conv1 (1x1, stride 1) applies the residual ReLU mask itself
-        if prod is not None and _S2_ADDEND:
+        if prod is not None and fusion.knob("s2_addend"):
             prod.accept_s2 = True  # ... and a 1x1 stride-2 projection's compact gradient
         # conv1 is x's last consumer in backward only when the GradSink carries the other branch
         # BN1's apply is left to conv2 (a stage-1 3x3 conv applies it on load: conv3x3_fused.hip)
@@ -146,8 +148,9 @@ class Basic:
                 self.bp = _BN(store, width, "shortcut_bn")
 
     def __call__(self, x, training):
-        prod, cons = ops.GradSink.pair() if (training and x.device.type == "cuda" and _SINK) else (None, None)
-        if prod is not None and _MASKED_RES and self.c1.stride == 1:
+        gpu_train = training and x.device.type == "cuda"
+        prod, cons = ops.GradSink.pair() if (gpu_train and fusion.knob("sink")) else (None, None)
+        if prod is not None and fusion.knob("masked_res") and self.c1.stride == 1:
             prod.accept_masked = True
         o = self.b1.after_conv(self.c1, x, training, relu=True, sink=cons)
         if self.proj is None:
@@ -161,7 +164,7 @@ _ENV_APPLIED = False
 
 class ResNetCifar:
     def __init__(self, store: VariableStore, depth: int = 50, num_classes: int = 10, base_width: int = 64,
-                 zero_init_residual: bool = False):
+                 zero_init_residual: bool = False, plan_batch: int = 256):
         """``zero_init_residual``: the last BN of every residual branch starts with gamma = 0, so each block
         is the identity (plus its shortcut) at init -- the well-conditioned start of Goyal et al.'s large-batch
         recipe; without it the randomly initialised 50-layer net is ill-conditioned at lr 0.1 and 3-epoch runs
@@ -170,7 +173,6 @@ class ResNetCifar:
         global _ENV_APPLIED
         if not _ENV_APPLIED:  # TFX_FUSION profile (ops/fusion.py), once per process
             _ENV_APPLIED = True
-            from ..ops import fusion
             fusion.apply_env()
         kind, blocks = STAGES[depth]
         Block = Bottleneck if kind == "bottleneck" else Basic
@@ -193,6 +195,22 @@ class ResNetCifar:
                 self.fc_b = store.variable([num_classes], Zeros(), name="bias")
         self.num_classes = num_classes
         self.feat = cin
+        self._plans = {}
+        # the fusion plan of a training step, built with the model for the bench batch at CIFAR size
+        # (GPU stores); other batch sizes get theirs on first use (plan_for)
+        self.fusion_plan = self.plan_for(plan_batch) if str(store.device).startswith("cuda") else None
+
+    def plan_for(self, batch: int, hw: Tuple[int, int] = (32, 32)) -> Optional["fusion.FusionPlan"]:
+        """The fusion plan (ops/fusion.py) of a training step at ``batch`` images of ``hw``, for the
+        current fusion config; None where the native library (whose kernel-support predicates the
+        planner asks) is absent."""
+        key = (int(batch), tuple(hw), fusion.CONFIG.signature)
+        plan = self._plans.get(key)
+        if plan is None:
+            if not _native.load():
+                return None
+            plan = self._plans[key] = fusion.plan_resnet(self, int(batch), tuple(hw))
+        return plan
 
     def post_init(self):
         """Zero the stem weights of the padded input channels (3..7)."""
@@ -203,7 +221,10 @@ class ResNetCifar:
     def features(self, x: torch.Tensor, training: bool = True, defer_last: bool = False) -> torch.Tensor:
         """Stem and residual stages: the NHWC input of the classifier head.  ``defer_last``: the caller's
         head applies the last block's tail BN itself (ops.classifier_head_xent); anything else that reads
-        the output first materialises it (ops.nn.TailPending)."""
+        the output first materialises it (ops.nn.TailPending).  A GPU training step runs under this
+        batch's fusion plan: the ops consult its per-layer entries (fusion.layer_plan)."""
+        native = training and x.is_cuda and _native.use_native(x)
+        self.store.fusion_plan = self.plan_for(x.shape[0], tuple(x.shape[1:3])) if native else None
         o = self.stem_bn.after_conv(self.stem, x, training, relu=True)
         for i, blk in enumerate(self.blocks):
             if isinstance(blk, Bottleneck):

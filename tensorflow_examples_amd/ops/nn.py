@@ -70,10 +70,8 @@ _BNB_MAX_BYTES = 256 << 20
 # reductions of a stride-2 conv2's input BN and of the projection-shortcut BN (deferred to the next
 # weight-gradient launch's tail).  (Measured: profiles/r02_srfuse.  Rejected and removed: the same
 # reduction in the stride-2 parity-class data gradients' epilogues, a wash -- profiles/r02_s2bnb.)
-# test hooks: _SR_TAKE_PENDING = False leaves every deferred reduction to its own BN's backward
-# (the fallback path); _SR_DEFER = False never defers them (each BN reduces its own)
-_SR_TAKE_PENDING = True
-_SR_DEFER = True
+# Knobs (ops/fusion.py, group deferred_slot_reduce): sr_take off leaves every deferred reduction to
+# its own BN's backward (the fallback path); sr_defer off never defers them (each BN reduces its own)
 
 
 def _flip_ok(w, stride, pad, dil):
@@ -92,8 +90,7 @@ def _wflip(w, stride, pad, dil):
     return w.store.flipped3x3(w)
 
 
-# test hook: False keeps every tail BN backward materialised (the layer-wise path)
-_LAZY_BN_BWD = True
+# knob lazy_bn_bwd off keeps every tail BN backward materialised (the layer-wise path)
 PW_EXPAND_CALLS = [0]  # fused expanding-1x1 backward launches (tests)
 
 
@@ -101,7 +98,7 @@ class LazyBNGrad:
     """The input gradient of a residual + ReLU batch norm (a ResNet bottleneck's tail), NOT
     materialised: dy = A (g * mask) + B x + D per channel, with g the BN's output gradient, x its
     input, mask the forward's ReLU mask bits and (A, B, D) folded from ``save`` and ``red``.  The BN's
-    backward returns a zero-stride placeholder carrying this (``_tfx_lazy_bnbwd``); its producer conv
+    backward returns a zero-stride placeholder carrying this (fusion carrier "lazy_bnbwd"); its producer conv
     (the expanding 1x1 conv3) then forms dy on load inside its fused backward (pw_bwd.hip) -- or
     calls :meth:`materialize` (bn_bwd_apply, the layer-wise path) when it cannot.
 
@@ -129,16 +126,13 @@ class LazyBNGrad:
         return self.dy
 
 
-# test hooks: False keeps every block tail / plain BN applied by its own pass (the layer-wise forward)
-_DEFER_TAIL = True
-_DEFER_BN_IN = True
-_FUSE_CONV3_BWD = True  # False: the stage-1 3x3 conv's backward runs layer-wise (forward still fused)
+# knobs defer_tail / defer_bn_in off keep every block tail / plain BN applied by its own pass (the
+# layer-wise forward); fuse_conv3_bwd off runs the stage-1 3x3 conv's backward layer-wise
 PW_SQUEEZE_CALLS = [0]  # fused tail + conv1 forward launches (tests)
 # finalize folded into the layer-wise apply (bn_apply_fin): stage 3-4 BN layers (M <= 16384 rows: few
 # statistics rows, so every apply block can afford to reduce them).  Off by default: measured neutral
 # to +9 us/step in the bench (the ~5 us a finalize shows in a step trace is mostly the producer conv's
 # drain, which the next launch pays either way; profiles/r04_fold/README.md).  TFX_FUSION=+bn_finalize_fold
-_FOLD_FIN = False
 FOLD_FIN_CALLS = [0]  # applies that finalized their own statistics (tests)
 _FOLD_FIN_MAX_ROWS = 16384
 
@@ -154,7 +148,7 @@ class TailPending:
     __slots__ = ("x", "save", "res", "res_save", "_out", "mask", "done", "fin")
 
     def __init__(self, x, save, res, res_save, out, mask, fin=None):
-        # ``out`` carries this object as its ``_tfx_tail``: held weakly, or the pair is a reference cycle
+        # ``out`` carries this object (fusion carrier "tail"): held weakly, or the pair is a reference cycle
         # that only Python's full (rare) garbage collection frees -- with every step's tail activations
         # in it (an eager training loop ran out of HBM at ~280 steps of ResNet-50 at batch 128)
         self.x, self.save, self.res, self.res_save, self.mask = x, save, res, res_save, mask
@@ -191,7 +185,7 @@ class TailPending:
 
 def _settle(t):
     """Write a deferred block-tail output before anything but its fused consumer reads it."""
-    tp = getattr(t, "_tfx_tail", None) if t is not None else None
+    tp = fusion.carried(t, "tail") if t is not None else None
     if tp is not None and not tp.done:
         tp.materialize()
     return t
@@ -224,7 +218,7 @@ def _conv3_bwd_fused_ok(w, lazy, bnb, tp) -> bool:
     """The stage-1 3x3 conv's fused backward (conv3x3_fused.hip) applies: its output gradient is a plain
     ReLU BN's lazy input gradient, its input the deferred output of the plain ReLU BN ``bnb`` (the
     forward ran conv3x3_fwd_fused), whose backward partials nobody reduced yet."""
-    if not _FUSE_CONV3_BWD or lazy.mask is not None or lazy.sec is not None or lazy.dy is not None \
+    if not fusion.knob("fuse_conv3_bwd") or lazy.mask is not None or lazy.sec is not None or lazy.dy is not None \
             or not w.trainable:
         return False
     if bnb is None or bnb.mask is not None or not bnb.relu or bnb.deferred or bnb.red is not None or bnb.sr_pending:
@@ -232,18 +226,30 @@ def _conv3_bwd_fused_ok(w, lazy, bnb, tp) -> bool:
     return bnb.x is tp.x and lazy.g.shape == tp.x.shape
 
 
-def _conv3_fused_ok(x, w, stride, pad, dil, stats_into) -> bool:
-    """Stage-1 3x3 conv (64 -> 64, stride 1, pad 1, width 32) with a BN workspace: conv3x3_fused.hip."""
+def _std_geometry(x, w, stride, pad, dil) -> bool:
+    """A square-kernel, same-padding, undilated NHWC conv over ``x``'s channels (the planner's layers)."""
     sh = w.shape
-    if not (stride == 1 and pad == 1 and dil == 1 and isinstance(stats_into, BNWorkspace) and x.dim() == 4
-            and len(sh) == 4 and sh[1] == 3 and sh[2] == 3 and sh[3] == x.shape[-1] and x.is_contiguous()):
-        return False
+    return (x.dim() == 4 and len(sh) == 4 and sh[1] == sh[2] and pad == sh[1] // 2 and dil == 1
+            and sh[3] == x.shape[-1])
+
+
+_FUSED_INPUT = ("conv3x3_fwd_fused", "igemm_fwd_a_scale", "pw_fwd_squeeze")
+
+
+def _fwd_choice_unplanned(x, w, stride, pad, dil, stats_into, tp) -> str:
+    """The consumer of the deferred input ``tp`` for a conv no plan covers: the planner's rule
+    (fusion.fwd_rule) on this call's shapes -- one of _FUSED_INPUT, or "materialize"."""
+    if not (_std_geometry(x, w, stride, pad, dil) and x.is_contiguous() and isinstance(stats_into, BNWorkspace)):
+        return "materialize"
+    kind = "plain" if tp.res is None else ("tail" if tp.mask is not None else "other")
+    if kind == "other":
+        return "materialize"
     n, h, wd, c = x.shape
-    return bool(torch.ops.tfx.conv3x3_fused_supported(n, h, wd, c, sh[0]))
+    pre, fwd = fusion.fwd_rule(kind, c, w.shape[0], w.shape[1], stride, n, (h, wd), ws="obj")
+    return fwd if pre is None and fwd in _FUSED_INPUT else "materialize"
 
 
 STEM_WGRAD_CALLS = [0]  # stem weight gradients by stem.hip (tests)
-_STEM_WGRAD = True  # A/B hook: False runs the stem's weight gradient on the generic implicit GEMM
 
 
 _STEM_WS = {}
@@ -269,27 +275,6 @@ def _stem_ok(x, w, stride, pad, dil) -> bool:
 
 
 PW_APPLY_CALLS = [0]  # 1x1 forwards that applied their input BN on load (tests)
-_BN_ON_LOAD_1X1 = True  # A/B hook: False materialises a deferred plain BN before its 1x1 consumer
-
-
-def _pw_apply_ok(x, w, stride, pad, dil, stats_into) -> bool:
-    """Can this 1x1 conv apply its input's plain ReLU BN on load (one k-tile: <= 64 input channels)?"""
-    sh = w.shape
-    return (stride == 1 and pad == 0 and dil == 1 and isinstance(stats_into, BNWorkspace) and len(sh) == 4
-            and sh[1] == 1 and sh[2] == 1 and sh[3] == x.shape[-1] and x.shape[-1] <= 64 and x.shape[-1] % 8 == 0
-            and x.is_contiguous() and _DEFER_BN_IN and _BN_ON_LOAD_1X1)
-
-
-def _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into) -> bool:
-    """Can this conv's forward run fused with the deferred tail ``tp`` of its input (pw_fwd.hip)?
-    Only a residual + ReLU tail (residual and mask bits set): a plain deferred BN falls through."""
-    sh = w.shape
-    if tp.res is None or tp.mask is None:
-        return False
-    if not (stride == 1 and pad == 0 and dil == 1 and isinstance(stats_into, BNWorkspace) and len(sh) == 4
-            and sh[1] == 1 and sh[2] == 1 and sh[3] == x.shape[-1] and x.is_contiguous()):
-        return False
-    return bool(torch.ops.tfx.pw_fwd_squeeze_supported(sh[3], sh[0], x.numel() // sh[3]))
 
 
 def _pw_expand_ok(x, w, stride, pad, dil, lazy, sink) -> bool:
@@ -340,54 +325,74 @@ class _Conv2d(torch.autograd.Function):
         ctx.w, ctx.cfg, ctx.sink, ctx.bnb = w, (stride, pad, dil), sink, bnb
         ctx.native = _native.use_native(x)
         ctx.save_for_backward(x)
+        # the layer's entry of its model's fusion plan (training steps only: eval passes no statistics
+        # workspace); None = no plan covers this conv -- the same rules decide at call time
+        lp = ctx.lp = fusion.layer_plan(w) if (ctx.native and stats_into is not None) else None
         if ctx.native:
             if _flip_ok(w, stride, pad, dil):
                 w.store.flip_stale = True  # the weights may have changed since the last refresh
-            tp = getattr(x, "_tfx_tail", None)
+            tp = fusion.carried(x, "tail")
             if tp is not None and not tp.done:
-                if tp.res is None and _conv3_fused_ok(x, w, stride, pad, dil, stats_into):
-                    # BN + ReLU of the input applied on load, 3x3 conv from a halo tile, the output
-                    # BN's statistics (conv3x3_fused.hip); x stays unwritten until something reads it
-                    ws = stats_into
-                    tp.ensure_fin()
-                    y, ws.pending_save = torch.ops.tfx.conv3x3_fwd_fused(tp.x, tp.save, w.value, ws.get(x.device),
-                                                                         *ws.finalize_args)
-                    ctx.pending_in = tp
-                    CONV3_FWD_CALLS[0] += 1
-                    fusion.note("bn_on_load", w.name, "conv3x3_fwd_fused")
-                    return y
-                if tp.res is None and _pw_apply_ok(x, w, stride, pad, dil, stats_into):
-                    # a plain ReLU BN applied on load by this single-k-tile 1x1 conv (igemm a_scale):
-                    # x stays unwritten (the fused backward forms it on load too)
-                    ws = stats_into
-                    tp.ensure_fin()
-                    y, ws.pending_save = torch.ops.tfx.conv_fwd_bn_in(tp.x, tp.save, w.value, ws.get(x.device),
-                                                                      *ws.finalize_args)
-                    ctx.pending_in = tp
-                    PW_APPLY_CALLS[0] += 1
-                    fusion.note("bn_on_load", w.name, "igemm_fwd_a_scale")
-                    return y
-                if _pw_squeeze_ok(x, w, stride, pad, dil, tp, stats_into):
-                    # the previous block's tail apply + this conv + its BN statistics in one launch:
-                    # x (and the tail's mask bits) are written here (pw_fwd.hip)
-                    ws = stats_into
-                    tp.ensure_fin()
-                    y, ws.pending_save = torch.ops.tfx.pw_fwd_squeeze(
-                        tp.x, tp.save, tp.res, tp.res_save, w.value, x, tp.mask, ws.get(x.device), *ws.finalize_args)
-                    tp.done = True
-                    PW_SQUEEZE_CALLS[0] += 1
-                    fusion.note("block_boundary_fwd", w.name, "pw_fwd_squeeze")
-                    return y
+                if lp is not None:
+                    want = lp.fwd if (lp.pre is None and lp.fwd in _FUSED_INPUT) else "materialize"
+                else:
+                    want = _fwd_choice_unplanned(x, w, stride, pad, dil, stats_into, tp)
+                ok_ws = isinstance(stats_into, BNWorkspace) and x.is_contiguous()
+                if want == "conv3x3_fwd_fused":
+                    if ok_ws and tp.res is None:
+                        # BN + ReLU of the input applied on load, 3x3 conv from a halo tile, the output
+                        # BN's statistics (conv3x3_fused.hip); x stays unwritten until something reads it
+                        ws = stats_into
+                        tp.ensure_fin()
+                        y, ws.pending_save = torch.ops.tfx.conv3x3_fwd_fused(tp.x, tp.save, w.value,
+                                                                             ws.get(x.device), *ws.finalize_args)
+                        ctx.pending_in = tp
+                        CONV3_FWD_CALLS[0] += 1
+                        fusion.note("bn_on_load", w.name, "conv3x3_fwd_fused")
+                        return y
+                    fusion.miss(w.name, want, "input is not a deferred plain BN")
+                elif want == "igemm_fwd_a_scale":
+                    if ok_ws and tp.res is None:
+                        # a plain ReLU BN applied on load by this single-k-tile 1x1 conv (igemm a_scale):
+                        # x stays unwritten (the fused backward forms it on load too)
+                        ws = stats_into
+                        tp.ensure_fin()
+                        y, ws.pending_save = torch.ops.tfx.conv_fwd_bn_in(tp.x, tp.save, w.value, ws.get(x.device),
+                                                                          *ws.finalize_args)
+                        ctx.pending_in = tp
+                        PW_APPLY_CALLS[0] += 1
+                        fusion.note("bn_on_load", w.name, "igemm_fwd_a_scale")
+                        return y
+                    fusion.miss(w.name, want, "input is not a deferred plain BN")
+                elif want == "pw_fwd_squeeze":
+                    if ok_ws and tp.res is not None and tp.mask is not None:
+                        # the previous block's tail apply + this conv + its BN statistics in one launch:
+                        # x (and the tail's mask bits) are written here (pw_fwd.hip)
+                        ws = stats_into
+                        tp.ensure_fin()
+                        y, ws.pending_save = torch.ops.tfx.pw_fwd_squeeze(
+                            tp.x, tp.save, tp.res, tp.res_save, w.value, x, tp.mask, ws.get(x.device),
+                            *ws.finalize_args)
+                        tp.done = True
+                        PW_SQUEEZE_CALLS[0] += 1
+                        fusion.note("block_boundary_fwd", w.name, "pw_fwd_squeeze")
+                        return y
+                    fusion.miss(w.name, want, "input is not a deferred residual tail")
                 if tp.fin is not None and tp.res_save is None:
                     fusion.note("bn_finalize_fold", w.name, "bn_apply_fin")
                 else:
                     fusion.note("layerwise", w.name, "bn_apply_into")
                 tp.materialize()
+            elif lp is not None and lp.fwd in _FUSED_INPUT:
+                fusion.miss(w.name, lp.fwd, "input already written")
             if isinstance(stats_into, BNWorkspace):
                 ws = stats_into
-                stem = _STEM_WGRAD and _stem_ok(x, w, stride, pad, dil)
+                if lp is not None:
+                    stem = lp.fwd == "stem_fwd"
+                else:
+                    stem = fusion.knob("stem_wgrad") and _stem_ok(x, w, stride, pad, dil)
                 m_out = _conv_rows(x, w, stride, pad, dil)
-                rows = ws.fin_rows() if (_FOLD_FIN and not stem and m_out <= _FOLD_FIN_MAX_ROWS and
+                rows = ws.fin_rows() if (fusion.knob("fold_fin") and not stem and m_out <= _FOLD_FIN_MAX_ROWS and
                                          torch.ops.tfx.bn_apply_fin_supported(w.shape[0])) else None
                 if rows is not None:
                     # epilogue statistics into a few zeroed scratch rows; the finalize is owed (ws.fin) --
@@ -418,8 +423,15 @@ class _Conv2d(torch.autograd.Function):
         stride, pad, dil = ctx.cfg
         need_dx = ctx.needs_input_grad[0]
         tp = getattr(ctx, "pending_in", None)
-        lazy = getattr(gy, "_tfx_lazy_bnbwd", None) if ctx.native else None
-        if tp is not None and not tp.done and lazy is not None and need_dx and _conv3_bwd_fused_ok(w, lazy, ctx.bnb, tp):
+        lazy = fusion.carried(gy, "lazy_bnbwd") if ctx.native else None
+        lp = ctx.lp
+        planned = lp.bwd if lp is not None else None
+
+        def allowed(kernel):  # the plan's fused backward for this layer (no plan: every rule may fire)
+            return lp is None or planned == kernel
+
+        if tp is not None and not tp.done and lazy is not None and need_dx and allowed("conv3x3_bwd_fused") \
+                and _conv3_bwd_fused_ok(w, lazy, ctx.bnb, tp):
             # the stage-1 3x3 conv's whole backward: the output BN's backward apply and the input BN's ReLU
             # output formed on load, data + weight gradient, the input BN's backward partials
             # (conv3x3_fused.hip) -- neither dy nor x is ever written
@@ -431,12 +443,16 @@ class _Conv2d(torch.autograd.Function):
             dx = _negctl("conv3_fused_bwd", dx, w)
             _grad_ready(w)
             return dx, None, None, None, None, None, None, None, None
-        if tp is not None and not (tp.res is None and lazy is not None and need_dx and ctx.native
-                                   and _pw_expand_ok(x, w, stride, pad, dil, lazy, ctx.sink)):
+        if planned == "conv3x3_bwd_fused":
+            fusion.miss(w.name, planned, "no fusible lazy gradient / pending input")
+        expand = (ctx.native and lazy is not None and need_dx and allowed("pw_bwd_expand")
+                  and _pw_expand_ok(x, w, stride, pad, dil, lazy, ctx.sink))
+        if tp is not None and not (tp.res is None and expand):
             tp.materialize()  # the forward applied the input BN on load only
         if ctx.native:
             if lazy is not None:
-                if need_dx and _pw_squeeze_bwd_ok(x, w, stride, pad, dil, lazy, ctx.sink, ctx.bnb):
+                if need_dx and allowed("pw_bwd_squeeze") and _pw_squeeze_bwd_ok(x, w, stride, pad, dil, lazy, ctx.sink,
+                                                                                ctx.bnb):
                     # BN1's backward apply + this conv's data AND weight gradient in one launch, the
                     # residual branch's masked gradient added and the previous tail BN's backward
                     # partials reduced in the dx epilogue (pw_bwd.hip F1)
@@ -450,7 +466,7 @@ class _Conv2d(torch.autograd.Function):
                     dx = _negctl("lazy_bn_bwd", dx, w)
                     _grad_ready(w)
                     return dx, None, None, None, None, None, None, None, None
-                if need_dx and _pw_expand_ok(x, w, stride, pad, dil, lazy, ctx.sink):
+                if expand:
                     # the tail BN's backward apply + this conv's data AND weight gradient in one
                     # launch; dy never written (pw_bwd.hip).  The BN2 backward partials of dx ride along.
                     # a2_lazy: the forward applied BN2 on load (x never written) -- formed on load here too
@@ -477,11 +493,17 @@ class _Conv2d(torch.autograd.Function):
                     dx = _negctl("lazy_bn_bwd", dx, w)
                     _grad_ready(w)
                     return dx, None, None, None, None, None, None, None, None
+                if planned in ("pw_bwd_squeeze", "pw_bwd_expand"):
+                    fusion.miss(w.name, planned, "the lazy gradient / sink state does not fit")
                 fusion.note("layerwise", w.name, "bn_bwd_apply")
                 gy = lazy.materialize()
+            elif planned in ("pw_bwd_squeeze", "pw_bwd_expand"):
+                fusion.miss(w.name, planned, "the output gradient arrived materialised")
             gy = gy.contiguous()
             sink = ctx.sink
-            if not need_dx and w.trainable and _STEM_WGRAD and not _PENDING_SR and _stem_ok(x, w, stride, pad, dil):
+            stem_w = (planned == "stem_wgrad") if lp is not None else (fusion.knob("stem_wgrad") and
+                                                                        _stem_ok(x, w, stride, pad, dil))
+            if not need_dx and w.trainable and stem_w and not _PENDING_SR:
                 # the CIFAR stem (8 padded input channels, no input gradient): one block per image (stem.hip)
                 torch.ops.tfx.stem_wgrad(gy, x.contiguous(), w.grad, _stem_ws(gy.device, w.shape[0]))
                 STEM_WGRAD_CALLS[0] += 1
@@ -530,7 +552,7 @@ class _Conv2d(torch.autograd.Function):
                     if sink is not None:  # mode "produce": park it for the last consumer
                         sink.put(dx)
                         dx = None
-                    elif bnb is not None and stride == 2 and _SR_DEFER and w.trainable and bnb.mask is None \
+                    elif bnb is not None and stride == 2 and fusion.knob("sr_defer") and w.trainable and bnb.mask is None \
                             and not bnb.deferred and bnb.red is None:
                         # dx is the complete output gradient of the BN that produced x: its backward
                         # partials go into the BN's slots now, their reduction rides in the tail of the
@@ -538,8 +560,8 @@ class _Conv2d(torch.autograd.Function):
                         torch.ops.tfx.bn_bwd_reduce_into(dx, bnb.x, bnb.save, bnb.relu, None, bnb.ws)
                         sr_bnb = bnb
             if w.trainable:
-                if sr_bnb is not None or (_SR_TAKE_PENDING and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device):
-                    take = _SR_TAKE_PENDING and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device
+                if sr_bnb is not None or (fusion.knob("sr_take") and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device):
+                    take = fusion.knob("sr_take") and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device
                     t2 = _PENDING_SR.pop(0) if take else None
                     t1 = sr_bnb
                     r1, r2 = torch.ops.tfx.conv_wgrad_sr2(
@@ -575,7 +597,7 @@ def conv2d(x: torch.Tensor, w: Variable, stride: int = 1, pad: int = 0, dil: int
     Ignored on CPU."""
     gpu = x.device.type == "cuda"
     ws = bn_stats_into if (bn_stats_into is not None and gpu) else None
-    bnb = getattr(x, "_tfx_bnb", None) if (gpu and fuse_input_bn_backward) else None
+    bnb = fusion.carried(x, "bnb") if (gpu and fuse_input_bn_backward) else None
     return _Conv2d.apply(x, w.store.anchor, w, stride, pad, dil, ws, grad_sink if gpu else None, bnb)
 
 
@@ -685,7 +707,7 @@ class BNWorkspace:
 
 class BNBackwardFusion:
     """What a consumer conv's data-gradient epilogue needs to reduce a BN's backward (attached to
-    the BN output as ``_tfx_bnb``): the BN input, its [mean|invstd|scale|shift], the residual
+    the BN output as fusion carrier "bnb"): the BN input, its [mean|invstd|scale|shift], the residual
     layer's ReLU mask bits, the slot workspace and the parameter-gradient views.  The conv fills
     ``red`` ([sum g' | sum g' xhat]) (or a later weight-gradient launch does, from the slots); the BN
     backward then runs only its apply pass."""
@@ -837,10 +859,10 @@ class _BatchNorm(torch.autograd.Function):
             fuse_res = res_lazy and pending and relu
             # residual + ReLU tail whose only first reader is the next block's conv1: leave the apply
             # to that conv (TailPending) -- it forms out / mask while loading its input
-            defer_tail = defer_apply and _DEFER_TAIL and pending and relu and res is not None and \
+            defer_tail = defer_apply and fusion.knob("defer_tail") and pending and relu and res is not None and \
                 x.shape[-1] % 8 == 0 and (fuse_res or not res_lazy)
             # plain ReLU BN whose only reader is a 3x3 conv that applies it on load
-            defer_plain = defer_apply and _DEFER_BN_IN and pending and relu and res is None and x.shape[-1] % 8 == 0
+            defer_plain = defer_apply and fusion.knob("defer_bn_in") and pending and relu and res is None and x.shape[-1] % 8 == 0
             if res_lazy and not fuse_res:
                 res = torch.ops.tfx.bn_apply_train(res_bnb.x, None, res_bnb.save, False)[0]
             defer_out = defer and pending and res is None and bnb_out is not None and _vec_ok(x.shape[-1])
@@ -854,12 +876,12 @@ class _BatchNorm(torch.autograd.Function):
                     owed = None
                 if defer_plain:
                     y = torch.empty_like(x)
-                    y._tfx_tail = TailPending(x, save, None, None, y, None, fin=owed)
+                    fusion.carry(y, "tail", TailPending(x, save, None, None, y, None, fin=owed))
                 elif defer_tail:
                     y = torch.empty_like(x)
                     mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
-                    y._tfx_tail = TailPending(x, save, res_bnb.x if fuse_res else res.contiguous(),
-                                              res_bnb.save if fuse_res else None, y, mask, fin=owed)
+                    fusion.carry(y, "tail", TailPending(x, save, res_bnb.x if fuse_res else res.contiguous(),
+                                                        res_bnb.save if fuse_res else None, y, mask, fin=owed))
                 elif fuse_res:
                     y, mask = torch.ops.tfx.bn_apply_res_bn(x, res_bnb.x, save, res_bnb.save, relu)
                 elif defer_out:
@@ -876,7 +898,7 @@ class _BatchNorm(torch.autograd.Function):
             # residual + ReLU: the backward needs only the 1-bit ReLU mask, not the residual tensor
             assert not fuse_res or mask is not None
             ctx.save_for_backward(x, None if mask is not None else res, save, mask)
-            ctx.tp = getattr(y, "_tfx_tail", None) if (defer_plain or defer_tail) and pending else None
+            ctx.tp = fusion.carried(y, "tail") if (defer_plain or defer_tail) and pending else None
             if training and bnb_out is not None and (res is None or not relu or mask is not None) \
                     and x.shape[-1] % 8 == 0:
                 train_p = gamma is not None and gamma.trainable
@@ -910,7 +932,7 @@ class _BatchNorm(torch.autograd.Function):
             # tensor write less per identity block
             masked = ctx.has_res and ctx.res_sink is not None and mask is not None and \
                 getattr(ctx.res_sink, "accept_masked", False) and relu
-            if ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and _LAZY_BN_BWD and relu \
+            if ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and fusion.knob("lazy_bn_bwd") and relu \
                     and mask is not None and res is None and _res_bn_sec_ok(ctx, gy, mask, relu, masked) \
                     and x.shape[-1] % 4 == 0 \
                     and torch.ops.tfx.pw_bwd_expand_supported(x.shape[-1] // 4, x.numel() // x.shape[-1]):
@@ -919,7 +941,7 @@ class _BatchNorm(torch.autograd.Function):
                 rb = ctx.res_bnb
                 dx = _zero_scalar(x.dtype, x.device).expand(x.shape)
                 lz = LazyBNGrad(gy, x, save, ctx.bnb.red, relu, mask, sec=rb)
-                dx._tfx_lazy_bnbwd = lz
+                fusion.carry(dx, "lazy_bnbwd", lz)
                 rb.sec_lazy = lz
                 rb.in_mask, dres = mask, gy
                 ctx.bnb.red = None
@@ -932,7 +954,7 @@ class _BatchNorm(torch.autograd.Function):
                 pass_mask = relu
                 # the residual BN's slot reduction is deferred to the tail of the next weight-gradient
                 # launch (this block's conv3, which autograd runs before the residual BN)
-                defer = _SR_DEFER
+                defer = fusion.knob("sr_defer")
                 dx, dres, red2 = torch.ops.tfx.bn_bwd_apply_sec(gy, x, save, ctx.bnb.red, relu, mask, rb.x, rb.save,
                                                                  rb.ws, rb.dgamma if p_t else None,
                                                                  rb.dbeta if p_t else None, not pass_mask, not defer)
@@ -949,20 +971,20 @@ class _BatchNorm(torch.autograd.Function):
                 assert not relu and not ctx.has_res
                 dx, dres = torch.ops.tfx.bn_bwd_apply(gy, x, None, save, ctx.bnb.red, True, ctx.bnb.in_mask, False)
                 ctx.bnb.red = ctx.bnb.in_mask = None
-            elif ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and _LAZY_BN_BWD and masked \
+            elif ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and fusion.knob("lazy_bn_bwd") and masked \
                     and res is None and relu and mask is not None:
                 # residual + ReLU tail whose residual gradient is parked as (gy, mask): dx stays lazy --
                 # the producing conv forms it on load (LazyBNGrad)
                 dx = _zero_scalar(x.dtype, x.device).expand(x.shape)
-                dx._tfx_lazy_bnbwd = LazyBNGrad(gy, x, save, ctx.bnb.red, relu, mask)
+                fusion.carry(dx, "lazy_bnbwd", LazyBNGrad(gy, x, save, ctx.bnb.red, relu, mask))
                 dres = None
                 ctx.bnb.red = None
-            elif ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and _LAZY_BN_BWD and relu \
+            elif ctx.bnb is not None and ctx.bnb.red is not None and ctx.lazy_bwd and fusion.knob("lazy_bn_bwd") and relu \
                     and not ctx.has_res and mask is None and ctx.bnb.in_mask is None:
                 # plain ReLU BN fed by a conv: dx stays lazy (LazyBNGrad, ReLU mask recomputed from x) --
                 # a squeezing 1x1 producer forms it on load (pw_bwd.hip F1), any other materialises it
                 dx = _zero_scalar(x.dtype, x.device).expand(x.shape)
-                dx._tfx_lazy_bnbwd = LazyBNGrad(gy, x, save, ctx.bnb.red, relu, None)
+                fusion.carry(dx, "lazy_bnbwd", LazyBNGrad(gy, x, save, ctx.bnb.red, relu, None))
                 dres = None
                 ctx.bnb.red = None
             elif ctx.bnb is not None and ctx.bnb.red is not None:
@@ -1008,7 +1030,7 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
 
     ``workspace``: the layer's slot tensor or :class:`BNWorkspace` (then a statistics finalize
     done by the producing conv is picked up).  On the GPU in training mode the output carries a
-    :class:`BNBackwardFusion` (``_tfx_bnb``) for a consumer conv that opts into reducing this
+    :class:`BNBackwardFusion` (fusion carrier "bnb") for a consumer conv that opts into reducing this
     BN's backward in its data-gradient epilogue.
 
     ``fuse_residual_bn_backward``: ``residual`` is another BN's output used ONLY here (a ResNet
@@ -1034,7 +1056,7 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
         workspace = None
     sink = residual_grad_sink if (x.device.type == "cuda" and residual is not None) else None
     bnb_out = [] if (x.device.type == "cuda" and training) else None
-    rb = getattr(residual, "_tfx_bnb", None) if residual is not None else None
+    rb = fusion.carried(residual, "bnb") if residual is not None else None
     res_bnb = None
     if rb is not None and (rb.deferred or fuse_residual_bn_backward):
         res_bnb = (rb, bool(fuse_residual_bn_backward))
@@ -1042,7 +1064,7 @@ def batch_norm(x, gamma: Optional[Variable], beta: Optional[Variable], running_m
                          workspace, stats_ready and training and workspace is not None, sink, wsobj, bnb_out, res_bnb,
                          bool(defer_output), bool(lazy_backward), bool(defer_apply))
     if bnb_out:
-        y._tfx_bnb = bnb_out[0]
+        fusion.carry(y, "bnb", bnb_out[0])
     return y
 
 
@@ -1283,8 +1305,6 @@ def softmax_cross_entropy(logits, labels, naive: bool = False, unit_seed: bool =
 
 
 # ---- fused classifier head (training step): gap -> linear -> mean softmax xent, one launch (head.hip)
-_FUSE_HEAD = True  # test / A-B hook: False composes global_avg_pool, linear and softmax_cross_entropy
-_HEAD_TAIL = True  # test / A-B hook: False materialises a deferred last tail before the fused head
 HEAD_FUSED_CALLS = [0]
 HEAD_TAIL_CALLS = [0]
 _CHECK_SEED = os.environ.get("TFX_CHECK_SEED", "0") == "1"
@@ -1355,9 +1375,9 @@ class _HeadXent(torch.autograd.Function):
 def _head_tail(feat):
     """(TailPending, BNBackwardFusion) when ``feat`` is a ReLU + identity-residual tail BN's output that
     was never written and whose backward reduction nobody owes yet: the fused head takes both over."""
-    tp = getattr(feat, "_tfx_tail", None)
-    bnb = getattr(feat, "_tfx_bnb", None)
-    if not _HEAD_TAIL or tp is None or tp.done or bnb is None:
+    tp = fusion.carried(feat, "tail")
+    bnb = fusion.carried(feat, "bnb")
+    if not fusion.knob("head_tail") or tp is None or tp.done or bnb is None:
         return None
     if tp.res is None or tp.res_save is not None or tp.mask is None or bnb.mask is not tp.mask or not bnb.relu:
         return None
@@ -1375,7 +1395,7 @@ def classifier_head_xent(feat, w: Variable, b: Optional[Variable], labels, naive
     (csrc/kernels/head.hip); otherwise, and for TF1's naive loss, the three ops compose.  On the fused
     path the gradients are formed for a backward seed of exactly 1: a scaled seed (loss scaling,
     ``(loss * k).backward()``) is not applied -- such callers pass ``unit_seed=False``."""
-    fused = (_FUSE_HEAD and unit_seed and not naive and feat.is_cuda and feat.dim() == 4
+    fused = (fusion.knob("fuse_head") and unit_seed and not naive and feat.is_cuda and feat.dim() == 4
              and feat.dtype == torch.bfloat16 and labels.dtype == torch.long and labels.is_cuda
              and w.value.dtype == torch.bfloat16 and w.value.dim() == 2 and w.value.is_contiguous()
              and _native.use_native(feat))

@@ -74,10 +74,9 @@ def test_resnet50_fold_matches_separate_finalize(gpu):
     img = torch.randint(0, 256, (256, 32, 32, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
     lab = torch.randint(0, 10, (256,), generator=torch.Generator().manual_seed(6)).to(gpu)
     out = {}
-    prev = tnn._FOLD_FIN
-    try:
-        for fold in (True, False):
-            tnn._FOLD_FIN = fold
+    from tensorflow_examples_amd.ops import fusion
+    for fold in (True, False):
+        with fusion.override(fold_fin=fold):
             # zero-init residuals: a random-init step is chaotic in f32 rounding order
             # (profiles/r04_determinism), so only the well-conditioned start compares two paths
             st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=3, zero_init_residual=True)
@@ -90,8 +89,6 @@ def test_resnet50_fold_matches_separate_finalize(gpu):
             stats = {b.gamma.name: (b.mean.detach().clone(), b.var.detach().clone()) for b in bns}
             dirty = [b.gamma.name for b in bns if b.ws.buf is not None and float(b.ws.buf.abs().max()) != 0.0]
             out[fold] = (loss, calls, stats, dirty)
-    finally:
-        tnn._FOLD_FIN = prev
     (l1, c1, s1, d1), (l0, c0, s0, d0) = out[True], out[False]
     assert c0 == 0 and c1 >= 20, (c1, c0)
     assert not d1 and not d0, (d1, d0)

@@ -112,18 +112,16 @@ def test_resnet50_deferred_bn1_matches_layerwise(gpu):
         torch.cuda.synchronize()
         return float(loss), st.grad.clone(), st
 
-    saved = nnops._DEFER_BN_IN
-    try:
+    from tensorflow_examples_amd.ops import fusion
+    with fusion.override():  # the default knobs, restored after
         n0, n1, n2 = nnops.CONV3_FWD_CALLS[0], nnops.CONV3_BWD_CALLS[0], nnops.PW_APPLY_CALLS[0]
         l0, g0, st = run()
         assert nnops.CONV3_FWD_CALLS[0] - n0 == 3, "the three stage-1 conv2 run fused"
         assert nnops.CONV3_BWD_CALLS[0] - n1 == 3, "... forward and backward"
         assert nnops.PW_APPLY_CALLS[0] - n2 == 3, "the three stage-1 conv3 apply BN2 on load"
         l1, g1, _ = run()
-        nnops._DEFER_BN_IN = False
-        l2, g2, _ = run()
-    finally:
-        nnops._DEFER_BN_IN = saved
+        with fusion.override(defer_bn_in=False):
+            l2, g2, _ = run()
     assert abs(l0 - l2) <= max(4 * abs(l0 - l1), 0.01 * abs(l2)), (l0, l1, l2)
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)

@@ -27,9 +27,10 @@ def test_set_groups_and_restore():
         fusion.set_groups(fusion.PROFILES["r2"])
         on = fusion.enabled()
         assert {g for g, v in on.items() if v} == fusion.PROFILES["r2"]
-        assert tnn._DEFER_TAIL is False and tnn._FUSE_HEAD is True and tnn._FOLD_FIN is False
+        assert fusion.knob("defer_tail") is False and fusion.knob("fuse_head") is True
+        assert fusion.knob("fold_fin") is False
         fusion.set_groups(set(fusion.GROUPS))
-        assert all(fusion.enabled().values()) and tnn._FOLD_FIN is True
+        assert all(fusion.enabled().values()) and fusion.knob("fold_fin") is True
     finally:
         fusion.restore(prev)
     assert fusion.enabled() == prev
@@ -81,3 +82,115 @@ def test_bn_workspace_rows_once_per_step():
     st.zero_grad()
     assert ws.fin_rows() is not None
     assert tnn.BNWorkspace(8).fin_rows() is None  # no store: no scratch
+
+
+# the fused-group table of tests/test_resnet50_train_gpu.py::test_resnet50_fusion_plan (the GPU step's
+# recorder at batch 256): the plan built on the CPU must predict it
+GPU_TABLE = {
+    ("block_boundary_fwd", "pw_fwd_squeeze"): 6,
+    ("bn_on_load", "conv3x3_fwd_fused"): 3,
+    ("bn_on_load", "igemm_fwd_a_scale"): 3,
+    ("lazy_bn_bwd", "pw_bwd_expand"): 3,
+    ("lazy_bn_bwd", "pw_bwd_squeeze"): 2,
+    ("conv3_fused_bwd", "conv3x3_bwd_fused"): 3,
+    ("stem_kernels", "stem_wgrad"): 1,
+    ("bn_epilogue", "stem_fwd"): 1,
+    ("fused_head", "head_xent"): 1,
+    ("head_tail", "head_xent_tail"): 1,
+    ("s2_addend", "igemm_dgrad_compact"): 3,
+}
+
+
+def _native_or_skip():
+    from tensorflow_examples_amd.ops import _native
+    if not _native.load():
+        pytest.skip("native library not built (the planner asks the kernels' support predicates)")
+
+
+def test_resnet50_plan_built_on_cpu_matches_gpu_table():
+    """The ResNet-50 fusion plan at batch 256, built without a GPU: the same fused-kernel counts as the
+    GPU step's recorder table, every conv planned (53 forwards), and the per-layer choices where the
+    kernels' shape limits put them (stage 1 fully fused, stage 2 only at the block boundaries)."""
+    _native_or_skip()
+    from tensorflow_examples_amd.models.resnet import build_resnet_cifar
+    st, m = build_resnet_cifar(device="cpu", depth=50, dtype=torch.float32)
+    plan = m.plan_for(256)
+    assert plan is m.plan_for(256)  # cached per (batch, size, config)
+    assert len(plan.layers) == 53
+    fc = plan.fused_counts()
+    assert {gk: n for gk, n in fc.items() if gk in GPU_TABLE} == GPU_TABLE
+    assert fc[("bn_epilogue", "igemm_fwd_stats")] == 53 - 1 - 6 - 3 - 3  # every other conv: epilogue statistics
+    lay = plan.layers
+    assert lay["resnet50/stage1_block2/conv1"].fwd == "pw_fwd_squeeze"
+    assert lay["resnet50/stage1_block2/conv2"].bwd == "conv3x3_bwd_fused"
+    assert lay["resnet50/stage2_block2/conv2"].pre == "bn_apply_into"  # 128 channels: no fused consumer
+    assert lay["resnet50/stage3_block2/conv1"].input == "tail" and lay["resnet50/stage3_block2/conv1"].pre
+    assert "igemm_dgrad_compact" in lay["resnet50/stage2_block1/shortcut"].extra
+    assert "stage1_block2/conv2" in plan.table()
+
+
+def test_plan_follows_the_fusion_config():
+    """Switching a group off changes the plan (and a new plan is built for the new config)."""
+    _native_or_skip()
+    from tensorflow_examples_amd.models.resnet import build_resnet_cifar
+    st, m = build_resnet_cifar(device="cpu", depth=50, dtype=torch.float32)
+    p0 = m.plan_for(256)
+    with fusion.override(defer_tail=False, defer_bn_in=False):
+        p1 = m.plan_for(256)
+        assert p1 is not p0
+        c = p1.fused_counts()
+        assert c[("block_boundary_fwd", "pw_fwd_squeeze")] == 0
+        assert c[("bn_on_load", "conv3x3_fwd_fused")] == 0 and c[("conv3_fused_bwd", "conv3x3_bwd_fused")] == 0
+        assert ("head_tail", "head_xent_tail") not in c
+    with fusion.override(**{k: False for k in fusion.KNOBS}):
+        c = m.plan_for(256).counts()
+        assert set(g for g, _ in c) <= {"conv", "bn_epilogue"}  # statistics-only epilogues, nothing fused
+    assert m.plan_for(256) is p0  # config restored: the cached plan again
+    # smaller batch: the stage-1 fused kernels' row limits are per-batch (the planner asks per shape)
+    assert len(m.plan_for(64).layers) == 53
+
+
+def test_resnet18_plan():
+    """Basic-block ResNets plan too: no deferred applies, projection shortcuts, the stem kernels."""
+    _native_or_skip()
+    from tensorflow_examples_amd.models.resnet import build_resnet_cifar
+    st, m = build_resnet_cifar(device="cpu", depth=18, dtype=torch.float32)
+    plan = m.plan_for(128)
+    assert len(plan.layers) == 1 + 8 * 2 + 3
+    assert all(lp.input == "tensor" and lp.pre is None for lp in plan.layers.values())
+    assert plan.layers["resnet18/conv0"].fwd == "stem_fwd"
+
+
+def test_knob_override_and_unknown_knob():
+    assert fusion.knob("sr_defer") is True
+    s0 = fusion.CONFIG.signature
+    with fusion.override(sr_defer=False):
+        assert fusion.knob("sr_defer") is False and fusion.knob("sr_take") is True
+        assert not fusion.enabled()["deferred_slot_reduce"] and fusion.CONFIG.signature != s0
+    assert fusion.knob("sr_defer") is True and fusion.CONFIG.signature == s0
+    with pytest.raises(KeyError):
+        with fusion.override(no_such_knob=True):
+            pass
+    assert fusion.knob("sr_defer") is True
+
+
+def test_carriers_ride_with_their_tensor():
+    a, b = torch.zeros(3), torch.zeros(3)
+    obj = object()
+    fusion.carry(a, "tail", obj)
+    assert fusion.carried(a, "tail") is obj
+    assert fusion.carried(b, "tail") is None and fusion.carried(a, "bnb") is None
+    assert fusion.carried(None, "tail") is None
+    with pytest.raises(KeyError):
+        fusion.carry(a, "no_such_kind", obj)
+
+
+def test_unplanned_rule_matches_planner():
+    """A conv outside a planned model takes the planner's rule on its call's shapes."""
+    _native_or_skip()
+    assert fusion.fwd_rule("plain", 64, 64, 3, 1, 256, (32, 32)) == (None, "conv3x3_fwd_fused")
+    assert fusion.fwd_rule("plain", 64, 256, 1, 1, 256, (32, 32)) == (None, "igemm_fwd_a_scale")
+    assert fusion.fwd_rule("plain", 128, 512, 1, 1, 256, (16, 16)) == ("bn_apply_into", "igemm_fwd_stats")
+    assert fusion.fwd_rule("tail", 256, 64, 1, 1, 256, (32, 32)) == (None, "pw_fwd_squeeze")
+    assert fusion.fwd_rule("tensor", 64, 64, 1, 1, 8, (4, 4), ws="raw") == (None, "igemm_fwd_stats_only")
+    assert fusion.fwd_rule("tensor", 64, 64, 1, 1, 8, (4, 4), ws="none") == (None, "igemm_fwd")

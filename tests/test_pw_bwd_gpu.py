@@ -166,7 +166,8 @@ def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
         torch.cuda.synchronize()
         return st.grad.clone(), st
 
-    saved, saved_ok, saved_sq = nnops._LAZY_BN_BWD, nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok
+    from tensorflow_examples_amd.ops import fusion
+    saved_ok, saved_sq = nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok
     try:
         n0, n1 = nnops.PW_EXPAND_CALLS[0], nnops.PW_SQUEEZE_BWD_CALLS[0]
         g0, st = run()
@@ -179,10 +180,10 @@ def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
         nnops._pw_squeeze_bwd_ok = lambda *a: False
         g3, _ = run()
         nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok = saved_ok, saved_sq
-        nnops._LAZY_BN_BWD = False
-        g2, _ = run()
+        with fusion.override(lazy_bn_bwd=False):
+            g2, _ = run()
     finally:
-        nnops._LAZY_BN_BWD, nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok = saved, saved_ok, saved_sq
+        nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok = saved_ok, saved_sq
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12

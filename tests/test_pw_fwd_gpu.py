@@ -90,16 +90,14 @@ def test_resnet50_deferred_tails_match_layerwise(gpu):
         torch.cuda.synchronize()
         return float(loss), st.grad.clone(), st
 
-    saved = nnops._DEFER_TAIL
-    try:
+    from tensorflow_examples_amd.ops import fusion
+    with fusion.override():  # the default knobs, restored after
         n0 = nnops.PW_SQUEEZE_CALLS[0]
         l0, g0, st = run()
         assert nnops.PW_SQUEEZE_CALLS[0] - n0 == 6, "stage-1 and stage-2 tails fused into the next conv1 (3 + 3 boundaries)"
         l1, g1, _ = run()
-        nnops._DEFER_TAIL = False
-        l2, g2, _ = run()
-    finally:
-        nnops._DEFER_TAIL = saved
+        with fusion.override(defer_tail=False):
+            l2, g2, _ = run()
     # the first-step loss of a random-init ResNet-50 moves ~0.4% between two runs of the SAME path
     # (f32-atomic BN statistics, amplified through 50 layers; scripts/dev/diag_fwd.py): bound the
     # fused-vs-layerwise gap by that spread, with a 1% floor -- the kernel test above pins the
