@@ -119,6 +119,9 @@ struct IgemmArgs {
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s);
 // persistent 1x1-forward mode (igemm_persist.hip): 0 off, 2 / 3 ring depth; returns the previous mode
 int igemm_persist_set(int mode);
+// a plain ReLU BN applied on load by a 1x1 forward of M x N x K (conv_fwd_bn_in) beyond one k-tile:
+// the persistent kernel's A-operand transform takes this shape
+bool igemm_fwd_bna_supported(int64_t M, int64_t N, int64_t K);
 
 // ---------------------------------------------------------------- fused pointwise-conv backward (pw_bwd.hip)
 // Backward of a bottleneck's expanding 1x1 conv (CN -> CW = 4 CN) fused with the block-tail BN's

@@ -125,10 +125,13 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
       abort();
     }
   }
-  // the A-operand BN transform: single-k-tile pointwise forward with the fused statistics epilogue
+  // the A-operand BN transform: pointwise forward with the fused statistics epilogue -- single k-tile
+  // (register path), or the persistent kernel's on-load transform beyond
   if (a.a_scale && !(a.stats && mode == MODE_FWD && a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 &&
-                     a.pw == 0 && a.K <= BKT_HOST && a.K % 8 == 0 && a.a_shift)) {
-    fprintf(stderr, "igemm_launch: A-operand transform needs a 1x1 stride-1 forward with K <= 64 and BN stats\n");
+                     a.pw == 0 && a.a_shift && a.K % 8 == 0 &&
+                     (a.K <= BKT_HOST || igemm_fwd_bna_supported(a.M, a.N, a.K)))) {
+    fprintf(stderr, "igemm_launch: A-operand transform needs a 1x1 stride-1 forward with BN stats (K <= 64, or "
+                    "the persistent kernel's shapes)\n");
     abort();
   }
   // 1x1 stride-1 unpadded convs (two thirds of ResNet-50's) are plain GEMMs over the NHWC rows:

@@ -23,7 +23,12 @@
 namespace tfx {
 namespace {
 
-template <int BM, int BN, int GLS, bool STATS>
+// BNA: the A operand is a plain ReLU BN's input, applied on load -- A[m][k] -> relu(A a_scale[k] +
+// a_shift[k]) -- in registers, after each fragment's LDS read (the ring stays a raw LDS-DMA copy).  The
+// per-channel coefficients are staged in LDS once per block (K <= BNA_KMAX).
+constexpr int BNA_KMAX = 1024;  // 8 KB of coefficients: 128x128 tiles keep 2 blocks per CU
+
+template <int BM, int BN, int GLS, bool STATS, bool BNA = false>
 __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_BYTES = BM * BKT * 2, B_BYTES = BN * BKT * 2;
@@ -36,6 +41,8 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
   __shared__ __attribute__((aligned(16))) char ga2[GLS >= 3 ? A_BYTES : 16];
   __shared__ __attribute__((aligned(16))) char gb2[GLS >= 3 ? B_BYTES : 16];
   __shared__ __attribute__((aligned(16))) float red[STATS ? 2 * BN * 2 : 4];  // [wm][col][sum | sumsq]
+  __shared__ __attribute__((aligned(16))) float bsc[BNA ? BNA_KMAX : 4];     // a_scale, a_shift
+  __shared__ __attribute__((aligned(16))) float bsh[BNA ? BNA_KMAX : 4];
   auto img_a = [&](auto S) __attribute__((always_inline)) -> char* {
     constexpr int st = decltype(S)::value;
     if constexpr (st == 0) return ga0;
@@ -93,12 +100,29 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   };
-  auto compute = [&](const char* ia, const char* ib) __attribute__((always_inline)) {
+  // kbase: the k-tile's first channel (BNA coefficients)
+  auto compute = [&](const char* ia, const char* ib, int kbase) __attribute__((always_inline)) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8_t fa[TM], fb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[i] = frag<KM_DENSE, BM>(ia, 0, wm * WM + i * 16, kk, lane);
+      if constexpr (BNA) {
+        // the lane's 8 channels of this 32-deep half: kbase + 32 kk + 8 (lane >> 4) + 0..7
+        const int c = kbase + 32 * kk + 8 * (lane >> 4);
+        const float4 s0 = *reinterpret_cast<const float4*>(&bsc[c]), s1 = *reinterpret_cast<const float4*>(&bsc[c + 4]);
+        const float4 h0 = *reinterpret_cast<const float4*>(&bsh[c]), h1 = *reinterpret_cast<const float4*>(&bsh[c + 4]);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float f[8];
+          unpack8(__builtin_bit_cast(U4, fa[i]), f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f);
+          fa[i] = __builtin_bit_cast(bf16x8_t, pack8(f));
+        }
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[j] = frag<KM_DENSE, BN>(ib, 0, wn * WN + j * 16, kk, lane);
 #pragma unroll
@@ -175,6 +199,14 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
     }
   };
 
+  if constexpr (BNA) {
+    // the coefficients into LDS before the ring starts (its loads are the only ones outstanding later)
+    for (int i = t; i < a.K; i += 256) {
+      bsc[i] = a.a_scale[i];
+      bsh[i] = a.a_shift[i];
+    }
+    __syncthreads();
+  }
   zero();
   issue(0, IC<0>{});
   if constexpr (GLS >= 3) issue(1, IC<1>{});
@@ -191,7 +223,7 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
         }
         issue(st + GLS - 1, IC<(st_ + GLS - 1) % GLS>{});
         __builtin_amdgcn_sched_barrier(0);
-        compute(img_a(S), img_b(S));
+        compute(img_a(S), img_b(S), (st % nkt) * BKT);
         __builtin_amdgcn_sched_barrier(0);
       }
     });
@@ -222,15 +254,15 @@ int g_persist = [] {
 }();
 int persist_mode() { return g_persist; }
 
-template <int BM, int BN, int GLS, bool STATS>
+template <int BM, int BN, int GLS, bool STATS, bool BNA = false>
 void launch_p(IgemmArgs& a, hipStream_t s) {
   a.tiles_m = a.M / BM;
   a.tiles_n = a.N / BN;
   const int ntiles = a.tiles_m * a.tiles_n;
-  constexpr int lds = (BM + BN) * BKT * 2 * GLS;
+  constexpr int lds = (BM + BN) * BKT * 2 * GLS + (BNA ? 2 * BNA_KMAX * 4 : 0);
   constexpr int bpc = 163840 / lds < 4 ? 163840 / lds : 4;  // resident blocks per CU (4 waves each)
   const int grid = std::min(ntiles, num_cus() * bpc);
-  igemm_persist_kernel<BM, BN, GLS, STATS><<<grid, 256, 0, s>>>(a);
+  igemm_persist_kernel<BM, BN, GLS, STATS, BNA><<<grid, 256, 0, s>>>(a);
 }
 
 }  // namespace
@@ -245,16 +277,36 @@ int igemm_persist_set(int mode) {
 // fewer tiles the per-tile kernel's split-K over two wave groups keeps more of the chip busy, and at
 // K = 64 (one k-tile per tile) it loses 1 us of 40 (the A/B over the ResNet-50 1x1 shapes,
 // profiles/r05_persist/README.md).
+static bool persist_shape_ok(const IgemmArgs& a) {
+  return a.out_mode == OUT_BF16 && !a.trans_out && !a.bias && !a.relu && !a.addend && !a.bnb_x && a.M > 0 &&
+         a.M % 128 == 0 && a.N % 64 == 0 && a.K % BKT == 0 && a.K >= 2 * BKT && a.ldc == a.N && a.lda % 8 == 0 &&
+         a.ldb % 8 == 0 && (a.stats == nullptr || a.stat_slots > 0);
+}
+
 bool igemm_fwd_persist_ok(const IgemmArgs& a) {
+  if (a.a_scale) return igemm_fwd_persist_bna_ok(a);
   const int bn = a.N % 128 == 0 ? 128 : 64;
-  return persist_mode() != 0 && a.M > 0 && (int64_t)(a.M / 128) * (a.N / bn) >= 4 * num_cus() && a.out_mode == OUT_BF16 && !a.trans_out && !a.bias && !a.relu && !a.addend &&
-         !a.a_scale && !a.bnb_x && a.M % 128 == 0 && a.N % 64 == 0 && a.K % BKT == 0 && a.K >= 2 * BKT &&
-         a.ldc == a.N && a.lda % 8 == 0 && a.ldb % 8 == 0 && (a.stats == nullptr || a.stat_slots > 0);
+  return persist_mode() != 0 && (int64_t)(a.M / 128) * (a.N / bn) >= 4 * num_cus() && persist_shape_ok(a);
+}
+
+// the A-operand BN transform (a plain ReLU BN applied on load by this 1x1 conv): any tile count (it
+// replaces a whole BN apply pass), K <= BNA_KMAX channels of coefficients in LDS
+bool igemm_fwd_persist_bna_ok(const IgemmArgs& a) {
+  return a.a_scale && a.a_shift && a.stats && a.K <= BNA_KMAX && persist_shape_ok(a);
+}
+
+bool igemm_fwd_bna_supported(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && M % 128 == 0 && N % 64 == 0 && K % BKT == 0 && K >= 2 * BKT && K <= BNA_KMAX;
 }
 
 // X[M][C] . W[Ko][C]^T (A = X rows, B = W rows, both K-major; + BN statistics when a.stats)
 void igemm_fwd_persist(IgemmArgs& a, hipStream_t s) {
   const bool st = a.stats != nullptr;
+  if (a.a_scale) {  // BN on load: ring depth 2 (the coefficient arrays take 16 KB of LDS)
+    if (a.N % 128 == 0) launch_p<128, 128, 2, true, true>(a, s);
+    else launch_p<128, 64, 2, true, true>(a, s);
+    return;
+  }
   const int gls = persist_mode();
   if (a.N % 128 == 0) {
     if (gls == 3) { st ? launch_p<128, 128, 3, true>(a, s) : launch_p<128, 128, 3, false>(a, s); }

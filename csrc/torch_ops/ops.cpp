@@ -344,15 +344,22 @@ bool conv_stem_fwd(bool on) {
 }
 
 // conv_fwd_bn of relu(x * in_save[2C..3C) + in_save[3C..4C)) -- a plain ReLU BN applied on load by this
-// 1x1 stride-1 conv (C <= 64: one k-tile), so the BN output is never written.  Returns (y, save).
+// 1x1 stride-1 conv (C <= 64: one k-tile, register path; wider: the persistent kernel transforms each
+// A fragment after its LDS read), so the BN output is never written.  Returns (y, save).
+bool conv_fwd_bn_in_supported(int64_t M, int64_t Ko, int64_t C) {
+  return (C <= 64 && C % 8 == 0) || tfx::igemm_fwd_bna_supported(M, Ko, C);
+}
+
 std::tuple<Tensor, Tensor> conv_fwd_bn_in(Tensor x, Tensor in_save, Tensor w, Tensor ws, optional<Tensor> gamma,
                                           optional<Tensor> beta, optional<Tensor> run_mean, optional<Tensor> run_var,
                                           double momentum, double eps) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
   CHECK_F32(in_save); CHECK_CONTIG(in_save);
   auto g = geom(x.sizes().vec(), w.sizes().vec(), 1, 0, 1);
-  TORCH_CHECK(g.R == 1 && g.S == 1 && g.C <= 64 && in_save.numel() == 4 * g.C,
-              "conv_fwd_bn_in: 1x1 conv with <= 64 input channels and the input BN's [4][C] save");
+  TORCH_CHECK(g.R == 1 && g.S == 1 && in_save.numel() == 4 * g.C &&
+                  (g.C <= 64 || tfx::igemm_fwd_bna_supported(g.N * g.P * g.Q, g.Ko, g.C)),
+              "conv_fwd_bn_in: 1x1 conv with <= 64 input channels (or a persistent-kernel shape) and the input "
+              "BN's [4][C] save");
   auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
   auto save = at::empty({4 * g.Ko}, x.options().dtype(at::kFloat));
   auto a = conv_args(g, 1, 0, 1);
@@ -1879,6 +1886,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_apply_fin_supported", &bn_apply_fin_supported);
   m.def("bn_apply_fin_into", &bn_apply_fin_into);
   m.def("conv_fwd_bn_in", &conv_fwd_bn_in);
+  m.def("conv_fwd_bn_in_supported", &conv_fwd_bn_in_supported);
   m.def("stem_wgrad", &stem_wgrad);
   m.def("conv_stem_fwd", &conv_stem_fwd);
   m.def("stem_wgrad_ws_floats", &stem_wgrad_ws_floats);

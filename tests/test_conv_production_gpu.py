@@ -134,3 +134,37 @@ def test_persistent_pointwise_forward_matches_per_tile_kernel(gpu, shape):
         assert _rel(yb, res[0][0]) < 2e-3 and _rel(y, res[0][2]) < 2e-3
         assert _rel(save[:Ko], res[0][1][:Ko]) < 1e-4 and _rel(save[Ko:2 * Ko], res[0][1][Ko:2 * Ko]) < 1e-4
         assert _rel(save[:Ko], mean_r) < 2e-2
+
+
+# the stage 2-4 conv3 shapes (1x1 expand, input = the plain ReLU BN2 output) at batch 256 and 128
+BNA_SHAPES = [(B, hw, hw, c, 4 * c) for B in (256, 128) for hw, c in ((16, 128), (8, 256), (4, 512))]
+
+
+@pytest.mark.parametrize("shape", BNA_SHAPES, ids=["%dx%dx%d_c%d_k%d" % s for s in BNA_SHAPES])
+def test_bn_on_load_wide_pointwise_forward(gpu, shape):
+    """conv_fwd_bn_in beyond one k-tile (the persistent kernel's A-operand BN transform): the conv of
+    relu(x * scale + shift) against fp32, and its fused statistics against the same conv run on the
+    materialised BN output (bn_apply_train + conv_fwd_bn)."""
+    N, H, W, C, Ko = shape
+    assert torch.ops.tfx.conv_fwd_bn_in_supported(N * H * W, Ko, C)
+    g = torch.Generator(device=gpu).manual_seed(11 + C)
+    x = _bf(torch.randn(N, H, W, C, device=gpu, generator=g) * 1.3 + 0.2)
+    w = _bf(torch.randn(Ko, 1, 1, C, device=gpu, generator=g) * (1.0 / math.sqrt(C)))
+    # an input BN's [mean | invstd | scale | shift]
+    sc = torch.rand(C, device=gpu, generator=g) + 0.5
+    sh = torch.randn(C, device=gpu, generator=g) * 0.5
+    in_save = torch.cat([torch.zeros(C, device=gpu), torch.ones(C, device=gpu), sc, sh]).contiguous()
+    a_ref = torch.relu(x.float() * sc + sh)
+    yr = torch.einsum("nhwc,kc->nhwk", _bf(a_ref).float(), w.float().reshape(Ko, C))
+    gamma = torch.rand(Ko, device=gpu, generator=g) + 0.5
+    beta = torch.randn(Ko, device=gpu, generator=g)
+    ws = torch.zeros(64 * 2 * Ko + 64, device=gpu)
+    y, save = torch.ops.tfx.conv_fwd_bn_in(x, in_save, w, ws, gamma, beta, None, None, 0.1, 1e-5)
+    ws2 = torch.zeros_like(ws)
+    a_mat = torch.ops.tfx.bn_apply_train(x, None, in_save, True)[0]
+    y2, save2 = torch.ops.tfx.conv_fwd_bn(a_mat, w, 1, 0, 1, ws2, gamma, beta, None, None, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    assert _rel(y, yr) < 1e-2
+    assert _rel(y, y2) < 2e-3  # same bf16 A operand, summation order only
+    assert _rel(save[:2 * Ko], save2[:2 * Ko]) < 1e-3
+    assert float(ws[:64 * 2 * Ko].abs().max()) == 0.0, "statistics slots left dirty"
