@@ -532,6 +532,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   static_assert(KS == 1 || TM * TN * 4096 <= NSTG * STAGE, "accumulator hand-off must fit its LDS region");
   static_assert(!GL || (A_BYTES % 4096 == 0 && (STAGE - A_BYTES) % 4096 == 0), "hand-off pairs tile the arrays");
   static_assert(KS * NSTG * STAGE <= 163840, "LDS budget");
+  static_assert(GLS <= 6 && (KS == 1 || GLS <= 3), "ring depth: <= 6 stages (<= 3 per group with in-block split-K)");
   // GL: one __shared__ array per ring stage.  LDS lowering gives each array its own alias scope, so
   // the waitcnt pass can prove that a fragment read of stage s does not alias the LDS-DMA in flight
   // into another stage; with every stage in one array hipcc waits vmcnt(0) before each read and the
@@ -550,6 +551,13 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
   __shared__ __attribute__((aligned(16))) char gb1[GLS >= 2 ? GB : 16];
   __shared__ __attribute__((aligned(16))) char ga2[GLS >= 3 ? GA : 16];
   __shared__ __attribute__((aligned(16))) char gb2[GLS >= 3 ? GB : 16];
+  // deep rings (KS = 1: up to 6 stages, GLS - 1 k-tiles in flight in one block's LDS)
+  __shared__ __attribute__((aligned(16))) char ga3[GLS >= 4 ? GA : 16];
+  __shared__ __attribute__((aligned(16))) char gb3[GLS >= 4 ? GB : 16];
+  __shared__ __attribute__((aligned(16))) char ga4[GLS >= 5 ? GA : 16];
+  __shared__ __attribute__((aligned(16))) char gb4[GLS >= 5 ? GB : 16];
+  __shared__ __attribute__((aligned(16))) char ga5[GLS >= 6 ? GA : 16];
+  __shared__ __attribute__((aligned(16))) char gb5[GLS >= 6 ? GB : 16];
   __shared__ __attribute__((aligned(16))) char ha0[HA];
   __shared__ __attribute__((aligned(16))) char hb0[HB];
   __shared__ __attribute__((aligned(16))) char ha1[GLS >= 2 ? HA : 16];
@@ -563,13 +571,19 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
     constexpr int st = decltype(S)::value;
     if constexpr (st == 0) return ga0;
     else if constexpr (st == 1) return ga1;
-    else return ga2;
+    else if constexpr (st == 2) return ga2;
+    else if constexpr (st == 3) return ga3;
+    else if constexpr (st == 4) return ga4;
+    else return ga5;
   };
   auto img_b0 = [&](auto S) -> char* {
     constexpr int st = decltype(S)::value;
     if constexpr (st == 0) return gb0;
     else if constexpr (st == 1) return gb1;
-    else return gb2;
+    else if constexpr (st == 2) return gb2;
+    else if constexpr (st == 3) return gb3;
+    else if constexpr (st == 4) return gb4;
+    else return gb5;
   };
   const int t = threadIdx.x & 255, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
 
@@ -733,9 +747,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
     auto img_a = [&](auto G, auto S) -> char* {
       constexpr int g = decltype(G)::value, st = decltype(S)::value;
       if constexpr (g == 0) {
-        if constexpr (st == 0) return ga0;
-        else if constexpr (st == 1) return ga1;
-        else return ga2;
+        return img_a0(S);
       } else {
         if constexpr (st == 0) return ha0;
         else if constexpr (st == 1) return ha1;
@@ -745,9 +757,7 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
     auto img_b = [&](auto G, auto S) -> char* {
       constexpr int g = decltype(G)::value, st = decltype(S)::value;
       if constexpr (g == 0) {
-        if constexpr (st == 0) return gb0;
-        else if constexpr (st == 1) return gb1;
-        else return gb2;
+        return img_b0(S);
       } else {
         if constexpr (st == 0) return hb0;
         else if constexpr (st == 1) return hb1;
@@ -792,46 +802,25 @@ __global__ void __launch_bounds__(256 * KS, igemm_waves(BM, BN, STG, EPI, KS, GL
           compute_ab(img_a(G, IC<st>{}), 0, img_b(G, IC<st>{}), 0);
           __builtin_amdgcn_sched_barrier(0);
         };
-        issue_gl(kt0, G, IC<0>{});
-        if constexpr (GLS >= 3) issue_gl(kt0 + 1, G, IC<1>{});
+        // prologue: tiles 0 .. GLS-2 into stages 0 .. GLS-2
+        static_for<GLS - 1>([&](auto P) { issue_gl(kt0 + decltype(P)::value, G, P); });
         int it = 0;
         if constexpr (PF) {
-          for (; it + GLS < kh; it += GLS) {
-            body(IC<0>{}, it);
-            body(IC<1>{}, it + 1);
-            if constexpr (GLS >= 3) body(IC<2>{}, it + 2);
-          }
+          for (; it + GLS < kh; it += GLS) static_for<GLS>([&](auto S) { body(S, it + decltype(S)::value); });
           const int rem = kh - it;  // 1 .. GLS steps left, the final one peeled
-          if constexpr (GLS >= 3) {
-            if (rem == 3) {
-              body(IC<0>{}, it);
-              body(IC<1>{}, it + 1);
-              last(IC<2>{});
-            } else if (rem == 2) {
-              body(IC<0>{}, it);
-              last(IC<1>{});
-            } else {
-              last(IC<0>{});
+          static_for<GLS>([&](auto R) {
+            constexpr int r = decltype(R)::value;
+            if (rem == r + 1) {
+              static_for<r>([&](auto S) { body(S, it + decltype(S)::value); });
+              last(R);
             }
-          } else {
-            if (rem == 2) {
-              body(IC<0>{}, it);
-              last(IC<1>{});
-            } else {
-              last(IC<0>{});
-            }
-          }
+          });
         } else {
-          for (; it + GLS <= kh; it += GLS) {
-            body(IC<0>{}, it);
-            body(IC<1>{}, it + 1);
-            if constexpr (GLS >= 3) body(IC<2>{}, it + 2);
-          }
+          for (; it + GLS <= kh; it += GLS) static_for<GLS>([&](auto S) { body(S, it + decltype(S)::value); });
           const int rem = kh - it;  // < GLS
-          if (rem > 0) body(IC<0>{}, it);
-          if constexpr (GLS >= 3) {
-            if (rem > 1) body(IC<1>{}, it + 1);
-          }
+          static_for<GLS - 1>([&](auto S) {
+            if (rem > decltype(S)::value) body(S, it + decltype(S)::value);
+          });
         }
       }
     };
@@ -1390,6 +1379,8 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   if (gls > 0) {
     // LDS-DMA ring: single k-tile -> GLS 1; otherwise the deepest ring (<= 3) that fits the LDS
     const bool single = nkt == 1 && splits == 1;
+    // (the kernel takes rings of up to 6 stages at KS = 1; deep rings -- one 4-wave block per CU holding
+    // 4-6 stages -- lost at every ResNet-50 conv pass, profiles/r05_deep, and are not instantiated)
 #define TFX_GL_LAUNCH(SW)                                                                              \
     if constexpr (KS == 1) {                                                                           \
       if (single) { igemm_kernel<AK, BK, BM, BN, SW, 1, EPI, 1, 1><<<grid, NT, 0, s>>>(a); return; }   \

@@ -27,6 +27,7 @@ from conv_bench import resnet50_convs  # noqa: E402
 
 NSLOT = 64
 # (tile, ks, gls, want): tile 1 = 128x128, 2 = 128x64, 3 = 256x64
+# (deep rings -- gls 4-6, one 4-wave block per CU -- were candidates once and never won: profiles/r05_deep)
 BF16_CANDS = [(t, 0, g, 0) for t in (1, 2, 3) for g in (0, 2, 3)] + [(t, 2, g, 0) for t in (1, 2) for g in (0, 2)]
 ATOMIC_CANDS = [(t, k, g, w) for t in (1, 2) for k in (1, 2) for g in (0, 3) for w in (256, 512)]
 

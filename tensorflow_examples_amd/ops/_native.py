@@ -15,7 +15,8 @@ import threading
 import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
-OPS_LIB = os.path.join(_LIB_DIR, "libtfx_ops.so")
+# TFX_OPS_LIB: another build of the kernel library (same-box A/B runs of two builds)
+OPS_LIB = os.environ.get("TFX_OPS_LIB") or os.path.join(_LIB_DIR, "libtfx_ops.so")
 RT_LIB = os.path.join(_LIB_DIR, "libtfx_rt.so")
 
 _lock = threading.Lock()
