@@ -147,7 +147,8 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
         return;
       case MODE_DGRAD:  // dY[M][Ko] . W[Ko][C]
         a.lda = a.Ko; a.ldb = a.C;
-        igemm_dgrad_pointwise(a, s);
+        if (igemm_dgrad_persist_ok(a)) igemm_dgrad_persist(a, s);  // many-tile fused-BN data gradients
+        else igemm_dgrad_pointwise(a, s);
         return;
       case MODE_WGRAD:  // dY^T[Ko][pix] . X[pix][C]
         a.lda = a.Ko; a.ldb = a.C;

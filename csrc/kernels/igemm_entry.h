@@ -21,6 +21,9 @@ bool igemm_fwd_persist_ok(const IgemmArgs& a);
 // ... with the A-operand BN transform (a_scale / a_shift: a plain ReLU BN applied on load)
 bool igemm_fwd_persist_bna_ok(const IgemmArgs& a);
 void igemm_fwd_persist(IgemmArgs& a, hipStream_t s);
+// ... and the fused-BN 1x1 data gradient (EPI_BNB, MN-major W)
+bool igemm_dgrad_persist_ok(const IgemmArgs& a);
+void igemm_dgrad_persist(IgemmArgs& a, hipStream_t s);
 
 // ---- measured launch configurations (igemm.hip; table from scripts/tune_convs.py)
 // family = which entry above launched; a config overrides the built-in heuristics of launch_shape /

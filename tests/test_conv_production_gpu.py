@@ -168,3 +168,56 @@ def test_bn_on_load_wide_pointwise_forward(gpu, shape):
     assert _rel(y, y2) < 2e-3  # same bf16 A operand, summation order only
     assert _rel(save[:2 * Ko], save2[:2 * Ko]) < 1e-3
     assert float(ws[:64 * 2 * Ko].abs().max()) == 0.0, "statistics slots left dirty"
+
+
+# the 1x1 stride-1 data gradients the persistent kernel takes (>= 4 128x64 tiles per CU, K >= 128)
+PW_DGRAD = [s for s in SHAPES if s[5] == 1 and s[6] == 1 and s[4] >= 128 and s[3] % 64 == 0 and
+            (s[0] * s[1] * s[2] // 128) * (s[3] // 64) >= 1024]
+
+
+@pytest.mark.parametrize("variant", ["addend_masked", "addend", "plain_relu_recomputed"])
+@pytest.mark.parametrize("shape", PW_DGRAD, ids=[_ids(s) for s in PW_DGRAD])
+def test_persistent_fused_bn_dgrad_matches_per_tile_kernel(gpu, shape, variant):
+    """The persistent 1x1 fused-BN data gradient (igemm_persist.hip EPI_BNB: MN-major W, the residual
+    addend and its ReLU mask bits summed in, the BN-backward partials of the input BN with the mask
+    from the BN's bits or recomputed from x) against the one-tile-per-block kernel and fp32."""
+    N, H, W, C, Ko, R, st = shape
+    g = torch.Generator(device=gpu).manual_seed(3 + C + Ko)
+    M = N * H * W
+    gy = _bf(torch.randn(N, H, W, Ko, device=gpu, generator=g))
+    w = _bf(torch.randn(Ko, 1, 1, C, device=gpu, generator=g) * (1.0 / math.sqrt(Ko)))
+    bx = _bf(torch.randn(N, H, W, C, device=gpu, generator=g) * 1.2 + 0.1)
+    mean, inv = torch.randn(C, device=gpu, generator=g) * 0.1, torch.rand(C, device=gpu, generator=g) + 0.5
+    gam, bet = torch.rand(C, device=gpu, generator=g) + 0.5, torch.randn(C, device=gpu, generator=g) * 0.3
+    save = torch.cat([mean, inv, gam * inv, bet - mean * inv * gam]).contiguous()
+    add = _bf(torch.randn(N, H, W, C, device=gpu, generator=g)) if variant != "plain_relu_recomputed" else None
+    amask = (torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device=gpu, generator=g)
+             if variant == "addend_masked" else None)
+    bmask = (torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device=gpu, generator=g)
+             if variant != "plain_relu_recomputed" else None)
+    res = {}
+    prev = torch.ops.tfx.igemm_persist_dgrad(0)  # opt-in path (slower than the per-tile kernel)
+    try:
+        for mode in (0, 2):
+            torch.ops.tfx.igemm_persist_dgrad(1 if mode else 0)
+            ws = torch.zeros(64 * 2 * C + 64, device=gpu)
+            a_in = add.clone() if add is not None else None  # an unmasked addend is summed in place
+            dx, red = torch.ops.tfx.conv_dgrad_bn(gy, w, [N, H, W, C], 1, 0, 1, a_in, bx, save, bmask, True, ws,
+                                                  None, None, amask, True, False, None)
+            torch.cuda.synchronize()
+            assert float(ws[:64 * 2 * C].abs().max()) == 0.0, "BN slots left dirty"
+            res[mode] = (dx.clone(), red.clone())
+    finally:
+        torch.ops.tfx.igemm_persist_dgrad(prev)
+    # fp32 reference of the stored gradient
+    ref = torch.einsum("nhwk,kc->nhwc", gy.float(), w.float().reshape(Ko, C))
+    if add is not None:
+        af = add.float()
+        if amask is not None:
+            bits = ((amask.reshape(-1, 1) >> torch.arange(8, device=gpu, dtype=torch.uint8)) & 1).reshape(N, H, W, C)
+            af = af * bits.float()
+        ref = ref + af
+    dx2, red2 = res[2]
+    assert _rel(dx2, ref) < 1e-2
+    assert _rel(dx2, res[0][0]) < 2e-3
+    assert _rel(red2, res[0][1]) < 2e-3
