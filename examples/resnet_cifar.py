@@ -100,6 +100,8 @@ def main(_):
     dp = GradAllReduce(store, bucket_bytes=int(FLAGS.bucket_mb * (1 << 20))) if world > 1 else None
     trainer = ClassifierTrainer(store, model, opt, dp)
     shard = np.arange(rank, len(xtr), world)
+    # this rank's shard, gathered once (not a 150 MB copy at every epoch start)
+    xs, ys = (xtr, ytr) if world == 1 else (xtr[shard], ytr[shard])
     steps_per_epoch = len(shard) // FLAGS.batch_size
     total = FLAGS.max_steps or steps_per_epoch * FLAGS.epochs
     bounds = [int(float(f) * total) for f in FLAGS.lr_boundaries.split(",") if f]
@@ -112,7 +114,7 @@ def main(_):
     for ep in range(FLAGS.epochs):
         if step - start_step >= total:
             break
-        src = batches([xtr[shard], ytr[shard]], FLAGS.batch_size, seed=ep * 1000 + rank + 7919 * FLAGS.seed)
+        src = batches([xs, ys], FLAGS.batch_size, seed=ep * 1000 + rank + 7919 * FLAGS.seed)
         for img, lab in DevicePrefetcher(src, dev):
             lr = FLAGS.learning_rate * world * (0.1 ** sum(step >= b for b in bounds))
             if FLAGS.warmup_steps and step < FLAGS.warmup_steps:
