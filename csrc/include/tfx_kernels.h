@@ -119,6 +119,8 @@ struct IgemmArgs {
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s);
 // persistent 1x1-forward mode (igemm_persist.hip): 0 off, 2 / 3 ring depth; returns the previous mode
 int igemm_persist_set(int mode);
+// the persistent kernel's A-operand BN transform form: 1 registers, 2 in-LDS pass; returns the previous
+int igemm_bna_mode_set(int mode);
 // the persistent fused-BN 1x1 data gradient (opt-in: slower than the per-tile kernel); returns the previous
 int igemm_persist_dgrad_set(int on);
 // a plain ReLU BN applied on load by a 1x1 forward of M x N x K (conv_fwd_bn_in) beyond one k-tile:

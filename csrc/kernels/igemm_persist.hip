@@ -24,8 +24,11 @@ namespace tfx {
 namespace {
 
 // BNA: the A operand is a plain ReLU BN's input, applied on load -- A[m][k] -> relu(A a_scale[k] +
-// a_shift[k]) -- in registers, after each fragment's LDS read (the ring stays a raw LDS-DMA copy).  The
-// per-channel coefficients are staged in LDS once per block (K <= BNA_KMAX).
+// a_shift[k]).  1 = in registers, after each fragment's LDS read (every wave of a wave row transforms
+// the rows it reads); 2 = in LDS, once per element: when a stage has landed, the block rewrites its A
+// image in place (4 16-byte chunks per thread) before an LDS-only barrier and the MFMAs.  The ring stays
+// a raw LDS-DMA copy either way.  The per-channel coefficients are staged in LDS once per block
+// (K <= BNA_KMAX).
 constexpr int BNA_KMAX = 1024;  // 8 KB of coefficients: 128x128 tiles keep 2 blocks per CU
 
 // EPI: EPI_STATS = the forward's BN statistics of the output (stat_slots rows); EPI_BNB = a data
@@ -33,7 +36,7 @@ constexpr int BNA_KMAX = 1024;  // 8 KB of coefficients: 128x128 tiles keep 2 bl
 // slots), with the residual-branch addend (and its ReLU mask bits) summed in; EPI_PLAIN = stores only.
 // BKIND: the B operand's layout -- KM_DENSE (forward: W[Ko][C], K-major rows) or MN_DENSE (1x1 data
 // gradient: W[Ko][C] with k = Ko rows and the output channels as columns).
-template <int BM, int BN, int GLS, int EPI, bool BNA = false, int BKIND = KM_DENSE>
+template <int BM, int BN, int GLS, int EPI, int BNA = 0, int BKIND = KM_DENSE>
 __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
   constexpr bool STATS = EPI == EPI_STATS, BNB = EPI == EPI_BNB;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -115,7 +118,7 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
       bf16x8_t fa[TM], fb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[i] = frag<KM_DENSE, BM>(ia, 0, wm * WM + i * 16, kk, lane);
-      if constexpr (BNA) {
+      if constexpr (BNA == 1) {
         // the lane's 8 channels of this 32-deep half: kbase + 32 kk + 8 (lane >> 4) + 0..7
         const int c = kbase + 32 * kk + 8 * (lane >> 4);
         const float4 s0 = *reinterpret_cast<const float4*>(&bsc[c]), s1 = *reinterpret_cast<const float4*>(&bsc[c + 4]);
@@ -293,7 +296,29 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
     }
   };
 
-  if constexpr (BNA) {
+  // BNA 2: the landed A image of one stage, transformed in place (physical chunk p of row r holds
+  // logical k-chunk p ^ (r & 7): kmaj_off's swizzle), then an LDS-only barrier before any fragment read
+  auto bn_in_lds = [&](char* ia, int kbase) __attribute__((always_inline)) {
+    static_assert(BM * BKT * 2 == 4 * 256 * 16, "4 chunks per thread");
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = t + 256 * u, r = q >> 3, pc = q & 7, c = kbase + 8 * (pc ^ (r & 7));
+      lds_bf16x8* ptr = (lds_bf16x8*)((lds_char*)ia + (r * 128 + (pc << 4)));
+      const float4 s0 = *reinterpret_cast<const float4*>(&bsc[c]), s1 = *reinterpret_cast<const float4*>(&bsc[c + 4]);
+      const float4 h0 = *reinterpret_cast<const float4*>(&bsh[c]), h1 = *reinterpret_cast<const float4*>(&bsh[c + 4]);
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+      float f[8];
+      unpack8(__builtin_bit_cast(U4, *ptr), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f);
+      *ptr = __builtin_bit_cast(bf16x8_t, pack8(f));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  if constexpr (BNA != 0) {
     // the coefficients into LDS before the ring starts (its loads are the only ones outstanding later)
     for (int i = t; i < a.K; i += 256) {
       bsc[i] = a.a_scale[i];
@@ -321,6 +346,7 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
         if constexpr (BNB) {
           if (st % nkt == nkt - 1) epi_prefetch(tile_of(st / nkt));
         }
+        if constexpr (BNA == 2) bn_in_lds(img_a(S), (st % nkt) * BKT);
         __builtin_amdgcn_sched_barrier(0);
         compute(img_a(S), img_b(S), (st % nkt) * BKT);
         __builtin_amdgcn_sched_barrier(0);
@@ -353,7 +379,7 @@ int g_persist = [] {
 }();
 int persist_mode() { return g_persist; }
 
-template <int BM, int BN, int GLS, int EPI, bool BNA = false, int BKIND = KM_DENSE>
+template <int BM, int BN, int GLS, int EPI, int BNA = 0, int BKIND = KM_DENSE>
 void launch_p(IgemmArgs& a, hipStream_t s) {
   a.tiles_m = a.M / BM;
   a.tiles_n = a.N / BN;
@@ -374,6 +400,18 @@ void launch_p(IgemmArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+// the A-operand BN transform's form (TFX_BNA_MODE / igemm_bna_mode_set): 1 = registers, 2 = in LDS
+int g_bna_mode = [] {
+  const char* e = getenv("TFX_BNA_MODE");
+  return e && atoi(e) == 2 ? 2 : 1;
+}();
+
+int igemm_bna_mode_set(int mode) {
+  const int prev = g_bna_mode;
+  if (mode == 1 || mode == 2) g_bna_mode = mode;
+  return prev;
+}
 
 int igemm_persist_set(int mode) {
   const int prev = g_persist;
@@ -411,9 +449,14 @@ bool igemm_fwd_bna_supported(int64_t M, int64_t N, int64_t K) {
 void igemm_fwd_persist(IgemmArgs& a, hipStream_t s) {
   const bool st = a.stats != nullptr;
   constexpr int S = EPI_STATS, P = EPI_PLAIN;
-  if (a.a_scale) {  // BN on load: ring depth 2 (the coefficient arrays take 16 KB of LDS)
-    if (a.N % 128 == 0) launch_p<128, 128, 2, S, true>(a, s);
-    else launch_p<128, 64, 2, S, true>(a, s);
+  if (a.a_scale) {  // BN on load: ring depth 2 (the coefficient arrays take 8 KB of LDS)
+    if (g_bna_mode == 2) {
+      if (a.N % 128 == 0) launch_p<128, 128, 2, S, 2>(a, s);
+      else launch_p<128, 64, 2, S, 2>(a, s);
+    } else {
+      if (a.N % 128 == 0) launch_p<128, 128, 2, S, 1>(a, s);
+      else launch_p<128, 64, 2, S, 1>(a, s);
+    }
     return;
   }
   const int gls = persist_mode();

@@ -1822,6 +1822,7 @@ void dp_ring_sim(Tensor buf, int64_t nblocks, double duration_us, int64_t passes
 }
 
 int64_t igemm_persist_mode(int64_t mode) { return tfx::igemm_persist_set((int)mode); }
+int64_t igemm_bna_mode(int64_t mode) { return tfx::igemm_bna_mode_set((int)mode); }
 int64_t igemm_persist_dgrad(int64_t on) { return tfx::igemm_persist_dgrad_set((int)on); }
 
 TORCH_LIBRARY(tfx, m) {
@@ -1829,6 +1830,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("image_normalize_into", &image_normalize_into);
   m.def("augment_normalize", &augment_normalize);
   m.def("igemm_persist_mode", &igemm_persist_mode);
+  m.def("igemm_bna_mode", &igemm_bna_mode);
   m.def("igemm_persist_dgrad", &igemm_persist_dgrad);
   m.def("dp_ring_sim(Tensor(a!) buf, int nblocks, float duration_us, int passes) -> ()", &dp_ring_sim);
   m.def("augment_normalize_into(Tensor x, Tensor offsets, float[] mean, float[] stdv, int pad, Tensor(a!) y) -> ()",

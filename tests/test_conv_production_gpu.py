@@ -140,8 +140,9 @@ def test_persistent_pointwise_forward_matches_per_tile_kernel(gpu, shape):
 BNA_SHAPES = [(B, hw, hw, c, 4 * c) for B in (256, 128) for hw, c in ((16, 128), (8, 256), (4, 512))]
 
 
+@pytest.mark.parametrize("form", [1, 2], ids=["registers", "in_lds"])
 @pytest.mark.parametrize("shape", BNA_SHAPES, ids=["%dx%dx%d_c%d_k%d" % s for s in BNA_SHAPES])
-def test_bn_on_load_wide_pointwise_forward(gpu, shape):
+def test_bn_on_load_wide_pointwise_forward(gpu, shape, form):
     """conv_fwd_bn_in beyond one k-tile (the persistent kernel's A-operand BN transform): the conv of
     relu(x * scale + shift) against fp32, and its fused statistics against the same conv run on the
     materialised BN output (bn_apply_train + conv_fwd_bn)."""
@@ -159,7 +160,11 @@ def test_bn_on_load_wide_pointwise_forward(gpu, shape):
     gamma = torch.rand(Ko, device=gpu, generator=g) + 0.5
     beta = torch.randn(Ko, device=gpu, generator=g)
     ws = torch.zeros(64 * 2 * Ko + 64, device=gpu)
-    y, save = torch.ops.tfx.conv_fwd_bn_in(x, in_save, w, ws, gamma, beta, None, None, 0.1, 1e-5)
+    prev = torch.ops.tfx.igemm_bna_mode(form)  # 1: transform after each fragment read, 2: in-LDS pass
+    try:
+        y, save = torch.ops.tfx.conv_fwd_bn_in(x, in_save, w, ws, gamma, beta, None, None, 0.1, 1e-5)
+    finally:
+        torch.ops.tfx.igemm_bna_mode(prev)
     ws2 = torch.zeros_like(ws)
     a_mat = torch.ops.tfx.bn_apply_train(x, None, in_save, True)[0]
     y2, save2 = torch.ops.tfx.conv_fwd_bn(a_mat, w, 1, 0, 1, ws2, gamma, beta, None, None, 0.1, 1e-5)
