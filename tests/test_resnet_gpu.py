@@ -142,6 +142,7 @@ def test_deferred_slot_reductions_fallback_and_off_agree(gpu):
     from tensorflow_examples_amd.ops import fusion
     g0, st = run()
     g1, _ = run()
+    g1b, _ = run()
     with fusion.override(sr_take=False):
         g2, _ = run()
     with fusion.override(sr_defer=False):
@@ -149,7 +150,10 @@ def test_deferred_slot_reductions_fallback_and_off_agree(gpu):
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
-        noise = (g1[sl] - g0[sl]).norm().item() / n
+        # the floor: the larger of two default-vs-default distances.  One draw alone made the 4x gate a
+        # ratio of two single noise draws, which a 10-element tensor (fc/bias, whose gradient depends on
+        # the forward's atomic-order noise only) exceeded once in a few hundred runs
+        noise = max((g1[sl] - g0[sl]).norm().item(), (g1b[sl] - g0[sl]).norm().item()) / n
         for gx, tag in ((g2, "fallback"), (g3, "off")):
             e = (gx[sl] - g0[sl]).norm().item() / n
             assert e <= max(4 * noise, 1e-3), (tag, v.name, e, noise)
