@@ -120,13 +120,15 @@ def test_resnet50_deferred_bn1_matches_layerwise(gpu):
         assert nnops.CONV3_BWD_CALLS[0] - n1 == 3, "... forward and backward"
         assert nnops.PW_APPLY_CALLS[0] - n2 == 3, "the three stage-1 conv3 apply BN2 on load"
         l1, g1, _ = run()
+        l1b, g1b, _ = run()
         with fusion.override(defer_bn_in=False):
             l2, g2, _ = run()
-    assert abs(l0 - l2) <= max(4 * abs(l0 - l1), 0.01 * abs(l2)), (l0, l1, l2)
+    assert abs(l0 - l2) <= max(4 * max(abs(l0 - l1), abs(l0 - l1b)), 0.01 * abs(l2)), (l0, l1, l1b, l2)
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
-        noise = (g1[sl] - g0[sl]).norm().item() / n
+        # floor: the larger of two same-path distances (one draw made the gate a ratio of two single draws)
+        noise = max((g1[sl] - g0[sl]).norm().item(), (g1b[sl] - g0[sl]).norm().item()) / n
         e = (g2[sl] - g0[sl]).norm().item() / n
         assert e <= max(4 * noise, 2e-3), (v.name, e, noise)
 

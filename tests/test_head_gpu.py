@@ -170,12 +170,14 @@ def test_resnet_head_takes_over_last_tail(gpu):
 
     l0, g0 = run(False)
     l1, g1 = run(False)
+    l1b, g1b = run(False)
     l2, g2 = run(True)
     assert torch.isfinite(g2).all()
-    assert abs(l2 - l0) <= 4 * abs(l1 - l0) + 1e-2, (l0, l1, l2)
+    assert abs(l2 - l0) <= 4 * max(abs(l1 - l0), abs(l1b - l0)) + 1e-2, (l0, l1, l1b, l2)
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
-        noise = (g1[sl] - g0[sl]).norm().item() / n
+        # floor: the larger of two same-path distances (one draw made the gate a ratio of two single draws)
+        noise = max((g1[sl] - g0[sl]).norm().item(), (g1b[sl] - g0[sl]).norm().item()) / n
         e = (g2[sl] - g0[sl]).norm().item() / n
         assert e <= max(4 * noise, 1e-3), (v.name, e, noise)

@@ -174,6 +174,7 @@ def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
         assert nnops.PW_EXPAND_CALLS[0] - n0 == 3, "stage-1 blocks run fused (projection block 1 with F3-SEC)"
         assert nnops.PW_SQUEEZE_BWD_CALLS[0] - n1 == 2, "stage-1 identity blocks' conv1 backward runs fused (F1)"
         g1, _ = run()
+        g1b, _ = run()
         # lazy gradients, but every conv declines the fused kernels: LazyBNGrad.materialize (the
         # projection tail's reduces the shortcut BN there, or in the shortcut BN's backward if first)
         nnops._pw_expand_ok = lambda *a: False
@@ -187,7 +188,8 @@ def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
-        noise = (g1[sl] - g0[sl]).norm().item() / n
+        # floor: the larger of two same-path distances (one draw made the gate a ratio of two single draws)
+        noise = max((g1[sl] - g0[sl]).norm().item(), (g1b[sl] - g0[sl]).norm().item()) / n
         for gx in (g2, g3):
             e = (gx[sl] - g0[sl]).norm().item() / n
             assert e <= max(4 * noise, 2e-3), (v.name, e, noise)

@@ -96,16 +96,18 @@ def test_resnet50_deferred_tails_match_layerwise(gpu):
         l0, g0, st = run()
         assert nnops.PW_SQUEEZE_CALLS[0] - n0 == 6, "stage-1 and stage-2 tails fused into the next conv1 (3 + 3 boundaries)"
         l1, g1, _ = run()
+        l1b, g1b, _ = run()
         with fusion.override(defer_tail=False):
             l2, g2, _ = run()
     # the first-step loss of a random-init ResNet-50 moves ~0.4% between two runs of the SAME path
     # (f32-atomic BN statistics, amplified through 50 layers; scripts/dev/diag_fwd.py): bound the
     # fused-vs-layerwise gap by that spread, with a 1% floor -- the kernel test above pins the
     # fused values bit-exactly
-    assert abs(l0 - l2) <= max(4 * abs(l0 - l1), 0.01 * abs(l2)), (l0, l1, l2)
+    assert abs(l0 - l2) <= max(4 * max(abs(l0 - l1), abs(l0 - l1b)), 0.01 * abs(l2)), (l0, l1, l1b, l2)
     for v in st.trainable():
         sl = slice(v.offset, v.offset + v.numel)
         n = g0[sl].norm().item() + 1e-12
-        noise = (g1[sl] - g0[sl]).norm().item() / n
+        # floor: the larger of two same-path distances (one draw made the gate a ratio of two single draws)
+        noise = max((g1[sl] - g0[sl]).norm().item(), (g1b[sl] - g0[sl]).norm().item()) / n
         e = (g2[sl] - g0[sl]).norm().item() / n
         assert e <= max(4 * noise, 2e-3), (v.name, e, noise)
