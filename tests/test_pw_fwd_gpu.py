@@ -88,7 +88,7 @@ def test_resnet50_deferred_tails_match_layerwise(gpu):
         loss = ops.softmax_cross_entropy(m(xin, training=True), lab)
         loss.backward()
         torch.cuda.synchronize()
-        return float(loss), st.grad.clone(), st
+        return float(loss.detach()), st.grad.clone(), st
 
     from tensorflow_examples_amd.ops import fusion
     with fusion.override():  # the default knobs, restored after
