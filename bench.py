@@ -25,10 +25,10 @@ Launch modes (the process-per-task model of R/distributed/distributed.py:7-14,37
 Timing: W untimed warmup steps; barrier + synchronize; K timed steps; barrier + synchronize; the
 MAX elapsed over ranks is reported.  Rank 0 prints ONE JSON line.
 
-``--host-input [zerocopy|copy]``: batches live in pinned host memory (the tf.data/feed_dict path)
-and go through the framework's pinned ring (data/pipeline.py): ``zerocopy`` -- the fused input
-kernel reads the pinned slot over the host link; ``copy`` -- an async H2D copy per step on a side
-stream into device slots.
+``--host-input [zerocopy|copy|none]``: by default (``zerocopy``) the batches live in pinned host memory
+(the tf.data/feed_dict path) and go through the framework's pinned ring (data/pipeline.py): the fused
+input kernel reads the pinned slot over the host link every step; ``copy`` -- an async H2D copy per
+step on a side stream into device slots; ``none`` -- batches resident on the device.
 ``--impl torch`` runs a stock PyTorch-ROCm eager ResNet-50 (torch.nn + MIOpen, channels_last, bf16
 autocast) for a labelled comparison; the headline is ``--impl native``.
 ``--device cpu`` runs the same step on the CPU reference ops over gloo (tests of the launch path).
@@ -66,10 +66,11 @@ def parse(argv=None):
                          "RCCL all-reduces are captured too -- measured on a 1-rank RCCL group: 8.09-8.16 ms graph vs "
                          "8.27-9.03 ms eager, profiles/r02_final/dp_graph_ab.txt; TFX_DP_GRAPH=0 keeps N>1 eager)")
     ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager step launches")
-    ap.add_argument("--host-input", nargs="?", const="zerocopy", default=None, choices=["copy", "zerocopy"],
-                    help="batches live in pinned host memory: 'zerocopy' (default when given) = the input kernel "
-                         "reads the pinned slot over the host link; 'copy' = async H2D into device slots on a "
-                         "side stream (data/pipeline.py PinnedRing)")
+    ap.add_argument("--host-input", nargs="?", const="zerocopy", default="zerocopy", choices=["copy", "zerocopy", "none"],
+                    help="where the batches live: 'zerocopy' (default) = pinned host memory, the input kernel reads "
+                         "the pinned slot over the host link (the north star's pinned-host input pipeline); 'copy' = "
+                         "pinned host memory, async H2D into device slots on a side stream (data/pipeline.py "
+                         "PinnedRing); 'none' = batches resident on the device")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--backend", default=None, help="process-group backend (default nccl = RCCL, gloo on cpu)")
@@ -124,7 +125,7 @@ def run(a):
             torch.cuda.synchronize()
 
     ring = None
-    if a.host_input and cuda:
+    if a.host_input != "none" and cuda:
         ring = PinnedRing.for_batches(host, dev, depth=2, zero_copy=a.host_input == "zerocopy")
         data = None
     else:
@@ -142,7 +143,8 @@ def run(a):
         opt = MomentumOptimizer(store, a.lr, momentum=0.9, weight_decay=5e-4)
         dp = GradAllReduce(store, bucket_bytes=int(a.bucket_mb * (1 << 20)),
                            compress_bf16=a.allreduce_dtype == "bf16") if dist.is_initialized() else None
-        trainer = ClassifierTrainer(store, model, opt, dp)
+        # the optimizer kernel clears the gradients in its pass: no gradient fill launch in the step
+        trainer = ClassifierTrainer(store, model, opt, dp, fuse_zero_grad=True)
 
         label_fuse = os.environ.get("TFX_LABEL_FUSE", "1") == "1"  # 0: separate label copy (A/B)
 

@@ -68,8 +68,7 @@ struct IgemmArgs {
   int relu = 0;
   // optional per-column BN statistics of the (bf16-rounded) output: [NSLOT][2][N] f32, pre-zeroed
   float* stats = nullptr;
-  // rows of `stats` the epilogue adds into (tile row tm -> row tm % stat_slots): NSLOT, or fewer for
-  // a BN whose finalize is folded into its apply (bn_apply_fin reads only these rows per block)
+  // rows of `stats` the epilogue adds into (tile row tm -> row tm % stat_slots)
   int stat_slots = NSLOT;
   FastDiv fd_C, fd_S, fd_Ko, fd_PQ, fd_Q;
   int zero_out = 1;
@@ -119,13 +118,7 @@ struct IgemmArgs {
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s);
 // persistent 1x1-forward mode (igemm_persist.hip): 0 off, 2 / 3 ring depth; returns the previous mode
 int igemm_persist_set(int mode);
-// the persistent kernel's A-operand BN transform form: 1 registers, 2 in-LDS pass; returns the previous
-int igemm_bna_mode_set(int mode);
-// the persistent fused-BN 1x1 data gradient (opt-in: slower than the per-tile kernel); returns the previous
-int igemm_persist_dgrad_set(int on);
-// a plain ReLU BN applied on load by a 1x1 forward of M x N x K (conv_fwd_bn_in) beyond one k-tile:
-// the persistent kernel's A-operand transform takes this shape
-bool igemm_fwd_bna_supported(int64_t M, int64_t N, int64_t K);
+int igemm_probe_set(int v);  // TEMPORARY cost probe (igemm.hip)
 
 // ---------------------------------------------------------------- fused pointwise-conv backward (pw_bwd.hip)
 // Backward of a bottleneck's expanding 1x1 conv (CN -> CW = 4 CN) fused with the block-tail BN's
@@ -257,13 +250,7 @@ void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float
 void bn_slot_reduce(float* slots, int C, float* red, float* dgamma, float* dbeta, hipStream_t s);
 void bn_eval_prep(int C, const float* gamma, const float* beta, float eps, const float* run_mean,
                   const float* run_var, float* save, hipStream_t s);
-// the apply with the finalize folded in (bn_apply_fin_kernel): statistics in nsl (<= 16) rows
-// [nsl][2][C] that the caller zeroes between uses; y == nullptr: the finalize alone (one block)
-bool bn_apply_fin_ok(int C);
 bool igemm_xt_enabled();  // TFX_IGEMM_XT (igemm.hip)
-void bn_apply_fin(const uint16_t* x, const uint16_t* res, const float* slots, int nsl, int64_t M, int C,
-                  const float* gamma, const float* beta, float eps, float momentum, float* run_mean, float* run_var,
-                  float* save, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s);
 // mask (optional, residual + ReLU on the C % 8 == 0 path): 1 bit per element, the ReLU mask of y
 void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t M, int C, bool relu,
               uint16_t* y, uint8_t* mask, hipStream_t s);
@@ -339,7 +326,8 @@ void stem_fwd(const uint16_t* x, const uint16_t* w, int N, int Ko, uint16_t* y, 
 // ---------------------------------------------------------------- optimizers (flat buffers)
 void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, float* v, int64_t n,
                      const float* lr, float gscale, float wd, float b1, float b2, float eps, const float* step,
-                     const float* sumsq, float max_norm, uint16_t* pbf, const int* skip, hipStream_t s);
+                     const float* sumsq, float max_norm, uint16_t* pbf, const int* skip, float* gz,
+                     hipStream_t s);
 void sumsq_flat(const void* g, bool g_bf16, int64_t n, float* out, hipStream_t s);
 void cast_f32_bf16(const float* x, int64_t n, uint16_t* y, hipStream_t s);
 

@@ -274,160 +274,6 @@ __global__ void __launch_bounds__(256) bn_apply_gen_kernel(const uint16_t* __res
   }
 }
 
-// ------------------------------------------------------------------ apply with the finalize folded in
-// The producing conv's epilogue added the batch statistics into `nsl` (<= 16) zeroed rows [nsl][2][C]
-// (IgemmArgs stat_slots; the rows live in the VariableStore scratch that is zeroed with the gradients
-// once per step, ops/nn.py BNWorkspace.fin_rows).  Instead of a separate finalize launch, every block
-// of the apply reduces those rows itself in its prologue -- nsl x 2C floats, L2-resident after the
-// first block of an XCD -- and keeps scale / shift in LDS; block 0 writes save =
-// [mean|invstd|scale|shift] (the backward reads it) and the running statistics.  Nothing re-zeroes the
-// rows here (a last-reader counter on one address serialised ~512 returning atomics at the memory
-// side: +10 us per launch, profiles/r04_fold).  nvec = 0: the finalize alone (bn_finalize_rows).
-// KM = ceil(nsl / threads-per-vector) load rounds per thread, unrolled (a runtime loop would
-// serialise the round trips).
-template <bool RES, bool RELU, int KM>
-__global__ void __launch_bounds__(256) bn_apply_fin_kernel(const uint16_t* __restrict__ x,
-                                                           const uint16_t* __restrict__ res, const float* __restrict__ slots,
-                                                           int nsl, int64_t M, int C, const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, float eps, float momentum,
-                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                           float* __restrict__ save, int64_t nvec,
-                                                           uint16_t* __restrict__ y, uint8_t* __restrict__ mask) {
-  // [part][k][vector]: consecutive vectors in consecutive banks (conflict-free writes and reads)
-  __shared__ __attribute__((aligned(16))) float part[256 * 16];
-  __shared__ __attribute__((aligned(16))) float ssc[2048], ssh[2048];
-  const int t = threadIdx.x;
-  const int nv = C >> 3;    // channel vectors, 256 % nv == 0 (host)
-  const int tpv = 256 / nv;  // threads per vector
-  const int v = t % nv, pr = t / nv;
-  const int cv = v * 8;
-  // Every global load of the prologue is an unconditional buffer load (a null operand gets a
-  // zero-extent resource and reads zeros): a load under a pointer test compiles to a branch that
-  // drains the load counter at the join -- one memory round trip per operand instead of one in all.
-  // The first vector of the apply goes out first, so its latency hides under the prologue's.
-  auto rs = [](const void* p, int64_t bytes) {
-    const int n = bytes > 0x7fffffff ? 0x7fffffff : (int)bytes;
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? n : 0, 0x00020000);
-  };
-  const __amdgpu_buffer_rsrc_t rx = rs(x, nvec * 16), rr = rs(res, nvec * 16);
-  const int64_t i0 = (int64_t)blockIdx.x * 256 + t;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  U4 xa = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)(i0 * 16), 0, 0));
-  U4 ra = RES ? __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(rr, (uint32_t)(i0 * 16), 0, 0)) : U4{};
-  const __amdgpu_buffer_rsrc_t rg = rs(gamma, C * 4), rb = rs(beta, C * 4), rm = rs(run_mean, C * 4),
-                               rv = rs(run_var, C * 4), rsl = rs(slots, (int64_t)nsl * 2 * C * 4);
-  float g8[8], b8[8], rm8[8], rv8[8];
-  {
-    float4 q[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t o = (uint32_t)(cv + 4 * h) * 4u;
-      q[h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, o, 0, 0));
-      q[2 + h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rb, o, 0, 0));
-      q[4 + h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rm, o, 0, 0));
-      q[6 + h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float4 a = q[h], b = q[2 + h], c = q[4 + h], d = q[6 + h];
-      g8[4 * h] = a.x; g8[4 * h + 1] = a.y; g8[4 * h + 2] = a.z; g8[4 * h + 3] = a.w;
-      b8[4 * h] = b.x; b8[4 * h + 1] = b.y; b8[4 * h + 2] = b.z; b8[4 * h + 3] = b.w;
-      rm8[4 * h] = c.x; rm8[4 * h + 1] = c.y; rm8[4 * h + 2] = c.z; rm8[4 * h + 3] = c.w;
-      rv8[4 * h] = d.x; rv8[4 * h + 1] = d.y; rv8[4 * h + 2] = d.z; rv8[4 * h + 3] = d.w;
-    }
-  }
-  float ps[8], pq[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ps[k] = pq[k] = 0.f;
-  {
-    float4 ld[KM][4];
-#pragma unroll
-    for (int i = 0; i < KM; ++i) {
-      const int s = pr + i * tpv;  // rows past nsl: out of the resource's extent, read as zeros
-      const uint32_t o = ((uint32_t)s * 2u * (uint32_t)C + (uint32_t)cv) * 4u;
-      ld[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsl, o, 0, 0));
-      ld[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsl, o + 16u, 0, 0));
-      ld[i][2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsl, o + (uint32_t)C * 4u, 0, 0));
-      ld[i][3] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsl, o + (uint32_t)C * 4u + 16u, 0, 0));
-    }
-#pragma unroll
-    for (int i = 0; i < KM; ++i) {
-      ps[0] += ld[i][0].x; ps[1] += ld[i][0].y; ps[2] += ld[i][0].z; ps[3] += ld[i][0].w;
-      ps[4] += ld[i][1].x; ps[5] += ld[i][1].y; ps[6] += ld[i][1].z; ps[7] += ld[i][1].w;
-      pq[0] += ld[i][2].x; pq[1] += ld[i][2].y; pq[2] += ld[i][2].z; pq[3] += ld[i][2].w;
-      pq[4] += ld[i][3].x; pq[5] += ld[i][3].y; pq[6] += ld[i][3].z; pq[7] += ld[i][3].w;
-    }
-  }
-  if (tpv > 1) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      part[(pr * 16 + k) * nv + v] = ps[k];
-      part[(pr * 16 + 8 + k) * nv + v] = pq[k];
-    }
-    __syncthreads();
-  }
-  if (pr == 0) {
-    for (int j = 1; j < tpv; ++j) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        ps[k] += part[(j * 16 + k) * nv + v];
-        pq[k] += part[(j * 16 + 8 + k) * nv + v];
-      }
-    }
-    const float inv_m = 1.f / (float)M;
-    const bool has_g = gamma != nullptr;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = cv + k;
-      const float mean = ps[k] * inv_m;
-      const float var = fmaxf(pq[k] * inv_m - mean * mean, 0.f);
-      const float invstd = rsqrtf(var + eps);
-      const float sc = (has_g ? g8[k] : 1.f) * invstd, sh = b8[k] - mean * sc;
-      ssc[c] = sc;
-      ssh[c] = sh;
-      if (blockIdx.x == 0) {
-        save[c] = mean;
-        save[C + c] = invstd;
-        save[2 * C + c] = sc;
-        save[3 * C + c] = sh;
-        if (run_mean) {
-          const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-          run_mean[c] = (1.f - momentum) * rm8[k] + momentum * mean;
-          run_var[c] = (1.f - momentum) * rv8[k] + momentum * unb;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  float sc[8], sh[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    sc[k] = ssc[cv + k];
-    sh[k] = ssh[cv + k];
-  }
-  // software-pipelined apply: the next vector's loads (zeros past the end) go out before this one's math
-  for (int64_t i = i0; i < nvec; i += stride) {
-    const uint32_t on = (uint32_t)((i + stride) * 16);
-    const U4 xn = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(rx, on, 0, 0));
-    const U4 rn = RES ? __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(rr, on, 0, 0)) : U4{};
-    float f[8], r[8];
-    unpack8(xa, f);
-    if (RES) unpack8(ra, r);
-    uint32_t bits = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float z = fmaf(f[k], sc[k], sh[k]);
-      if (RES) z += r[k];
-      bits |= (z > 0.f ? 1u : 0u) << k;
-      f[k] = RELU ? fmaxf(z, 0.f) : z;
-    }
-    reinterpret_cast<U4*>(y)[i] = pack8(f);
-    if (RES && RELU && mask) mask[i] = (uint8_t)bits;
-    xa = xn;
-    ra = rn;
-  }
-}
-
 // ------------------------------------------------------------------ backward reduce
 // RES && RELU: the ReLU mask comes from the forward's mask bits (``mask``, one byte per vector)
 template <bool RES, bool RELU, int U>
@@ -725,33 +571,6 @@ void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t
     const int g = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_apply_gen_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, n, C, y)));
   }
-}
-
-bool bn_apply_fin_ok(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0; }
-
-// grid of the folded apply: bn_apply's (4 vectors per thread, <= 4096 blocks), but at most ~16 MB of
-// prologue reads (every block re-reads the nsl x 2C floats, L2 hits after the first block per XCD)
-// and at least 256 blocks
-void bn_apply_fin(const uint16_t* x, const uint16_t* res, const float* slots, int nsl, int64_t M, int C,
-                  const float* gamma, const float* beta, float eps, float momentum, float* run_mean, float* run_var,
-                  float* save, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s) {
-  const int64_t nvec = y ? M * C / 8 : 0;  // no output: the finalize alone, one block
-  int cap = (int)((16ll << 20) / ((int64_t)nsl * 8 * C));
-  cap = cap < 256 ? 256 : cap;
-  const int g0 = nvec ? fixed_channel_grid(nvec, C) : 1, g = g0 < cap ? g0 : cap;  // C/8 divides 256: any grid keeps the channel period
-  const int tpv = 256 / (C / 8);
-  const int km = (nsl + tpv - 1) / tpv;
-  const bool has_res = res != nullptr;
-#define TFX_FIN_LAUNCH(KM_)                                                                                    \
-  TFX_DISPATCH_RR(has_res, relu, (bn_apply_fin_kernel<R_, L_, KM_><<<g, 256, 0, s>>>(                        \
-                                     x, res, slots, nsl, M, C, gamma, beta, eps, momentum, run_mean, run_var, save, \
-                                     nvec, y, mask)))
-  if (km <= 1) { TFX_FIN_LAUNCH(1); }
-  else if (km <= 2) { TFX_FIN_LAUNCH(2); }
-  else if (km <= 4) { TFX_FIN_LAUNCH(4); }
-  else if (km <= 8) { TFX_FIN_LAUNCH(8); }
-  else { TFX_FIN_LAUNCH(16); }
-#undef TFX_FIN_LAUNCH
 }
 
 void bn_apply_res_bn(const uint16_t* x, const uint16_t* res_x, const float* save, const float* res_save, int64_t M,

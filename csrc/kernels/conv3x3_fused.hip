@@ -40,9 +40,6 @@ __device__ __forceinline__ U4 mask_u4(U4 v, bool keep) {
   return v;
 }
 
-// PROBE (cost probes only, csrc/probes/conv3x3_probe.hip; production = 0): bit 0 skips the MFMAs, bit 1 the
-// BN transform of the staged halo (raw copy), bit 2 the epilogue stores / statistics
-template <int PROBE = 0>
 __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * C3_HBYTES + 9 * C3_WTAP];
   char* wimg = smem + 2 * C3_HBYTES;
@@ -95,8 +92,7 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
       unpack8(__builtin_bit_cast(U4, s.v[i]), f);
 #pragma unroll
       for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f);
-      if constexpr (PROBE & 2) *reinterpret_cast<pw_u32x4*>(img + pw_kmaj(hp, hch)) = s.v[i];
-      else *reinterpret_cast<U4*>(img + pw_kmaj(hp, hch)) = mask_u4(pack8(f), in);
+      *reinterpret_cast<U4*>(img + pw_kmaj(hp, hch)) = mask_u4(pack8(f), in);
     }
   };
   // wave tile: output row r = wv & 3 of the tile (32 pixels = 2 m-tiles), 32 output channels (wv >> 2)
@@ -125,14 +121,10 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           fb[j] = pw_frag_kmaj(wimg, tap * C3_WTAP, wcb + 16 * j, 4 * kk, lane);
-        if constexpr (!(PROBE & 1)) {
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-        } else {
-          acc[0][0][0] += (float)fa[0][0] + (float)fb[0][0] + (float)fa[1][0] + (float)fb[1][0];
-        }
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
       }
     }
   };
@@ -140,10 +132,6 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
   // 16-column tiles so each lane holds 8 consecutive channels of one pixel: one 16-byte store per pixel
   // group (16 pixels x 64 contiguous bytes per wave-instruction) instead of two 8-byte ones
   auto epi = [&](const f32x4_t (&acc)[2][2], int tile) {
-    if constexpr (PROBE & 4) {
-      if (acc[0][0][0] == 12345.f) bs[0] += 1.f;  // keep the loop live
-      return;
-    }
     const int n = tile / tiles_img, y0 = (tile % tiles_img) * C3_TR;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -221,10 +209,6 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
 // (141 KB): the halos are single-buffered, the next tile's raw halos wait in registers.
 constexpr int C3_YBYTES = C3_BM * 128;  // raw y1 interior, K-major rows
 
-// PROBE (cost probes only; production = 0): bit 0 skips the data-gradient MFMAs, bit 1 the weight-gradient
-// MFMAs, bit 2 the BN transforms of the staged halos (raw copies), bit 3 the data-gradient epilogue (dx
-// stores, BN1 partials), bit 4 the slab store
-template <int PROBE = 0>
 __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[9 * C3_WTAP + 2 * C3_HBYTES + C3_YBYTES + 16 + 9 * C3_C * 4];
   __shared__ float bnacc[2 * C3_C];  // BN1 backward partials of the block (sum g', sum g' xhat)
@@ -309,8 +293,7 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
           const float gg = fmaf(y2[k], s2[k], h2[k]) > 0.f ? g[k] : 0.f;
           g[k] = fmaf(cA[k], gg, fmaf(cB[k], y2[k], cD[k]));
         }
-        if constexpr (PROBE & 4) *reinterpret_cast<pw_u32x4*>(timg + pw_kmaj(hp, hch)) = st.g[i];
-        else *reinterpret_cast<U4*>(timg + pw_kmaj(hp, hch)) = mask_u4(pack8(g), in);
+        *reinterpret_cast<U4*>(timg + pw_kmaj(hp, hch)) = mask_u4(pack8(g), in);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -329,8 +312,7 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
         unpack8(__builtin_bit_cast(U4, st.y1[i]), y1);
 #pragma unroll
         for (int k = 0; k < 8; ++k) y1[k] = fmaxf(fmaf(y1[k], s1[k], h1[k]), 0.f);
-        if constexpr (PROBE & 4) *reinterpret_cast<pw_u32x4*>(aimg + pw_kmaj(hp, hch)) = st.y1[i];
-        else *reinterpret_cast<U4*>(aimg + pw_kmaj(hp, hch)) = mask_u4(pack8(y1), in);
+        *reinterpret_cast<U4*>(aimg + pw_kmaj(hp, hch)) = mask_u4(pack8(y1), in);
         // raw y1 of the tile interior; border pixels go to a trash slot past the image (no branch)
         const bool inner = ((unsigned)(hy - 1) < (unsigned)C3_TR) & ((unsigned)(hx - 1) < (unsigned)C3_IW);
         *reinterpret_cast<pw_u32x4*>(yimg + (inner ? pw_kmaj((hy - 1) * C3_IW + hx - 1, hch) : C3_YBYTES)) = st.y1[i];
@@ -372,14 +354,10 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
         for (int j = 0; j < 2; ++j)
           fb[j] = pw_frag_tr(wimg, tap * C3_WTAP + 32 * kk * 128, dcb + 16 * j, lane,
                              [](int r, int c) { return pw_mn<64>(r, c); });
-        if constexpr (!(PROBE & 1)) {
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-        } else {
-          acc[0][0][0] += (float)fa[0][0] + (float)fb[0][0] + (float)fa[1][0] + (float)fb[1][0];
-        }
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
       }
     }
   };
@@ -389,9 +367,7 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
   // two 8-byte ones.  The partials are sum g' and sum g' y1 (xhat is affine in y1: centred and scaled
   // once per block, below) -- two coefficients per channel live here instead of four.
   auto dgrad_epi = [&](const f32x4_t (&acc)[2][2], int tile) {
-    if constexpr (PROBE & 8) {
-      if (acc[0][0][0] == 12345.f) bnacc[0] = 1.f;  // keep the loop live
-    } else {
+    {
       const int n = tile / tiles_img, y0 = (tile % tiles_img) * C3_TR;
       const int g = lane >> 4, col = dcb + 16 * (g & 1) + 8 * (g >> 1);
       float bs[8], bq[8];
@@ -457,13 +433,9 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
       for (int nn = 0; nn < 9; ++nn) {
         if (nn + 2 < 9) fbq[(nn + 2) % 3] = fbld(nn + 2);
         __builtin_amdgcn_sched_barrier(0);  // the prefetch issues before this step's MFMAs
-        if constexpr (!(PROBE & 2)) {
 #pragma unroll
-          for (int m = 0; m < 2; ++m)
-            accw[m][nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fbq[nn % 3], accw[m][nn], 0, 0, 0);
-        } else {
-          accw[0][nn][0] += (float)fa[0][0] + (float)fbq[nn % 3][0] + (float)fa[1][0];
-        }
+        for (int m = 0; m < 2; ++m)
+          accw[m][nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fbq[nn % 3], accw[m][nn], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);  // bound the fragment reads hoisted ahead
       }
     }
@@ -501,15 +473,11 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
 
   // ---- weight-gradient accumulators -> this block's slab, register order (coalesced 16-B stores)
   float* slab = a.slab + (size_t)blockIdx.x * (C3_C * 576);
-  if constexpr (PROBE & 16) {
-    if (accw[0][0][0] == 12345.f) slab[t] = 1.f;  // keep the loop live
-  } else {
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int nn = 0; nn < 9; ++nn)
-        *reinterpret_cast<f32x4_t*>(slab + ((size_t)(m * 9 + nn) * PW_NT + t) * 4) = accw[m][nn];
-  }
+    for (int nn = 0; nn < 9; ++nn)
+      *reinterpret_cast<f32x4_t*>(slab + ((size_t)(m * 9 + nn) * PW_NT + t) * 4) = accw[m][nn];
   // ---- BN1 partials of the block -> its slot (one global atomic per value); the block summed g' and
   // g' y1, so sum g' xhat = is1 (sum g' y1) - mu1 is1 (sum g')
   __syncthreads();
@@ -528,13 +496,13 @@ bool conv3x3_fused_ok(int N, int H, int W, int C, int K) {
 
 void conv3x3_fwd_fused(const Conv3Args& a, hipStream_t s) {
   const int ntiles = a.N * (a.H / C3_TR);
-  conv3x3_fwd_fused_kernel<0><<<std::min(256, ntiles), PW_NT, 0, s>>>(a);
+  conv3x3_fwd_fused_kernel<<<std::min(256, ntiles), PW_NT, 0, s>>>(a);
 }
 
 int conv3x3_bwd_fused_grid(int N, int H) { return std::min(256, N * (H / C3_TR)); }
 
 void conv3x3_bwd_fused(const Conv3BwdArgs& a, int nblocks, hipStream_t s) {
-  conv3x3_bwd_fused_kernel<0><<<nblocks, PW_NT, 0, s>>>(a);
+  conv3x3_bwd_fused_kernel<<<nblocks, PW_NT, 0, s>>>(a);
 }
 
 }  // namespace tfx

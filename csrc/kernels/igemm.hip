@@ -99,7 +99,18 @@ int igemm_tune_traced(int* out, int cap) {
   return n;
 }
 
+// TEMPORARY cost probe (round 6): bit 0 = the A operand reads nothing (zero-extent resource: every A
+// load returns zeros without a memory access), bit 1 = the same for B
+int g_probe_io = 0;
+int igemm_probe_set(int v) {
+  const int p = g_probe_io;
+  g_probe_io = v;
+  return p;
+}
+
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
+  if (g_probe_io & 1) a.a_bytes = 0;
+  if (g_probe_io & 2) a.b_bytes = 0;
   if (a.out_mode == OUT_F32_ATOMIC && a.zero_out) {
     const size_t rows = a.trans_out ? a.N : a.M;
     TFX_HIP_CHECK(hipMemsetAsync(a.Cp, 0, sizeof(float) * rows * a.ldc, s));
@@ -125,13 +136,11 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
       abort();
     }
   }
-  // the A-operand BN transform: pointwise forward with the fused statistics epilogue -- single k-tile
-  // (register path), or the persistent kernel's on-load transform beyond
+  // the A-operand BN transform: pointwise forward with the fused statistics epilogue, single k-tile only
+  // (the register path's single-tile kernel is the one that applies it)
   if (a.a_scale && !(a.stats && mode == MODE_FWD && a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 &&
-                     a.pw == 0 && a.a_shift && a.K % 8 == 0 &&
-                     (a.K <= BKT_HOST || igemm_fwd_bna_supported(a.M, a.N, a.K)))) {
-    fprintf(stderr, "igemm_launch: A-operand transform needs a 1x1 stride-1 forward with BN stats (K <= 64, or "
-                    "the persistent kernel's shapes)\n");
+                     a.pw == 0 && a.a_shift && a.K % 8 == 0 && a.K <= BKT_HOST)) {
+    fprintf(stderr, "igemm_launch: A-operand transform needs a 1x1 stride-1 forward with BN stats and K <= 64\n");
     abort();
   }
   // 1x1 stride-1 unpadded convs (two thirds of ResNet-50's) are plain GEMMs over the NHWC rows:
@@ -147,8 +156,7 @@ void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
         return;
       case MODE_DGRAD:  // dY[M][Ko] . W[Ko][C]
         a.lda = a.Ko; a.ldb = a.C;
-        if (igemm_dgrad_persist_ok(a)) igemm_dgrad_persist(a, s);  // many-tile fused-BN data gradients
-        else igemm_dgrad_pointwise(a, s);
+        igemm_dgrad_pointwise(a, s);
         return;
       case MODE_WGRAD:  // dY^T[Ko][pix] . X[pix][C]
         a.lda = a.Ko; a.ldb = a.C;

@@ -18,12 +18,7 @@ void igemm_wgrad_t_x(IgemmArgs& a, hipStream_t s);       // im2col(X)^T . dY (tr
 void igemm_gemm(IgemmArgs& a, hipStream_t s);            // plain GEMMs (FC layers, LSTM)
 // persistent 1x1 forward (igemm_persist.hip): one continuous LDS-DMA ring over all of a block's tiles
 bool igemm_fwd_persist_ok(const IgemmArgs& a);
-// ... with the A-operand BN transform (a_scale / a_shift: a plain ReLU BN applied on load)
-bool igemm_fwd_persist_bna_ok(const IgemmArgs& a);
 void igemm_fwd_persist(IgemmArgs& a, hipStream_t s);
-// ... and the fused-BN 1x1 data gradient (EPI_BNB, MN-major W)
-bool igemm_dgrad_persist_ok(const IgemmArgs& a);
-void igemm_dgrad_persist(IgemmArgs& a, hipStream_t s);
 
 // ---- measured launch configurations (igemm.hip; table from scripts/tune_convs.py)
 // family = which entry above launched; a config overrides the built-in heuristics of launch_shape /

@@ -37,15 +37,25 @@ __device__ __forceinline__ void load4<uint16_t>(const uint16_t* g, int64_t i, fl
 // kind: 0 = SGD, 1 = momentum (heavy ball, TF MomentumOptimizer form), 2 = Nesterov momentum,
 //       3 = Adam (bias-corrected, L2 wd added to g), 4 = AdamW (decoupled wd)
 template <typename TG, int KIND>
-__global__ void __launch_bounds__(256) opt_kernel(float* __restrict__ p, const TG* __restrict__ g,
+__global__ void __launch_bounds__(256) opt_kernel(float* __restrict__ p, const TG* g,
                                                   float* __restrict__ m, float* __restrict__ v, int64_t n4,
                                                   const float* __restrict__ lr_ptr, float gscale, float wd,
                                                   float b1, float b2, float eps, const float* __restrict__ step_ptr,
                                                   const float* __restrict__ sumsq, float max_norm,
-                                                  uint16_t* __restrict__ pbf, const int* __restrict__ skip) {
+                                                  uint16_t* __restrict__ pbf, const int* __restrict__ skip,
+                                                  float* gz) {  // may alias g: no __restrict__ on either
+  // gz (optional): the f32 gradient buffer, zeroed in the same pass (the next step's split-K weight
+  // gradients accumulate into it with atomics) -- the step then needs no separate gradient fill.  It is
+  // g itself on the f32 path; with the bf16 DP wire g is the reduced bf16 twin and gz its f32 source.
   // a nonzero skip word (e.g. the persistent LSTM's sticky health word: this step's gradients came
-  // from a launch that gave up on a hand-off) leaves parameters, moments and the shadow untouched
-  if (skip && *skip) return;
+  // from a launch that gave up on a hand-off) leaves parameters, moments and the shadow untouched --
+  // the gradients are still cleared (they are this step's, discarded)
+  if (skip && *skip) {
+    if (gz)
+      for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+        reinterpret_cast<float4*>(gz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   const float lr = *lr_ptr;
   const float gs = gscale * clip_factor(sumsq, max_norm);
   float bc1 = 1.f, bc2 = 1.f;
@@ -59,6 +69,7 @@ __global__ void __launch_bounds__(256) opt_kernel(float* __restrict__ p, const T
     float pp[4] = {pv.x, pv.y, pv.z, pv.w};
     float gg[4];
     load4<TG>(g, i, gg);
+    if (gz) reinterpret_cast<float4*>(gz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (KIND == 0) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) pp[k] -= lr * fmaf(gg[k], gs, wd * pp[k]);
@@ -138,16 +149,17 @@ static inline int ogrid(int64_t n4) {
 
 void optimizer_apply(int kind, float* p, const void* g, bool g_bf16, float* m, float* v, int64_t n,
                      const float* lr, float gscale, float wd, float b1, float b2, float eps, const float* step,
-                     const float* sumsq, float max_norm, uint16_t* pbf, const int* skip, hipStream_t s) {
+                     const float* sumsq, float max_norm, uint16_t* pbf, const int* skip, float* gz,
+                     hipStream_t s) {
   const int64_t n4 = n / 4;  // host wrapper pads flat buffers to a multiple of 4 elements
   const int grid = ogrid(n4);
 #define TFX_OPT(K)                                                                                     \
   if (g_bf16)                                                                                          \
     opt_kernel<uint16_t, K><<<grid, 256, 0, s>>>(p, (const uint16_t*)g, m, v, n4, lr, gscale, wd, b1, b2, \
-                                                 eps, step, sumsq, max_norm, pbf, skip);               \
+                                                 eps, step, sumsq, max_norm, pbf, skip, gz);           \
   else                                                                                                 \
     opt_kernel<float, K><<<grid, 256, 0, s>>>(p, (const float*)g, m, v, n4, lr, gscale, wd, b1, b2, eps, \
-                                              step, sumsq, max_norm, pbf, skip);
+                                              step, sumsq, max_norm, pbf, skip, gz);
   switch (kind) {
     case 0: TFX_OPT(0); break;
     case 1: TFX_OPT(1); break;

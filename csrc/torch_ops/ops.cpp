@@ -271,71 +271,6 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   return {y, save};
 }
 
-// conv_fwd_bn without the finalize: the epilogue adds the statistics into the stat_slots zeroed rows
-// ws = [stat_slots][2][Ko] and the BN's apply finalizes them itself (bn_apply_fin_into), or
-// bn_finalize_rows does when the consumer cannot.  Always the implicit GEMM (never the stem route).
-Tensor conv_fwd_bn_nofin(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor ws, int64_t stat_slots) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
-  TORCH_CHECK(stat_slots >= 1 && stat_slots <= 16, "conv_fwd_bn_nofin: 1..16 statistics rows");
-  auto g = geom(x.sizes().vec(), w.sizes().vec(), stride, pad, dil);
-  auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
-  auto a = conv_args(g, stride, pad, dil);
-  a.A = bf(x); a.B = bf(w); a.Cp = y.data_ptr();
-  a.a_bytes = x.nbytes(); a.b_bytes = w.nbytes();
-  a.M = g.N * g.P * g.Q; a.N = g.Ko; a.K = g.R * g.S * g.C; a.ldb = a.K; a.ldc = g.Ko;
-  a.out_mode = tfx::OUT_BF16;
-  CHECK_F32(ws); CHECK_CONTIG(ws);
-  TORCH_CHECK(ws.numel() >= stat_slots * 2 * g.Ko, "conv_fwd_bn_nofin: statistics rows too small");
-  a.stats = ws.data_ptr<float>();
-  a.stat_slots = (int)stat_slots;
-  tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
-  return y;
-}
-
-// the finalize of a conv_fwd_bn_nofin's rows alone (one block of bn_apply_fin_kernel): save =
-// [mean|invstd|scale|shift], running statistics updated; the rows stay (zeroed with the gradients)
-void bn_finalize_rows(Tensor rows, int64_t nsl, int64_t M, optional<Tensor> gamma, optional<Tensor> beta,
-                      optional<Tensor> run_mean, optional<Tensor> run_var, double momentum, double eps, Tensor save) {
-  CHECK_F32(rows); CHECK_CONTIG(rows); CHECK_F32(save); CHECK_CONTIG(save);
-  const int64_t C = save.numel() / 4;
-  TORCH_CHECK(tfx::bn_apply_fin_ok((int)C) && nsl >= 1 && nsl <= 16 && rows.numel() >= nsl * 2 * C,
-              "bn_finalize_rows: shapes");
-  tfx::bn_apply_fin(nullptr, nullptr, rows.data_ptr<float>(), (int)nsl, M, (int)C, fp(gamma), fp(beta), (float)eps,
-                    (float)momentum, fpm(run_mean), fpm(run_var), save.data_ptr<float>(), false, nullptr, nullptr,
-                    cur_stream());
-}
-
-// BN apply (out = relu?(x sc + sh (+ res)), mask bits with res) with the finalize folded in: scale /
-// shift from the nsl statistics rows ws = [nsl][2][C] (conv_fwd_bn_nofin), save and the running stats
-// written by block 0; the rows are left for the caller to zero (the gradient fill of the next step).
-bool bn_apply_fin_supported(int64_t C) { return tfx::bn_apply_fin_ok((int)C); }
-
-void bn_apply_fin_into(Tensor x, optional<Tensor> res, Tensor ws, int64_t nsl, optional<Tensor> gamma,
-                       optional<Tensor> beta, optional<Tensor> run_mean, optional<Tensor> run_var, double momentum,
-                       double eps, bool relu, Tensor save, Tensor out, optional<Tensor> mask) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(out); CHECK_CONTIG(out);
-  CHECK_F32(ws); CHECK_CONTIG(ws); CHECK_F32(save); CHECK_CONTIG(save);
-  const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(tfx::bn_apply_fin_ok((int)C) && out.numel() == x.numel() && save.numel() == 4 * C,
-              "bn_apply_fin_into: shapes");
-  TORCH_CHECK(nsl >= 1 && nsl <= 16, "bn_apply_fin_into: 1..16 statistics rows");
-  TORCH_CHECK(ws.numel() >= nsl * 2 * C, "bn_apply_fin_into: statistics rows too small");
-  const uint16_t* r = nullptr;
-  if (res.has_value() && res->defined()) {
-    CHECK_BF16(*res); CHECK_CONTIG(*res);
-    TORCH_CHECK(res->numel() == x.numel(), "bn_apply_fin_into: residual");
-    r = bf(*res);
-  }
-  uint8_t* mk = nullptr;
-  if (mask.has_value() && mask->defined()) {
-    TORCH_CHECK(r && relu && mask->numel() * 8 == x.numel(), "bn_apply_fin_into: mask");
-    mk = mask->data_ptr<uint8_t>();
-  }
-  tfx::bn_apply_fin(bf(x), r, ws.data_ptr<float>(), (int)nsl, M, (int)C, fp(gamma), fp(beta), (float)eps,
-                    (float)momentum, fpm(run_mean), fpm(run_var), save.data_ptr<float>(), relu, bfm(out), mk,
-                    cur_stream());
-}
-
 // A/B hook for the stem forward kernel; returns the previous setting
 bool conv_stem_fwd(bool on) {
   const bool prev = g_stem_fwd;
@@ -344,11 +279,9 @@ bool conv_stem_fwd(bool on) {
 }
 
 // conv_fwd_bn of relu(x * in_save[2C..3C) + in_save[3C..4C)) -- a plain ReLU BN applied on load by this
-// 1x1 stride-1 conv (C <= 64: one k-tile, register path; wider: the persistent kernel transforms each
-// A fragment after its LDS read), so the BN output is never written.  Returns (y, save).
-bool conv_fwd_bn_in_supported(int64_t M, int64_t Ko, int64_t C) {
-  return (C <= 64 && C % 8 == 0) || tfx::igemm_fwd_bna_supported(M, Ko, C);
-}
+// 1x1 stride-1 conv of C <= 64 input channels (one k-tile, register path), so the BN output is never
+// written.  Returns (y, save).  (Wider forms were measured slower than the apply pass, profiles/r05_bna.)
+bool conv_fwd_bn_in_supported(int64_t M, int64_t Ko, int64_t C) { return M > 0 && Ko > 0 && C <= 64 && C % 8 == 0; }
 
 std::tuple<Tensor, Tensor> conv_fwd_bn_in(Tensor x, Tensor in_save, Tensor w, Tensor ws, optional<Tensor> gamma,
                                           optional<Tensor> beta, optional<Tensor> run_mean, optional<Tensor> run_var,
@@ -356,10 +289,8 @@ std::tuple<Tensor, Tensor> conv_fwd_bn_in(Tensor x, Tensor in_save, Tensor w, Te
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w);
   CHECK_F32(in_save); CHECK_CONTIG(in_save);
   auto g = geom(x.sizes().vec(), w.sizes().vec(), 1, 0, 1);
-  TORCH_CHECK(g.R == 1 && g.S == 1 && in_save.numel() == 4 * g.C &&
-                  (g.C <= 64 || tfx::igemm_fwd_bna_supported(g.N * g.P * g.Q, g.Ko, g.C)),
-              "conv_fwd_bn_in: 1x1 conv with <= 64 input channels (or a persistent-kernel shape) and the input "
-              "BN's [4][C] save");
+  TORCH_CHECK(g.R == 1 && g.S == 1 && in_save.numel() == 4 * g.C && g.C <= 64 && g.C % 8 == 0,
+              "conv_fwd_bn_in: 1x1 conv with <= 64 input channels and the input BN's [4][C] save");
   auto y = at::empty({g.N, g.P, g.Q, g.Ko}, x.options());
   auto save = at::empty({4 * g.Ko}, x.options().dtype(at::kFloat));
   auto a = conv_args(g, 1, 0, 1);
@@ -1302,7 +1233,8 @@ Tensor scale_by_scalar(Tensor x, Tensor scal, bool out_bf16) {
 // ------------------------------------------------------------------ optimizers
 void optimizer_apply(int64_t kind, Tensor p, Tensor g, optional<Tensor> m, optional<Tensor> v, Tensor lr,
                      double gscale, double wd, double b1, double b2, double eps, optional<Tensor> step,
-                     optional<Tensor> sumsq, double max_norm, optional<Tensor> pbf, optional<Tensor> skip_if) {
+                     optional<Tensor> sumsq, double max_norm, optional<Tensor> pbf, optional<Tensor> skip_if,
+                     optional<Tensor> zero_grad) {
   CHECK_DEV(p); CHECK_F32(p); CHECK_CONTIG(p); CHECK_CONTIG(g);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() % 4 == 0, "flat buffers must match and be padded to 4");
   const bool gb = g.scalar_type() == at::kBFloat16;
@@ -1320,8 +1252,14 @@ void optimizer_apply(int64_t kind, Tensor p, Tensor g, optional<Tensor> m, optio
     TORCH_CHECK(skip_if->is_cuda() && skip_if->scalar_type() == at::kInt && skip_if->numel() >= 1, "skip_if word");
     skip = skip_if->data_ptr<int>();
   }
+  float* gz = nullptr;  // the f32 gradient buffer cleared in the same pass (the next step accumulates into it)
+  if (zero_grad.has_value() && zero_grad->defined()) {
+    CHECK_F32(*zero_grad); CHECK_CONTIG(*zero_grad);
+    TORCH_CHECK(zero_grad->is_cuda() && zero_grad->numel() == p.numel(), "zero_grad: the f32 flat gradient buffer");
+    gz = zero_grad->data_ptr<float>();
+  }
   tfx::optimizer_apply(kind, p.data_ptr<float>(), g.data_ptr(), gb, fpm(m), fpm(v), p.numel(), lr.data_ptr<float>(),
-                       gscale, wd, b1, b2, eps, fp(step), fp(sumsq), max_norm, pb, skip, cur_stream());
+                       gscale, wd, b1, b2, eps, fp(step), fp(sumsq), max_norm, pb, skip, gz, cur_stream());
 }
 
 Tensor sumsq(Tensor g) {
@@ -1822,16 +1760,12 @@ void dp_ring_sim(Tensor buf, int64_t nblocks, double duration_us, int64_t passes
 }
 
 int64_t igemm_persist_mode(int64_t mode) { return tfx::igemm_persist_set((int)mode); }
-int64_t igemm_bna_mode(int64_t mode) { return tfx::igemm_bna_mode_set((int)mode); }
-int64_t igemm_persist_dgrad(int64_t on) { return tfx::igemm_persist_dgrad_set((int)on); }
 
 TORCH_LIBRARY(tfx, m) {
   m.def("image_normalize", &image_normalize);
   m.def("image_normalize_into", &image_normalize_into);
   m.def("augment_normalize", &augment_normalize);
   m.def("igemm_persist_mode", &igemm_persist_mode);
-  m.def("igemm_bna_mode", &igemm_bna_mode);
-  m.def("igemm_persist_dgrad", &igemm_persist_dgrad);
   m.def("dp_ring_sim(Tensor(a!) buf, int nblocks, float duration_us, int passes) -> ()", &dp_ring_sim);
   m.def("augment_normalize_into(Tensor x, Tensor offsets, float[] mean, float[] stdv, int pad, Tensor(a!) y) -> ()",
         &augment_normalize_into);
@@ -1885,10 +1819,6 @@ TORCH_LIBRARY(tfx, m) {
   m.def("bn_bwd_apply(Tensor g, Tensor x, Tensor? res, Tensor save, Tensor red, bool relu, Tensor? mask, "
         "bool want_dres=True) -> (Tensor, Tensor)", &bn_bwd_apply);
   m.def("conv_fwd_bn", &conv_fwd_bn);
-  m.def("conv_fwd_bn_nofin", &conv_fwd_bn_nofin);
-  m.def("bn_finalize_rows", &bn_finalize_rows);
-  m.def("bn_apply_fin_supported", &bn_apply_fin_supported);
-  m.def("bn_apply_fin_into", &bn_apply_fin_into);
   m.def("conv_fwd_bn_in", &conv_fwd_bn_in);
   m.def("conv_fwd_bn_in_supported", &conv_fwd_bn_in_supported);
   m.def("stem_wgrad", &stem_wgrad);
@@ -1924,6 +1854,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("accuracy_count", &accuracy_count);
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
+  m.def("igemm_probe", [](int64_t v) -> int64_t { return tfx::igemm_probe_set((int)v); });
   m.def("optimizer_apply", &optimizer_apply);
   m.def("lstm_seq_residency", &lstm_seq_residency);
   m.def("affine_fwd", &affine_fwd);

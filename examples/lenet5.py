@@ -46,7 +46,7 @@ def main(_):
     store, model = build_lenet5(device=dev, dtype=dtype, seed=0)
     print("LeNet-5: %d parameters (%d padded)" % (model.effective_params(), store.num_params()))
     opt = MomentumOptimizer(store, FLAGS.learning_rate, 0.9)
-    trainer = ClassifierTrainer(store, model, opt)
+    trainer = ClassifierTrainer(store, model, opt, fuse_zero_grad=True)  # optimizer clears the grads
     log = runlog.RunLog(store, opt, FLAGS.logs_path, FLAGS.logdir, FLAGS.save_checkpoint_steps)
     start = log.restore()  # resume from --logdir's latest checkpoint (0: fresh run)
     xtr, ytr = mnist.train.images, mnist.train.labels.astype(np.int64)

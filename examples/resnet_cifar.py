@@ -12,6 +12,7 @@ graph-capture step (with its warm-up) and the evaluations are timed apart.
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/resnet_cifar.py --depth=50 --batch_size=256
 """
+import itertools
 import os
 import sys
 import time
@@ -98,11 +99,13 @@ def main(_):
     start_step = log.restore()  # every rank restores the same checkpoint (then broadcast keeps them equal)
     broadcast_variables(store)
     dp = GradAllReduce(store, bucket_bytes=int(FLAGS.bucket_mb * (1 << 20))) if world > 1 else None
-    trainer = ClassifierTrainer(store, model, opt, dp)
+    trainer = ClassifierTrainer(store, model, opt, dp, fuse_zero_grad=True)  # optimizer clears the grads
     shard = np.arange(rank, len(xtr), world)
     # this rank's shard, gathered once (not a 150 MB copy at every epoch start)
     xs, ys = (xtr, ytr) if world == 1 else (xtr[shard], ytr[shard])
     steps_per_epoch = len(shard) // FLAGS.batch_size
+    # an ABSOLUTE step budget (like the other examples): a resumed run trains up to `total`, not `total` more;
+    # the LR boundaries / warm-up use the absolute step, and the epochs the checkpoint covers are skipped
     total = FLAGS.max_steps or steps_per_epoch * FLAGS.epochs
     bounds = [int(float(f) * total) for f in FLAGS.lr_boundaries.split(",") if f]
     step, seen = start_step, 0
@@ -111,10 +114,14 @@ def main(_):
     t_start = time.time()
     t0, t_eval, t_capture, t_save = None, 0.0, 0.0, 0.0  # steady state starts after the first (capture) step
     test_acc = None
-    for ep in range(FLAGS.epochs):
-        if step - start_step >= total:
+    ep0 = min(start_step // max(steps_per_epoch, 1), FLAGS.epochs)
+    skip = start_step - ep0 * steps_per_epoch  # batches of the resumed epoch the checkpoint already covers
+    for ep in range(ep0, FLAGS.epochs):
+        if step >= total:
             break
         src = batches([xs, ys], FLAGS.batch_size, seed=ep * 1000 + rank + 7919 * FLAGS.seed)
+        if skip > 0:
+            src, skip = itertools.islice(src, skip, None), 0
         for img, lab in DevicePrefetcher(src, dev):
             lr = FLAGS.learning_rate * world * (0.1 ** sum(step >= b for b in bounds))
             if FLAGS.warmup_steps and step < FLAGS.warmup_steps:
@@ -167,16 +174,21 @@ def main(_):
                 sync()
                 ts = time.time()
                 log.maybe_save(step)  # device -> host copy + file write, timed apart like the evaluations
+                if world > 1:  # every rank waits here, so every rank subtracts the same interval
+                    dist.barrier(group=ctl)
                 t_save += time.time() - ts
-            if step - start_step >= total:
+            if step >= total:
                 break
-        # per-epoch test accuracy (rank 0; the other ranks wait at the next collective), timed apart
+        # per-epoch test accuracy (rank 0), timed apart: the other ranks wait at a control-group barrier
+        # inside the same interval (not in the next collective, which would count as training time)
         sync()
         te = time.time()
         if rank == 0:
             test_acc = evaluate(model, xte, yte, dev, dtype)
             print("epoch %d test accuracy %.4f" % (ep + 1, test_acc), flush=True)
             log.scalars(step, test_accuracy=test_acc)
+        if world > 1:
+            dist.barrier(group=ctl)
         t_eval += time.time() - te
     sync()
     t_end = time.time()

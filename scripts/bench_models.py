@@ -62,7 +62,7 @@ def bench_lenet(a, dev):
         from tensorflow_examples_amd.optim import MomentumOptimizer
         from tensorflow_examples_amd.train import ClassifierTrainer
         store, m = build_lenet5(device=dev)
-        tr = ClassifierTrainer(store, m, MomentumOptimizer(store, 0.05, 0.9))
+        tr = ClassifierTrainer(store, m, MomentumOptimizer(store, 0.05, 0.9), fuse_zero_grad=True)
         xi = to_model_input(x)
         if a.graph:
             tr.capture(xi, y)

@@ -24,17 +24,13 @@ conv3_fused_bwd        stage-1 3x3 conv backward in one launch (conv3x3_bwd_fuse
 stem_kernels           CIFAR stem forward / weight gradient (stem.hip)              generic implicit GEMM
 fused_head             pool + FC + softmax-xent + input gradient (head.hip)         three composed ops
 head_tail              last tail BN applied inside the fused head (TAIL mode)       bn_apply before the head
-bn_finalize_fold       stage 2-4 BN finalize inside the layer-wise apply: every     bn_finalize launch after the
-                       block reduces the conv epilogue's few statistics rows         conv (conv_fwd_bn)
-                       itself (bn_apply_fin); the rows live in the store's
-                       gradient scratch, re-zeroed by VariableStore.zero_grad
 =====================  ==========================================================  ===============================
 
 Three parts:
 
 * :class:`FusionConfig` (``CONFIG``): which groups are on, as named knobs (one or two per group) that
   the ops read through :func:`knob`.  ``TFX_FUSION`` selects a profile at import: ``all`` (default:
-  every group but the opt-in ``bn_finalize_fold``), ``r2`` (epilogue fusions only), ``none``
+  every group), ``r2`` (epilogue fusions only), ``none``
   (layer-wise), or a comma list of ``-group`` / ``+group`` edits applied to ``all``.  :func:`set_groups`
   / :func:`override` switch them at run time (tests, A/B runs).
 * :class:`FusionPlan`: the per-layer plan, built when the model is constructed
@@ -61,11 +57,10 @@ from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Tuple
 
 GROUPS = ("bn_epilogue", "grad_sink", "masked_res", "s2_addend", "deferred_slot_reduce", "block_boundary_fwd",
-          "bn_on_load", "lazy_bn_bwd", "conv3_fused_bwd", "stem_kernels", "fused_head", "head_tail",
-          "bn_finalize_fold")
-# bn_finalize_fold is opt-in (``TFX_FUSION=+bn_finalize_fold``): measured neutral, profiles/r04_fold
+          "bn_on_load", "lazy_bn_bwd", "conv3_fused_bwd", "stem_kernels", "fused_head", "head_tail")
+# (a BN-finalize-folded-into-the-apply group was measured neutral and removed: profiles/r04_fold)
 PROFILES = {
-    "all": set(GROUPS) - {"bn_finalize_fold"},
+    "all": set(GROUPS),
     "r2": {"bn_epilogue", "grad_sink", "masked_res", "s2_addend", "deferred_slot_reduce", "fused_head"},
     "none": set(),
 }
@@ -86,7 +81,6 @@ GROUP_KNOBS: Dict[str, Tuple[str, ...]] = {
     "stem_kernels": ("stem_wgrad",),
     "fused_head": ("fuse_head",),
     "head_tail": ("head_tail",),
-    "bn_finalize_fold": ("fold_fin",),
 }
 KNOBS = tuple(k for g in GROUPS for k in GROUP_KNOBS[g])
 
@@ -153,14 +147,32 @@ def set_groups(on: Iterable[str]) -> Dict[str, bool]:
     return prev
 
 
-def restore(state: Dict[str, bool]) -> None:
-    """Restore a state returned by :func:`set_groups` (knob dict) or :func:`enabled` (group dict)."""
-    if set(state) <= set(GROUPS):
-        set_groups([g for g, v in state.items() if v])
-        return
+def restore_knobs(state: Dict[str, bool]) -> None:
+    """Restore a COMPLETE knob state, as returned by :func:`knobs` / :func:`set_groups`."""
+    if set(state) != set(KNOBS):
+        raise ValueError("restore_knobs needs every knob (%s); got %s" % (", ".join(KNOBS), sorted(state)))
     for k, v in state.items():
         CONFIG.set(k, v)
     _stem_fwd(CONFIG.knobs["stem_wgrad"])
+
+
+def restore_groups(state: Dict[str, bool]) -> None:
+    """Restore a COMPLETE group state, as returned by :func:`enabled`."""
+    if set(state) != set(GROUPS):
+        raise ValueError("restore_groups needs every group (%s); got %s" % (", ".join(GROUPS), sorted(state)))
+    set_groups([g for g, v in state.items() if v])
+
+
+def restore(state: Dict[str, bool]) -> None:
+    """Restore a complete state returned by :func:`set_groups` / :func:`knobs` (knob dict) or
+    :func:`enabled` (group dict).  Three knob names are also group names (masked_res, s2_addend,
+    lazy_bn_bwd), so a partial dict is ambiguous: anything but a complete one raises."""
+    if set(state) == set(KNOBS):
+        restore_knobs(state)
+    elif set(state) == set(GROUPS):
+        restore_groups(state)
+    else:
+        raise ValueError("fusion.restore: neither a complete knob dict nor a complete group dict: %s" % sorted(state))
 
 
 @contextlib.contextmanager
@@ -223,7 +235,6 @@ KERNEL_GROUP = {
     "igemm_fwd": "conv", "conv3x3_bwd_fused": "conv3_fused_bwd", "pw_bwd_expand": "lazy_bn_bwd",
     "pw_bwd_squeeze": "lazy_bn_bwd", "stem_wgrad": "stem_kernels", "igemm_dgrad_compact": "s2_addend",
     "head_xent": "fused_head", "head_xent_tail": "head_tail", "bn_apply_into": "layerwise",
-    "bn_apply_fin": "bn_finalize_fold",
 }
 
 

@@ -129,12 +129,6 @@ class LazyBNGrad:
 # knobs defer_tail / defer_bn_in off keep every block tail / plain BN applied by its own pass (the
 # layer-wise forward); fuse_conv3_bwd off runs the stage-1 3x3 conv's backward layer-wise
 PW_SQUEEZE_CALLS = [0]  # fused tail + conv1 forward launches (tests)
-# finalize folded into the layer-wise apply (bn_apply_fin): stage 3-4 BN layers (M <= 16384 rows: few
-# statistics rows, so every apply block can afford to reduce them).  Off by default: measured neutral
-# to +9 us/step in the bench (the ~5 us a finalize shows in a step trace is mostly the producer conv's
-# drain, which the next launch pays either way; profiles/r04_fold/README.md).  TFX_FUSION=+bn_finalize_fold
-FOLD_FIN_CALLS = [0]  # applies that finalized their own statistics (tests)
-_FOLD_FIN_MAX_ROWS = 16384
 
 
 class TailPending:
@@ -145,41 +139,23 @@ class TailPending:
     on load WITHOUT writing it (conv3x3_fwd_fused) -- whatever reads ``out`` later (that conv's
     weight gradient) calls :meth:`materialize` (bn_apply_into), as does any consumer that cannot fuse.
     Everything that reads ``out`` runs after that conv in the block's forward order."""
-    __slots__ = ("x", "save", "res", "res_save", "_out", "mask", "done", "fin")
+    __slots__ = ("x", "save", "res", "res_save", "_out", "mask", "done")
 
-    def __init__(self, x, save, res, res_save, out, mask, fin=None):
+    def __init__(self, x, save, res, res_save, out, mask):
         # ``out`` carries this object (fusion carrier "tail"): held weakly, or the pair is a reference cycle
         # that only Python's full (rare) garbage collection frees -- with every step's tail activations
         # in it (an eager training loop ran out of HBM at ~280 steps of ResNet-50 at batch 128)
         self.x, self.save, self.res, self.res_save, self.mask = x, save, res, res_save, mask
         self._out = weakref.ref(out)
         self.done = False
-        # the BNWorkspace whose finalize is still owed (conv_fwd_bn_nofin): ``save`` is unwritten until
-        # the apply runs it in-kernel (materialize) or a fused consumer calls ensure_fin first
-        self.fin = fin
 
     @property
     def out(self):
         return self._out()
 
-    def ensure_fin(self) -> None:
-        if self.fin is not None:
-            self.fin.settle_fin(self.save)
-            self.fin = None
-
     def materialize(self) -> None:
         if not self.done:
-            ws = self.fin
-            if ws is not None and ws.fin is not None and self.res_save is None:
-                torch.ops.tfx.bn_apply_fin_into(self.x, self.res, ws.fin[2], ws.fin[1], *ws.finalize_args,
-                                                True, self.save, self.out, self.mask)
-                ws.fin = None
-                _owed_done(ws)
-                self.fin = None
-                FOLD_FIN_CALLS[0] += 1
-            else:
-                self.ensure_fin()
-                torch.ops.tfx.bn_apply_into(self.x, self.res, self.save, self.res_save, self.out, self.mask)
+            torch.ops.tfx.bn_apply_into(self.x, self.res, self.save, self.res_save, self.out, self.mask)
             self.done = True
 
 
@@ -343,7 +319,6 @@ class _Conv2d(torch.autograd.Function):
                         # BN + ReLU of the input applied on load, 3x3 conv from a halo tile, the output
                         # BN's statistics (conv3x3_fused.hip); x stays unwritten until something reads it
                         ws = stats_into
-                        tp.ensure_fin()
                         y, ws.pending_save = torch.ops.tfx.conv3x3_fwd_fused(tp.x, tp.save, w.value,
                                                                              ws.get(x.device), *ws.finalize_args)
                         ctx.pending_in = tp
@@ -356,7 +331,6 @@ class _Conv2d(torch.autograd.Function):
                         # a plain ReLU BN applied on load by this single-k-tile 1x1 conv (igemm a_scale):
                         # x stays unwritten (the fused backward forms it on load too)
                         ws = stats_into
-                        tp.ensure_fin()
                         y, ws.pending_save = torch.ops.tfx.conv_fwd_bn_in(tp.x, tp.save, w.value, ws.get(x.device),
                                                                           *ws.finalize_args)
                         ctx.pending_in = tp
@@ -369,7 +343,6 @@ class _Conv2d(torch.autograd.Function):
                         # the previous block's tail apply + this conv + its BN statistics in one launch:
                         # x (and the tail's mask bits) are written here (pw_fwd.hip)
                         ws = stats_into
-                        tp.ensure_fin()
                         y, ws.pending_save = torch.ops.tfx.pw_fwd_squeeze(
                             tp.x, tp.save, tp.res, tp.res_save, w.value, x, tp.mask, ws.get(x.device),
                             *ws.finalize_args)
@@ -378,10 +351,7 @@ class _Conv2d(torch.autograd.Function):
                         fusion.note("block_boundary_fwd", w.name, "pw_fwd_squeeze")
                         return y
                     fusion.miss(w.name, want, "input is not a deferred residual tail")
-                if tp.fin is not None and tp.res_save is None:
-                    fusion.note("bn_finalize_fold", w.name, "bn_apply_fin")
-                else:
-                    fusion.note("layerwise", w.name, "bn_apply_into")
+                fusion.note("layerwise", w.name, "bn_apply_into")
                 tp.materialize()
             elif lp is not None and lp.fwd in _FUSED_INPUT:
                 fusion.miss(w.name, lp.fwd, "input already written")
@@ -391,19 +361,6 @@ class _Conv2d(torch.autograd.Function):
                     stem = lp.fwd == "stem_fwd"
                 else:
                     stem = fusion.knob("stem_wgrad") and _stem_ok(x, w, stride, pad, dil)
-                m_out = _conv_rows(x, w, stride, pad, dil)
-                rows = ws.fin_rows() if (fusion.knob("fold_fin") and not stem and m_out <= _FOLD_FIN_MAX_ROWS and
-                                         torch.ops.tfx.bn_apply_fin_supported(w.shape[0])) else None
-                if rows is not None:
-                    # epilogue statistics into a few zeroed scratch rows; the finalize is owed (ws.fin) --
-                    # the BN's apply runs it in-kernel, or ws.settle_fin launches it for other consumers
-                    nsl = max(1, min(BNWorkspace.FIN_ROWS, m_out // 4096))
-                    y = torch.ops.tfx.conv_fwd_bn_nofin(x.contiguous(), w.value, stride, pad, dil, rows, nsl)
-                    ws.pending_save = torch.empty(4 * w.shape[0], dtype=torch.float32, device=x.device)
-                    ws.fin = (m_out, nsl, rows)
-                    _OWED_FIN.append(ws)
-                    fusion.note("bn_epilogue", w.name, "igemm_fwd_stats")
-                    return y
                 # epilogue statistics, then the finalize: the BN only applies
                 y, ws.pending_save = torch.ops.tfx.conv_fwd_bn(x.contiguous(), w.value, stride, pad, dil,
                                                                ws.get(x.device), *ws.finalize_args)
@@ -663,31 +620,12 @@ class BNWorkspace:
     statistics and leaves [mean | invstd | scale | shift] in ``pending_save``."""
     NSLOT = 64  # = tfx::NSLOT (csrc/include/tfx_kernels.h), checked on first GPU use
 
-    FIN_ROWS = 16  # forward statistics rows of a folded finalize (conv_fwd_bn_nofin), at most
-
     def __init__(self, channels: int, store=None):
         self.c = channels
         self.buf = None
         self.finalize_args = None
         self.pending_save = None
-        # (rows M, statistics rows nsl) while the finalize of a conv_fwd_bn_nofin is owed
-        self.fin = None
-        # the folded finalize's forward statistics rows live in the store's gradient-zeroed scratch
-        # (VariableStore.reserve_scratch): zeroed with the gradients once per step, so the apply that
-        # reads them never has to re-zero them (no cross-block "last reader" round trip)
         self.store = store
-        self.rows_off = store.reserve_scratch(self.FIN_ROWS * 2 * channels) if store is not None else None
-        self.rows_epoch = -1
-
-    def fin_rows(self) -> Optional[torch.Tensor]:
-        """This step's zeroed statistics rows for a folded finalize, or None (no store scratch, or the
-        rows were already used since the last VariableStore.zero_grad)."""
-        st = self.store
-        if st is None or st.scratch is None or self.rows_epoch == st.grad_epoch:
-            return None
-        self.rows_epoch = st.grad_epoch
-        n = self.FIN_ROWS * 2 * self.c
-        return st.scratch[self.rows_off:self.rows_off + n]
 
     def get(self, device) -> torch.Tensor:
         if self.buf is None or self.buf.device != device:
@@ -695,14 +633,6 @@ class BNWorkspace:
                 assert int(torch.ops.tfx.bn_nslot()) == self.NSLOT, "BNWorkspace.NSLOT != tfx::NSLOT"
             self.buf = torch.zeros(self.NSLOT * 2 * self.c, dtype=torch.float32, device=device)
         return self.buf
-
-    def settle_fin(self, save: torch.Tensor) -> None:
-        """Run the owed finalize (bn_finalize_rows: one block) into ``save``, if any."""
-        if self.fin is not None:
-            m, nsl, rows = self.fin
-            torch.ops.tfx.bn_finalize_rows(rows, nsl, m, *self.finalize_args, save)
-            self.fin = None
-            _owed_done(self)
 
 
 class BNBackwardFusion:
@@ -763,27 +693,11 @@ _PENDING_SR: List["BNBackwardFusion"] = []
 _XENT_MEAN_MAX = 1024
 
 
-# BN workspaces whose conv epilogue owed a folded finalize this step (conv_fwd_bn_nofin); an entry
-# leaves the list when its finalize runs (settle_fin / the folded apply), so any training loop that
-# enables the group keeps it bounded, not only ClassifierTrainer's reset
-_OWED_FIN: List["BNWorkspace"] = []
-
-
-def _owed_done(ws: "BNWorkspace") -> None:
-    for i, w in enumerate(_OWED_FIN):
-        if w is ws:
-            del _OWED_FIN[i]
-            return
-
-
 def reset_pending_slot_reductions() -> None:
-    """Forget deferred reductions / finalizes of an abandoned step (an exception part-way through)."""
+    """Forget deferred reductions of an abandoned step (an exception part-way through)."""
     for b in _PENDING_SR:
         b.sr_pending = False
     _PENDING_SR.clear()
-    for ws in _OWED_FIN:
-        ws.fin = None  # never finalized: its rows are re-zeroed with the gradients (zero_grad)
-    _OWED_FIN.clear()
 
 
 def _resolve_pending(b: "BNBackwardFusion") -> None:
@@ -867,21 +781,16 @@ class _BatchNorm(torch.autograd.Function):
                 res = torch.ops.tfx.bn_apply_train(res_bnb.x, None, res_bnb.save, False)[0]
             defer_out = defer and pending and res is None and bnb_out is not None and _vec_ok(x.shape[-1])
             if pending:
-                # the producing conv's epilogue already finalized the statistics (conv_fwd_bn) -- or
-                # owes the finalize (wsobj.fin): a deferred apply takes it along, anything else runs it
+                # the producing conv's epilogue already finalized the statistics (conv_fwd_bn)
                 save, wsobj.pending_save = wsobj.pending_save, None
-                owed = wsobj if wsobj.fin is not None else None
-                if owed is not None and not (defer_plain or (defer_tail and not fuse_res)):
-                    owed.settle_fin(save)
-                    owed = None
                 if defer_plain:
                     y = torch.empty_like(x)
-                    fusion.carry(y, "tail", TailPending(x, save, None, None, y, None, fin=owed))
+                    fusion.carry(y, "tail", TailPending(x, save, None, None, y, None))
                 elif defer_tail:
                     y = torch.empty_like(x)
                     mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
                     fusion.carry(y, "tail", TailPending(x, save, res_bnb.x if fuse_res else res.contiguous(),
-                                                        res_bnb.save if fuse_res else None, y, mask, fin=owed))
+                                                        res_bnb.save if fuse_res else None, y, mask))
                 elif fuse_res:
                     y, mask = torch.ops.tfx.bn_apply_res_bn(x, res_bnb.x, save, res_bnb.save, relu)
                 elif defer_out:
@@ -919,8 +828,6 @@ class _BatchNorm(torch.autograd.Function):
             x, res, save, mask = ctx.saved_tensors
             if not training:
                 raise RuntimeError("backward through eval-mode batch norm is not supported on the GPU path")
-            if ctx.tp is not None:  # a deferred apply nobody consumed still owes the finalize
-                ctx.tp.ensure_fin()
             if ctx.bnb is not None:
                 if ctx.bnb.sec_lazy is not None:  # the tail's conv3 has not run yet: reduce here
                     ctx.bnb.sec_lazy.materialize()
@@ -1383,7 +1290,6 @@ def _head_tail(feat):
         return None
     if bnb.deferred or bnb.red is not None or bnb.sr_pending or bnb.x is not tp.x:
         return None
-    tp.ensure_fin()  # the head reads save
     return tp, bnb
 
 

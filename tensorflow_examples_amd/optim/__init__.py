@@ -59,7 +59,7 @@ class Optimizer:
 
     def apply_gradients(self, grad_scale: float = 1.0, sumsq: Optional[torch.Tensor] = None,
                         max_norm: float = 0.0, skip_if: Optional[torch.Tensor] = None,
-                        grad: Optional[torch.Tensor] = None) -> None:
+                        grad: Optional[torch.Tensor] = None, zero_grad: bool = False) -> None:
         """p <- update(p, grad_scale * g); refreshes the bf16 shadow. ``sumsq`` (device scalar
         ||g||^2) enables clip-by-global-norm at ``max_norm``.  ``skip_if`` (a device int32 word, GPU):
         when it is nonzero at execution time the update is skipped ON THE DEVICE -- parameters,
@@ -67,7 +67,10 @@ class Optimizer:
         its steps this way); only the native dense path has that guard, so ``skip_if`` with sparse
         variables or a CPU store raises.  ``iterations`` (host count of calls) still advances.
         ``grad``: the flat gradient buffer to apply instead of the store's f32 one (same layout; f32 or
-        bf16 -- the DP bf16 wire format hands its all-reduced bf16 buffer straight to the kernel)."""
+        bf16 -- the DP bf16 wire format hands its all-reduced bf16 buffer straight to the kernel).
+        ``zero_grad``: the native kernel also clears the store's f32 gradient buffer in the same pass (the
+        next ``VariableStore.zero_grad`` is then a no-op): the training step needs no separate gradient
+        fill.  The gradients read zero after the call -- callers that inspect them leave it off."""
         st = self.store
         if skip_if is not None and (st.sparse or not _native.use_native(st.master)):
             # the device-side skip is honoured only by the native dense kernel: refuse rather than apply
@@ -85,10 +88,13 @@ class Optimizer:
         if not st.vars:
             return
         if _native.use_native(st.master):
+            gz = st.grad if zero_grad else None
             torch.ops.tfx.optimizer_apply(self.kind, st.master, st.grad if grad is None else grad, self.m, self.v,
                                           self.lr_t, grad_scale,
                                           self.wd, self.b1, self.b2, self.eps, self.step_t, sumsq, max_norm,
-                                          st.shadow, skip_if)
+                                          st.shadow, skip_if, gz)
+            if gz is not None:
+                st.grads_clean = True
             return
         with torch.no_grad():
             g = (st.grad if grad is None else grad.float()) * grad_scale

@@ -2,7 +2,8 @@
 
 ``ClassifierTrainer`` runs one synchronous step of an image classifier on the flat
 variable store: zero grads -> forward -> softmax-xent -> backward (bucketed RCCL
-all-reduce overlapped) -> fused optimizer (+bf16 shadow refresh).  Optionally the whole
+all-reduce overlapped) -> fused optimizer (+bf16 shadow refresh; with ``fuse_zero_grad`` it also
+clears the gradients for the next step, so no fill launch remains).  Optionally the whole
 step is captured once into a HIP graph and replayed (launch-bound small models).
 """
 from __future__ import annotations
@@ -22,8 +23,11 @@ from .variables import VariableStore
 
 class ClassifierTrainer:
     def __init__(self, store: VariableStore, model: Callable, optimizer: Optimizer,
-                 dp: Optional[GradAllReduce] = None, naive_xent: bool = False):
+                 dp: Optional[GradAllReduce] = None, naive_xent: bool = False, fuse_zero_grad: bool = False):
         self.store, self.model, self.opt, self.dp = store, model, optimizer, dp
+        # fuse_zero_grad: the optimizer kernel clears the gradients in its pass (no fill launch per step);
+        # the store's gradients then read zero after each step
+        self.fuse_zero_grad = fuse_zero_grad
         self.naive = naive_xent
         self.graph = None
         self._static = None
@@ -64,7 +68,7 @@ class ClassifierTrainer:
                 self.dp.finish()
             scale, grad = self.dp.grad_scale, self.dp.reduced_grad
         with trace.range("optimizer"):
-            self.opt.apply_gradients(grad_scale=scale, grad=grad)
+            self.opt.apply_gradients(grad_scale=scale, grad=grad, zero_grad=self.fuse_zero_grad)
         return loss.detach()
 
     def input_buffer(self):

@@ -264,11 +264,10 @@ class VariableStore:
         self.state: Dict[str, torch.Tensor] = {}  # non-trainable state (BN running stats, global_step)
         self.master: Optional[torch.Tensor] = None
         self.grad: Optional[torch.Tensor] = None
-        # f32 scratch zeroed together with the gradients (one fill per step): the forward statistics
-        # rows of BN layers whose finalize is folded into their apply (ops.nn.BNWorkspace)
-        self.scratch: Optional[torch.Tensor] = None
-        self._scratch_n = 0
-        self.grad_epoch = 0  # bumped by zero_grad: scratch users detect a step without one
+        # True while the gradient buffer is known to be all zeros (a fresh buffer, or the optimizer
+        # cleared it in its pass: Optimizer.apply_gradients(zero_grad=True)); zero_grad then skips the fill
+        self.grads_clean = True
+        self.grad_epoch = 0  # bumped by zero_grad (a step counter for gradient consumers)
         self.shadow: Optional[torch.Tensor] = None
         self._flip = None          # flipped 3x3 filter copies (flip_index / flipped3x3)
         self.flip_stale = True
@@ -321,14 +320,6 @@ class VariableStore:
         self.by_name[full] = v
         return v
 
-    def reserve_scratch(self, n: int) -> int:
-        """Reserve n f32 of gradient-zeroed scratch (before finalize); returns its offset in ``scratch``."""
-        if self.master is not None:
-            raise RuntimeError("VariableStore already finalized")
-        off = self._scratch_n
-        self._scratch_n = _round_up(off + int(n), ALIGN)
-        return off
-
     def add_state(self, name: str, t: torch.Tensor) -> torch.Tensor:
         full = self.unique_name(name)
         t = t.to(self.device)
@@ -344,10 +335,8 @@ class VariableStore:
             off = _round_up(off + v.numel, ALIGN)
         self.total = max(off, ALIGN)
         self.master = torch.zeros(self.total, dtype=torch.float32, device=self.device)
-        # gradients and the scratch share one allocation, so zero_grad is still one fill
-        self._grad_ext = torch.zeros(self.total + self._scratch_n, dtype=torch.float32, device=self.device)
-        self.grad = self._grad_ext[:self.total]
-        self.scratch = self._grad_ext[self.total:] if self._scratch_n else None
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.grads_clean = True  # all zeros (see zero_grad)
         if self.compute_dtype != torch.float32:
             self.shadow = torch.zeros(self.total, dtype=self.compute_dtype, device=self.device)
         if init:
@@ -431,7 +420,12 @@ class VariableStore:
         return f["buf"][off:off + v.numel].view(shape)
 
     def zero_grad(self) -> None:
-        self._grad_ext.zero_()
+        """Clear the gradients before a backward.  Skipped when the previous optimizer launch already
+        cleared them in its pass (``Optimizer.apply_gradients(zero_grad=True)`` sets ``grads_clean``):
+        the graphed training step then holds no separate fill."""
+        if not self.grads_clean:
+            self.grad.zero_()
+        self.grads_clean = False  # the caller is about to accumulate into them
         self.grad_epoch += 1
 
     def trainable(self) -> List[Variable]:

@@ -134,95 +134,3 @@ def test_persistent_pointwise_forward_matches_per_tile_kernel(gpu, shape):
         assert _rel(yb, res[0][0]) < 2e-3 and _rel(y, res[0][2]) < 2e-3
         assert _rel(save[:Ko], res[0][1][:Ko]) < 1e-4 and _rel(save[Ko:2 * Ko], res[0][1][Ko:2 * Ko]) < 1e-4
         assert _rel(save[:Ko], mean_r) < 2e-2
-
-
-# the stage 2-4 conv3 shapes (1x1 expand, input = the plain ReLU BN2 output) at batch 256 and 128
-BNA_SHAPES = [(B, hw, hw, c, 4 * c) for B in (256, 128) for hw, c in ((16, 128), (8, 256), (4, 512))]
-
-
-@pytest.mark.parametrize("form", [1, 2], ids=["registers", "in_lds"])
-@pytest.mark.parametrize("shape", BNA_SHAPES, ids=["%dx%dx%d_c%d_k%d" % s for s in BNA_SHAPES])
-def test_bn_on_load_wide_pointwise_forward(gpu, shape, form):
-    """conv_fwd_bn_in beyond one k-tile (the persistent kernel's A-operand BN transform): the conv of
-    relu(x * scale + shift) against fp32, and its fused statistics against the same conv run on the
-    materialised BN output (bn_apply_train + conv_fwd_bn)."""
-    N, H, W, C, Ko = shape
-    assert torch.ops.tfx.conv_fwd_bn_in_supported(N * H * W, Ko, C)
-    g = torch.Generator(device=gpu).manual_seed(11 + C)
-    x = _bf(torch.randn(N, H, W, C, device=gpu, generator=g) * 1.3 + 0.2)
-    w = _bf(torch.randn(Ko, 1, 1, C, device=gpu, generator=g) * (1.0 / math.sqrt(C)))
-    # an input BN's [mean | invstd | scale | shift]
-    sc = torch.rand(C, device=gpu, generator=g) + 0.5
-    sh = torch.randn(C, device=gpu, generator=g) * 0.5
-    in_save = torch.cat([torch.zeros(C, device=gpu), torch.ones(C, device=gpu), sc, sh]).contiguous()
-    a_ref = torch.relu(x.float() * sc + sh)
-    yr = torch.einsum("nhwc,kc->nhwk", _bf(a_ref).float(), w.float().reshape(Ko, C))
-    gamma = torch.rand(Ko, device=gpu, generator=g) + 0.5
-    beta = torch.randn(Ko, device=gpu, generator=g)
-    ws = torch.zeros(64 * 2 * Ko + 64, device=gpu)
-    prev = torch.ops.tfx.igemm_bna_mode(form)  # 1: transform after each fragment read, 2: in-LDS pass
-    try:
-        y, save = torch.ops.tfx.conv_fwd_bn_in(x, in_save, w, ws, gamma, beta, None, None, 0.1, 1e-5)
-    finally:
-        torch.ops.tfx.igemm_bna_mode(prev)
-    ws2 = torch.zeros_like(ws)
-    a_mat = torch.ops.tfx.bn_apply_train(x, None, in_save, True)[0]
-    y2, save2 = torch.ops.tfx.conv_fwd_bn(a_mat, w, 1, 0, 1, ws2, gamma, beta, None, None, 0.1, 1e-5)
-    torch.cuda.synchronize()
-    assert _rel(y, yr) < 1e-2
-    assert _rel(y, y2) < 2e-3  # same bf16 A operand, summation order only
-    assert _rel(save[:2 * Ko], save2[:2 * Ko]) < 1e-3
-    assert float(ws[:64 * 2 * Ko].abs().max()) == 0.0, "statistics slots left dirty"
-
-
-# the 1x1 stride-1 data gradients the persistent kernel takes (>= 4 128x64 tiles per CU, K >= 128)
-PW_DGRAD = [s for s in SHAPES if s[5] == 1 and s[6] == 1 and s[4] >= 128 and s[3] % 64 == 0 and
-            (s[0] * s[1] * s[2] // 128) * (s[3] // 64) >= 1024]
-
-
-@pytest.mark.parametrize("variant", ["addend_masked", "addend", "plain_relu_recomputed"])
-@pytest.mark.parametrize("shape", PW_DGRAD, ids=[_ids(s) for s in PW_DGRAD])
-def test_persistent_fused_bn_dgrad_matches_per_tile_kernel(gpu, shape, variant):
-    """The persistent 1x1 fused-BN data gradient (igemm_persist.hip EPI_BNB: MN-major W, the residual
-    addend and its ReLU mask bits summed in, the BN-backward partials of the input BN with the mask
-    from the BN's bits or recomputed from x) against the one-tile-per-block kernel and fp32."""
-    N, H, W, C, Ko, R, st = shape
-    g = torch.Generator(device=gpu).manual_seed(3 + C + Ko)
-    M = N * H * W
-    gy = _bf(torch.randn(N, H, W, Ko, device=gpu, generator=g))
-    w = _bf(torch.randn(Ko, 1, 1, C, device=gpu, generator=g) * (1.0 / math.sqrt(Ko)))
-    bx = _bf(torch.randn(N, H, W, C, device=gpu, generator=g) * 1.2 + 0.1)
-    mean, inv = torch.randn(C, device=gpu, generator=g) * 0.1, torch.rand(C, device=gpu, generator=g) + 0.5
-    gam, bet = torch.rand(C, device=gpu, generator=g) + 0.5, torch.randn(C, device=gpu, generator=g) * 0.3
-    save = torch.cat([mean, inv, gam * inv, bet - mean * inv * gam]).contiguous()
-    add = _bf(torch.randn(N, H, W, C, device=gpu, generator=g)) if variant != "plain_relu_recomputed" else None
-    amask = (torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device=gpu, generator=g)
-             if variant == "addend_masked" else None)
-    bmask = (torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device=gpu, generator=g)
-             if variant != "plain_relu_recomputed" else None)
-    res = {}
-    prev = torch.ops.tfx.igemm_persist_dgrad(0)  # opt-in path (slower than the per-tile kernel)
-    try:
-        for mode in (0, 2):
-            torch.ops.tfx.igemm_persist_dgrad(1 if mode else 0)
-            ws = torch.zeros(64 * 2 * C + 64, device=gpu)
-            a_in = add.clone() if add is not None else None  # an unmasked addend is summed in place
-            dx, red = torch.ops.tfx.conv_dgrad_bn(gy, w, [N, H, W, C], 1, 0, 1, a_in, bx, save, bmask, True, ws,
-                                                  None, None, amask, True, False, None)
-            torch.cuda.synchronize()
-            assert float(ws[:64 * 2 * C].abs().max()) == 0.0, "BN slots left dirty"
-            res[mode] = (dx.clone(), red.clone())
-    finally:
-        torch.ops.tfx.igemm_persist_dgrad(prev)
-    # fp32 reference of the stored gradient
-    ref = torch.einsum("nhwk,kc->nhwc", gy.float(), w.float().reshape(Ko, C))
-    if add is not None:
-        af = add.float()
-        if amask is not None:
-            bits = ((amask.reshape(-1, 1) >> torch.arange(8, device=gpu, dtype=torch.uint8)) & 1).reshape(N, H, W, C)
-            af = af * bits.float()
-        ref = ref + af
-    dx2, red2 = res[2]
-    assert _rel(dx2, ref) < 1e-2
-    assert _rel(dx2, res[0][0]) < 2e-3
-    assert _rel(red2, res[0][1]) < 2e-3

@@ -106,8 +106,8 @@ def test_resnet_cifar_example_dp2(tmp_path):
     first = ckpt.latest_checkpoint(str(tmp_path))
     mg = ckpt.read_meta_graph(first)
     assert len(mg["trainable_variables"]) > 50 and mg["saver"]["version"] == 2
-    # resume: the second run restores the checkpoint and continues from its global step
-    out2 = _torchrun("resnet_cifar.py", 2, "--depth=18", "--batch_size=8", "--max_steps=2", "--synthetic_train=256",
+    # resume: the second run restores the checkpoint and trains up to the ABSOLUTE --max_steps
+    out2 = _torchrun("resnet_cifar.py", 2, "--depth=18", "--batch_size=8", "--max_steps=4", "--synthetic_train=256",
                      "--eval_examples=100", f"--logdir={tmp_path}", f"--export_dir={tmp_path / 'export'}")
     second = ckpt.latest_checkpoint(str(tmp_path))
     assert int(first.rsplit("-", 1)[1]) == 2 and int(second.rsplit("-", 1)[1]) == 4, (first, second, out2[-500:])

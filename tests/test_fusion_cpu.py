@@ -1,6 +1,5 @@
-"""The fusion-plan module (ops/fusion.py) and the gradient-zeroed store scratch, on the CPU: profile
-parsing, switching groups on and off (and restoring them), the opt-in group staying out of the default
-profile, the plan recorder's table, and VariableStore.reserve_scratch / zero_grad / grad_epoch."""
+"""The fusion-plan module (ops/fusion.py) on the CPU: profile parsing, switching groups on and off (and
+restoring them), the plan recorder's table, and VariableStore.zero_grad's fused-clear bookkeeping."""
 import pytest
 import torch
 
@@ -13,8 +12,8 @@ def test_profiles_parse():
     assert fusion.parse_profile("all") == fusion.PROFILES["all"]
     assert fusion.parse_profile("") == fusion.PROFILES["all"]
     assert fusion.parse_profile("none") == set()
-    assert "bn_finalize_fold" not in fusion.PROFILES["all"]  # opt-in (profiles/r04_fold)
-    assert fusion.parse_profile("+bn_finalize_fold") == fusion.PROFILES["all"] | {"bn_finalize_fold"}
+    assert fusion.PROFILES["all"] == set(fusion.GROUPS)
+    assert fusion.parse_profile("-head_tail,+head_tail") == fusion.PROFILES["all"]
     assert fusion.parse_profile("-head_tail,-bn_on_load") == fusion.PROFILES["all"] - {"head_tail", "bn_on_load"}
     assert fusion.PROFILES["r2"] <= fusion.PROFILES["all"]
     with pytest.raises(ValueError):
@@ -28,9 +27,9 @@ def test_set_groups_and_restore():
         on = fusion.enabled()
         assert {g for g, v in on.items() if v} == fusion.PROFILES["r2"]
         assert fusion.knob("defer_tail") is False and fusion.knob("fuse_head") is True
-        assert fusion.knob("fold_fin") is False
+        assert fusion.knob("lazy_bn_bwd") is False
         fusion.set_groups(set(fusion.GROUPS))
-        assert all(fusion.enabled().values()) and fusion.knob("fold_fin") is True
+        assert all(fusion.enabled().values()) and fusion.knob("lazy_bn_bwd") is True
     finally:
         fusion.restore(prev)
     assert fusion.enabled() == prev
@@ -51,37 +50,43 @@ def test_recorder_table():
     assert plan["fused_head"] == [("fc", "head_xent")]
 
 
-def test_store_scratch_zeroed_with_grads():
+def test_zero_grad_skips_fill_only_after_a_fused_clear():
+    """VariableStore.zero_grad fills the gradients unless the buffer is known clean: fresh, or cleared by
+    the optimizer kernel (Optimizer.apply_gradients(zero_grad=True) sets grads_clean on the GPU path).
+    A backward in between always leaves the flag false, so a stale gradient is never kept."""
     st = VariableStore(device="cpu", seed=0)
     st.variable([10], Zeros(), name="w")
-    off = st.reserve_scratch(100)
-    off2 = st.reserve_scratch(7)
-    assert off == 0 and off2 >= 100
     st.finalize()
-    assert st.scratch is not None and st.scratch.numel() >= off2 + 7
-    assert st.grad.numel() == st.total and st.grad.data_ptr() == st._grad_ext.data_ptr()
-    st.scratch.fill_(3.0)
-    st.grad.fill_(2.0)
+    assert st.grads_clean  # a fresh buffer is all zeros
     e0 = st.grad_epoch
     st.zero_grad()
-    assert st.grad_epoch == e0 + 1
-    assert float(st.scratch.abs().max()) == 0.0 and float(st.grad.abs().max()) == 0.0
-    with pytest.raises(RuntimeError):
-        st.reserve_scratch(4)  # after finalize
+    assert st.grad_epoch == e0 + 1 and not st.grads_clean
+    st.grad.fill_(2.0)  # a backward accumulates
+    st.zero_grad()  # not clean: filled
+    assert float(st.grad.abs().max()) == 0.0
+    st.grad.fill_(2.0)
+    st.grads_clean = True  # what the fused optimizer clear reports -- trusted: no fill
+    st.zero_grad()
+    assert float(st.grad.abs().max()) == 2.0 and not st.grads_clean
 
 
-def test_bn_workspace_rows_once_per_step():
-    st = VariableStore(device="cpu", seed=0)
-    ws = tnn.BNWorkspace(8, st)
-    st.variable([4], Zeros(), name="w")
-    st.finalize()
-    st.zero_grad()
-    r1 = ws.fin_rows()
-    assert r1 is not None and r1.numel() == tnn.BNWorkspace.FIN_ROWS * 2 * 8
-    assert ws.fin_rows() is None  # used already this step: the caller falls back to the finalize launch
-    st.zero_grad()
-    assert ws.fin_rows() is not None
-    assert tnn.BNWorkspace(8).fin_rows() is None  # no store: no scratch
+def test_restore_needs_complete_state():
+    """fusion.restore takes only a complete knob dict or a complete group dict: masked_res, s2_addend and
+    lazy_bn_bwd are both knob and group names, so a partial dict would be ambiguous."""
+    prev = fusion.knobs()
+    try:
+        fusion.set_groups(fusion.PROFILES["r2"])
+        for bad in ({}, {"lazy_bn_bwd": True}, {"masked_res": False, "s2_addend": True}):
+            with pytest.raises(ValueError):
+                fusion.restore(bad)
+        assert {g for g, v in fusion.enabled().items() if v} == fusion.PROFILES["r2"]  # untouched
+        fusion.restore(prev)  # complete knob dict
+        assert fusion.knobs() == prev
+        fusion.set_groups(set())
+        fusion.restore({g: True for g in fusion.GROUPS})  # complete group dict
+        assert all(fusion.enabled().values())
+    finally:
+        fusion.restore_knobs(prev)
 
 
 # the fused-group table of tests/test_resnet50_train_gpu.py::test_resnet50_fusion_plan (the GPU step's
