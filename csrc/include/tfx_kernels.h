@@ -118,7 +118,6 @@ struct IgemmArgs {
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s);
 // persistent 1x1-forward mode (igemm_persist.hip): 0 off, 2 / 3 ring depth; returns the previous mode
 int igemm_persist_set(int mode);
-int igemm_probe_set(int v);  // TEMPORARY cost probe (igemm.hip)
 
 // ---------------------------------------------------------------- fused pointwise-conv backward (pw_bwd.hip)
 // Backward of a bottleneck's expanding 1x1 conv (CN -> CW = 4 CN) fused with the block-tail BN's

@@ -99,18 +99,7 @@ int igemm_tune_traced(int* out, int cap) {
   return n;
 }
 
-// TEMPORARY cost probe (round 6): bit 0 = the A operand reads nothing (zero-extent resource: every A
-// load returns zeros without a memory access), bit 1 = the same for B
-int g_probe_io = 0;
-int igemm_probe_set(int v) {
-  const int p = g_probe_io;
-  g_probe_io = v;
-  return p;
-}
-
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s) {
-  if (g_probe_io & 1) a.a_bytes = 0;
-  if (g_probe_io & 2) a.b_bytes = 0;
   if (a.out_mode == OUT_F32_ATOMIC && a.zero_out) {
     const size_t rows = a.trans_out ? a.N : a.M;
     TFX_HIP_CHECK(hipMemsetAsync(a.Cp, 0, sizeof(float) * rows * a.ldc, s));

@@ -1854,7 +1854,6 @@ TORCH_LIBRARY(tfx, m) {
   m.def("accuracy_count", &accuracy_count);
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
-  m.def("igemm_probe", [](int64_t v) -> int64_t { return tfx::igemm_probe_set((int)v); });
   m.def("optimizer_apply", &optimizer_apply);
   m.def("lstm_seq_residency", &lstm_seq_residency);
   m.def("affine_fwd", &affine_fwd);

@@ -98,7 +98,7 @@ class LMTrainer:
         # while it is set: a timed-out hand-off never reaches the weights)
         dev = self.store.master.device
         guard = rnn_ops.health_word(dev) if dev.type == "cuda" else None
-        if guard is not None and self.dp is not None:
+        if guard is not None and self.dp is not None and getattr(self.dp, "world", 1) > 1:
             # every rank skips together: a failed rank's gradient is inside everyone's all-reduced sum
             # (a 4-byte MAX on the DP group, stream-ordered: no host sync)
             import torch.distributed as dist
