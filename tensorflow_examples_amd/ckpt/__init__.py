@@ -1,19 +1,24 @@
-"""Checkpoints with TF1's on-disk LAYOUT and our own container format.
+"""Checkpoints in TF1's on-disk layout AND TF's V2 tensor-bundle format.
 
 ``Saver.save(store, "<dir>/model.ckpt", global_step=N)`` writes::
 
     <dir>/checkpoint                          text: model_checkpoint_path / all_model_checkpoint_paths
-    <dir>/model.ckpt-N.index                  JSON index: name -> dtype, shape, crc32c (format tfx-ckpt-v1)
-    <dir>/model.ckpt-N.data-00000-of-00001    safetensors container with every tensor (f32)
+    <dir>/model.ckpt-N.index                  SSTable of BundleEntryProto (dtype, shape, offset, size, crc32c)
+    <dir>/model.ckpt-N.data-00000-of-00001    the raw little-endian tensor bytes
     <dir>/model.ckpt-N.meta                   MetaGraphDef protobuf (graph_def, saver_def, collections)
     <dir>/graph.pbtxt                         text GraphDef (write_graph; TF1's Supervisor writes it)
 
-Variables keep their TF names (``global_step``, ``weights/Variable``, ``biases/Variable_1``, ...).
-The data file is safetensors (loaded with the safe loader, nothing executable); CRC32C of every
-tensor is verified on restore.  ``.meta`` is a binary MetaGraphDef encoded by ``summary.meta_graph_def``:
-the graph (one ``VariableV2`` node per variable unless the caller passes the model's nodes), TF1's
-default SaverDef, the ``variables`` / ``trainable_variables`` collections (serialized VariableDefs)
-and a ``tfx_meta`` collection holding the caller's metadata as JSON; ``read_meta_graph`` parses it.  ``export_saved_model`` writes the SavedModel-shaped directory
+The ``.index`` / ``.data`` pair is TensorFlow's tensor bundle (``ckpt/bundle.py``: LevelDB-format table,
+BundleHeaderProto under the empty key, masked CRC32C per tensor and per table block).  The round-1..5
+container (JSON index + safetensors data) is still written with ``TFX_CKPT_FORMAT=safetensors`` (or
+``Saver(fmt="safetensors")``) and read either way: the reader tells them apart by the index's bytes.
+Variables keep their TF names (``global_step``, ``weights/Variable``, ``biases/Variable_1``, ...);
+CRC32C of every tensor is verified on restore.  ``.meta`` is a binary MetaGraphDef encoded by
+``summary.meta_graph_def``: the graph -- one ``VariableV2`` node per variable with its ``dtype`` /
+``shape`` attrs, its ``/read`` and ``/Assign`` nodes, and the ``save/*`` ops the SaverDef names
+(:func:`saver_graph_nodes`) -- TF1's default SaverDef, the ``variables`` / ``trainable_variables``
+collections (serialized VariableDefs) and a ``tfx_meta`` collection holding the caller's metadata as
+JSON; ``read_meta_graph`` parses it.  ``export_saved_model`` writes the SavedModel-shaped directory
 ``saved_model.pb`` + ``variables/variables.{index,data-00000-of-00001}``; ``saved_model.pb`` is a SavedModel
 protobuf (one MetaGraphDef tagged ``serve`` with the graph, SaverDef, variable collections and the serving
 SignatureDefs; ``read_saved_model`` parses it).
@@ -32,8 +37,10 @@ import torch
 from safetensors.torch import load_file, save_file
 
 from .. import runtime, summary
+from . import bundle
 
-FORMAT = "tfx-ckpt-v1"
+FORMAT = "tfx-ckpt-v1"  # the JSON + safetensors container (opt-in)
+DEFAULT_FORMAT = os.environ.get("TFX_CKPT_FORMAT", "tf")  # "tf" = tensor bundle, "safetensors"
 SM_MAGIC = b"TFXSM001"
 
 
@@ -45,25 +52,85 @@ def _default_nodes(names: List[str]) -> List[Dict]:
     return [{"name": n, "op": "VariableV2", "inputs": [], "device": ""} for n in names]
 
 
+def saver_graph_nodes(tensors: Dict[str, torch.Tensor], var_nodes: Optional[List[Dict]] = None) -> List[Dict]:
+    """The GraphDef nodes of TF1's default (V2, non-sharded) Saver over ``tensors`` -- what the SaverDef's
+    ``save/Const:0`` / ``save/control_dependency:0`` / ``save/restore_all`` name -- plus each variable's
+    ``VariableV2`` (dtype / shape attrs), ``<v>/read`` (Identity) and ``<v>/Assign`` nodes (the names its
+    VariableDef refers to).  ``var_nodes``: the caller's variable nodes (device placement kept)."""
+    names = sorted(tensors)
+    dev = {n["name"]: n.get("device", "") for n in (var_nodes or [])}
+    dts = {k: bundle._TORCH_DT[v.dtype] for k, v in tensors.items()}
+    nodes = []
+    for n in names:
+        d = dev.get(n, "")
+        t = dts[n]
+        nodes.append({"name": n, "op": "VariableV2", "inputs": [], "device": d,
+                      "attrs": {"dtype": summary.attr_type(t), "shape": summary.attr_shape(tensors[n].shape),
+                                "container": summary.attr_str(""), "shared_name": summary.attr_str("")}})
+        nodes.append({"name": n + "/read", "op": "Identity", "inputs": [n], "device": d,
+                      "attrs": {"T": summary.attr_type(t), "_class": summary.attr_str_list(["loc:@" + n])}})
+        nodes.append({"name": n + "/Assign", "op": "Assign", "inputs": [n, n + "/initial_value"], "device": d,
+                      "attrs": {"T": summary.attr_type(t), "use_locking": summary.attr_bool(True),
+                                "validate_shape": summary.attr_bool(True),
+                                "_class": summary.attr_str_list(["loc:@" + n])}})
+    str_attr = {"dtype": summary.attr_type(7)}
+    nodes.append({"name": "save/Const", "op": "Const", "inputs": [],
+                  "attrs": dict(str_attr, value=summary.attr_string_tensor(["model"]))})
+    for op in ("SaveV2", "RestoreV2"):
+        nodes.append({"name": "save/%s/tensor_names" % op, "op": "Const", "inputs": [],
+                      "attrs": dict(str_attr, value=summary.attr_string_tensor(names, [len(names)]))})
+        nodes.append({"name": "save/%s/shape_and_slices" % op, "op": "Const", "inputs": [],
+                      "attrs": dict(str_attr, value=summary.attr_string_tensor([""] * len(names), [len(names)]))})
+    types = summary.attr_type_list([dts[n] for n in names])
+    nodes.append({"name": "save/SaveV2", "op": "SaveV2",
+                  "inputs": ["save/Const", "save/SaveV2/tensor_names", "save/SaveV2/shape_and_slices", *names],
+                  "attrs": {"dtypes": types}})
+    nodes.append({"name": "save/control_dependency", "op": "Identity", "inputs": ["save/Const", "^save/SaveV2"],
+                  "attrs": {"T": summary.attr_type(7), "_class": summary.attr_str_list(["loc:@save/Const"])}})
+    nodes.append({"name": "save/RestoreV2", "op": "RestoreV2",
+                  "inputs": ["save/Const", "save/RestoreV2/tensor_names", "save/RestoreV2/shape_and_slices"],
+                  "attrs": {"dtypes": types}})
+    assigns = []
+    for i, n in enumerate(names):
+        an = "save/Assign" if i == 0 else "save/Assign_%d" % i
+        assigns.append(an)
+        nodes.append({"name": an, "op": "Assign", "inputs": [n, "save/RestoreV2:%d" % i if i else "save/RestoreV2"],
+                      "attrs": {"T": summary.attr_type(dts[n]), "use_locking": summary.attr_bool(True),
+                                "validate_shape": summary.attr_bool(True),
+                                "_class": summary.attr_str_list(["loc:@" + n])}})
+    nodes.append({"name": "save/restore_all", "op": "NoOp", "inputs": ["^" + a for a in assigns]})
+    return nodes
+
+
 def _write_tensors(prefix: str, tensors: Dict[str, torch.Tensor], meta: Optional[dict],
                    graph_nodes: Optional[List[Dict]] = None, trainable: Optional[Dict[str, bool]] = None,
-                   max_to_keep: int = 5) -> None:
+                   max_to_keep: int = 5, fmt: Optional[str] = None) -> None:
     cpu = {k: v.detach().cpu().contiguous() for k, v in tensors.items()}
-    save_file(cpu, prefix + ".data-00000-of-00001", metadata={"format": FORMAT})
-    index = {"format": FORMAT, "num_shards": 1,
-             "tensors": {k: {"dtype": str(v.dtype).replace("torch.", ""), "shape": list(v.shape), "crc32c": _crc(v)}
-                         for k, v in cpu.items()}}
-    with open(prefix + ".index", "w") as f:
-        json.dump(index, f, indent=1, sort_keys=True)
+    fmt = fmt or DEFAULT_FORMAT
+    if fmt == "safetensors":
+        save_file(cpu, prefix + ".data-00000-of-00001", metadata={"format": FORMAT})
+        index = {"format": FORMAT, "num_shards": 1,
+                 "tensors": {k: {"dtype": str(v.dtype).replace("torch.", ""), "shape": list(v.shape), "crc32c": _crc(v)}
+                             for k, v in cpu.items()}}
+        with open(prefix + ".index", "w") as f:
+            json.dump(index, f, indent=1, sort_keys=True)
+    elif fmt == "tf":
+        bundle.write_bundle(prefix, cpu)
+    else:
+        raise ValueError("checkpoint format %r (tf | safetensors)" % fmt)
     names = sorted(cpu)
     trainable = trainable or {}
-    nodes = graph_nodes if graph_nodes is not None else _default_nodes(names)
+    nodes = saver_graph_nodes(cpu, graph_nodes)
+    if graph_nodes is not None:  # the caller's non-variable nodes too (the model graph)
+        have = {n["name"] for n in nodes}
+        nodes = [n for n in graph_nodes if n["name"] not in have] + nodes
     tr = [n for n in names if trainable.get(n, False)]
     body = summary.meta_graph_def(
         summary.graph_def(nodes), saver=summary.saver_def(max_to_keep),
         collections={"variables": [summary.variable_def(n, trainable.get(n, False)) for n in names],
                      "trainable_variables": [summary.variable_def(n, True) for n in tr],
-                     "tfx_meta": [json.dumps({"format": FORMAT, "meta": meta or {}, "time": time.time()}).encode()]})
+                     "tfx_meta": [json.dumps({"format": FORMAT if fmt == "safetensors" else "tf-tensor-bundle",
+                                              "meta": meta or {}, "time": time.time()}).encode()]})
     with open(prefix + ".meta", "wb") as f:
         f.write(body)
 
@@ -108,6 +175,9 @@ def store_graph_nodes(store, device_of=lambda name: "") -> List[Dict]:
 
 
 def read_checkpoint(prefix: str, verify: bool = True) -> Dict[str, torch.Tensor]:
+    """Every tensor of a checkpoint, CRC-checked: TF's tensor bundle or the JSON + safetensors container."""
+    if bundle.is_bundle_index(prefix + ".index"):
+        return bundle.read_bundle(prefix, verify)
     with open(prefix + ".index") as f:
         index = json.load(f)
     if index.get("format") != FORMAT:
@@ -121,8 +191,9 @@ def read_checkpoint(prefix: str, verify: bool = True) -> Dict[str, torch.Tensor]
 
 
 class Saver:
-    def __init__(self, max_to_keep: int = 5):
+    def __init__(self, max_to_keep: int = 5, fmt: Optional[str] = None):
         self.max_to_keep = max_to_keep
+        self.fmt = fmt  # None = DEFAULT_FORMAT ("tf" tensor bundle unless TFX_CKPT_FORMAT says otherwise)
         self._kept: List[str] = []
 
     def save(self, store, save_path: str, global_step: Optional[int] = None, extra: Optional[Dict] = None,
@@ -136,7 +207,7 @@ class Saver:
         for k, v in (extra or {}).items():
             tensors[k] = torch.as_tensor(v)
         trainable = {v.name: bool(v.trainable) for v in getattr(store, "vars", [])}
-        _write_tensors(prefix, tensors, meta, graph_nodes, trainable, self.max_to_keep)
+        _write_tensors(prefix, tensors, meta, graph_nodes, trainable, self.max_to_keep, self.fmt)
         self._kept = [p for p in _read_state(d) if p != prefix] + [prefix]
         while self.max_to_keep and len(self._kept) > self.max_to_keep:
             old = self._kept.pop(0)
@@ -198,7 +269,7 @@ def export_saved_model(store, export_dir: str, signature: Optional[dict] = None,
                        tags=("serve",)) -> str:
     """The SavedModel directory layout: ``saved_model.pb`` -- a SavedModel protobuf (schema version 1, one
     MetaGraphDef tagged ``tags`` with the graph, TF1's default SaverDef, the variable collections and the
-    serving ``signature_defs``) -- and ``variables/variables.{index,data-00000-of-00001}`` (our container).
+    serving ``signature_defs``) -- and ``variables/variables.{index,data-00000-of-00001}`` (the tensor bundle).
     ``signature_defs``: {key: {"inputs": {name: (tensor, dtype, shape)}, "outputs": {...},
     "method_name": ...}}; ``signature`` is free-form caller metadata kept in the ``tfx_meta`` collection."""
     os.makedirs(os.path.join(export_dir, "variables"), exist_ok=True)
@@ -214,8 +285,11 @@ def export_saved_model(store, export_dir: str, signature: Optional[dict] = None,
         sigs[key] = summary.signature_def(ins, outs, d.get("method_name", "tensorflow/serving/predict"))
     meta = {"format": FORMAT, "signature": signature or {},
             "variables": [{"name": v.name, "shape": list(v.shape)} for v in store.vars]}
+    cpu = {k: v.detach().cpu() for k, v in values.items()}
+    sv = saver_graph_nodes(cpu, nodes)
+    have = {n["name"] for n in sv}
     mg = summary.meta_graph_def(
-        summary.graph_def(nodes), tags=tags, saver=summary.saver_def(),
+        summary.graph_def([n for n in nodes if n["name"] not in have] + sv), tags=tags, saver=summary.saver_def(),
         collections={"variables": [summary.variable_def(n, trainable.get(n, False)) for n in names],
                      "trainable_variables": [summary.variable_def(n, True) for n in names if trainable.get(n)],
                      "tfx_meta": [json.dumps(meta).encode()]},

@@ -73,8 +73,9 @@ def _bytes_field(field: int, data: bytes) -> bytes:
 
 
 def graph_def(nodes: Sequence[Dict]) -> bytes:
-    """Minimal GraphDef: node { name op input* device } + versions { producer }.
-    ``nodes`` = [{"name", "op", "inputs": [...], "device": "..."}]."""
+    """GraphDef: node { name op input* device attr* } + versions { producer }.
+    ``nodes`` = [{"name", "op", "inputs": [...], "device": "...", "attrs": {name: AttrValue bytes}}]
+    (``attrs`` optional: the ``attr_*`` helpers below encode the values)."""
     out = bytearray()
     for n in nodes:
         nd = _bytes_field(1, n["name"].encode()) + _bytes_field(2, n["op"].encode())
@@ -82,6 +83,8 @@ def graph_def(nodes: Sequence[Dict]) -> bytes:
             nd += _bytes_field(3, i.encode())
         if n.get("device"):
             nd += _bytes_field(4, n["device"].encode())
+        for k in sorted(n.get("attrs", {})):  # map<string, AttrValue> attr = 5
+            nd += _bytes_field(5, _bytes_field(1, k.encode()) + _bytes_field(2, n["attrs"][k]))
         out += _bytes_field(1, nd)
     out += _bytes_field(4, b"\x08\x1a")  # versions { producer: 26 }
     return bytes(out)
@@ -91,14 +94,56 @@ def _varint_field(field: int, v: int) -> bytes:
     return _varint(field << 3) + _varint(int(v))
 
 
+# AttrValue encoders (oneof: list 1, s 2, i 3, f 4, b 5, type 6, shape 7, tensor 8)
+def attr_type(dtype: int) -> bytes:
+    return _varint_field(6, dtype)
+
+
+def attr_bool(v: bool) -> bytes:
+    return _varint_field(5, 1 if v else 0)
+
+
+def attr_str(v: str) -> bytes:
+    return _bytes_field(2, v.encode())
+
+
+def attr_shape(shape: Sequence[int]) -> bytes:
+    return _bytes_field(7, b"".join(_bytes_field(2, _varint_field(1, int(d))) for d in shape))
+
+
+def attr_type_list(dtypes: Sequence[int]) -> bytes:
+    return _bytes_field(1, b"".join(_varint_field(6, d) for d in dtypes))
+
+
+def attr_str_list(values: Sequence[str]) -> bytes:
+    return _bytes_field(1, b"".join(_bytes_field(2, v.encode()) for v in values))
+
+
+def attr_string_tensor(values: Sequence[str], shape: Optional[Sequence[int]] = None) -> bytes:
+    """A DT_STRING TensorProto {dtype 7, tensor_shape, string_val*} as an AttrValue (a Const's value)."""
+    shp = b"".join(_bytes_field(2, _varint_field(1, int(d))) for d in (shape if shape is not None else []))
+    t = _varint_field(1, 7) + _bytes_field(2, shp) + b"".join(_bytes_field(8, v.encode()) for v in values)
+    return _bytes_field(8, t)
+
+
+def parse_node_attrs(node_bytes: bytes) -> Dict[str, Dict[int, list]]:
+    """A NodeDef's attr map as {name: parsed AttrValue fields}."""
+    out = {}
+    for eb in _parse(bytes(node_bytes)).get(5, []):
+        e = _parse(eb)
+        out[e[1][0].decode()] = _parse(e.get(2, [b""])[0])
+    return out
+
+
 def saver_def(max_to_keep: int = 5, sharded: bool = False) -> bytes:
     """SaverDef { filename_tensor_name, save_tensor_name, restore_op_name, max_to_keep, [sharded],
     keep_checkpoint_every_n_hours, version: V2 } with the names TF1's default (non-sharded) Saver uses --
     the one the Supervisor builds; ``sharded`` is written only when set (proto3 default false).
 
-    The ``.meta`` / ``saved_model.pb`` these go into are STRUCTURAL protobufs (field numbers and names of
-    TF1's MetaGraphDef / SavedModel, read back by this package's own parsers): their GraphDef nodes carry
-    no dtype/shape attrs and no ``save/*`` ops, so TensorFlow itself could not import them as graphs."""
+    The checkpoint ``.meta`` graph carries the ops this SaverDef names (``ckpt.saver_graph_nodes``:
+    ``save/Const``, ``save/SaveV2``, ``save/control_dependency``, ``save/RestoreV2``, one ``save/Assign*`` per
+    variable, ``save/restore_all``) and its VariableV2 nodes their dtype / shape attrs.  Whether TensorFlow
+    imports these bytes is unpinned here (TF is not importable); this package's parsers read them back."""
     return (_bytes_field(1, b"save/Const:0") + _bytes_field(2, b"save/control_dependency:0") +
             _bytes_field(3, b"save/restore_all") + _varint_field(4, max_to_keep) +
             (_varint_field(5, 1) if sharded else b"") + b"\x35" + struct.pack("<f", 10000.0) + _varint_field(7, 2))
@@ -197,7 +242,7 @@ def parse_graph_def(b: bytes) -> List[Dict]:
         f = _parse(nb)
         nodes.append({"name": f[1][0].decode(), "op": f.get(2, [b""])[0].decode(),
                       "inputs": [i.decode() for i in f.get(3, [])],
-                      "device": f.get(4, [b""])[0].decode()})
+                      "device": f.get(4, [b""])[0].decode(), "attrs": parse_node_attrs(nb)})
     return nodes
 
 

@@ -106,7 +106,23 @@ def test_meta_is_metagraphdef_and_graph_pbtxt(tmp_path):
     back = ckpt.read_graph(gp)
     assert [(n["name"], n["op"], n["inputs"], n["device"]) for n in back] == \
         [(n["name"], n["op"], n["inputs"], n["device"]) for n in nodes]
-    assert summary.parse_graph_def(summary.graph_def(nodes)) == back
+    assert [{k: n[k] for k in ("name", "op", "inputs", "device")} for n in
+            summary.parse_graph_def(summary.graph_def(nodes))] == back
+    # the .meta graph: the caller's model nodes, then TF1's default-Saver ops the SaverDef names, and every
+    # variable a VariableV2 with dtype / shape attrs (+ its /read and /Assign)
+    for v in a.vars:
+        an = by[v.name]["attrs"]
+        assert an["dtype"][6] == [1] and summary.parse_graph_def(b"") == []
+        from tensorflow_examples_amd.ckpt import bundle
+        assert bundle.parse_shape_proto(an["shape"][7][0]) == list(v.shape)
+        assert by[v.name + "/read"]["op"] == "Identity" and by[v.name + "/Assign"]["op"] == "Assign"
+    saved = sorted(ckpt.read_checkpoint(p))
+    assert by["save/Const"]["op"] == "Const"
+    assert by["save/SaveV2"]["inputs"][3:] == saved and by["save/RestoreV2"]["op"] == "RestoreV2"
+    assert by["save/control_dependency"]["inputs"] == ["save/Const", "^save/SaveV2"]
+    restores = [i[1:] for i in by["save/restore_all"]["inputs"]]
+    assert len(restores) == len(saved) and all(by[r]["op"] == "Assign" for r in restores)
+    assert [by[r]["inputs"][0] for r in restores] == saved
 
 
 def test_supervisor_writes_graph_pbtxt(tmp_path):
@@ -129,8 +145,70 @@ def test_supervisor_writes_graph_pbtxt(tmp_path):
     sv.prepare_or_wait_for_session()
     assert ckpt.read_graph(os.path.join(str(tmp_path), "graph.pbtxt")) == nodes
     p = sv.save(11)
-    assert ckpt.read_meta_graph(p)["nodes"] == nodes
+    got = {n["name"]: n for n in ckpt.read_meta_graph(p)["nodes"]}
+    assert got["weights/Variable"]["device"] == "/job:ps/task:0" and "save/restore_all" in got
     # a restarted chief restores instead of re-initialising
     sv2 = Supervisor(True, _Client(_store(7)), logdir=str(tmp_path))
     sv2.prepare_or_wait_for_session()
     assert sv2.restored_from == p and torch.equal(sv2.client.store.master, st.master)
+
+
+def test_tensor_bundle_format(tmp_path):
+    """The default checkpoint is TF's V2 tensor bundle: the .index is an SSTable (footer magic, blocks with
+    masked-CRC32C trailers, several data blocks once the entries pass 4 KB) whose empty key holds the
+    BundleHeaderProto and every other key a BundleEntryProto {dtype, shape, offset, size, crc32c} into the
+    raw .data shard.  Parity with TensorFlow's own reader is unpinned (TF is not importable here)."""
+    from tensorflow_examples_amd.ckpt import bundle
+    g = torch.Generator().manual_seed(0)
+    t = {"scope_%03d/w" % i: torch.randn(3, i + 1, generator=g) for i in range(150)}  # > 4 KB of index
+    t["global_step"] = torch.tensor(42.0)
+    t["embedding/bf16"] = torch.randn(5, 4, generator=g).to(torch.bfloat16)
+    t["counter"] = torch.tensor([1, 2, 3], dtype=torch.int64)
+    t["mask"] = torch.tensor([True, False])
+    prefix = str(tmp_path / "model.ckpt-42")
+    bundle.write_bundle(prefix, t)
+    raw = open(prefix + ".index", "rb").read()
+    assert raw[-8:] == bundle.TABLE_MAGIC.to_bytes(8, "little")
+    items = bundle.read_sstable(raw)
+    assert items[0][0] == b"" and [k for k, _ in items[1:]] == sorted(k.encode() for k in t)
+    header, entries = bundle.read_bundle_index(prefix)
+    assert header == {"num_shards": 1, "endianness": 0, "version": 1}
+    data = open(prefix + ".data-00000-of-00001", "rb").read()
+    assert sum(e["size"] for e in entries.values()) == len(data)
+    e = entries["embedding/bf16"]
+    assert e["dtype"] == 14 and e["shape"] == [5, 4] and e["size"] == 40
+    assert entries["global_step"]["dtype"] == 1 and entries["global_step"]["shape"] == []
+    assert entries["counter"]["dtype"] == 9 and entries["mask"]["dtype"] == 10
+    back = bundle.read_bundle(prefix)
+    assert set(back) == set(t) and all(torch.equal(back[k], t[k]) for k in t)
+    # the index has several data blocks (the table's 4 KB block size) and each block trailer is checked
+    idx_blocks = bundle._read_block(raw, bundle._handle(*_index_handle(raw)), True)
+    assert len(idx_blocks) >= 2
+    bad = bytearray(raw)
+    bad[10] ^= 0x40  # inside the first data block
+    open(prefix + ".index", "wb").write(bytes(bad))
+    with pytest.raises(ValueError):
+        bundle.read_bundle(prefix)
+
+
+def _index_handle(raw):
+    from tensorflow_examples_amd.ckpt import bundle
+    footer = raw[-48:]
+    _, j = bundle._read_varint(footer, 0)
+    _, j = bundle._read_varint(footer, j)
+    off, j = bundle._read_varint(footer, j)
+    size, _ = bundle._read_varint(footer, j)
+    return off, size
+
+
+def test_saver_formats(tmp_path):
+    """Saver writes the tensor bundle by default and the JSON + safetensors container on request; the reader
+    takes either (and older checkpoints of the latter keep loading)."""
+    from tensorflow_examples_amd.ckpt import bundle
+    a = _store(8)
+    pt = ckpt.Saver().save(a, str(tmp_path / "tf" / "model.ckpt"), global_step=1)
+    ps = ckpt.Saver(fmt="safetensors").save(a, str(tmp_path / "st" / "model.ckpt"), global_step=1)
+    assert bundle.is_bundle_index(pt + ".index") and not bundle.is_bundle_index(ps + ".index")
+    assert open(ps + ".index").read().lstrip().startswith("{")
+    x, y = ckpt.read_checkpoint(pt), ckpt.read_checkpoint(ps)
+    assert set(x) == set(y) and all(torch.equal(x[k], y[k]) for k in x)
