@@ -86,6 +86,48 @@ def run(mode, a, data, w0, negctl=None):
             "nan": any(v != v for v in losses), "seconds": time.time() - t0}
 
 
+def run_dp(a, data, w0, wire="bf16", bucket_mb=32.0):
+    """The fused bf16 run through the data-parallel path: this process is one rank of a process group
+    (RANK / WORLD_SIZE / MASTER_* in the environment; gloo on one GPU in the tests, RCCL on a node).  Each
+    rank trains on its 1/world slice of every batch, the gradients go through GradAllReduce with the
+    ``wire`` format (f32, or the bf16 twin the optimizer reads directly), averaged by grad_scale -- the
+    same update as one process on the whole batch except that each rank's BN statistics cover its slice.
+    Returns the run record with the rank-mean window losses (rank 0: test accuracy)."""
+    import torch.distributed as dist
+    from tensorflow_examples_amd.parallel import GradAllReduce, broadcast_variables, init_distributed
+    dev = init_distributed(backend=os.environ.get("TFX_DP_BACKEND", "gloo"), device="cuda")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    xtr, ytr, xte, yte = data
+    st, m = build_resnet_cifar(device=dev, depth=a.depth, dtype=torch.bfloat16, seed=a.seed, zero_init_residual=True)
+    st.master.copy_(w0.to(dev))
+    st.refresh_shadow()
+    broadcast_variables(st)
+    opt = MomentumOptimizer(st, a.lr, momentum=0.9, weight_decay=a.wd)
+    dp = GradAllReduce(st, bucket_bytes=int(bucket_mb * (1 << 20)), compress_bf16=wire == "bf16")
+    tr = ClassifierTrainer(st, m, opt, dp)
+    half = a.batch // world
+    losses = []
+    t0 = time.time()
+    for i in range(a.steps):
+        opt.set_learning_rate(a.lr * min(1.0, (i + 1) / a.warmup))
+        sl = slice(a.batch * i + half * rank, a.batch * i + half * (rank + 1))
+        losses.append(tr.step(to_model_input(xtr[sl].to(dev)), ytr[sl].to(dev)))
+    lt = torch.stack([l.float() for l in losses]).to(dev)
+    dist.all_reduce(lt)  # the rank-mean loss of every step (= the full-batch loss with per-rank BN)
+    losses = [float(v) / world for v in lt.cpu()]
+    correct = 0.0
+    if rank == 0:
+        with torch.no_grad():
+            for i in range(0, len(xte), 500):
+                xe = to_model_input(xte[i:i + 500].to(dev))
+                correct += float(ops.accuracy(m(xe, training=False), yte[i:i + 500].to(dev))) * len(xe)
+    torch.cuda.synchronize()
+    return {"mode": "fused_dp%d_%s" % (world, wire), "window_loss": window_means(losses),
+            "final_loss50": float(np.mean(losses[-WINDOW:])), "test_accuracy": correct / len(xte),
+            "nan": any(v != v for v in losses), "seconds": time.time() - t0, "rank": rank,
+            "buckets": len(dp.buckets), "wire_used_bf16": dp.reduced_grad is not None}
+
+
 def compare(ref, other, rel_tol, acc_tol):
     rel = [abs(o - r) / r for r, o in zip(ref["window_loss"], other["window_loss"])]
     dacc = abs(other["test_accuracy"] - ref["test_accuracy"])

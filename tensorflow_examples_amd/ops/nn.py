@@ -228,17 +228,33 @@ def _fwd_choice_unplanned(x, w, stride, pad, dil, stats_into, tp) -> str:
 STEM_WGRAD_CALLS = [0]  # stem weight gradients by stem.hip (tests)
 
 
-_STEM_WS = {}
+def _model_state(store) -> dict:
+    """Per-model runtime state of the fused ops (the model's VariableStore ``fused_state``): two models in
+    one process -- a train and an eval model, interleaved runs -- never share a workspace or a pending
+    deferred reduction.  A conv / BN used outside a store (tests of single ops) gets a process-wide dict."""
+    return store.fused_state if store is not None else _NO_STORE_STATE
 
 
-def _stem_ws(device, ko) -> torch.Tensor:
-    """stem.hip's zeroed dW workspace copies (left zero by every launch), one per device."""
-    ws = _STEM_WS.get(device)
-    if ws is None:
-        ws = torch.zeros(int(torch.ops.tfx.stem_wgrad_ws_floats(ko)), dtype=torch.float32, device=device)
-        if not torch.cuda.is_current_stream_capturing():  # never cache a graph-pool tensor (see _head_state)
-            _STEM_WS[device] = ws
-    return ws
+_NO_STORE_STATE: dict = {}
+
+
+def _cached_buffer(store, key, make) -> torch.Tensor:
+    """A persistent per-model device buffer, allocated once OUTSIDE any graph capture when possible: a
+    tensor allocated during a capture lives in that graph's private pool and is never cached (its
+    allocation -- and zero fill -- are then recorded in the graph, so each replay still starts clean)."""
+    st = _model_state(store)
+    t = st.get(key)
+    if t is None:
+        t = make()
+        if not torch.cuda.is_current_stream_capturing():
+            st[key] = t
+    return t
+
+
+def _stem_ws(store, device, ko) -> torch.Tensor:
+    """stem.hip's zeroed dW workspace copies (left zero by every launch), one per model and device."""
+    return _cached_buffer(store, ("stem_ws", str(device), int(ko)), lambda: torch.zeros(
+        int(torch.ops.tfx.stem_wgrad_ws_floats(ko)), dtype=torch.float32, device=device))
 
 
 def _stem_ok(x, w, stride, pad, dil) -> bool:
@@ -460,9 +476,9 @@ class _Conv2d(torch.autograd.Function):
             sink = ctx.sink
             stem_w = (planned == "stem_wgrad") if lp is not None else (fusion.knob("stem_wgrad") and
                                                                         _stem_ok(x, w, stride, pad, dil))
-            if not need_dx and w.trainable and stem_w and not _PENDING_SR:
+            if not need_dx and w.trainable and stem_w and not _pending_sr(w.store):
                 # the CIFAR stem (8 padded input channels, no input gradient): one block per image (stem.hip)
-                torch.ops.tfx.stem_wgrad(gy, x.contiguous(), w.grad, _stem_ws(gy.device, w.shape[0]))
+                torch.ops.tfx.stem_wgrad(gy, x.contiguous(), w.grad, _stem_ws(w.store, gy.device, w.shape[0]))
                 STEM_WGRAD_CALLS[0] += 1
                 fusion.note("stem_kernels", w.name, "stem_wgrad")
                 _grad_ready(w)
@@ -517,9 +533,10 @@ class _Conv2d(torch.autograd.Function):
                         torch.ops.tfx.bn_bwd_reduce_into(dx, bnb.x, bnb.save, bnb.relu, None, bnb.ws)
                         sr_bnb = bnb
             if w.trainable:
-                if sr_bnb is not None or (fusion.knob("sr_take") and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device):
-                    take = fusion.knob("sr_take") and _PENDING_SR and _PENDING_SR[0].ws.device == gy.device
-                    t2 = _PENDING_SR.pop(0) if take else None
+                pend = _pending_sr(w.store)
+                if sr_bnb is not None or (fusion.knob("sr_take") and pend and pend[0].ws.device == gy.device):
+                    take = fusion.knob("sr_take") and pend and pend[0].ws.device == gy.device
+                    t2 = pend.pop(0) if take else None
                     t1 = sr_bnb
                     r1, r2 = torch.ops.tfx.conv_wgrad_sr2(
                         gy, x, w.grad, stride, pad, dil, True, t1.ws if t1 is not None else None,
@@ -642,10 +659,11 @@ class BNBackwardFusion:
     ``red`` ([sum g' | sum g' xhat]) (or a later weight-gradient launch does, from the slots); the BN
     backward then runs only its apply pass."""
     __slots__ = ("x", "save", "mask", "relu", "ws", "dgamma", "dbeta", "red", "in_mask", "deferred",
-                 "sr_pending", "sec_lazy")
+                 "sr_pending", "sec_lazy", "store")
 
-    def __init__(self, x, save, mask, relu, ws, dgamma, dbeta):
+    def __init__(self, x, save, mask, relu, ws, dgamma, dbeta, store=None):
         self.x, self.save, self.mask, self.relu, self.ws = x, save, mask, relu, ws
+        self.store = store  # the model's VariableStore: its pending-reduction list (_pending_sr)
         self.dgamma, self.dbeta, self.red = dgamma, dbeta, None
         # set by a residual consumer (bn_bwd_apply_sec): the incoming gradient arrives unmasked,
         # the true gradient is g * in_mask (the consumer's ReLU mask bits)
@@ -653,7 +671,7 @@ class BNBackwardFusion:
         # the BN's output was never written (batch_norm(defer_output=True)): its only consumer, a
         # residual BN, normalizes ``x`` with ``save`` on the fly
         self.deferred = False
-        # backward partials sit in ``ws`` waiting for a later launch to reduce them (_PENDING_SR)
+        # backward partials sit in ``ws`` waiting for a later launch to reduce them (_pending_sr)
         self.sr_pending = False
         # a projection tail's LazyBNGrad that still owes this (shortcut) BN's reduction
         self.sec_lazy = None
@@ -683,27 +701,39 @@ def _bn_ref(x, gamma, beta, rm, rv, momentum, eps, res, relu, training, update=T
     return y.to(x.dtype)
 
 
-# BN layers whose backward partials wait in their slot workspace for the next weight-gradient
-# launch to reduce them in its tail blocks (conv_wgrad_sr2) -- or for their own backward to reduce
-# them (bn_slots_reduce) if no such launch came first
-_PENDING_SR: List["BNBackwardFusion"] = []
+def _pending_sr(store) -> List["BNBackwardFusion"]:
+    """The model's BN layers whose backward partials wait in their slot workspace for the next
+    weight-gradient launch OF THE SAME MODEL to reduce them in its tail blocks (conv_wgrad_sr2) -- or for
+    their own backward to reduce them (bn_slots_reduce) if no such launch came first."""
+    st = _model_state(store)
+    lst = st.get("pending_sr")
+    if lst is None:
+        lst = st["pending_sr"] = []
+    return lst
+
+
+def pending_slot_reductions(store=None) -> List["BNBackwardFusion"]:
+    """The deferred BN-backward reductions still pending for ``store``'s model (tests: empty after a step)."""
+    return list(_pending_sr(store))
 
 
 # single-launch mean loss for small batches (else: per-row kernel + mean + scale launches)
 _XENT_MEAN_MAX = 1024
 
 
-def reset_pending_slot_reductions() -> None:
-    """Forget deferred reductions of an abandoned step (an exception part-way through)."""
-    for b in _PENDING_SR:
+def reset_pending_slot_reductions(store=None) -> None:
+    """Forget ``store``'s deferred reductions of an abandoned step (an exception part-way through)."""
+    pend = _pending_sr(store)
+    for b in pend:
         b.sr_pending = False
-    _PENDING_SR.clear()
+    pend.clear()
 
 
 def _resolve_pending(b: "BNBackwardFusion") -> None:
     if b.sr_pending:
-        if b in _PENDING_SR:
-            _PENDING_SR.remove(b)
+        pend = _pending_sr(b.store)
+        if b in pend:
+            pend.remove(b)
         b.red = torch.ops.tfx.bn_slots_reduce(b.ws, b.x.shape[-1], b.dgamma, b.dbeta)
         b.sr_pending = False
 
@@ -812,7 +842,7 @@ class _BatchNorm(torch.autograd.Function):
                     and x.shape[-1] % 8 == 0:
                 train_p = gamma is not None and gamma.trainable
                 ctx.bnb = BNBackwardFusion(x, save, mask, relu, ws, gamma.grad if train_p else None,
-                                           beta.grad if train_p else None)
+                                           beta.grad if train_p else None, gamma.store if gamma is not None else None)
                 ctx.bnb.deferred = defer_out
                 bnb_out.append(ctx.bnb)
             return y
@@ -867,7 +897,7 @@ class _BatchNorm(torch.autograd.Function):
                                                                  rb.dbeta if p_t else None, not pass_mask, not defer)
                 if defer:
                     rb.red, rb.sr_pending = None, True
-                    _PENDING_SR.append(rb)
+                    _pending_sr(rb.store).append(rb)
                 else:
                     rb.red = red2
                 if pass_mask:
@@ -1215,20 +1245,10 @@ def softmax_cross_entropy(logits, labels, naive: bool = False, unit_seed: bool =
 HEAD_FUSED_CALLS = [0]
 HEAD_TAIL_CALLS = [0]
 _CHECK_SEED = os.environ.get("TFX_CHECK_SEED", "0") == "1"
-_HEAD_STATE = {}
-
-
-def _head_state(device) -> torch.Tensor:
-    """The fused head's self-resetting loss accumulator (3 zeroed int64 per device, left zero by every
-    launch): allocated once, outside any graph capture's private pool when possible."""
-    st = _HEAD_STATE.get(device)
-    if st is None:
-        st = torch.zeros(3, dtype=torch.int64, device=device)
-        # a tensor allocated during a capture lives in that graph's private pool: never cache it (the
-        # zero fill is then recorded in the graph, so each replay still starts from a zero word)
-        if not torch.cuda.is_current_stream_capturing():
-            _HEAD_STATE[device] = st
-    return st
+def _head_state(store, device) -> torch.Tensor:
+    """The fused head's self-resetting loss accumulator (3 zeroed int64 per model and device, left zero by
+    every launch): allocated once, outside any graph capture's private pool when possible."""
+    return _cached_buffer(store, ("head_state", str(device)), lambda: torch.zeros(3, dtype=torch.int64, device=device))
 
 
 class _HeadXent(torch.autograd.Function):
@@ -1246,13 +1266,13 @@ class _HeadXent(torch.autograd.Function):
             tp, bnb = tail
             rows = torch.empty(2 * feat.numel() // (feat.shape[1] * feat.shape[2]), dtype=torch.float32,
                                device=feat.device)
-            loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, bias, labels, _head_state(feat.device), tp.x,
+            loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, bias, labels, _head_state(w.store, feat.device), tp.x,
                                                          tp.res, tp.save, tp.mask, rows)
             ctx.tail_bnb, ctx.tail_rows = bnb, rows
             HEAD_TAIL_CALLS[0] += 1
             fusion.note("head_tail", w.name, "head_xent_tail")
         else:
-            loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, bias, labels, _head_state(feat.device), None,
+            loss, dfeat, f, dz = torch.ops.tfx.head_xent(feat, w.value, bias, labels, _head_state(w.store, feat.device), None,
                                                          None, None, None, None)
         ctx.save_for_backward(dfeat, f, dz)
         HEAD_FUSED_CALLS[0] += 1

@@ -45,7 +45,7 @@ class ClassifierTrainer:
 
     def _step_impl(self, x, y):
         # roctx ranges (TFX_ROCTX=1) label the phases on a rocprofv3 --marker-trace timeline
-        reset_pending_slot_reductions()  # nothing deferred survives an abandoned step
+        reset_pending_slot_reductions(self.store)  # nothing deferred survives an abandoned step
         self.store.zero_grad()
         with trace.range("forward"):
             head = getattr(self.model, "training_loss", None)

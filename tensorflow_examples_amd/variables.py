@@ -268,6 +268,10 @@ class VariableStore:
         # cleared it in its pass: Optimizer.apply_gradients(zero_grad=True)); zero_grad then skips the fill
         self.grads_clean = True
         self.grad_epoch = 0  # bumped by zero_grad (a step counter for gradient consumers)
+        # per-model runtime state of the fused ops (ops/nn.py _model_state): the stem / head workspaces and
+        # the BN-backward reductions deferred to a later launch of THIS model's backward -- never shared
+        # between two models of one process
+        self.fused_state: Dict[str, object] = {}
         self.shadow: Optional[torch.Tensor] = None
         self._flip = None          # flipped 3x3 filter copies (flip_index / flipped3x3)
         self.flip_stale = True

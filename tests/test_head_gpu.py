@@ -165,7 +165,7 @@ def test_resnet_head_takes_over_last_tail(gpu):
             loss.backward()
             torch.cuda.synchronize()
             assert (opsnn.HEAD_TAIL_CALLS[0] - n0) == (1 if tail else 0)
-            assert not opsnn._PENDING_SR
+            assert not opsnn.pending_slot_reductions(st)
             return loss.item(), st.grad.clone()
 
     l0, g0 = run(False)

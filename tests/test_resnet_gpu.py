@@ -136,7 +136,7 @@ def test_deferred_slot_reductions_fallback_and_off_agree(gpu):
         st.zero_grad()
         ops.softmax_cross_entropy(m(xin, training=True), lab).backward()
         torch.cuda.synchronize()
-        assert not nnops._PENDING_SR, "a deferred reduction was never resolved"
+        assert not nnops.pending_slot_reductions(st), "a deferred reduction was never resolved"
         return st.grad.clone(), st
 
     from tensorflow_examples_amd.ops import fusion
