@@ -67,7 +67,7 @@ def test_head_xent_deterministic_graph_and_state(gpu):
     feat = torch.randn(N, 4, 4, C, device=gpu).to(torch.bfloat16)
     labels = torch.randint(0, O, (N,), device=gpu)
     st, w, b = _store(gpu, O, C)
-    state = opsnn._head_state(gpu)
+    state = opsnn._head_state(None, gpu)
     outs = [torch.ops.tfx.head_xent(feat, w.value, b.master, labels, state) for _ in range(3)]
     torch.cuda.synchronize()
     assert int(state.abs().sum().item()) == 0, "the state word must be left zero"
@@ -98,7 +98,7 @@ def test_head_xent_nonfinite_loss_is_nan(gpu):
     feat[3, 0, 0, 5] = float("inf")
     labels = torch.zeros(N, dtype=torch.long, device=gpu)
     st, w, b = _store(gpu, O, C)
-    state = opsnn._head_state(gpu)
+    state = opsnn._head_state(None, gpu)
     loss = torch.ops.tfx.head_xent(feat, w.value, b.master, labels, state)[0]
     torch.cuda.synchronize()
     assert torch.isnan(loss).item()
@@ -124,7 +124,7 @@ def test_head_xent_tail_mode_matches_applied_input(gpu, N, H, W, C, O):
     torch.ops.tfx.bn_apply_into(y3, res, save, None, out, mask_ref)
     labels = torch.randint(0, O, (N,), device=gpu)
     st, w, b = _store(gpu, O, C)
-    state = opsnn._head_state(gpu)
+    state = opsnn._head_state(None, gpu)
     ref = torch.ops.tfx.head_xent(out, w.value, b.master, labels, state)
     mask = torch.zeros_like(mask_ref)
     rows = torch.empty(N * 2 * C, device=gpu)
