@@ -70,8 +70,6 @@ struct IgemmArgs {
   float* stats = nullptr;
   // rows of `stats` the epilogue adds into (tile row tm -> row tm % stat_slots)
   int stat_slots = NSLOT;
-  // persistent kernels: each block takes a contiguous range of tile ids (XCD-affine rows, xcd_affine())
-  int xcd_contig = 0;
   FastDiv fd_C, fd_S, fd_Ko, fd_PQ, fd_Q;
   int zero_out = 1;
   // MODE_DGRAD_CLS: one output-parity class (cph, cpw) of a stride-2 data gradient.  The GEMM rows
@@ -120,10 +118,6 @@ struct IgemmArgs {
 void igemm_launch(IgemmArgs a, int mode, hipStream_t s);
 // persistent 1x1-forward mode (igemm_persist.hip): 0 off, 2 / 3 ring depth; returns the previous mode
 int igemm_persist_set(int mode);
-// TFX_BN_XCD (default 1): XCD-affine row mappings -- the fixed-channel BN passes walk contiguous eighths
-// of their tensors per XCD and the persistent GEMM blocks contiguous tile ranges, matching the implicit
-// GEMMs' xcd_remap, so producer -> consumer activations stay in one XCD's L2 (batchnorm.hip)
-bool xcd_affine();
 
 // ---------------------------------------------------------------- fused pointwise-conv backward (pw_bwd.hip)
 // Backward of a bottleneck's expanding 1x1 conv (CN -> CW = 4 CN) fused with the block-tail BN's

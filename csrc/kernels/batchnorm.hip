@@ -216,34 +216,14 @@ __global__ void bn_eval_prep_kernel(int C, const float* __restrict__ gamma, cons
 // residual itself (twice: reduce and apply).
 // RBN: the residual is another BN's INPUT, normalized here on the fly with its rsave -- that BN
 // (a ResNet projection shortcut's, used only as this residual) never writes its output.
-// XCD-contiguous element mapping of the fixed-channel passes (seg > 0): logical block L =
-// xcd_remap(blockIdx) owns the vectors [L seg, (L+1) seg), so (with the hardware's round-robin dispatch)
-// XCD x walks the x-th eighth of the tensor -- the same rows the implicit GEMMs' xcd_remap gives XCD x
-// (tile id = tm * tiles_n + tn, contiguous per XCD).  A GEMM output is then read by the BN pass, and the
-// BN output by the next GEMM, from the XCD's own L2 instead of across XCDs.  seg is a multiple of 256
-// and 256 % (C / 8) == 0, so each thread's channel vector stays fixed.  seg = 0: the grid-stride form.
-__device__ __forceinline__ void vec_span(int64_t nvec, int64_t seg, int64_t& i0, int64_t& end, int64_t& stride) {
-  if (seg > 0) {
-    const int64_t L = xcd_remap(blockIdx.x, gridDim.x);
-    i0 = L * seg + threadIdx.x;
-    end = (L + 1) * seg < nvec ? (L + 1) * seg : nvec;
-    stride = 256;
-  } else {
-    i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    end = nvec;
-    stride = (int64_t)gridDim.x * 256;
-  }
-}
-
 template <bool RES, bool RELU, bool RBN = false>
 __global__ void __launch_bounds__(256) bn_apply_vec_kernel(const uint16_t* __restrict__ x,
                                                            const uint16_t* __restrict__ res,
                                                            const float* __restrict__ save, int64_t nvec, int C,
                                                            uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
-                                                           const float* __restrict__ rsave = nullptr,
-                                                           int64_t seg = 0) {
-  int64_t i0, end, stride;
-  vec_span(nvec, seg, i0, end, stride);
+                                                           const float* __restrict__ rsave = nullptr) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
   const int c0 = (int)(i0 % (C >> 3)) * 8;
   float sc[8], sh[8], rsc[8], rsh[8];
 #pragma unroll
@@ -272,11 +252,11 @@ __global__ void __launch_bounds__(256) bn_apply_vec_kernel(const uint16_t* __res
     if (RES && RELU && mask) mask[i] = (uint8_t)bits;
   };
   int64_t i = i0;
-  for (; i + stride < end; i += 2 * stride) {
+  for (; i + stride < nvec; i += 2 * stride) {
     one(i);
     one(i + stride);
   }
-  if (i < end) one(i);
+  if (i < nvec) one(i);
 }
 
 template <bool RES, bool RELU>
@@ -424,9 +404,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* _
                                                                uint16_t* __restrict__ dres,
                                                                const uint16_t* __restrict__ x2 = nullptr,
                                                                const float* __restrict__ save2 = nullptr,
-                                                               float* __restrict__ slots2 = nullptr, int64_t seg = 0) {
-  int64_t i0, end, stride;
-  vec_span(nvec, seg, i0, end, stride);
+                                                               float* __restrict__ slots2 = nullptr) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
   const int c0 = (int)(i0 % (C >> 3)) * 8;
   const float inv_m = 1.f / (float)M;
   float A[8], B[8], D[8], sc[8], sh[8];
@@ -448,7 +428,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(const uint16_t* _
       q2[k] = 0.f;
     }
   }
-  for (int64_t i = i0; i < end; i += stride) {
+  for (int64_t i = i0; i < nvec; i += stride) {
     float gf[8], xf[8], o[8], x2f[8];
     unpack8(reinterpret_cast<const U4*>(g)[i], gf);
     unpack8(reinterpret_cast<const U4*>(x)[i], xf);
@@ -547,22 +527,6 @@ int fixed_channel_grid(int64_t nvec, int C) {
   return g;
 }
 
-}  // namespace (reopened below)
-// TFX_BN_XCD (read once; A/B hook): 1 = the XCD-contiguous mappings (vec_span; igemm_persist.hip)
-bool xcd_affine() {
-  static const bool v = [] {
-    const char* e = getenv("TFX_BN_XCD");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
-namespace {
-// the segment (vectors per block, a multiple of 256) of an XCD-contiguous pass over nvec vectors on g blocks
-int64_t xcd_seg(int64_t nvec, int g) {
-  if (!xcd_affine() || g < 8) return 0;
-  return (nvec + (int64_t)g * 256 - 1) / ((int64_t)g * 256) * 256;
-}
-
 #define TFX_DISPATCH_RR(RES, RELU, ...)                              \
   if (RES) {                                                         \
     if (RELU) { constexpr bool R_ = true, L_ = true; __VA_ARGS__; }   \
@@ -602,9 +566,7 @@ void bn_apply(const uint16_t* x, const uint16_t* res, const float* save, int64_t
   if (C % 8 == 0) {
     const int64_t nvec = n / 8;
     const int g = fixed_channel_grid(nvec, C);
-    const int64_t seg = xcd_seg(nvec, g);
-    TFX_DISPATCH_RR(has_res, relu, (bn_apply_vec_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, nvec, C, y, mask,
-                                                                                  nullptr, seg)));
+    TFX_DISPATCH_RR(has_res, relu, (bn_apply_vec_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, nvec, C, y, mask)));
   } else {
     const int g = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_apply_gen_kernel<R_, L_><<<g, 256, 0, s>>>(x, res, save, n, C, y)));
@@ -615,11 +577,10 @@ void bn_apply_res_bn(const uint16_t* x, const uint16_t* res_x, const float* save
                      int C, bool relu, uint16_t* y, uint8_t* mask, hipStream_t s) {
   const int64_t nvec = M * C / 8;
   const int g = fixed_channel_grid(nvec, C);
-  const int64_t seg = xcd_seg(nvec, g);
   if (relu)
-    bn_apply_vec_kernel<true, true, true><<<g, 256, 0, s>>>(x, res_x, save, nvec, C, y, mask, res_save, seg);
+    bn_apply_vec_kernel<true, true, true><<<g, 256, 0, s>>>(x, res_x, save, nvec, C, y, mask, res_save);
   else
-    bn_apply_vec_kernel<true, false, true><<<g, 256, 0, s>>>(x, res_x, save, nvec, C, y, mask, res_save, seg);
+    bn_apply_vec_kernel<true, false, true><<<g, 256, 0, s>>>(x, res_x, save, nvec, C, y, mask, res_save);
 }
 
 void bn_backward(const uint16_t* g, const uint16_t* x, const uint16_t* res, const uint8_t* mask, const float* save,
@@ -668,13 +629,12 @@ void bn_backward_apply_sec(const uint16_t* g, const uint16_t* x, const uint8_t* 
   const int mult = cv / gcd(cv, 256);
   int ga = grid_for(nvec, 256 * 4, 1024);
   ga = (ga + mult - 1) / mult * mult;
-  const int64_t seg = xcd_seg(nvec, ga);
   if (relu)
     bn_bwd_apply_vec_kernel<true, true, true><<<ga, 256, 0, s>>>(g, x, mask, save, red, nvec, M, C, dx, dres, x2,
-                                                                 save2, slots2, seg);
+                                                                 save2, slots2);
   else
     bn_bwd_apply_vec_kernel<true, false, true><<<ga, 256, 0, s>>>(g, x, mask, save, red, nvec, M, C, dx, dres,
-                                                                  x2, save2, slots2, seg);
+                                                                  x2, save2, slots2);
 }
 
 // the apply half of bn_backward, for a red[] produced elsewhere (a conv dgrad epilogue)
@@ -687,9 +647,8 @@ void bn_backward_apply(const uint16_t* g, const uint16_t* x, const uint16_t* res
   if (vec_ok(C) && (!has_res || !relu || mask)) {
     const int64_t nvec = n / 8;
     const int ga = fixed_channel_grid(nvec, C);
-    const int64_t seg = xcd_seg(nvec, ga);
     TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_vec_kernel<R_, L_><<<ga, 256, 0, s>>>(
-                                       g, x, mask, save, red, nvec, M, C, dx, dres, nullptr, nullptr, nullptr, seg)));
+                                       g, x, mask, save, red, nvec, M, C, dx, dres)));
   } else {
     const int ga = grid_for(n, 256 * 4);
     TFX_DISPATCH_RR(has_res, relu, (bn_bwd_apply_gen_kernel<R_, L_><<<ga, 256, 0, s>>>(

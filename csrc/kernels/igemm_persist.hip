@@ -60,13 +60,7 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
   const int bid = xcd_remap(blockIdx.x, grid);
   const int tiles_n = a.tiles_n, ntiles = a.tiles_m * a.tiles_n;
   const int nkt = a.K / BKT;
-  // this block's tiles: a CONTIGUOUS range of tile ids (tile = tm * tiles_n + tn), so with xcd_remap XCD x
-  // walks the x-th eighth of the output rows -- the rows the XCD-contiguous BN passes read from its L2
-  // (batchnorm.hip vec_span); a_xcd = 0: the round-robin form (tile bid + k grid)
-  const int t_begin = a.xcd_contig ? (int)((int64_t)bid * ntiles / grid) : bid;
-  const int my = a.xcd_contig ? (int)((int64_t)(bid + 1) * ntiles / grid) - t_begin
-                              : (ntiles - bid + grid - 1) / grid;  // >= 1: the host sizes grid <= ntiles
-  const int t_step = a.xcd_contig ? 1 : grid;
+  const int my = (ntiles - bid + grid - 1) / grid;  // >= 1: the host sizes grid <= ntiles
   const int total = my * nkt;
 
   // tile-0 loaders (every row / column valid: M % BM == N % BN == 0); a tile's offsets add a scalar
@@ -80,7 +74,7 @@ __global__ void __launch_bounds__(256) igemm_persist_kernel(IgemmArgs a) {
   constexpr int NPT = LA::NP + LB::NP;
   uint32_t oa[LA::NP], ob[LB::NP];
 
-  auto tile_of = [&](int ti) __attribute__((always_inline)) { return t_begin + ti * t_step; };
+  auto tile_of = [&](int ti) __attribute__((always_inline)) { return bid + ti * grid; };
   // step s of this block = k-tile (s mod nkt) of its tile (s div nkt); s >= total: zero pieces (BAD)
   auto issue = [&](int s, auto S) __attribute__((always_inline)) {
     const int ti = s / nkt, kt = s - ti * nkt;
@@ -254,7 +248,6 @@ void launch_p(IgemmArgs& a, hipStream_t s) {
     return n;
   }();
   const int grid = std::min(ntiles, num_cus() * bpc);
-  a.xcd_contig = xcd_affine() ? 1 : 0;
   igemm_persist_kernel<BM, BN, GLS, EPI><<<grid, 256, 0, s>>>(a);
 }
 
