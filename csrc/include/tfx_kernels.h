@@ -243,6 +243,13 @@ void sgemm_launch(const float* A, const float* B, float* C, const float* bias, i
 // ---------------------------------------------------------------- batch norm (NHWC)
 // slots: persistent per-layer workspace [NSLOT][2][C] f32, zero between uses (consumers re-zero it)
 void bn_stats(const uint16_t* x, int64_t M, int C, float* slots, hipStream_t s);
+// Deterministic-reduction test mode (op set_deterministic): the reductions whose f32 atomic order varies
+// from run to run take a fixed order instead -- forward BN statistics recomputed by bn_stats_det before
+// each finalize, split-K weight gradients unsplit (one block per output tile), slab reductions in one
+// group.  Slower; for tests that compare fused and layer-wise paths bit-for-bit-stable.
+void set_det_mode(bool on);
+bool det_mode();
+void bn_stats_det(const uint16_t* x, int64_t M, int C, float* slots, hipStream_t s);
 void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float* beta, float eps,
                  float momentum, float* run_mean, float* run_var, float* save, hipStream_t s);
 // slots -> red = [sum g' | sum g' xhat] (+= into dbeta / dgamma when given), slots re-zeroed

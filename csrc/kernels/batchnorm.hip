@@ -548,6 +548,30 @@ void bn_stats(const uint16_t* x, int64_t M, int C, float* slots, hipStream_t s) 
   }
 }
 
+// ---- deterministic-reduction test mode
+static bool g_det = false;
+void set_det_mode(bool on) { g_det = on; }
+bool det_mode() { return g_det; }
+
+__global__ void __launch_bounds__(256) zero_f32_kernel(float* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
+}
+
+// The batch statistics of x into the zeroed-first slots with at most NSLOT blocks: block b owns slot b
+// alone (one adder per address, onto zero: exact), its rows in a fixed grid-stride order and a fixed LDS
+// tree -- the finalize's fixed-order slot sum then gives the same bits on every run.  The producing
+// kernels' epilogue statistics (up to 32 adders per slot address, in arrival order) are discarded.
+void bn_stats_det(const uint16_t* x, int64_t M, int C, float* slots, hipStream_t s) {
+  zero_f32_kernel<<<64, 256, 0, s>>>(slots, (int64_t)NSLOT * 2 * C);
+  if (vec_ok(C)) {
+    const int rpb = 256 / (C / 8);
+    bn_stats_vec_kernel<<<std::min(NSLOT, grid_for(M, rpb * 8)), 256, 0, s>>>(x, M, C, slots);
+  } else {
+    dim3 grid((C + 63) / 64, std::min(NSLOT, grid_for(M, 64)));
+    bn_stats_gen_kernel<<<grid, 256, 0, s>>>(x, M, C, slots);
+  }
+}
+
 void bn_finalize(float* slots, int64_t M, int C, const float* gamma, const float* beta, float eps, float momentum,
                  float* run_mean, float* run_var, float* save, hipStream_t s) {
   bn_finalize_kernel<<<(C + 15) / 16, 256, 0, s>>>(slots, M, C, gamma, beta, eps, momentum, run_mean, run_var,

@@ -1352,7 +1352,9 @@ void launch_t(IgemmArgs& a, hipStream_t s, int want_mult = 1, int min_kps = 4) {
   int splits = 1;
   constexpr int want = 256;  // one block per CU: measured best (fewer f32 atomic partials)
   const int want_blocks = g_tc.want > 0 ? g_tc.want : want * want_mult;
-  if (a.out_mode == OUT_F32_ATOMIC) splits = pick_splits(tiles, nkt, want_blocks, min_kps);
+  // (deterministic mode: one block per output tile, its single atomic add per element onto the zeroed
+  // gradient is exact)
+  if (a.out_mode == OUT_F32_ATOMIC && !det_mode()) splits = pick_splits(tiles, nkt, want_blocks, min_kps);
   a.kps = (nkt + splits - 1) / splits;
   if constexpr (KS == 2) {
     // each 4-wave group takes kps/2 k-tiles: a multiple of 4 keeps both halves even (no zero step).

@@ -112,14 +112,14 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
   };
 
   // a2_save: conv3's input is relu(BN2(y2)) formed on load from y2 (a.a2 holds y2); this thread's
-  // narrow chunk is channels 8 (t % NTPR) .. +7
+  // narrow chunk is channels 8 (t % NTPR) .. +7.  Scale / shift live in an LDS table, read per tile:
+  // held in registers (16 per lane) they pushed the SEC variant past 256 VGPRs into scratch, and every
+  // scratch reload inside the loop waited vmcnt(0) -- draining the next tiles' loads with it.
   const bool a2_bn = a.a2_save != nullptr;
-  float a2s[8], a2h[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int c = 8 * (t % C::NTPR) + k;
-    a2s[k] = a2_bn ? a.a2_save[2 * CN + c] : 1.f;
-    a2h[k] = a2_bn ? a.a2_save[3 * CN + c] : 0.f;
+  __shared__ float a2tab[2 * CN];
+  for (int c = t; c < CN; c += PW_NT) {
+    a2tab[c] = a2_bn ? a.a2_save[2 * CN + c] : 1.f;
+    a2tab[CN + c] = a2_bn ? a.a2_save[3 * CN + c] : 0.f;
   }
   // dgrad wave tile: rows 16 (wv & 1), columns DCOLS (wv >> 1); SWAP orientation -> lane holds row
   // (lane & 15), columns dcb + (lane >> 4) * 4 + r of each 16-col tile
@@ -214,6 +214,12 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
       if (a2_bn) {  // uniform: BN2 + ReLU of the staged y2 piece (rows past M are never stored)
         float f[8];
         unpack8(__builtin_bit_cast(U4, v), f);
+        const float4 s0 = *reinterpret_cast<const float4*>(a2tab + 8 * cc);
+        const float4 s1 = *reinterpret_cast<const float4*>(a2tab + 8 * cc + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(a2tab + CN + 8 * cc);
+        const float4 h1 = *reinterpret_cast<const float4*>(a2tab + CN + 8 * cc + 4);
+        const float a2s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float a2h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], a2s[k], a2h[k]), 0.f);
         v = __builtin_bit_cast(pw_u32x4, pack8(f));
@@ -274,9 +280,12 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
   };
 
   // ---- main loop over this block's m-tiles (tile0, tile0 + tstep, ...): staged two ahead
+  // ysc first: in the loop it is issued before the next tiles' loads, so the waitcnt pass (which merges
+  // the prologue's and the back edge's outstanding loads at the loop header) sees the same order here --
+  // issued last, its wait at the header drained every load in flight
+  issue_ys(tile0);
   issue(st0, tile0);
   issue(st1, tile0 + tstep);
-  issue_ys(tile0);
   __syncthreads();  // W3 image written
   for (int tile = tile0; tile < ntiles; tile += 2 * tstep) {
     stage(st0, smem, tile + tstep);
@@ -659,9 +668,9 @@ __global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __rest
                                                              float* __restrict__ dw, float* __restrict__ sr_slots,
                                                              int sr_C, float* __restrict__ sr_red,
                                                              float* __restrict__ sr_dgamma,
-                                                             float* __restrict__ sr_dbeta, PwSecReduce sec) {
+                                                             float* __restrict__ sr_dbeta, PwSecReduce sec, int rg) {
   constexpr int E = MAP == 2 ? 64 * 576 : 4 * CN * CN;
-  const int ngemm = (E / 256) * PW_RG;
+  const int ngemm = (E / 256) * rg;
   const int nsr = sr_C ? (sr_C + 15) / 16 : 0;
   if ((int)blockIdx.x >= ngemm + nsr) {
     // SEC: 16 channels per block, 16 slot-lanes x NSLOT/16 slots each (q halves only)
@@ -735,12 +744,12 @@ __global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __rest
   const int e = (blockIdx.x % (E / 256)) * 256 + threadIdx.x, grp = blockIdx.x / (E / 256);
   float acc = 0.f;
   int b = grp;
-  for (; b + 3 * PW_RG < nslab; b += 4 * PW_RG) {
-    const float v0 = slab[(size_t)b * E + e], v1 = slab[(size_t)(b + PW_RG) * E + e];
-    const float v2 = slab[(size_t)(b + 2 * PW_RG) * E + e], v3 = slab[(size_t)(b + 3 * PW_RG) * E + e];
+  for (; b + 3 * rg < nslab; b += 4 * rg) {
+    const float v0 = slab[(size_t)b * E + e], v1 = slab[(size_t)(b + rg) * E + e];
+    const float v2 = slab[(size_t)(b + 2 * rg) * E + e], v3 = slab[(size_t)(b + 3 * rg) * E + e];
     acc += (v0 + v1) + (v2 + v3);
   }
-  for (; b < nslab; b += PW_RG) acc += slab[(size_t)b * E + e];
+  for (; b < nslab; b += rg) acc += slab[(size_t)b * E + e];
   if constexpr (MAP == 0) atomicAdd(dw + pw_slab_to_dw<CN>(e), acc);
   else if constexpr (MAP == 1) atomicAdd(dw + pw_slab_to_dw1<4 * CN, CN>(e), acc);
   else atomicAdd(dw + pw_slab_to_dw_c3(e), acc);
@@ -779,18 +788,19 @@ void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_s
                     float* sr_dgamma, float* sr_dbeta, const PwSecReduce& sec, hipStream_t s, int map) {
   const int E = map == 2 ? 64 * 576 : 4 * CN * CN;
   const int nsr = sr_slots ? (sr_C + 15) / 16 : 0;
-  const int grid = (E / 256) * PW_RG + nsr + (sec.C ? (sec.C + 15) / 16 : 0);
+  const int rg = det_mode() ? 1 : PW_RG;  // one adder per dW element in the deterministic mode
+  const int grid = (E / 256) * rg + nsr + (sec.C ? (sec.C + 15) / 16 : 0);
   switch (CN) {
     case 64:
       if (map == 0)
         pw_slab_reduce_kernel<64, 0><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
-                                                          sr_dgamma, sr_dbeta, sec);
+                                                          sr_dgamma, sr_dbeta, sec, rg);
       else if (map == 1)
         pw_slab_reduce_kernel<64, 1><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
-                                                          sr_dgamma, sr_dbeta, sec);
+                                                          sr_dgamma, sr_dbeta, sec, rg);
       else
         pw_slab_reduce_kernel<64, 2><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
-                                                          sr_dgamma, sr_dbeta, sec);
+                                                          sr_dgamma, sr_dbeta, sec, rg);
       break;
     default: abort();
   }

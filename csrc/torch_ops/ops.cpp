@@ -240,6 +240,17 @@ void check_bn_ws(const Tensor& ws, int64_t C) {
   TORCH_CHECK(ws.numel() >= tfx::NSLOT * 2 * C, "BN workspace too small for the fused epilogue");
 }
 
+// deterministic mode: the producer's epilogue statistics replaced by a fixed-order recompute from y
+void det_restat(const Tensor& y, float* slots, int64_t M, int64_t C) {
+  if (tfx::det_mode()) tfx::bn_stats_det(bf(y), M, (int)C, slots, cur_stream());
+}
+
+bool set_deterministic(bool on) {
+  const bool prev = tfx::det_mode();
+  tfx::set_det_mode(on);
+  return prev;
+}
+
 bool g_stem_fwd = true;  // conv_fwd_bn routes the CIFAR stem (8 channels, 32x32, 64 outputs) to stem.hip
 
 // conv forward whose epilogue produces the following BN's batch statistics, then the finalize:
@@ -266,6 +277,7 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   } else {
     tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
   }
+  det_restat(y, a.stats, a.M, g.Ko);
   tfx::bn_finalize(a.stats, a.M, g.Ko, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
                    fpm(run_var), save.data_ptr<float>(), cur_stream());
   return {y, save};
@@ -303,6 +315,7 @@ std::tuple<Tensor, Tensor> conv_fwd_bn_in(Tensor x, Tensor in_save, Tensor w, Te
   a.a_scale = in_save.data_ptr<float>() + 2 * g.C;
   a.a_shift = in_save.data_ptr<float>() + 3 * g.C;
   tfx::igemm_launch(a, tfx::MODE_FWD, cur_stream());
+  det_restat(y, a.stats, a.M, g.Ko);
   tfx::bn_finalize(a.stats, a.M, g.Ko, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
                    fpm(run_var), save.data_ptr<float>(), cur_stream());
   return {y, save};
@@ -338,6 +351,7 @@ std::tuple<Tensor, Tensor> pw_fwd_squeeze(Tensor y3, Tensor save3, Tensor res, o
     a.save_r = res_save->data_ptr<float>();
   }
   tfx::pw_fwd_squeeze(a, tfx::pw_fwd_squeeze_grid((int)CI, (int)CO, M), cur_stream());
+  det_restat(y1, a.slots1, M, CO);
   tfx::bn_finalize(a.slots1, M, (int)CO, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
                    fpm(run_var), save.data_ptr<float>(), cur_stream());
   return {y1, save};
@@ -389,6 +403,7 @@ std::tuple<Tensor, Tensor> conv3x3_fwd_fused(Tensor x, Tensor save_in, Tensor w,
   a.x = bf(x); a.save_in = save_in.data_ptr<float>(); a.w = bf(w); a.y = bfm(y); a.slots = ws.data_ptr<float>();
   a.N = N; a.H = H;
   tfx::conv3x3_fwd_fused(a, cur_stream());
+  det_restat(y, a.slots, (int64_t)N * H * W, K);
   tfx::bn_finalize(a.slots, (int64_t)N * H * W, K, fp(gamma), fp(beta), (float)eps, (float)momentum, fpm(run_mean),
                    fpm(run_var), save.data_ptr<float>(), cur_stream());
   return {y, save};
@@ -806,7 +821,8 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd_train(Tensor x, optional<Tensor> gamma
   }
   auto s = cur_stream();
   float* sl = slots.data_ptr<float>();
-  if (!have_stats) tfx::bn_stats(bf(x), M, C, sl, s);
+  if (tfx::det_mode()) tfx::bn_stats_det(bf(x), M, (int)C, sl, s);
+  else if (!have_stats) tfx::bn_stats(bf(x), M, C, sl, s);
   tfx::bn_finalize(sl, M, C, fp(gamma), fp(beta), eps, momentum, fpm(run_mean), fpm(run_var),
                    save.data_ptr<float>(), s);
   Tensor mask;
@@ -1823,6 +1839,7 @@ TORCH_LIBRARY(tfx, m) {
   m.def("conv_fwd_bn_in_supported", &conv_fwd_bn_in_supported);
   m.def("stem_wgrad", &stem_wgrad);
   m.def("conv_stem_fwd", &conv_stem_fwd);
+  m.def("set_deterministic", &set_deterministic);
   m.def("stem_wgrad_ws_floats", &stem_wgrad_ws_floats);
   m.def("stem_wgrad_supported", &stem_wgrad_supported);
   m.def("conv_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, int dil, Tensor? addend, "

@@ -199,3 +199,18 @@ def test_unplanned_rule_matches_planner():
     assert fusion.fwd_rule("tail", 256, 64, 1, 1, 256, (32, 32)) == (None, "pw_fwd_squeeze")
     assert fusion.fwd_rule("tensor", 64, 64, 1, 1, 8, (4, 4), ws="raw") == (None, "igemm_fwd_stats_only")
     assert fusion.fwd_rule("tensor", 64, 64, 1, 1, 8, (4, 4), ws="none") == (None, "igemm_fwd")
+
+
+def test_deterministic_mode_switch_restores():
+    """ops.deterministic toggles the native library's deterministic-reduction mode (host state: no GPU
+    needed) for the block only, nested blocks included."""
+    _native_or_skip()
+    from tensorflow_examples_amd import ops
+    tfx = torch.ops.tfx
+    assert tfx.set_deterministic(False) is False  # default off
+    with ops.deterministic():
+        assert tfx.set_deterministic(True) is True
+        with ops.deterministic(False):
+            assert tfx.set_deterministic(False) is False
+        assert tfx.set_deterministic(True) is True
+    assert tfx.set_deterministic(False) is False

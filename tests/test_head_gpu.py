@@ -147,10 +147,12 @@ def test_head_xent_tail_mode_matches_applied_input(gpu, N, H, W, C, O):
 
 def test_resnet_head_takes_over_last_tail(gpu):
     """ResNet-50/CIFAR training_loss: the fused head applies the last block's tail BN and reduces its
-    backward (HEAD_TAIL_CALLS).  A random-init bf16 ResNet-50 amplifies the f32-atomic order noise of
-    its BN statistics from layer to layer, so the gradients are compared with the materialised-tail
-    path per variable against the noise floor of two runs of the same path (as
-    test_resnet_gpu.test_deferred_slot_reductions_fallback_and_off_agree)."""
+    backward (HEAD_TAIL_CALLS) vs the materialised tail, in the deterministic-reduction mode: the same
+    loss bits and every variable within the fixed gate (det_util.DET_TOL; the tail mode's f32 in-kernel
+    tail vs the bf16 materialised one is the largest fused-vs-layer-wise gap of the suite, ~1.9e-2 on
+    bn0); the tail-mode input gradient scaled by 0.95 must fail it."""
+    from det_util import assert_gate_catches, assert_within_gate, scaled_output
+    from tensorflow_examples_amd import ops
     from tensorflow_examples_amd.models.resnet import build_resnet_cifar, to_model_input
     img = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, device=gpu)
     lab = torch.randint(0, 10, (32,), device=gpu)
@@ -168,16 +170,12 @@ def test_resnet_head_takes_over_last_tail(gpu):
             assert not opsnn.pending_slot_reductions(st)
             return loss.item(), st.grad.clone()
 
-    l0, g0 = run(False)
-    l1, g1 = run(False)
-    l1b, g1b = run(False)
-    l2, g2 = run(True)
+    with ops.deterministic():
+        l0, g0 = run(False)
+        l2, g2 = run(True)
+        with scaled_output("head_xent", lambda a, o: [o[1]] if a[5] is not None else []):
+            _, gn = run(True)
     assert torch.isfinite(g2).all()
-    assert abs(l2 - l0) <= 4 * max(abs(l1 - l0), abs(l1b - l0)) + 1e-2, (l0, l1, l1b, l2)
-    for v in st.trainable():
-        sl = slice(v.offset, v.offset + v.numel)
-        n = g0[sl].norm().item() + 1e-12
-        # floor: the larger of two same-path distances (one draw made the gate a ratio of two single draws)
-        noise = max((g1[sl] - g0[sl]).norm().item(), (g1b[sl] - g0[sl]).norm().item()) / n
-        e = (g2[sl] - g0[sl]).norm().item() / n
-        assert e <= max(4 * noise, 1e-3), (v.name, e, noise)
+    assert l0 == l2, (l0, l2)
+    assert_within_gate(g0, g2, st, "head tail mode")
+    assert_gate_catches(g0, gn, st, "tail-mode input gradient x0.95")

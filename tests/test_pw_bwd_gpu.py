@@ -149,8 +149,10 @@ def test_pw_bwd_squeeze_matches_reference(gpu, shape):
 
 def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
     """ResNet-50 first-step gradients with the identity blocks' tail BN backward fused into conv3's
-    backward (default) vs materialised by bn_bwd_apply (layer-wise): equal up to the f32-atomic noise
-    floor measured between two fused runs."""
+    backward (default) vs materialised by bn_bwd_apply (layer-wise), in the deterministic-reduction
+    mode: the same loss bits and every variable within the fixed gate (det_util.DET_TOL); the fused
+    kernels' input gradients scaled by 0.95 must fail that gate."""
+    from det_util import assert_gate_catches, assert_within_gate, scaled_output
     from tensorflow_examples_amd import ops
     from tensorflow_examples_amd.ops import nn as nnops
 
@@ -162,34 +164,34 @@ def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
     def run():
         st, m = build_resnet_cifar(device=gpu, depth=50, dtype=torch.bfloat16, seed=3)
         st.zero_grad()
-        ops.softmax_cross_entropy(m(xin, training=True), lab).backward()
+        loss = ops.softmax_cross_entropy(m(xin, training=True), lab)
+        loss.backward()
         torch.cuda.synchronize()
-        return st.grad.clone(), st
+        return float(loss.detach()), st.grad.clone(), st
 
     from tensorflow_examples_amd.ops import fusion
     saved_ok, saved_sq = nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok
     try:
-        n0, n1 = nnops.PW_EXPAND_CALLS[0], nnops.PW_SQUEEZE_BWD_CALLS[0]
-        g0, st = run()
-        assert nnops.PW_EXPAND_CALLS[0] - n0 == 3, "stage-1 blocks run fused (projection block 1 with F3-SEC)"
-        assert nnops.PW_SQUEEZE_BWD_CALLS[0] - n1 == 2, "stage-1 identity blocks' conv1 backward runs fused (F1)"
-        g1, _ = run()
-        g1b, _ = run()
-        # lazy gradients, but every conv declines the fused kernels: LazyBNGrad.materialize (the
-        # projection tail's reduces the shortcut BN there, or in the shortcut BN's backward if first)
-        nnops._pw_expand_ok = lambda *a: False
-        nnops._pw_squeeze_bwd_ok = lambda *a: False
-        g3, _ = run()
-        nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok = saved_ok, saved_sq
-        with fusion.override(lazy_bn_bwd=False):
-            g2, _ = run()
+        with ops.deterministic():
+            n0, n1 = nnops.PW_EXPAND_CALLS[0], nnops.PW_SQUEEZE_BWD_CALLS[0]
+            l0, g0, st = run()
+            assert nnops.PW_EXPAND_CALLS[0] - n0 == 3, "stage-1 blocks run fused (projection block 1 with F3-SEC)"
+            assert nnops.PW_SQUEEZE_BWD_CALLS[0] - n1 == 2, "stage-1 identity blocks' conv1 backward runs fused (F1)"
+            # negative control: both fused kernels' input gradients x0.95
+            with scaled_output("pw_bwd_expand", lambda a, o: [o[0]]), \
+                    scaled_output("pw_bwd_squeeze", lambda a, o: [o[0]]):
+                _, gn, _ = run()
+            # lazy gradients, but every conv declines the fused kernels: LazyBNGrad.materialize (the
+            # projection tail's reduces the shortcut BN there, or in the shortcut BN's backward if first)
+            nnops._pw_expand_ok = lambda *a: False
+            nnops._pw_squeeze_bwd_ok = lambda *a: False
+            l3, g3, _ = run()
+            nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok = saved_ok, saved_sq
+            with fusion.override(lazy_bn_bwd=False):
+                l2, g2, _ = run()
     finally:
         nnops._pw_expand_ok, nnops._pw_squeeze_bwd_ok = saved_ok, saved_sq
-    for v in st.trainable():
-        sl = slice(v.offset, v.offset + v.numel)
-        n = g0[sl].norm().item() + 1e-12
-        # floor: the larger of two same-path distances (one draw made the gate a ratio of two single draws)
-        noise = max((g1[sl] - g0[sl]).norm().item(), (g1b[sl] - g0[sl]).norm().item()) / n
-        for gx in (g2, g3):
-            e = (gx[sl] - g0[sl]).norm().item() / n
-            assert e <= max(4 * noise, 2e-3), (v.name, e, noise)
+    assert l0 == l2 == l3, (l0, l2, l3)
+    assert_within_gate(g0, g2, st, "lazy_bn_bwd off")
+    assert_within_gate(g0, g3, st, "fused kernels declined")
+    assert_gate_catches(g0, gn, st, "fused pw_bwd input gradients x0.95")
