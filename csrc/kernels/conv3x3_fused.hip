@@ -47,11 +47,13 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_fwd_fused_kernel(Conv3Args a
   const int tiles_img = a.H / C3_TR, ntiles = a.N * tiles_img;
 
   // ---- W [K][3][3][C] -> per-tap K-major images (row = output channel), resident
-  for (int q = t; q < 9 * C3_C * 8; q += PW_NT) {
-    const int co = q / 72, rem = q % 72, tap = rem / 8, ch = rem % 8;
-    *reinterpret_cast<pw_u32x4*>(wimg + tap * C3_WTAP + pw_kmaj(co, ch)) =
-        *reinterpret_cast<const pw_u32x4*>(a.w + (int64_t)co * 576 + tap * 64 + ch * 8);
-  }
+  pw_resident_copy<9 * C3_C * 8>(
+      t,
+      [&](int q) {
+        const int co = q / 72, rem = q % 72, tap = rem / 8, ch = rem % 8;
+        return reinterpret_cast<pw_u32x4*>(wimg + tap * C3_WTAP + pw_kmaj(co, ch));
+      },
+      [&](int q) { return reinterpret_cast<const pw_u32x4*>(a.w) + q; });
   // this thread's halo pieces: chunk t % 8 (fixed), halo pixels t / 8 + 64 i
   const int hch = t & 7;
   float sc[8], sh[8];
@@ -238,11 +240,13 @@ __global__ void __launch_bounds__(PW_NT, 1) conv3x3_bwd_fused_kernel(Conv3BwdArg
     coef[8 * C3_C + t] = -a.save1[t] * is1;
   }
   // ---- W [K][3][3][C] -> per-tap MN images (row = output channel co, columns = ci), resident
-  for (int q = t; q < 9 * C3_C * 8; q += PW_NT) {
-    const int co = q / 72, rem = q % 72, tap = rem / 8, ch = rem % 8;
-    *reinterpret_cast<pw_u32x4*>(wimg + tap * C3_WTAP + pw_mn<64>(co, ch)) =
-        *reinterpret_cast<const pw_u32x4*>(a.w + (int64_t)co * 576 + tap * 64 + ch * 8);
-  }
+  pw_resident_copy<9 * C3_C * 8>(
+      t,
+      [&](int q) {
+        const int co = q / 72, rem = q % 72, tap = rem / 8, ch = rem % 8;
+        return reinterpret_cast<pw_u32x4*>(wimg + tap * C3_WTAP + pw_mn<64>(co, ch));
+      },
+      [&](int q) { return reinterpret_cast<const pw_u32x4*>(a.w) + q; });
   const int64_t bytes = (int64_t)a.N * a.H * C3_IW * C3_C * 2;
   const __amdgpu_buffer_rsrc_t rg = pw_rsrc(a.g2, bytes), ry2 = pw_rsrc(a.y2, bytes), ry1 = pw_rsrc(a.y1, bytes);
   const __amdgpu_buffer_rsrc_t rdx = pw_rsrc(a.dx, bytes);

@@ -80,11 +80,9 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_expand_kernel(PwExpandArgs a)
     }
   }
   // ---- W3 [CW][CN] -> MN image (rows = k = wide channel), resident
-  for (int q = t; q < CW * CN / 8; q += PW_NT) {
-    const int k = q / (CN / 8), cc = q % (CN / 8);
-    *reinterpret_cast<pw_u32x4*>(wimg + pw_mn<CN>(k, cc)) =
-        *reinterpret_cast<const pw_u32x4*>(a.w + (int64_t)k * CN + 8 * cc);
-  }
+  pw_resident_copy<CW * CN / 8>(
+      t, [&](int q) { return reinterpret_cast<pw_u32x4*>(wimg + pw_mn<CN>(q / (CN / 8), q % (CN / 8))); },
+      [&](int q) { return reinterpret_cast<const pw_u32x4*>(a.w) + q; });
 
   const __amdgpu_buffer_rsrc_t rg = pw_rsrc(a.g, (int64_t)a.M * CW * 2), ry = pw_rsrc(a.y3, (int64_t)a.M * CW * 2);
   const __amdgpu_buffer_rsrc_t rm = pw_rsrc(a.mask3, (int64_t)a.M * CW / 8);
@@ -422,10 +420,9 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
     ncoef[4 * CO + t] = a.save1[3 * CO + t];
   }
   // ---- W1 [CO][CI] -> MN image (row = co), resident
-  for (int q = t; q < CO * CI / 8; q += PW_NT) {
-    const int co = q / (CI / 8), cc = q % (CI / 8);
-    *reinterpret_cast<pw_u32x4*>(wimg + pw_mn<CI>(co, cc)) = *reinterpret_cast<const pw_u32x4*>(a.w + (int64_t)co * CI + 8 * cc);
-  }
+  pw_resident_copy<CO * CI / 8>(
+      t, [&](int q) { return reinterpret_cast<pw_u32x4*>(wimg + pw_mn<CI>(q / (CI / 8), q % (CI / 8))); },
+      [&](int q) { return reinterpret_cast<const pw_u32x4*>(a.w) + q; });
   const int64_t wide = (int64_t)a.M * CI * 2, narrow = (int64_t)a.M * CO * 2;
   const __amdgpu_buffer_rsrc_t rg = pw_rsrc(a.g1, narrow), ry = pw_rsrc(a.y1, narrow), rx = pw_rsrc(a.x, wide);
   const __amdgpu_buffer_rsrc_t rad = pw_rsrc(a.addend, wide), ram = pw_rsrc(a.amask, (int64_t)a.M * CI / 8);

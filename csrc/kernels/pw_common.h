@@ -57,6 +57,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pw_rsrc(const void* p, int64_t
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, n, 0x00020000);
 }
 
+// Copy N16 16-byte pieces global -> LDS (a block's resident weight image) with every load in flight
+// before the first LDS store.  The plain `for (q = t; q < N16; q += PW_NT)` loop waits for each piece's
+// load before its store: one memory round trip per iteration, 4-16 of them before the main loop.
+// src(q) / dst(q): the piece's global source / LDS destination.  Pieces past N16 re-copy the last one
+// (identical duplicate writes: no branch around the loads).
+template <int N16, typename DST, typename SRC>
+__device__ __forceinline__ void pw_resident_copy(int t, DST dst, SRC src) {
+  constexpr int NPT = (N16 + PW_NT - 1) / PW_NT;
+  pw_u32x4 v[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) v[i] = *src(min(t + PW_NT * i, N16 - 1));
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) *dst(min(t + PW_NT * i, N16 - 1)) = v[i];
+}
+
 template <int... I, typename F>
 __device__ __forceinline__ void pw_sfor_impl(F&& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);

@@ -64,11 +64,13 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_fwd_squeeze_kernel(PwSqueezeArgs 
     }
   }
   // ---- W1 [CO][CI] -> K-major image (row = output channel, 64-channel chunks), resident
-  for (int q = t; q < CO * CI / 8; q += PW_NT) {
-    const int n = q / TPR, cc = q % TPR;
-    *reinterpret_cast<pw_u32x4*>(wimg + (cc >> 3) * (CO * 128) + pw_kmaj(n, cc & 7)) =
-        *reinterpret_cast<const pw_u32x4*>(a.w + (int64_t)n * CI + 8 * cc);
-  }
+  pw_resident_copy<CO * CI / 8>(
+      t,
+      [&](int q) {
+        const int n = q / TPR, cc = q % TPR;
+        return reinterpret_cast<pw_u32x4*>(wimg + (cc >> 3) * (CO * 128) + pw_kmaj(n, cc & 7));
+      },
+      [&](int q) { return reinterpret_cast<const pw_u32x4*>(a.w) + q; });
 
   const int64_t wide = (int64_t)a.M * CI * 2;
   const __amdgpu_buffer_rsrc_t ry = pw_rsrc(a.y3, wide), rr = pw_rsrc(a.res, wide);
