@@ -134,10 +134,13 @@ def main():
                 for fam, M, Nn, Kk in launches:
                     entries.append({"fam": fam, "M": M, "N": Nn, "K": Kk, "tile": best[0], "ks": best[1],
                                     "gls": best[2], "want": best[3], "us": round(med[best], 2),
-                                    "auto_us": round(auto, 2), "shape": [N, H, W, C, K, R, st], "pass": name})
+                                    "auto_us": round(auto, 2), "shape": [N, H, W, C, K, R, st], "pass": name,
+                                    "count": cnt})
         del x, w, y, gy, dw
-    # a GEMM shape reached from two convs keeps its first (larger-count-first order is not needed:
-    # identical (family, M, N, K) means an identical GEMM)
+    # a GEMM key reached from two convs keeps the row of the conv launched more often per step: a
+    # stride-2 3x3 conv and the stride-1 3x3 convs after it share their weight-gradient key but not
+    # their input layout (profiles/r06_tune_step); scripts/tune_step.py re-checks shared keys in the step
+    entries.sort(key=lambda e: -e.get("count", 0))
     if a.merge:
         # keep the merged table's entries of the passes not re-tuned now (dgrad_flip rows included)
         with open(a.merge) as f:

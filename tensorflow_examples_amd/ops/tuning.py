@@ -6,7 +6,8 @@ candidate configuration of every ResNet-50/CIFAR conv (forward with its fused BN
 data gradient with its fused BN-backward epilogue, weight gradient) on an MI355X and writes the
 winners -- keyed by (kernel family, M, N, K) -- to ``tune/igemm_gfx950.json``.  The table is loaded
 into the dispatcher when the kernel library loads; ``TFX_TUNE=0`` ignores it (A/B), ``TFX_TUNE_FILE``
-points at another table.
+points at another table.  ``scripts/tune_step.py`` then re-checks each row inside the graph-replayed
+training step (rows marked ``step-tuned``; profiles/r06_tune_step).
 """
 from __future__ import annotations
 
