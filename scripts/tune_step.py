@@ -34,6 +34,9 @@ from tensorflow_examples_amd.ops import _native, tuning  # noqa: E402
 
 BF16_CANDS = [(t, 0, g, 0) for t in (1, 2, 3) for g in (0, 2, 3)] + [(t, 2, g, 0) for t in (1, 2) for g in (0, 2)]
 ATOMIC_CANDS = [(t, k, g, w) for t in (1, 2) for k in (1, 2) for g in (0, 3) for w in (256, 512)]
+# --cands ext: the split-K block target off the 256 / 512 grid, ring depth 2, and ks 2 with a 3-deep ring
+BF16_EXT = BF16_CANDS + [(1, 2, 3, 0), (2, 2, 3, 0)]
+ATOMIC_EXT = [(t, k, g, w) for t in (1, 2) for k in (1, 2) for g in (0, 2, 3) for w in (128, 256, 384, 512, 768, 1024)]
 
 
 def main():
@@ -45,6 +48,9 @@ def main():
     ap.add_argument("--top", type=int, default=2)
     ap.add_argument("--margin", type=float, default=0.0015)
     ap.add_argument("--keys", default="", help="only these key indices (comma list, in step-time order)")
+    ap.add_argument("--cands", default="base", choices=["base", "ext"])
+    ap.add_argument("--min-launches", type=int, default=1, help="skip keys launched fewer times per step")
+    ap.add_argument("--families", default="", help="only these family names (comma list)")
     ap.add_argument("--budget-s", type=float, default=900.0, help="stop starting new keys after this long")
     ap.add_argument("--out", default="gpurun_out/tune_step/igemm_step.json")
     ap.add_argument("--report", default="gpurun_out/tune_step/report.json")
@@ -115,6 +121,9 @@ def main():
     keys = sorted(counts, key=lambda k: -counts[k] * k[1] * k[2] * k[3])
     if a.keys:
         keys = [keys[int(i)] for i in a.keys.split(",")]
+    keys = [k for k in keys if counts[k] >= a.min_launches]
+    if a.families:
+        keys = [k for k in keys if tuning.FAMILIES[k[0]] in a.families.split(",")]
     capture()
     base0 = statistics.median(timed(a.steps) for _ in range(3))
     print("table rows %d, step keys %d, baseline %.1f us/step" % (n_loaded, len(keys), base0), flush=True)
@@ -125,7 +134,10 @@ def main():
             print("budget reached after %d keys" % ki, flush=True)
             break
         fam = key[0]
-        cands = ATOMIC_CANDS if fam in tuning.ATOMIC_FAMILIES else BF16_CANDS
+        if a.cands == "ext":
+            cands = ATOMIC_EXT if fam in tuning.ATOMIC_FAMILIES else BF16_EXT
+        else:
+            cands = ATOMIC_CANDS if fam in tuning.ATOMIC_FAMILIES else BF16_CANDS
         now = cur.get(key)
         scr = {}
         for c in cands:
