@@ -231,6 +231,8 @@ struct PwSqueezeBwdArgs {
   int M = 0, CI = 0, CO = 0;
 };
 bool pw_bwd_squeeze_ok(int CI, int CO, int64_t M);
+int pw_bwd_squeeze_grid(int CI, int CO, int64_t M);                  // blocks (a multiple of the column split)
+int64_t pw_bwd_squeeze_slab_floats(int CI, int CO, int nblocks);     // wgrad slab workspace
 void pw_bwd_squeeze(const PwSqueezeBwdArgs& args, int nblocks, hipStream_t s);
 
 // ---------------------------------------------------------------- f32 GEMM (MFMA f32, exact)

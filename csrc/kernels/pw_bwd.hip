@@ -363,51 +363,65 @@ __device__ __forceinline__ U4 mask_bf16x8_pw(const U4& v, uint32_t bits) {
 //   wgrad  dW1 [CO x CI] += T1^T . X                   (X = conv1's input tile, MN image)
 // dy1 never exists in HBM and dx's tensors are read once: the launch moves g1, y1, X, the addend and
 // its mask, the previous tail's input and mask, and writes dx (ResNet-50/CIFAR stage 1: ~610 MB).
-template <int CI, int CO>
+// wide-column split of the F1 kernel per narrow width (see PwSqueezeBwdCfg)
+constexpr int pw_squeeze_split(int CO) { return CO == 128 ? 4 : 1; }
+
+// Wide columns split over S blocks (stage 2, CI = 512 / CO = 128: W1 is 128 KB, too big to sit in LDS
+// beside the tiles, and a CO x CI/2 wgrad accumulator spills at 256 VGPRs; S = 4 blocks each keep a
+// CO x CI/4 slice resident and take the same m-tiles' other columns -- the narrow g1 / y1 pieces are
+// read by all four, ~30 % of the launch's bytes).  Block b runs part
+// b % S over m-tiles b / S, b / S + grid / S, ...; its wgrad slab is slab (b % S) * grid / S + b / S.
+template <int CI, int CO, int S>
 struct PwSqueezeBwdCfg {
-  static constexpr int NTPR = CO / 4;                  // threads per narrow row (8-B pieces)
-  static constexpr int TPR = CI / 8;                   // threads per wide row (16-B pieces)
+  static constexpr int CIH = CI / S;                   // wide columns per block
+  static constexpr int NPC = CO * PW_BM / PW_NT;       // narrow channels per thread piece (4 or 8)
+  static constexpr int NTPR = CO / NPC;                // threads per narrow row
+  static constexpr int TPR = CIH / 8;                  // threads per wide row (16-B pieces)
   static constexpr int RSTEP = PW_NT / TPR;            // rows between a thread's wide pieces
   static constexpr int LPT = PW_BM * TPR / PW_NT;      // wide pieces per thread per tensor per tile
-  static constexpr int T_BYTES = PW_BM * CO * 2;       // T1 tile, K-major 64-channel rows
-  static constexpr int X_BYTES = PW_BM * CI * 2;       // X tile, MN image
+  static constexpr int T_BYTES = PW_BM * CO * 2;       // T1 tile: CO / 64 K-major images of 64-channel rows
+  static constexpr int X_BYTES = PW_BM * CIH * 2;      // X tile, MN image
   static constexpr int SLOT = T_BYTES + X_BYTES;
-  static constexpr int W_BYTES = CO * CI * 2;          // W1 MN image (rows = co), resident
-  static constexpr int D_BYTES = PW_BM * CI * 4;       // dgrad accumulator tile (f32), epilogue hand-off
-  static constexpr int DCOLS = CI / 4;                 // dgrad columns per wave (2 row x 4 col groups)
+  static constexpr int W_BYTES = CO * CIH * 2;         // W1 slice MN image (rows = co), resident
+  static constexpr int D_BYTES = PW_BM * CIH * 4;      // dgrad accumulator tile (f32), epilogue hand-off
+  static constexpr int DCOLS = CIH / 4;                // dgrad columns per wave (2 row x 4 col groups)
   static constexpr int DTN = DCOLS / 16;
   static constexpr int WROWS = CO / 2;                 // wgrad: co rows per wave (2 groups)
   static constexpr int WTM = WROWS / 16;
-  static constexpr int WCOLS = CI / 4;                 // wgrad: ci columns per wave (4 groups)
+  static constexpr int WCOLS = CIH / 4;                // wgrad: ci columns per wave (4 groups)
   static constexpr int WTN = WCOLS / 16;
-  static_assert(CO == 64, "T1 is one 64-channel K-major chunk");
+  static_assert(CO % 64 == 0 && (NPC == 4 || NPC == 8), "T1: 64-channel K-major chunks, 8 / 16-B pieces");
   static_assert(PW_BM * NTPR == PW_NT, "narrow tile mapping");
   static_assert(LPT >= 1 && PW_BM * TPR % PW_NT == 0, "wide tile mapping");
-  static_assert(2 * SLOT + W_BYTES + D_BYTES + (2 * CI + 5 * CO) * 4 <= 160 * 1024, "LDS budget");
+  static_assert(2 * SLOT + W_BYTES + D_BYTES + (2 * CIH + 5 * CO) * 4 <= 160 * 1024, "LDS budget");
+  static_assert(16 * PW_NT * 4 <= 2 * SLOT, "previous tail partials tree in the (free) slot area");
 };
+// byte offset of 16-B chunk c (8 narrow channels) of row r in the T1 image (64-channel K-major images)
+__device__ __forceinline__ int pw_toff(int r, int c) { return (c >> 3) * (PW_BM * 128) + pw_kmaj(r, c & 7); }
 
 // D tile (f32 [32][CI]): 16-B chunk q of row r at r * CI * 4 + ((q ^ (r & 7)) << 4)  (the SWAP writers put
 // 16 rows x 4 consecutive columns per instruction; the row-contiguous readers take 32 B of one row)
 template <int CI>
 __device__ __forceinline__ int pw_doff(int r, int q) { return r * CI * 4 + ((q ^ (r & 7)) << 4); }
 
-template <int CI, int CO>
+template <int CI, int CO, int S>
 __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdArgs a) {
-  using C = PwSqueezeBwdCfg<CI, CO>;
-  constexpr int LPT = C::LPT;
-  __shared__ __attribute__((aligned(16))) char smem[2 * C::SLOT + C::W_BYTES + C::D_BYTES + (2 * CI + 5 * CO) * 4];
+  using C = PwSqueezeBwdCfg<CI, CO, S>;
+  constexpr int LPT = C::LPT, CIH = C::CIH, NPC = C::NPC;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::SLOT + C::W_BYTES + C::D_BYTES + (2 * CIH + 5 * CO) * 4];
   char* wimg = smem + 2 * C::SLOT;
   char* dimg = wimg + C::W_BYTES;
   // previous tail BN's [invstd | -mean invstd] per wide channel; BN1's [A | B | D | scale | shift]
   float* pcoef = reinterpret_cast<float*>(dimg + C::D_BYTES);
-  float* ncoef = pcoef + 2 * CI;
+  float* ncoef = pcoef + 2 * CIH;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int ntiles = a.M / PW_BM;
+  const int part = S == 1 ? 0 : (int)blockIdx.x % S, col0 = part * CIH;  // this block's wide columns
 
-  for (int c = t; c < CI; c += PW_NT) {
-    const float is = a.psave[CI + c];
+  for (int c = t; c < CIH; c += PW_NT) {
+    const float is = a.psave[CI + col0 + c];
     pcoef[c] = is;
-    pcoef[CI + c] = -a.psave[c] * is;
+    pcoef[CIH + c] = -a.psave[col0 + c] * is;
   }
   if (t < CO) {
     const float inv_m = 1.f / (float)a.M;
@@ -419,18 +433,20 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
     ncoef[3 * CO + t] = sc;
     ncoef[4 * CO + t] = a.save1[3 * CO + t];
   }
-  // ---- W1 [CO][CI] -> MN image (row = co), resident
-  pw_resident_copy<CO * CI / 8>(
-      t, [&](int q) { return reinterpret_cast<pw_u32x4*>(wimg + pw_mn<CI>(q / (CI / 8), q % (CI / 8))); },
-      [&](int q) { return reinterpret_cast<const pw_u32x4*>(a.w) + q; });
+  // ---- W1 [CO][col0 .. col0 + CIH) -> MN image (row = co), resident
+  pw_resident_copy<CO * CIH / 8>(
+      t, [&](int q) { return reinterpret_cast<pw_u32x4*>(wimg + pw_mn<CIH>(q / (CIH / 8), q % (CIH / 8))); },
+      [&](int q) {
+        return reinterpret_cast<const pw_u32x4*>(a.w) + (q / (CIH / 8)) * (CI / 8) + col0 / 8 + q % (CIH / 8);
+      });
   const int64_t wide = (int64_t)a.M * CI * 2, narrow = (int64_t)a.M * CO * 2;
   const __amdgpu_buffer_rsrc_t rg = pw_rsrc(a.g1, narrow), ry = pw_rsrc(a.y1, narrow), rx = pw_rsrc(a.x, wide);
   const __amdgpu_buffer_rsrc_t rad = pw_rsrc(a.addend, wide), ram = pw_rsrc(a.amask, (int64_t)a.M * CI / 8);
   const __amdgpu_buffer_rsrc_t rpx = pw_rsrc(a.px, wide), rpm = pw_rsrc(a.pmask, (int64_t)a.M * CI / 8);
   const __amdgpu_buffer_rsrc_t rdx = pw_rsrc(a.dx, wide);
 
-  // narrow piece (g1 / y1 -> T1): row t / NTPR, channels nc0 .. nc0 + 3
-  const int nrow = t / C::NTPR, nc0 = 4 * (t % C::NTPR);
+  // narrow piece (g1 / y1 -> T1): row t / NTPR, channels nc0 .. nc0 + NPC - 1
+  const int nrow = t / C::NTPR, nc0 = NPC * (t % C::NTPR);
   // wide pieces (X, addend, previous tail input, masks; the dx epilogue): rows r0 + RSTEP i, channels
   // 8 chc .. 8 chc + 7 -- fixed for the launch, so the previous tail BN's partials stay per thread
   const int chc = t % C::TPR, r0 = t / C::TPR;
@@ -448,23 +464,29 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
     for (int n = 0; n < C::WTN; ++n) accw[i][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   // ---- register staging ring (two tiles): every operand of a tile, coalesced 8 / 16-B pieces
+  using NV = std::conditional_t<NPC == 4, pw_u32x2, pw_u32x4>;
   struct Stage {
-    pw_u32x2 g, y;
+    NV g, y;
     pw_u32x4 x[LPT], ad[LPT], px[LPT];
     uint32_t mk[LPT];  // addend mask byte | previous tail mask byte << 8
   };
   Stage st0, st1;
-  const int tile0 = blockIdx.x, tstep = gridDim.x;
+  const int tile0 = (int)blockIdx.x / S, tstep = (int)gridDim.x / S;
   auto issue = [&](Stage& s, int tile) {
     const bool ok = tile < ntiles;
     const uint32_t no = ok ? (uint32_t)((tile * PW_BM + nrow) * CO + nc0) * 2u : 0x80000000u;
-    s.g = __builtin_amdgcn_raw_buffer_load_b64(rg, no, 0, 0);
-    s.y = __builtin_amdgcn_raw_buffer_load_b64(ry, no, 0, 0);
+    if constexpr (NPC == 4) {
+      s.g = __builtin_amdgcn_raw_buffer_load_b64(rg, no, 0, 0);
+      s.y = __builtin_amdgcn_raw_buffer_load_b64(ry, no, 0, 0);
+    } else {
+      s.g = __builtin_amdgcn_raw_buffer_load_b128(rg, no, 0, 0);
+      s.y = __builtin_amdgcn_raw_buffer_load_b128(ry, no, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int row = tile * PW_BM + r0 + C::RSTEP * i;
-      const uint32_t o = ok ? (uint32_t)(row * CI + 8 * chc) * 2u : 0x80000000u;
-      const uint32_t ob = ok ? (uint32_t)(row * C::TPR + chc) : 0x80000000u;
+      const uint32_t o = ok ? (uint32_t)(row * CI + col0 + 8 * chc) * 2u : 0x80000000u;
+      const uint32_t ob = ok ? (uint32_t)(row * (CI / 8) + col0 / 8 + chc) : 0x80000000u;
       s.x[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, o, 0, 0);
       s.ad[i] = __builtin_amdgcn_raw_buffer_load_b128(rad, o, 0, 0);
       s.px[i] = __builtin_amdgcn_raw_buffer_load_b128(rpx, o, 0, 0);
@@ -477,28 +499,41 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
   pw_u32x4 ead[LPT], epx[LPT];
   uint32_t emk[LPT];
   auto stage = [&](const Stage& s, char* slot) {
-    float gf[4], yf[4], o[4];
-    const float4 A4 = *reinterpret_cast<const float4*>(ncoef + nc0);
-    const float4 B4 = *reinterpret_cast<const float4*>(ncoef + CO + nc0);
-    const float4 D4 = *reinterpret_cast<const float4*>(ncoef + 2 * CO + nc0);
-    const float4 S4 = *reinterpret_cast<const float4*>(ncoef + 3 * CO + nc0);
-    const float4 H4 = *reinterpret_cast<const float4*>(ncoef + 4 * CO + nc0);
-    const float A[4] = {A4.x, A4.y, A4.z, A4.w}, B[4] = {B4.x, B4.y, B4.z, B4.w}, D[4] = {D4.x, D4.y, D4.z, D4.w};
-    const float sc[4] = {S4.x, S4.y, S4.z, S4.w}, sh[4] = {H4.x, H4.y, H4.z, H4.w};
-    gf[0] = __uint_as_float(s.g[0] << 16); gf[1] = __uint_as_float(s.g[0] & 0xffff0000u);
-    gf[2] = __uint_as_float(s.g[1] << 16); gf[3] = __uint_as_float(s.g[1] & 0xffff0000u);
-    yf[0] = __uint_as_float(s.y[0] << 16); yf[1] = __uint_as_float(s.y[0] & 0xffff0000u);
-    yf[2] = __uint_as_float(s.y[1] << 16); yf[3] = __uint_as_float(s.y[1] & 0xffff0000u);
+    float gf[NPC], yf[NPC], o[NPC];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gg = fmaf(yf[k], sc[k], sh[k]) > 0.f ? gf[k] : 0.f;
-      o[k] = fmaf(A[k], gg, fmaf(B[k], yf[k], D[k]));
+    for (int h = 0; h < NPC / 2; ++h) {
+      gf[2 * h] = __uint_as_float(s.g[h] << 16);
+      gf[2 * h + 1] = __uint_as_float(s.g[h] & 0xffff0000u);
+      yf[2 * h] = __uint_as_float(s.y[h] << 16);
+      yf[2 * h + 1] = __uint_as_float(s.y[h] & 0xffff0000u);
     }
-    *reinterpret_cast<pw_u32x2*>(slot + pw_kmaj(nrow, nc0 >> 3) + ((nc0 >> 2) & 1) * 8) =
-        (pw_u32x2){pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+#pragma unroll
+    for (int q = 0; q < NPC / 4; ++q) {
+      const int c = nc0 + 4 * q;
+      const float4 A4 = *reinterpret_cast<const float4*>(ncoef + c);
+      const float4 B4 = *reinterpret_cast<const float4*>(ncoef + CO + c);
+      const float4 D4 = *reinterpret_cast<const float4*>(ncoef + 2 * CO + c);
+      const float4 S4 = *reinterpret_cast<const float4*>(ncoef + 3 * CO + c);
+      const float4 H4 = *reinterpret_cast<const float4*>(ncoef + 4 * CO + c);
+      const float A[4] = {A4.x, A4.y, A4.z, A4.w}, B[4] = {B4.x, B4.y, B4.z, B4.w}, D[4] = {D4.x, D4.y, D4.z, D4.w};
+      const float sc[4] = {S4.x, S4.y, S4.z, S4.w}, sh[4] = {H4.x, H4.y, H4.z, H4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gg = fmaf(yf[4 * q + k], sc[k], sh[k]) > 0.f ? gf[4 * q + k] : 0.f;
+        o[4 * q + k] = fmaf(A[k], gg, fmaf(B[k], yf[4 * q + k], D[k]));
+      }
+    }
+    if constexpr (NPC == 4) {
+      *reinterpret_cast<pw_u32x2*>(slot + pw_toff(nrow, nc0 >> 3) + ((nc0 >> 2) & 1) * 8) =
+          (pw_u32x2){pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+    } else {
+      *reinterpret_cast<pw_u32x4*>(slot + pw_toff(nrow, nc0 >> 3)) =
+          (pw_u32x4){pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]),
+                     pack_bf16x2(o[6], o[7])};
+    }
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      *reinterpret_cast<pw_u32x4*>(slot + C::T_BYTES + pw_mn<CI>(r0 + C::RSTEP * i, chc)) = s.x[i];
+      *reinterpret_cast<pw_u32x4*>(slot + C::T_BYTES + pw_mn<CIH>(r0 + C::RSTEP * i, chc)) = s.x[i];
       ead[i] = s.ad[i];
       epx[i] = s.px[i];
       emk[i] = s.mk[i];
@@ -509,34 +544,34 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
     __builtin_amdgcn_s_barrier();
   };
   auto compute = [&](const char* slot, int tile) {
-    // dgrad: acc_d[32 x CI] = T1[32 x CO] . W1 -> D tile (f32, LDS)
+    // dgrad: acc_d[32 x CIH] = T1[32 x CO] . W1 slice -> D tile (f32, LDS)
     {
       f32x4_t accd[C::DTN];
 #pragma unroll
       for (int j = 0; j < C::DTN; ++j) accd[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < CO / 32; ++kc) {
-        const bf16x8_t fa = pw_frag_kmaj(slot, 0, drb, 4 * kc, lane);
+        const bf16x8_t fa = pw_frag_kmaj(slot, ((4 * kc) >> 3) * (PW_BM * 128), drb, (4 * kc) & 7, lane);
 #pragma unroll
         for (int j = 0; j < C::DTN; ++j) {
-          const bf16x8_t fb = pw_frag_tr(wimg, 32 * kc * CI * 2, dcb + 16 * j, lane,
-                                         [](int r, int c) { return pw_mn<CI>(r, c); });
+          const bf16x8_t fb = pw_frag_tr(wimg, 32 * kc * CIH * 2, dcb + 16 * j, lane,
+                                         [](int r, int c) { return pw_mn<CIH>(r, c); });
           accd[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, accd[j], 0, 0, 0);  // SWAP
         }
       }
       const int drow = drb + (lane & 15);
 #pragma unroll
       for (int j = 0; j < C::DTN; ++j)
-        *reinterpret_cast<f32x4_t*>(dimg + pw_doff<CI>(drow, (dcb + 16 * j) / 4 + (lane >> 4))) = accd[j];
+        *reinterpret_cast<f32x4_t*>(dimg + pw_doff<CIH>(drow, (dcb + 16 * j) / 4 + (lane >> 4))) = accd[j];
     }
-    // wgrad: acc_w[CO x CI] += T1^T . X (k = the tile's 32 rows)
+    // wgrad: acc_w[CO x CIH] += T1^T . X (k = the tile's 32 rows)
     bf16x8_t fx[C::WTN];
 #pragma unroll
     for (int n = 0; n < C::WTN; ++n)
-      fx[n] = pw_frag_tr(slot + C::T_BYTES, 0, wcb + 16 * n, lane, [](int r, int c) { return pw_mn<CI>(r, c); });
+      fx[n] = pw_frag_tr(slot + C::T_BYTES, 0, wcb + 16 * n, lane, [](int r, int c) { return pw_mn<CIH>(r, c); });
 #pragma unroll
     for (int i = 0; i < C::WTM; ++i) {
-      const bf16x8_t ft = pw_frag_tr(slot, 0, wrb + 16 * i, lane, [](int r, int c) { return pw_kmaj(r, c); });
+      const bf16x8_t ft = pw_frag_tr(slot, 0, wrb + 16 * i, lane, [](int r, int c) { return pw_toff(r, c); });
 #pragma unroll
       for (int n = 0; n < C::WTN; ++n) accw[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ft, fx[n], accw[i][n], 0, 0, 0);
     }
@@ -544,15 +579,15 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
     // dx epilogue, row-contiguous: + masked addend -> bf16 16-B stores; previous tail BN partials
     const float4 pi0 = *reinterpret_cast<const float4*>(pcoef + 8 * chc);
     const float4 pi1 = *reinterpret_cast<const float4*>(pcoef + 8 * chc + 4);
-    const float4 pn0 = *reinterpret_cast<const float4*>(pcoef + CI + 8 * chc);
-    const float4 pn1 = *reinterpret_cast<const float4*>(pcoef + CI + 8 * chc + 4);
+    const float4 pn0 = *reinterpret_cast<const float4*>(pcoef + CIH + 8 * chc);
+    const float4 pn1 = *reinterpret_cast<const float4*>(pcoef + CIH + 8 * chc + 4);
     const float pis[8] = {pi0.x, pi0.y, pi0.z, pi0.w, pi1.x, pi1.y, pi1.z, pi1.w};
     const float pnm[8] = {pn0.x, pn0.y, pn0.z, pn0.w, pn1.x, pn1.y, pn1.z, pn1.w};
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int lrow = r0 + C::RSTEP * i;
-      const f32x4_t v0 = *reinterpret_cast<const f32x4_t*>(dimg + pw_doff<CI>(lrow, 2 * chc));
-      const f32x4_t v1 = *reinterpret_cast<const f32x4_t*>(dimg + pw_doff<CI>(lrow, 2 * chc + 1));
+      const f32x4_t v0 = *reinterpret_cast<const f32x4_t*>(dimg + pw_doff<CIH>(lrow, 2 * chc));
+      const f32x4_t v1 = *reinterpret_cast<const f32x4_t*>(dimg + pw_doff<CIH>(lrow, 2 * chc + 1));
       float ad[8], xv[8], v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       unpack8(mask_bf16x8_pw(__builtin_bit_cast(U4, ead[i]), emk[i] & 0xffu), ad);
       unpack8(__builtin_bit_cast(U4, epx[i]), xv);
@@ -560,7 +595,7 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
       for (int k = 0; k < 8; ++k) v[k] += ad[k];
       const U4 packed = pack8(v);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pw_u32x4, packed), rdx,
-                                             (uint32_t)((tile * PW_BM + lrow) * CI + 8 * chc) * 2u, 0, 0);
+                                             (uint32_t)((tile * PW_BM + lrow) * CI + col0 + 8 * chc) * 2u, 0, 0);
       float gv[8];
       unpack8(mask_bf16x8_pw(packed, emk[i] >> 8), gv);
 #pragma unroll
@@ -587,17 +622,18 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
     compute(smem + C::SLOT, t1);
   }
 
-  // ---- wgrad accumulators -> this block's slab, in register order (coalesced 16-B stores)
-  float* slab = a.slab + (size_t)blockIdx.x * (CO * CI);
+  // ---- wgrad accumulators -> this block's slab, in register order (coalesced 16-B stores); the slabs
+  // of one column part are contiguous
+  float* slab = a.slab + (size_t)(part * tstep + tile0) * (CO * CIH);
 #pragma unroll
   for (int i = 0; i < C::WTM; ++i)
 #pragma unroll
     for (int n = 0; n < C::WTN; ++n)
       *reinterpret_cast<f32x4_t*>(slab + ((size_t)(i * C::WTN + n) * PW_NT + t) * 4) = accw[i][n];
   // ---- previous tail BN partials: threads t, t + TPR, ... share channels 8 chc .. 8 chc + 7 -> LDS
-  // (the D tile, free now) tree over the RSTEP row groups, one atomic pair per channel
+  // (the staging slots, free now) tree over the RSTEP row groups, one atomic pair per channel
   __syncthreads();
-  float* red = reinterpret_cast<float*>(dimg);  // [16][RSTEP][TPR]
+  float* red = reinterpret_cast<float*>(smem);  // [16][RSTEP][TPR]
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     red[(k * C::RSTEP + r0) * C::TPR + chc] = bs[k];
@@ -610,20 +646,21 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
 #pragma unroll
     for (int r = 0; r < C::RSTEP; ++r) v += red[(kk * C::RSTEP + r) * C::TPR + ch];
     const int c = 8 * ch + (kk & 7);
-    atomicAdd(a.pslots + (size_t)(blockIdx.x % NSLOT) * 2 * CI + (kk >> 3) * CI + c, v);
+    atomicAdd(a.pslots + (size_t)(tile0 % NSLOT) * 2 * CI + (kk >> 3) * CI + col0 + c, v);
   }
 }
 
-// F1 slab element e = ((i * WTN + n) * NT + t) * 4 + r  ->  dW1 [co][ci]: lane = t & 63, wave = t >> 6;
-// co = WROWS (wave & 1) + 16 i + (lane >> 4) * 4 + r, ci = WCOLS (wave >> 1) + 16 n + (lane & 15)
-template <int CI, int CO>
-__device__ __forceinline__ int pw_slab_to_dw1(int e) {
-  using C = PwSqueezeBwdCfg<CI, CO>;
+// F1 slab element e = ((i * WTN + n) * NT + t) * 4 + r of column part p  ->  dW1 [co][ci]: lane = t & 63,
+// wave = t >> 6; co = WROWS (wave & 1) + 16 i + (lane >> 4) * 4 + r,
+// ci = p CIH + WCOLS (wave >> 1) + 16 n + (lane & 15)
+template <int CI, int CO, int S>
+__device__ __forceinline__ int pw_slab_to_dw1(int e, int p) {
+  using C = PwSqueezeBwdCfg<CI, CO, S>;
   const int r = e & 3, t = (e >> 2) % PW_NT, in = (e >> 2) / PW_NT;
   const int i = in / C::WTN, n = in % C::WTN;
   const int lane = t & 63, wv = t >> 6;
   const int co = C::WROWS * (wv & 1) + 16 * i + (lane >> 4) * 4 + r;
-  const int ci = C::WCOLS * (wv >> 1) + 16 * n + (lane & 15);
+  const int ci = p * C::CIH + C::WCOLS * (wv >> 1) + 16 * n + (lane & 15);
   return co * CI + ci;
 }
 
@@ -738,17 +775,21 @@ __global__ void __launch_bounds__(256) pw_slab_reduce_kernel(const float* __rest
     }
     return;
   }
-  const int e = (blockIdx.x % (E / 256)) * 256 + threadIdx.x, grp = blockIdx.x / (E / 256);
+  // F1 with its wide columns split over S blocks: S groups of nslab / S slabs of E / S elements each
+  constexpr int S = MAP == 1 ? pw_squeeze_split(CN) : 1, EH = E / S;
+  const int eg = (blockIdx.x % (E / 256)) * 256 + threadIdx.x, grp = blockIdx.x / (E / 256);
+  const int part = eg / EH, e = eg % EH, nper = nslab / S;
+  const float* sl = slab + (size_t)part * nper * EH;
   float acc = 0.f;
   int b = grp;
-  for (; b + 3 * rg < nslab; b += 4 * rg) {
-    const float v0 = slab[(size_t)b * E + e], v1 = slab[(size_t)(b + rg) * E + e];
-    const float v2 = slab[(size_t)(b + 2 * rg) * E + e], v3 = slab[(size_t)(b + 3 * rg) * E + e];
+  for (; b + 3 * rg < nper; b += 4 * rg) {
+    const float v0 = sl[(size_t)b * EH + e], v1 = sl[(size_t)(b + rg) * EH + e];
+    const float v2 = sl[(size_t)(b + 2 * rg) * EH + e], v3 = sl[(size_t)(b + 3 * rg) * EH + e];
     acc += (v0 + v1) + (v2 + v3);
   }
-  for (; b < nslab; b += rg) acc += slab[(size_t)b * E + e];
+  for (; b < nper; b += rg) acc += sl[(size_t)b * EH + e];
   if constexpr (MAP == 0) atomicAdd(dw + pw_slab_to_dw<CN>(e), acc);
-  else if constexpr (MAP == 1) atomicAdd(dw + pw_slab_to_dw1<4 * CN, CN>(e), acc);
+  else if constexpr (MAP == 1) atomicAdd(dw + pw_slab_to_dw1<4 * CN, CN, S>(e, part), acc);
   else atomicAdd(dw + pw_slab_to_dw_c3(e), acc);
 }
 
@@ -773,11 +814,22 @@ void pw_bwd_expand(const PwExpandArgs& args, int nblocks, hipStream_t s) {
 }
 
 bool pw_bwd_squeeze_ok(int CI, int CO, int64_t M) {
-  return CI == 256 && CO == 64 && M % PW_BM == 0 && M > 0 && (int64_t)M * CI < (1ll << 30);
+  return ((CI == 256 && CO == 64) || (CI == 512 && CO == 128)) && M % PW_BM == 0 && M > 0 &&
+         (int64_t)M * CI < (1ll << 30);
 }
 
+// one block per CU: S column parts x up to 256 / S m-tile strides
+int pw_bwd_squeeze_grid(int CI, int CO, int64_t M) {
+  (void)CI;
+  const int S = pw_squeeze_split(CO);
+  return S * (int)std::min<int64_t>(256 / S, M / PW_BM);
+}
+
+int64_t pw_bwd_squeeze_slab_floats(int CI, int CO, int nblocks) { return (int64_t)nblocks * CO * CI / pw_squeeze_split(CO); }
+
 void pw_bwd_squeeze(const PwSqueezeBwdArgs& args, int nblocks, hipStream_t s) {
-  if (args.CI == 256 && args.CO == 64) pw_bwd_squeeze_kernel<256, 64><<<nblocks, PW_NT, 0, s>>>(args);
+  if (args.CI == 256 && args.CO == 64) pw_bwd_squeeze_kernel<256, 64, 1><<<nblocks, PW_NT, 0, s>>>(args);
+  else if (args.CI == 512 && args.CO == 128) pw_bwd_squeeze_kernel<512, 128, pw_squeeze_split(128)><<<nblocks, PW_NT, 0, s>>>(args);
   else abort();
 }
 
@@ -798,6 +850,11 @@ void pw_slab_reduce(const float* slab, int nslab, int CN, float* dw, float* sr_s
       else
         pw_slab_reduce_kernel<64, 2><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
                                                           sr_dgamma, sr_dbeta, sec, rg);
+      break;
+    case 128:
+      if (map != 1) abort();
+      pw_slab_reduce_kernel<128, 1><<<grid, 256, 0, s>>>(slab, nslab, dw, sr_slots, sr_slots ? sr_C : 0, sr_red,
+                                                         sr_dgamma, sr_dbeta, sec, rg);
       break;
     default: abort();
   }

@@ -4,6 +4,7 @@
 #include "tfx_common.h"
 #include "tfx_kernels.h"
 
+#include <type_traits>
 #include <utility>
 
 namespace tfx {

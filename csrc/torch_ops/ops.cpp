@@ -716,8 +716,8 @@ std::tuple<Tensor, Tensor> pw_bwd_squeeze(Tensor g1, Tensor y1, Tensor save1, Te
   a.w = bf(w); a.addend = bf(addend); a.amask = amask.data_ptr<uint8_t>(); a.px = bf(px);
   a.psave = psave.data_ptr<float>(); a.pmask = pmask.data_ptr<uint8_t>(); a.pslots = pslots.data_ptr<float>();
   a.dx = bfm(dx); a.M = (int)M; a.CI = (int)CI; a.CO = (int)CO;
-  const int nb = tfx::pw_bwd_expand_grid((int)CO, M);
-  auto slab = at::empty({(int64_t)nb * CO * CI}, x.options().dtype(at::kFloat));
+  const int nb = tfx::pw_bwd_squeeze_grid((int)CI, (int)CO, M);
+  auto slab = at::empty({tfx::pw_bwd_squeeze_slab_floats((int)CI, (int)CO, nb)}, x.options().dtype(at::kFloat));
   a.slab = slab.data_ptr<float>();
   tfx::pw_bwd_squeeze(a, nb, cur_stream());
   tfx::pw_slab_reduce(a.slab, nb, (int)CO, dw.data_ptr<float>(), a.pslots, (int)CI, pred.data_ptr<float>(),

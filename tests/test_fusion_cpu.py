@@ -96,7 +96,7 @@ GPU_TABLE = {
     ("bn_on_load", "conv3x3_fwd_fused"): 3,
     ("bn_on_load", "igemm_fwd_a_scale"): 3,
     ("lazy_bn_bwd", "pw_bwd_expand"): 3,
-    ("lazy_bn_bwd", "pw_bwd_squeeze"): 2,
+    ("lazy_bn_bwd", "pw_bwd_squeeze"): 5,
     ("conv3_fused_bwd", "conv3x3_bwd_fused"): 3,
     ("stem_kernels", "stem_wgrad"): 1,
     ("bn_epilogue", "stem_fwd"): 1,
@@ -115,7 +115,7 @@ def _native_or_skip():
 def test_resnet50_plan_built_on_cpu_matches_gpu_table():
     """The ResNet-50 fusion plan at batch 256, built without a GPU: the same fused-kernel counts as the
     GPU step's recorder table, every conv planned (53 forwards), and the per-layer choices where the
-    kernels' shape limits put them (stage 1 fully fused, stage 2 only at the block boundaries)."""
+    kernels' shape limits put them (stage 1 fully fused, stage 2 at the block boundaries and the identity conv1 backward)."""
     _native_or_skip()
     from tensorflow_examples_amd.models.resnet import build_resnet_cifar
     st, m = build_resnet_cifar(device="cpu", depth=50, dtype=torch.float32)
@@ -129,6 +129,8 @@ def test_resnet50_plan_built_on_cpu_matches_gpu_table():
     assert lay["resnet50/stage1_block2/conv1"].fwd == "pw_fwd_squeeze"
     assert lay["resnet50/stage1_block2/conv2"].bwd == "conv3x3_bwd_fused"
     assert lay["resnet50/stage2_block2/conv2"].pre == "bn_apply_into"  # 128 channels: no fused consumer
+    assert lay["resnet50/stage2_block2/conv1"].bwd == "pw_bwd_squeeze"  # 512 <- 128: four-way column split
+    assert lay["resnet50/stage3_block2/conv1"].bwd != "pw_bwd_squeeze"
     assert lay["resnet50/stage3_block2/conv1"].input == "tail" and lay["resnet50/stage3_block2/conv1"].pre
     assert "igemm_dgrad_compact" in lay["resnet50/stage2_block1/shortcut"].extra
     assert "stage1_block2/conv2" in plan.table()

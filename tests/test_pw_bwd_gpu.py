@@ -100,12 +100,16 @@ def _mask_bits(mask, M, C, dev):
     return bits.reshape(M, C).float()
 
 
-@pytest.mark.parametrize("shape", [(256, 32, 32), (4, 8, 8), (3, 4, 8)])
-def test_pw_bwd_squeeze_matches_reference(gpu, shape):
+@pytest.mark.parametrize("shape,widths", [((256, 32, 32), (256, 64)), ((4, 8, 8), (256, 64)), ((3, 4, 8), (256, 64)),
+                                          ((256, 16, 16), (512, 128)), ((4, 8, 8), (512, 128)),
+                                          ((3, 4, 8), (512, 128))])
+def test_pw_bwd_squeeze_matches_reference(gpu, shape, widths):
     """F1: BN1 backward apply + conv1 dgrad (+ masked residual addend, + previous tail BN partials)
-    + conv1 wgrad in one launch, vs the layer-wise apply and fp32 GEMMs."""
+    + conv1 wgrad in one launch, vs the layer-wise apply and fp32 GEMMs.  Stage 1 (256 <- 64) and stage
+    2 (512 <- 128: wide columns split over four blocks) at the batch-256 production shape and small
+    ones (fewer m-tiles than blocks)."""
     N, H, W = shape
-    CI, CO, M = 256, 64, N * H * W
+    (CI, CO), M = widths, N * H * W
     torch.manual_seed(13)
     # BN1 (plain ReLU): input y1, output gradient g1, its backward reduction
     y1 = _bf(torch.randn(N, H, W, CO, device=gpu) * 1.1 + 0.2)
@@ -176,7 +180,8 @@ def test_resnet50_lazy_tail_backward_matches_layerwise(gpu):
             n0, n1 = nnops.PW_EXPAND_CALLS[0], nnops.PW_SQUEEZE_BWD_CALLS[0]
             l0, g0, st = run()
             assert nnops.PW_EXPAND_CALLS[0] - n0 == 3, "stage-1 blocks run fused (projection block 1 with F3-SEC)"
-            assert nnops.PW_SQUEEZE_BWD_CALLS[0] - n1 == 2, "stage-1 identity blocks' conv1 backward runs fused (F1)"
+            assert nnops.PW_SQUEEZE_BWD_CALLS[0] - n1 == 5, \
+                "stage-1 and stage-2 identity blocks' conv1 backward runs fused (F1)"
             # negative control: both fused kernels' input gradients x0.95
             with scaled_output("pw_bwd_expand", lambda a, o: [o[0]]), \
                     scaled_output("pw_bwd_squeeze", lambda a, o: [o[0]]):

@@ -176,7 +176,7 @@ def test_resnet50_fusion_plan(gpu):
         ("bn_on_load", "conv3x3_fwd_fused"): 3,
         ("bn_on_load", "igemm_fwd_a_scale"): 3,
         ("lazy_bn_bwd", "pw_bwd_expand"): 3,
-        ("lazy_bn_bwd", "pw_bwd_squeeze"): 2,
+        ("lazy_bn_bwd", "pw_bwd_squeeze"): 5,
         ("conv3_fused_bwd", "conv3x3_bwd_fused"): 3,
         ("stem_kernels", "stem_wgrad"): 1,
         ("bn_epilogue", "stem_fwd"): 1,
