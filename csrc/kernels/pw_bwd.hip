@@ -369,8 +369,8 @@ constexpr int pw_squeeze_split(int CO) { return CO == 128 ? 4 : 1; }
 // Wide columns split over S blocks (stage 2, CI = 512 / CO = 128: W1 is 128 KB, too big to sit in LDS
 // beside the tiles, and a CO x CI/2 wgrad accumulator spills at 256 VGPRs; S = 4 blocks each keep a
 // CO x CI/4 slice resident and take the same m-tiles' other columns -- the narrow g1 / y1 pieces are
-// read by all four, ~30 % of the launch's bytes).  Block b runs part
-// b % S over m-tiles b / S, b / S + grid / S, ...; its wgrad slab is slab (b % S) * grid / S + b / S.
+// read by all four, ~30 % of the launch's bytes).  Block b runs one part over m-tiles t0, t0 + grid / S,
+// ... (mapping in the kernel); its wgrad slab is slab part * grid / S + t0.
 template <int CI, int CO, int S>
 struct PwSqueezeBwdCfg {
   static constexpr int CIH = CI / S;                   // wide columns per block
@@ -416,7 +416,14 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
   float* ncoef = pcoef + 2 * CIH;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int ntiles = a.M / PW_BM;
-  const int part = S == 1 ? 0 : (int)blockIdx.x % S, col0 = part * CIH;  // this block's wide columns
+  // column part and first m-tile of this block.  With the grid a multiple of 8 S the split is XCD-aware:
+  // blocks are dispatched round-robin over the 8 XCDs (b % 8), and the S parts of one m-tile stride take
+  // consecutive slots of ONE XCD, so the narrow g1 / y1 pieces they all read are shared through that
+  // XCD's L2 instead of being fetched once per XCD.  Other grids: part b % S, tile b / S.
+  const int b = (int)blockIdx.x;
+  const bool xcd_split = S > 1 && (int)gridDim.x % (8 * S) == 0;
+  const int part = S == 1 ? 0 : xcd_split ? (b / 8) % S : b % S, col0 = part * CIH;  // this block's wide columns
+  const int tile0 = S == 1 ? b : xcd_split ? (b % 8) + 8 * (b / (8 * S)) : b / S;
 
   for (int c = t; c < CIH; c += PW_NT) {
     const float is = a.psave[CI + col0 + c];
@@ -471,7 +478,7 @@ __global__ void __launch_bounds__(PW_NT, 1) pw_bwd_squeeze_kernel(PwSqueezeBwdAr
     uint32_t mk[LPT];  // addend mask byte | previous tail mask byte << 8
   };
   Stage st0, st1;
-  const int tile0 = (int)blockIdx.x / S, tstep = (int)gridDim.x / S;
+  const int tstep = (int)gridDim.x / S;
   auto issue = [&](Stage& s, int tile) {
     const bool ok = tile < ntiles;
     const uint32_t no = ok ? (uint32_t)((tile * PW_BM + nrow) * CO + nc0) * 2u : 0x80000000u;
