@@ -3,6 +3,7 @@
 # own time limit and the steps are chained -- a crash, abort or time-out ends the session (no further
 # GPU work), a failing test does not.  Output under $O/; copy what is worth keeping to profiles/.
 #   tests    pytest -m gpu (the whole GPU suite, one process)
+#   smoke    __graft_entry__.smoke() (the driver's round-end smoke)
 #   bench    bench.py --steps 20 --warmup 5 (the driver's 1-GPU command)
 #   prof     rocprofv3 --kernel-trace --stats over a short bench, summarised by scripts/kstats.py
 #   pmc      PMC passes (MFMA busy, LDS conflicts, HBM bytes) over an eager bench, one run per pass
@@ -25,6 +26,9 @@ for s in $STEPS; do
         ${PYTEST_EXTRA:-} > $O/pytest_gpu.log 2>&1
       rc=$?; echo "pytest rc=$rc"; tail -5 $O/pytest_gpu.log
       [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -2 $O/smoke.log; [ $rc -eq 0 ] || exit $rc ;;
     bench)
       for i in ${BENCH_REPS:-1}; do
         timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_$i.log 2>&1
