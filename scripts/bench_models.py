@@ -4,6 +4,7 @@
     python scripts/bench_models.py --model lenet5   [--impl native|torch] [--graph]
     python scripts/bench_models.py --model word2vec [--impl native|torch] [--graph]
     python scripts/bench_models.py --model char_lstm [--impl native|torch] [--graph]
+    python scripts/bench_models.py --model resnet50 --impl torch [--graph]   (stock PyTorch comparison)
     python scripts/bench_models.py --model mnist_softmax   (CPU, config 1)
 
 Same timing discipline as bench.py: W untimed warmup steps, synchronize, K timed steps,
@@ -189,6 +190,37 @@ def bench_char_lstm(a, dev):
                 final_loss=float(loss))
 
 
+# ---------------------------------------------------------------- ResNet-50/CIFAR (stock PyTorch only)
+def bench_resnet50(a, dev):
+    """The headline step in stock PyTorch-ROCm (torch.nn + MIOpen, channels_last, bf16 autocast,
+    torch.optim.SGD foreach), optionally captured into a HIP graph -- a stronger comparison point than the
+    eager baseline of ``bench.py --impl torch`` (the native step is ``bench.py``).  The batch is a fixed
+    device-resident normalised image tensor."""
+    assert a.impl == "torch", "the native ResNet-50 step is bench.py"
+    import torch.nn as nn
+    from tensorflow_examples_amd.models.torch_baseline import TorchResNet50Cifar
+    B = a.batch or 256
+    torch.manual_seed(0)
+    net = TorchResNet50Cifar().to(dev).to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4, foreach=True)
+    x = torch.randn(B, 3, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (B,), device=dev)
+
+    def one():
+        opt.zero_grad(set_to_none=False)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = nn.functional.cross_entropy(net(x), y)
+        loss.backward()
+        opt.step()
+        return loss.detach()
+    run = graphed(one) if a.graph else one
+    dt, loss = timed(lambda i: run(), a.steps, a.warmup)
+    return dict(metric="images/sec ResNet-50/CIFAR-10 bf16 (1 GPU)", value=B * a.steps / dt, unit="images/sec",
+                ms_per_step=dt * 1e3 / a.steps,
+                config=dict(model="ResNet-50 (CIFAR-10 adaptation: 3x3 stem, bottleneck [3,4,6,3])", global_batch=B,
+                            seq_len=None), final_loss=float(loss))
+
+
 # ---------------------------------------------------------------- MNIST softmax (CPU)
 def bench_mnist_softmax(a, dev):
     from tensorflow_examples_amd.models.mnist_mlp import MnistSoftmax
@@ -216,7 +248,7 @@ def bench_mnist_softmax(a, dev):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", required=True, choices=["lenet5", "word2vec", "char_lstm", "mnist_softmax"])
+    ap.add_argument("--model", required=True, choices=["lenet5", "word2vec", "char_lstm", "mnist_softmax", "resnet50"])
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
@@ -229,10 +261,10 @@ def main(argv=None):
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     fn = {"lenet5": bench_lenet, "word2vec": bench_word2vec, "char_lstm": bench_char_lstm,
-          "mnist_softmax": bench_mnist_softmax}[a.model]
+          "mnist_softmax": bench_mnist_softmax, "resnet50": bench_resnet50}[a.model]
     rec = fn(a, dev)
     rec.update(impl=a.impl, hip_graph=bool(a.graph), steps=a.steps, warmup=a.warmup, n_gpus=1 if dev.type == "cuda" else 0,
-               dtype="bf16" if a.model in ("lenet5", "char_lstm") else "fp32", data="synthetic")
+               dtype="bf16" if a.model in ("lenet5", "char_lstm", "resnet50") else "fp32", data="synthetic")
     rec["value"] = round(rec["value"], 1)
     rec["ms_per_step"] = round(rec["ms_per_step"], 3)
     print(json.dumps(rec), flush=True)
