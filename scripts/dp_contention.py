@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--latency_us", type=float, default=15.0)
     ap.add_argument("--passes", type=int, default=2, help="read+write sweeps of the bucket per collective "
                     "(2 ~ a ring all-reduce's local traffic); -1 = stream for the whole ring time")
+    ap.add_argument("--wires", default="f32,bf16", help="gradient wires to sweep (comma list)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -59,7 +60,7 @@ def main():
     lab = torch.randint(0, 10, (a.batch,), generator=g).to(dev)
     x = to_model_input(img)
     rows = []
-    for wire in ("f32", "bf16"):
+    for wire in a.wires.split(","):
         for nb in [int(v) for v in a.blocks.split(",")]:
             if wire == "bf16" and nb == 0:
                 continue
